@@ -1,0 +1,180 @@
+/*
+ * gossiphip.h — C-ABI of libgossiphip, the MI355X-native batched
+ * gossip-membership / failure-detection / replica-placement engine.
+ *
+ * This is the drop-in boundary for the hot path of
+ * xiaoxin0515/P2P-File-system-with-Gossip-Detect-Failure-Management
+ * (SURVEY.md §8b). The reference has no FFI; its hot path sits behind Go
+ * methods and a net/rpc service. Each entry point below names the reference
+ * interface it replaces (file:line under the reference tree). Semantics:
+ * SPEC.md. Host bindings: INTEGRATION.md (cgo stub) and
+ * p2p-file-system-with-gossip-detect-failure-management_amd/gossipsim (ctypes).
+ *
+ * Conventions
+ *   - Every function returns 0 (GH_OK) or a negative GH_E* code; the reason is
+ *     in gh_last_error(h). The reference instead log.Fatal/log.Panic's
+ *     (slave/slave.go:214,262-270; master/master.go:130-135).
+ *   - Buffers are caller-owned host memory, read or written only during the
+ *     call. The handle owns all device memory (HBM) and the HIP stream.
+ *   - A handle is not thread-safe (call it from one thread; cgo callers use
+ *     runtime.LockOSThread).
+ *   - Member IDs are dense int32 in [0, n_members); file IDs dense int32 in
+ *     [0, max_files).
+ *   - There is no CPU fallback: gh_create fails with GH_ENODEV when no gfx950
+ *     device is usable.
+ */
+#ifndef GOSSIPHIP_H_
+#define GOSSIPHIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GH_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------- */
+#define GH_OK 0
+#define GH_EINVAL (-1)               /* bad argument / shape                    */
+#define GH_ENODEV (-2)               /* no usable HIP device                    */
+#define GH_ENOMEM (-3)               /* device allocation failed                */
+#define GH_EHIP (-4)                 /* HIP runtime error                       */
+#define GH_EPLACEMENT_STARVED (-5)   /* master/master.go:130-135 hang / panic   */
+#define GH_ERANGE (-6)               /* value out of encodable range            */
+
+/* ---- cell encoding (SPEC.md §1) -------------------------------------- */
+#define GH_ABSENT (-1)     /* not in MemberList                              */
+#define GH_TOMBSTONE (-2)  /* in RecentFailList (slave/slave.go:65)          */
+
+/* ---- modes ------------------------------------------------------------ */
+#define GH_PEER_PULL 0     /* receiver pulls k Philox-selected peers          */
+#define GH_PEER_RING 1     /* reference ring push, slave/slave.go:512-524     */
+#define GH_DETECT_CANONICAL 0
+#define GH_DETECT_QUIRK 1  /* Go range-over-mutated-slice skip, slave.go:464   */
+
+/* ---- events (SPEC.md §5) ---------------------------------------------- */
+#define GH_EV_JOIN 1       /* slave/slave.go:288 Join + :250 addNewMember     */
+#define GH_EV_LEAVE 2      /* slave/slave.go:310 Leave                        */
+#define GH_EV_CRASH 3      /* README.md:30 "CTRL+C to crash node"            */
+
+typedef struct gh_config {
+  int32_t n_members;     /* N; member IDs 0..N-1                             */
+  int32_t fanout;        /* k (pull mode), 1..8                              */
+  int32_t peer_mode;     /* GH_PEER_PULL | GH_PEER_RING                      */
+  int32_t detect_mode;   /* GH_DETECT_CANONICAL | GH_DETECT_QUIRK            */
+  int32_t t_fail;        /* PERIOD in rounds, slave/slave.go:24 (5)          */
+  int32_t t_cleanup;     /* COOLDOWN in rounds, slave/slave.go:25 (5)        */
+  int32_t min_members;   /* literal 4, slave/slave.go:504,511                */
+  int32_t replicas;      /* 4, master/master.go:131 (1..8)                   */
+  int32_t introducer;    /* INTRODUCER_ADDR, slave/slave.go:22 (0)           */
+  int32_t master;        /* master row whose list is Member_list (0)        */
+  int32_t device;        /* HIP device ordinal                               */
+  int32_t reserved0;
+  uint64_t seed;         /* Philox key for peers and placement draws         */
+  int64_t max_files;     /* file-metadata capacity (0 = no files)            */
+  int32_t reserved[8];
+} gh_config;
+
+typedef struct gh_event {
+  int32_t kind;          /* GH_EV_*                                          */
+  int32_t member;
+} gh_event;
+
+/* Counters accumulated over the rounds of one gh_step call. */
+typedef struct gh_round_stats {
+  int64_t rounds;         /* rounds executed by this call                    */
+  int64_t last_round;     /* `now` of the last round executed                */
+  int64_t detections;     /* cells removed by detectfailure (slave.go:472)   */
+  int64_t failed_members; /* Σ_rounds distinct members detected that round   */
+  int64_t remove_unknown; /* REMOVE/LEAVE of an unknown member (slave.go:280 panic) */
+  int64_t ring_empty;     /* ring sender with empty list (slave.go:517 div-by-0)   */
+  int64_t active_rows;    /* Σ_rounds rows passing the <4 guard              */
+  int64_t merged_cells;   /* cells advanced or added by MergeMemberList      */
+  int64_t released;       /* tombstones dropped by cleanFailList             */
+  int64_t tombstoned;     /* tombstones created by REMOVE/LEAVE delivery     */
+} gh_round_stats;
+
+/* One re-replication plan entry (master/master.go:27-31 Replicate_info). */
+typedef struct gh_plan_entry {
+  int32_t file;
+  int32_t node1;          /* first working replica, -1 if none (SPEC D5)     */
+  int32_t version;
+  int32_t n_new;
+  int32_t status;         /* GH_OK or GH_EPLACEMENT_STARVED                  */
+  int32_t new_nodes[8];   /* first n_new valid                               */
+} gh_plan_entry;
+
+/* Fills *cfg with the reference defaults (SURVEY.md §5 Config). */
+void gh_config_default(gh_config* cfg);
+
+/* Replaces InitSlave/InitMaster (slave/slave.go:95, master/master.go:38) for
+ * N members at once. Allocates hb (x2) and ts tables in HBM: 12*N*N bytes. */
+int gh_create(const gh_config* cfg, void** handle);
+void gh_destroy(void* h);
+const char* gh_last_error(void* h);
+int gh_abi_version(void);
+
+/* Whole-state transfer (host <-> HBM). Rows [row0, row0+n_rows) of the N x N
+ * tables; hb values >= 2^30 are rejected. `round` is the tick of the last
+ * completed round; pending REMOVEs are cleared on import. */
+int gh_import_state(void* h, const int32_t* hb, const int32_t* ts,
+                    const uint8_t* alive, int64_t row0, int64_t n_rows,
+                    int32_t round);
+int gh_export_state(void* h, int32_t* hb, int32_t* ts, uint8_t* alive,
+                    int64_t row0, int64_t n_rows);
+/* Every row alive and holding every member at (hb0, ts0): the synthetic
+ * full-membership start of BASELINE configs 2-4, filled on the device. */
+int gh_init_full(void* h, int32_t hb0, int32_t ts0, int32_t round);
+int gh_get_round(void* h, int32_t* round);
+
+/* Queue churn for the next round (GetMsg JOIN/LEAVE dispatch,
+ * slave/slave.go:224-240; crash = process death). */
+int gh_apply_events(void* h, const gh_event* ev, int64_t n);
+
+/* Run `rounds` synchronous gossip rounds (HeartBeat, slave/slave.go:499,
+ * driven by the 1 s loop of main.go:27-33, with MergeMemberList :414,
+ * detectfailure :460, cleanFailList :484). Blocks until done; stats may be
+ * NULL. */
+int gh_step(void* h, int32_t rounds, gh_round_stats* stats);
+
+/* Members detected in the last round as an N-bit bitmap (REMOVE broadcast
+ * set, slave/slave.go:338). */
+int gh_read_failed(void* h, uint32_t* bitmap, int64_t n_words);
+/* Rows that detected a failure in the last round (they call Fail_recover,
+ * slave/slave.go:479-481). Returns the count via *n_out (<= cap written). */
+int gh_read_detectors(void* h, int32_t* rows, int64_t cap, int64_t* n_out);
+/* "lsm" (slave/slave.go:558-561): observer's present members. */
+int gh_lsm(void* h, int32_t observer, int32_t* ids, int32_t* hb, int32_t* ts,
+           int64_t cap, int64_t* n_out);
+
+/* "put" placement: Handle_put_request (master/master.go:152) for n distinct
+ * files. replicas: [n][replicas] (-1 padded), versions [n], status [n]
+ * (GH_OK / GH_EPLACEMENT_STARVED). Returns GH_EPLACEMENT_STARVED if any file
+ * starved. */
+int gh_put(void* h, const int32_t* files, int64_t n, int32_t* replicas,
+           int32_t* versions, int32_t* status);
+/* Update_metadata (master/master.go:74) with available = observer's list;
+ * plan entries in file order. *n_plan = number of entries (<= cap written). */
+int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap,
+              int64_t* n_plan);
+/* get / ls (master/master.go:177-212): versions -1 if absent. */
+int gh_get_files(void* h, const int32_t* files, int64_t n, int32_t* replicas,
+                 int32_t* versions);
+/* delete (master/master.go:249-259): old replicas returned. */
+int gh_delete_files(void* h, const int32_t* files, int64_t n,
+                    int32_t* old_replicas);
+
+/* Device timing of the fused round kernel (HIP events on the engine's
+ * stream), for bench.py's roofline: enable, then read the sum of kernel
+ * durations (ms) and launch count since enabling. */
+int gh_set_timing(void* h, int32_t enable);
+int gh_read_timing(void* h, double* total_ms, int64_t* launches);
+/* Block until all queued device work has finished. */
+int gh_sync(void* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GOSSIPHIP_H_ */

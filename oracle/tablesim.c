@@ -1,0 +1,741 @@
+/*
+ * ORACLE / TEST INFRASTRUCTURE ONLY.
+ *
+ * tablesim — a plain-C CPU restatement of the reference's gossip membership,
+ * failure detection and replica placement, in the synchronous-round form of
+ * SPEC.md. It is the checker for libgossiphip's HIP path: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg load it. Nothing in
+ * the product path links or calls it.
+ *
+ * It is written as the straightforward multi-phase algorithm (phase A: steps
+ * 1-5 per row; snapshot copy; phase B: ring targets; phase C: merge), not the
+ * GPU's single-pass form, so that the two are independent implementations.
+ *
+ * Reference functions restated (paths under /root/reference):
+ *   removeMember        slave/slave.go:276-286   -> or_remove_member
+ *   MergeMemberList     slave/slave.go:414-440   -> or_merge_row
+ *   updateMemberList    slave/slave.go:442-458   -> phase_a (own hb++)
+ *   detectfailure       slave/slave.go:460-482   -> phase_a (detect)
+ *   cleanFailList       slave/slave.go:484-497   -> phase_a (clean)
+ *   HeartBeat           slave/slave.go:499-544   -> guard + ring targets
+ *   addNewMember/Join   slave/slave.go:250-308   -> apply_events (join)
+ *   Leave               slave/slave.go:310-336   -> apply_events (leave)
+ *   Init_replica        master/master.go:129-150 -> or_init_replica
+ *   Handle_put_request  master/master.go:152-175 -> or_put
+ *   Update_metadata     master/master.go:74-127  -> or_repair
+ *   Get_file_* / Delete master/master.go:177-259 -> or_get_files/or_delete_files
+ *
+ * Parity status: the reference has no tests, fixtures or runnable toolchain
+ * here (no Go), so this oracle is pinned by hand-derived known-answer tests
+ * (tests/golden/) and by cross-checking against the literal
+ * list-semantics replay oracle/listsim.py — not by reference outputs
+ * ("parity unpinned" against the reference binary itself).
+ */
+#include <limits.h>
+#include <omp.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/gossiphip.h"
+#include "philox.h"
+
+#define OR_MAX_DRAWS_PER_CALL (1u << 20)
+
+typedef struct ors {
+  gh_config cfg;
+  int32_t n;     /* members (columns)                                      */
+  int64_t rows;  /* observer rows (== n except in the bench sample)        */
+  int32_t round; /* last completed round                                   */
+  int32_t *hb, *ts, *snap;
+  uint8_t *alive, *active, *det_any;
+  int32_t *det_cnt, *det_min;   /* pending REMOVE set D_{r-1} (per column) */
+  int32_t *ndet_cnt, *ndet_min; /* detections of the current round         */
+  int32_t *targets;             /* ring mode: rows x 3                     */
+  gh_event *ev;
+  int64_t nev, evcap;
+  int64_t fcap;
+  int32_t *rep, *ver, *fts;
+  uint32_t *draws;
+  int threads;
+  char err[256];
+} ors;
+
+#define HB(s, i, c) ((s)->hb[(int64_t)(i) * (s)->n + (c)])
+#define TS(s, i, c) ((s)->ts[(int64_t)(i) * (s)->n + (c)])
+#define SNAP(s, i, c) ((s)->snap[(int64_t)(i) * (s)->n + (c)])
+
+static int fail(ors *s, int code, const char *msg) {
+  if (s) snprintf(s->err, sizeof s->err, "%s", msg);
+  return code;
+}
+
+int or_create(const gh_config *cfg, int64_t rows, void **out) {
+  if (!cfg || !out || cfg->n_members < 1 || rows < 1 || rows > cfg->n_members) return GH_EINVAL;
+  if (cfg->fanout < 1 || cfg->fanout > 8 || cfg->replicas < 1 || cfg->replicas > 8) return GH_EINVAL;
+  ors *s = (ors *)calloc(1, sizeof(ors));
+  s->cfg = *cfg;
+  s->n = cfg->n_members;
+  s->rows = rows;
+  int64_t cells = (int64_t)rows * s->n;
+  s->hb = (int32_t *)malloc(cells * 4);
+  s->ts = (int32_t *)malloc(cells * 4);
+  s->snap = (int32_t *)malloc(cells * 4);
+  s->alive = (uint8_t *)calloc(rows, 1);
+  s->active = (uint8_t *)calloc(rows, 1);
+  s->det_any = (uint8_t *)calloc(rows, 1);
+  s->det_cnt = (int32_t *)calloc(s->n, 4);
+  s->det_min = (int32_t *)malloc((size_t)s->n * 4);
+  s->ndet_cnt = (int32_t *)calloc(s->n, 4);
+  s->ndet_min = (int32_t *)malloc((size_t)s->n * 4);
+  s->targets = (int32_t *)malloc((size_t)rows * 3 * 4);
+  if (!s->hb || !s->ts || !s->snap) {
+    free(s->hb);
+    free(s->ts);
+    free(s->snap);
+    free(s);
+    return GH_ENOMEM;
+  }
+  for (int64_t x = 0; x < cells; ++x) {
+    s->hb[x] = GH_ABSENT;
+    s->ts[x] = 0;
+  }
+  for (int32_t c = 0; c < s->n; ++c) s->det_min[c] = s->ndet_min[c] = INT_MAX;
+  s->fcap = cfg->max_files;
+  if (s->fcap > 0) {
+    int R = cfg->replicas;
+    s->rep = (int32_t *)malloc(s->fcap * R * 4);
+    s->ver = (int32_t *)malloc(s->fcap * 4);
+    s->fts = (int32_t *)calloc(s->fcap, 4);
+    s->draws = (uint32_t *)calloc(s->fcap, 4);
+    for (int64_t x = 0; x < s->fcap * R; ++x) s->rep[x] = -1;
+    for (int64_t f = 0; f < s->fcap; ++f) s->ver[f] = -1;
+  }
+  s->threads = 1;
+  *out = s;
+  return GH_OK;
+}
+
+void or_destroy(void *h) {
+  ors *s = (ors *)h;
+  if (!s) return;
+  free(s->hb);
+  free(s->ts);
+  free(s->snap);
+  free(s->alive);
+  free(s->active);
+  free(s->det_any);
+  free(s->det_cnt);
+  free(s->det_min);
+  free(s->ndet_cnt);
+  free(s->ndet_min);
+  free(s->targets);
+  free(s->ev);
+  free(s->rep);
+  free(s->ver);
+  free(s->fts);
+  free(s->draws);
+  free(s);
+}
+
+const char *or_last_error(void *h) { return h ? ((ors *)h)->err : "null handle"; }
+
+int or_set_threads(void *h, int threads) {
+  ors *s = (ors *)h;
+  s->threads = threads < 1 ? 1 : threads;
+  return GH_OK;
+}
+
+int or_import_state(void *h, const int32_t *hb, const int32_t *ts, const uint8_t *alive,
+                    int64_t row0, int64_t n_rows, int32_t round) {
+  ors *s = (ors *)h;
+  if (row0 < 0 || n_rows < 0 || row0 + n_rows > s->rows) return fail(s, GH_EINVAL, "row range");
+  for (int64_t x = 0; x < n_rows * s->n; ++x) {
+    if (hb[x] < GH_TOMBSTONE || hb[x] >= (1 << 30)) return fail(s, GH_ERANGE, "hb out of range");
+  }
+  memcpy(s->hb + row0 * s->n, hb, n_rows * s->n * 4);
+  memcpy(s->ts + row0 * s->n, ts, n_rows * s->n * 4);
+  memcpy(s->alive + row0, alive, n_rows);
+  s->round = round;
+  for (int32_t c = 0; c < s->n; ++c) {
+    s->det_cnt[c] = 0;
+    s->det_min[c] = INT_MAX;
+  }
+  memset(s->det_any, 0, s->rows);
+  return GH_OK;
+}
+
+int or_export_state(void *h, int32_t *hb, int32_t *ts, uint8_t *alive, int64_t row0,
+                    int64_t n_rows) {
+  ors *s = (ors *)h;
+  if (row0 < 0 || n_rows < 0 || row0 + n_rows > s->rows) return fail(s, GH_EINVAL, "row range");
+  if (hb) memcpy(hb, s->hb + row0 * s->n, n_rows * s->n * 4);
+  if (ts) memcpy(ts, s->ts + row0 * s->n, n_rows * s->n * 4);
+  if (alive) memcpy(alive, s->alive + row0, n_rows);
+  return GH_OK;
+}
+
+int or_init_full(void *h, int32_t hb0, int32_t ts0, int32_t round) {
+  ors *s = (ors *)h;
+  if (hb0 < 0 || hb0 >= (1 << 30)) return fail(s, GH_ERANGE, "hb0");
+  int64_t cells = s->rows * s->n;
+  for (int64_t x = 0; x < cells; ++x) {
+    s->hb[x] = hb0;
+    s->ts[x] = ts0;
+  }
+  memset(s->alive, 1, s->rows);
+  s->round = round;
+  for (int32_t c = 0; c < s->n; ++c) {
+    s->det_cnt[c] = 0;
+    s->det_min[c] = INT_MAX;
+  }
+  return GH_OK;
+}
+
+int or_get_round(void *h, int32_t *round) {
+  *round = ((ors *)h)->round;
+  return GH_OK;
+}
+
+int or_apply_events(void *h, const gh_event *ev, int64_t n) {
+  ors *s = (ors *)h;
+  for (int64_t x = 0; x < n; ++x) {
+    if (ev[x].kind < GH_EV_JOIN || ev[x].kind > GH_EV_CRASH) return fail(s, GH_EINVAL, "event kind");
+    if (ev[x].member < 0 || ev[x].member >= s->rows) return fail(s, GH_EINVAL, "event member");
+  }
+  if (s->nev + n > s->evcap) {
+    s->evcap = (s->nev + n) * 2 + 16;
+    s->ev = (gh_event *)realloc(s->ev, s->evcap * sizeof(gh_event));
+  }
+  memcpy(s->ev + s->nev, ev, n * sizeof(gh_event));
+  s->nev += n;
+  return GH_OK;
+}
+
+/* removeMember(c) at row j (slave/slave.go:276-286). */
+static inline void or_remove_member(ors *s, int64_t j, int32_t c, gh_round_stats *st) {
+  int32_t v = HB(s, j, c);
+  if (v >= 0) {
+    HB(s, j, c) = GH_TOMBSTONE; /* appended to RecentFailList with its ts (:280) */
+    st->tombstoned++;
+  } else if (v == GH_ABSENT) {
+    st->remove_unknown++; /* reference: MemberList[-1] panic (:280) */
+  }
+}
+
+/* MergeMemberList (slave/slave.go:414-440) of one message `msg` (n cells,
+ * >=0 present) into row j at time r. */
+static inline int64_t or_merge_row(ors *s, int64_t j, const int32_t *msg, int32_t r) {
+  int64_t merged = 0;
+  int32_t *row = s->hb + j * s->n;
+  int32_t *trow = s->ts + j * s->n;
+  for (int32_t c = 0; c < s->n; ++c) {
+    int32_t m = msg[c];
+    if (m < 0) continue;
+    int32_t v = row[c];
+    /* present and lower (:424-426) or absent and not tombstoned (:430-438) */
+    if (v >= GH_ABSENT && m > v) {
+      row[c] = m;
+      trow[c] = r;
+      merged++;
+    }
+  }
+  return merged;
+}
+
+static void apply_events(ors *s, int32_t r, gh_round_stats *st) {
+  if (s->nev == 0) return;
+  /* crashes */
+  for (int64_t x = 0; x < s->nev; ++x)
+    if (s->ev[x].kind == GH_EV_CRASH) s->alive[s->ev[x].member] = 0;
+  /* leaves: every leaver stops first (Alive=false, slave/slave.go:551,334) */
+  uint8_t *leaving = (uint8_t *)calloc(s->rows, 1);
+  for (int64_t x = 0; x < s->nev; ++x) {
+    int32_t c = s->ev[x].member;
+    if (s->ev[x].kind == GH_EV_LEAVE && s->alive[c]) {
+      leaving[c] = 1;
+      s->alive[c] = 0;
+    }
+  }
+  for (int64_t x = 0; x < s->nev; ++x) {
+    int32_t c = s->ev[x].member;
+    if (s->ev[x].kind != GH_EV_LEAVE || !leaving[c]) continue;
+    leaving[c] = 0; /* once per leaver */
+    /* LEAVE goes to every member of c's list except c (:316-319) */
+    for (int64_t j = 0; j < s->rows; ++j) {
+      if (j == c || !s->alive[j] || c >= s->n || HB(s, c, j) < 0) continue;
+      or_remove_member(s, j, c, st); /* :232-235 */
+    }
+  }
+  free(leaving);
+  /* joins */
+  int any_join = 0;
+  for (int64_t x = 0; x < s->nev; ++x) {
+    int32_t c = s->ev[x].member;
+    if (s->ev[x].kind != GH_EV_JOIN) continue;
+    any_join = 1;
+    if (!s->alive[c]) { /* fresh process: empty MemberList (SPEC D7) */
+      for (int32_t m = 0; m < s->n; ++m) {
+        HB(s, c, m) = GH_ABSENT;
+        TS(s, c, m) = 0;
+      }
+      s->alive[c] = 1;
+    }
+  }
+  int32_t I = s->cfg.introducer;
+  if (any_join && I >= 0 && I < s->rows && s->alive[I]) {
+    int added = 0;
+    for (int64_t x = 0; x < s->nev; ++x) {
+      int32_t c = s->ev[x].member;
+      if (s->ev[x].kind != GH_EV_JOIN) continue;
+      if (HB(s, I, c) < 0) { /* !MemberInList (:228-230) -> addNewMember (:250-255) */
+        HB(s, I, c) = 0;
+        TS(s, I, c) = r;
+        added++;
+      }
+    }
+    if (added) {
+      /* full list to every member of I's list, I and the joiner included (:256-272) */
+      int32_t *msg = (int32_t *)malloc((size_t)s->n * 4);
+      memcpy(msg, s->hb + (int64_t)I * s->n, (size_t)s->n * 4);
+      for (int64_t j = 0; j < s->rows; ++j) {
+        if (!s->alive[j] || msg[j] < 0) continue;
+        st->merged_cells += or_merge_row(s, j, msg, r);
+      }
+      free(msg);
+    }
+  }
+  s->nev = 0;
+}
+
+/* Phase A for one alive row i: steps 1-5 of SPEC §2. Returns 1 if active. */
+static int phase_a(ors *s, int64_t i, int32_t r, gh_round_stats *st) {
+  int32_t n = s->n;
+  int32_t *row = s->hb + i * n;
+  int32_t *trow = s->ts + i * n;
+  /* step 1: REMOVE delivery */
+  for (int32_t c = 0; c < n; ++c) {
+    int32_t dc = s->det_cnt[c];
+    if (dc == 0 || (dc == 1 && s->det_min[c] == i)) continue;
+    or_remove_member(s, i, c, st);
+  }
+  /* step 2: guard */
+  int64_t L = 0;
+  for (int32_t c = 0; c < n; ++c) L += row[c] >= 0;
+  if (L < s->cfg.min_members) {
+    for (int32_t c = 0; c < n; ++c)
+      if (row[c] >= 0) trow[c] = r; /* :505-507 */
+    return 0;
+  }
+  st->active_rows++;
+  /* step 3: own heartbeat (:443-448) */
+  if (i < n && row[i] >= 0) {
+    row[i] += 1;
+    trow[i] = r;
+  }
+  /* step 4: detect (:460-477) */
+  int32_t limit = r - s->cfg.t_fail;
+  int quirk = s->cfg.detect_mode == GH_DETECT_QUIRK;
+  int32_t last_present = -1;
+  if (quirk)
+    for (int32_t c = n - 1; c >= 0; --c)
+      if (row[c] >= 0) {
+        last_present = c;
+        break;
+      }
+  int prev_cand = 0;
+  int64_t off = 0;
+  int found = 0;
+  for (int32_t c = 0; c < n; ++c) {
+    int32_t v = row[c];
+    if (v < 0) continue; /* not in the list */
+    int cand = (c != i) && v > 1 && trow[c] < limit;
+    if (!cand) {
+      prev_cand = 0;
+      continue;
+    }
+    int det = 1;
+    if (quirk) {
+      off = prev_cand ? off + 1 : 0;
+      det = ((off & 1) == 0) || c == last_present;
+    }
+    prev_cand = 1;
+    if (!det) continue;
+    row[c] = GH_TOMBSTONE; /* removeMember keeps the stale ts (:280) */
+    st->detections++;
+    found = 1;
+#pragma omp atomic
+    s->ndet_cnt[c] += 1;
+#pragma omp critical(or_detmin)
+    {
+      if ((int32_t)i < s->ndet_min[c]) s->ndet_min[c] = (int32_t)i;
+    }
+  }
+  if (found) s->det_any[i] = 1;
+  /* step 5: clean (:484-497) */
+  int32_t climit = r - s->cfg.t_cleanup;
+  for (int32_t c = 0; c < n; ++c) {
+    if (row[c] == GH_TOMBSTONE && trow[c] < climit) {
+      row[c] = GH_ABSENT;
+      st->released++;
+    }
+  }
+  return 1;
+}
+
+static void stats_add(gh_round_stats *a, const gh_round_stats *b) {
+  a->detections += b->detections;
+  a->failed_members += b->failed_members;
+  a->remove_unknown += b->remove_unknown;
+  a->ring_empty += b->ring_empty;
+  a->active_rows += b->active_rows;
+  a->merged_cells += b->merged_cells;
+  a->released += b->released;
+  a->tombstoned += b->tombstoned;
+}
+
+static void one_round(ors *s, gh_round_stats *acc) {
+  int32_t r = s->round + 1;
+  int32_t n = s->n;
+  int64_t rows = s->rows;
+  gh_round_stats st;
+  memset(&st, 0, sizeof st);
+  apply_events(s, r, &st);
+  memset(s->det_any, 0, rows);
+  for (int32_t c = 0; c < n; ++c) {
+    s->ndet_cnt[c] = 0;
+    s->ndet_min[c] = INT_MAX;
+  }
+  /* phase A */
+#pragma omp parallel num_threads(s->threads)
+  {
+    gh_round_stats ls;
+    memset(&ls, 0, sizeof ls);
+#pragma omp for schedule(static)
+    for (int64_t i = 0; i < rows; ++i) {
+      s->active[i] = 0;
+      if (!s->alive[i]) continue;
+      s->active[i] = (uint8_t)phase_a(s, i, r, &ls);
+    }
+#pragma omp critical(or_stats)
+    stats_add(&st, &ls);
+  }
+  /* snapshot of every active alive row after steps 1-5 (what it sends) */
+#pragma omp parallel for num_threads(s->threads) schedule(static)
+  for (int64_t i = 0; i < rows; ++i)
+    if (s->active[i]) memcpy(s->snap + i * n, s->hb + i * n, (size_t)n * 4);
+
+  /* phase B/C: targets and merge */
+  if (s->cfg.peer_mode == GH_PEER_RING) {
+    /* neighbours in list order (slave/slave.go:515-524) */
+    for (int64_t sdr = 0; sdr < rows; ++sdr) {
+      int32_t *t = s->targets + sdr * 3;
+      t[0] = t[1] = t[2] = -1;
+      if (!s->active[sdr]) continue;
+      const int32_t *sn = s->snap + sdr * n;
+      int64_t L = 0, idx = -1;
+      for (int32_t c = 0; c < n; ++c)
+        if (sn[c] >= 0) {
+          if (c == sdr) idx = L;
+          L++;
+        }
+      if (L == 0) {
+        st.ring_empty++;
+        continue;
+      }
+      int64_t want[3] = {idx - 1, idx + 1, idx + 2};
+      for (int q = 0; q < 3; ++q) {
+        int64_t v = want[q] % L; /* Go and C both truncate toward zero */
+        if (v < 0) v += L;
+        want[q] = v;
+      }
+      int64_t rank = 0;
+      for (int32_t c = 0; c < n; ++c)
+        if (sn[c] >= 0) {
+          for (int q = 0; q < 3; ++q)
+            if (want[q] == rank) t[q] = c;
+          rank++;
+        }
+    }
+    /* deliver: receiver i takes the max over every datagram addressed to it
+     * (sequential MergeMemberList calls in any order give the same row) */
+    int32_t *m = (int32_t *)malloc((size_t)n * 4);
+    uint8_t *hit = (uint8_t *)calloc(rows, 1);
+    for (int64_t sdr = 0; sdr < rows; ++sdr)
+      for (int q = 0; q < 3; ++q) {
+        int32_t tg = s->targets[sdr * 3 + q];
+        if (tg >= 0 && tg < rows) hit[tg] = 1;
+      }
+    for (int64_t i = 0; i < rows; ++i) {
+      if (!hit[i] || !s->alive[i]) continue;
+      for (int32_t c = 0; c < n; ++c) m[c] = -1;
+      for (int64_t sdr = 0; sdr < rows; ++sdr) {
+        if (!s->active[sdr]) continue;
+        const int32_t *t = s->targets + sdr * 3;
+        if (t[0] != i && t[1] != i && t[2] != i) continue;
+        const int32_t *sn = s->snap + sdr * n;
+        for (int32_t c = 0; c < n; ++c)
+          if (sn[c] > m[c]) m[c] = sn[c];
+      }
+      st.merged_cells += or_merge_row(s, i, m, r);
+    }
+    free(m);
+    free(hit);
+  } else {
+    int k = s->cfg.fanout;
+    uint64_t P = (uint64_t)rows;
+#pragma omp parallel num_threads(s->threads)
+    {
+      int64_t merged = 0;
+      int32_t *m = (int32_t *)malloc((size_t)n * 4);
+#pragma omp for schedule(static)
+      for (int64_t i = 0; i < rows; ++i) {
+        if (!s->alive[i] || P < 2) continue;
+        int have = 0;
+        for (int t = 0; t < k; ++t) {
+          uint32_t u = or_philox_word(s->cfg.seed, (uint32_t)i, (uint32_t)r, OR_TAG_PEER,
+                                      (uint32_t)(t >> 2), t & 3);
+          uint64_t q = ((uint64_t)u * (P - 1)) >> 32;
+          int64_t p = (int64_t)q + ((int64_t)q >= i);
+          if (!s->alive[p] || !s->active[p] || SNAP(s, p, i) < 0) continue;
+          const int32_t *sn = s->snap + p * n;
+          if (!have) {
+            for (int32_t c = 0; c < n; ++c) m[c] = sn[c];
+            have = 1;
+          } else {
+            for (int32_t c = 0; c < n; ++c)
+              if (sn[c] > m[c]) m[c] = sn[c];
+          }
+        }
+        if (have) merged += or_merge_row(s, i, m, r);
+      }
+      free(m);
+#pragma omp atomic
+      st.merged_cells += merged;
+    }
+  }
+  /* D_r becomes the pending REMOVE set of round r+1 */
+  int64_t nd = 0;
+  for (int32_t c = 0; c < n; ++c) {
+    s->det_cnt[c] = s->ndet_cnt[c];
+    s->det_min[c] = s->ndet_min[c];
+    nd += s->ndet_cnt[c] > 0;
+  }
+  st.failed_members = nd;
+  s->round = r;
+  acc->rounds++;
+  acc->last_round = r;
+  stats_add(acc, &st);
+}
+
+int or_step(void *h, int32_t rounds, gh_round_stats *stats) {
+  ors *s = (ors *)h;
+  gh_round_stats acc;
+  memset(&acc, 0, sizeof acc);
+  for (int32_t x = 0; x < rounds; ++x) one_round(s, &acc);
+  if (stats) *stats = acc;
+  return GH_OK;
+}
+
+int or_read_failed(void *h, uint32_t *bitmap, int64_t n_words) {
+  ors *s = (ors *)h;
+  if (n_words < (s->n + 31) / 32) return fail(s, GH_EINVAL, "bitmap too small");
+  memset(bitmap, 0, n_words * 4);
+  for (int32_t c = 0; c < s->n; ++c)
+    if (s->det_cnt[c] > 0) bitmap[c >> 5] |= 1u << (c & 31);
+  return GH_OK;
+}
+
+int or_read_detectors(void *h, int32_t *rows_out, int64_t cap, int64_t *n_out) {
+  ors *s = (ors *)h;
+  int64_t k = 0;
+  for (int64_t i = 0; i < s->rows; ++i)
+    if (s->det_any[i]) {
+      if (k < cap) rows_out[k] = (int32_t)i;
+      k++;
+    }
+  *n_out = k;
+  return GH_OK;
+}
+
+int or_lsm(void *h, int32_t obs, int32_t *ids, int32_t *hb, int32_t *ts, int64_t cap,
+           int64_t *n_out) {
+  ors *s = (ors *)h;
+  if (obs < 0 || obs >= s->rows) return fail(s, GH_EINVAL, "observer");
+  int64_t k = 0;
+  for (int32_t c = 0; c < s->n; ++c)
+    if (HB(s, obs, c) >= 0) {
+      if (k < cap) {
+        if (ids) ids[k] = c;
+        if (hb) hb[k] = HB(s, obs, c);
+        if (ts) ts[k] = TS(s, obs, c);
+      }
+      k++;
+    }
+  *n_out = k;
+  return GH_OK;
+}
+
+/* ---------------------------------------------------------------- files */
+
+/* Member_list of the master: present members of the master row, ID order
+ * (master/master.go:46 aliasing slave/slave.go:478). */
+static int32_t *candidates(ors *s, int64_t *M) {
+  int32_t *cand = (int32_t *)malloc((size_t)s->n * 4);
+  int64_t m = 0;
+  int32_t ms = s->cfg.master;
+  if (ms >= 0 && ms < s->rows)
+    for (int32_t c = 0; c < s->n; ++c)
+      if (HB(s, ms, c) >= 0) cand[m++] = c;
+  *M = m;
+  return cand;
+}
+
+/* Init_replica (master/master.go:129-150) with Philox draws. nodes[] holds
+ * `*len` valid entries; returns GH_OK or GH_EPLACEMENT_STARVED. */
+static int or_init_replica(ors *s, int32_t f, int32_t *nodes, int *len, const int32_t *cand,
+                           int64_t M, const uint8_t *is_cand_choosable) {
+  int R = s->cfg.replicas;
+  if (*len >= R) return GH_OK;
+  if (M <= 1) return GH_EPLACEMENT_STARVED; /* Intn(<=0) panics (:135) */
+  int64_t in_pool = 0;
+  for (int x = 0; x < *len; ++x)
+    if (nodes[x] >= 0 && nodes[x] < s->n && is_cand_choosable[nodes[x]]) in_pool++;
+  if ((M - 1) - in_pool < R - *len) return GH_EPLACEMENT_STARVED; /* infinite loop (:130) */
+  int32_t tmp[8];
+  int tl = *len;
+  for (int x = 0; x < tl; ++x) tmp[x] = nodes[x];
+  uint32_t d = s->draws[f];
+  uint32_t budget = OR_MAX_DRAWS_PER_CALL;
+  while (tl < R) {
+    if (budget-- == 0) return GH_EPLACEMENT_STARVED;
+    uint32_t u = or_philox_word(s->cfg.seed, (uint32_t)f, d, OR_TAG_PLACE, 0, 0);
+    d++;
+    uint64_t num = ((uint64_t)u * (uint64_t)(M - 1)) >> 32; /* r.Intn(len-1) (:135) */
+    int32_t a = cand[num];
+    int dup = 0;
+    for (int x = 0; x < tl; ++x) dup |= tmp[x] == a; /* isAddressExist (:137) */
+    if (!dup) tmp[tl++] = a;
+  }
+  s->draws[f] = d;
+  for (int x = 0; x < tl; ++x) nodes[x] = tmp[x];
+  *len = tl;
+  return GH_OK;
+}
+
+static uint8_t *choosable_map(ors *s, const int32_t *cand, int64_t M) {
+  uint8_t *map = (uint8_t *)calloc(s->n, 1);
+  for (int64_t x = 0; x + 1 < M; ++x) map[cand[x]] = 1; /* the last is never drawn */
+  return map;
+}
+
+int or_put(void *h, const int32_t *files, int64_t n, int32_t *replicas, int32_t *versions,
+           int32_t *status) {
+  ors *s = (ors *)h;
+  int R = s->cfg.replicas;
+  for (int64_t x = 0; x < n; ++x)
+    if (files[x] < 0 || files[x] >= s->fcap) return fail(s, GH_EINVAL, "file id");
+  int64_t M;
+  int32_t *cand = candidates(s, &M);
+  uint8_t *map = choosable_map(s, cand, M);
+  int rc = GH_OK;
+  for (int64_t x = 0; x < n; ++x) {
+    int32_t f = files[x];
+    int32_t *rp = s->rep + (int64_t)f * R;
+    if (s->ver[f] < 0) { /* Update_timestamp: new File_info (:239-245) */
+      s->ver[f] = 0;
+      for (int q = 0; q < R; ++q) rp[q] = -1;
+    }
+    s->fts[f] = s->round;
+    int len = 0;
+    while (len < R && rp[len] >= 0) len++;
+    int st = or_init_replica(s, f, rp, &len, cand, M, map);
+    if (st == GH_OK) s->ver[f] += 1; /* :159 */
+    else rc = GH_EPLACEMENT_STARVED;
+    if (status) status[x] = st;
+    if (versions) versions[x] = s->ver[f];
+    if (replicas)
+      for (int q = 0; q < R; ++q) replicas[x * R + q] = rp[q];
+  }
+  free(cand);
+  free(map);
+  return rc;
+}
+
+int or_repair(void *h, int32_t observer, gh_plan_entry *plan, int64_t cap, int64_t *n_plan) {
+  ors *s = (ors *)h;
+  if (observer < 0 || observer >= s->rows) return fail(s, GH_EINVAL, "observer");
+  int R = s->cfg.replicas;
+  int64_t M;
+  int32_t *cand = candidates(s, &M);
+  uint8_t *map = choosable_map(s, cand, M);
+  int64_t np = 0;
+  int rc = GH_OK;
+  for (int64_t f = 0; f < s->fcap; ++f) {
+    if (s->ver[f] < 0) continue;
+    int32_t *rp = s->rep + f * R;
+    int32_t working[8];
+    int wl = 0;
+    for (int q = 0; q < R; ++q) {
+      int32_t a = rp[q];
+      if (a < 0) continue;
+      if (a < s->n && HB(s, observer, a) >= 0) working[wl++] = a; /* :93-99 */
+    }
+    if (wl >= R) continue; /* :104 */
+    for (int q = 0; q < R; ++q) rp[q] = q < wl ? working[q] : -1; /* :106 */
+    int len = wl;
+    int st = or_init_replica(s, (int32_t)f, rp, &len, cand, M, map); /* :107 */
+    if (st != GH_OK) rc = GH_EPLACEMENT_STARVED;
+    if (np < cap) {
+      gh_plan_entry *e = plan + np;
+      memset(e, 0, sizeof *e);
+      e->file = (int32_t)f;
+      e->node1 = wl > 0 ? working[0] : -1; /* :120 */
+      e->version = s->ver[f];              /* :105 */
+      e->status = st;
+      int nn = 0;
+      for (int q = wl; q < len; ++q) e->new_nodes[nn++] = rp[q]; /* :110-115 */
+      for (int q = nn; q < 8; ++q) e->new_nodes[q] = -1;
+      e->n_new = nn;
+    }
+    np++;
+  }
+  free(cand);
+  free(map);
+  *n_plan = np;
+  return rc;
+}
+
+int or_get_files(void *h, const int32_t *files, int64_t n, int32_t *replicas,
+                 int32_t *versions) {
+  ors *s = (ors *)h;
+  int R = s->cfg.replicas;
+  for (int64_t x = 0; x < n; ++x) {
+    int32_t f = files[x];
+    if (f < 0 || f >= s->fcap) return fail(s, GH_EINVAL, "file id");
+    if (versions) versions[x] = s->ver[f];
+    if (replicas)
+      for (int q = 0; q < R; ++q) replicas[x * R + q] = s->ver[f] >= 0 ? s->rep[(int64_t)f * R + q] : -1;
+  }
+  return GH_OK;
+}
+
+int or_delete_files(void *h, const int32_t *files, int64_t n, int32_t *old_replicas) {
+  ors *s = (ors *)h;
+  int R = s->cfg.replicas;
+  for (int64_t x = 0; x < n; ++x) {
+    int32_t f = files[x];
+    if (f < 0 || f >= s->fcap) return fail(s, GH_EINVAL, "file id");
+    for (int q = 0; q < R; ++q) {
+      if (old_replicas) old_replicas[x * R + q] = s->ver[f] >= 0 ? s->rep[(int64_t)f * R + q] : -1;
+      s->rep[(int64_t)f * R + q] = -1;
+    }
+    s->ver[f] = -1;
+  }
+  return GH_OK;
+}
+
+void or_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  or_philox4x32_10_raw(ctr, key, out);
+}

@@ -1,0 +1,82 @@
+"""Cross-check the two independent CPU restatements of the reference:
+oracle/listsim.py (literal Go list semantics) and oracle/tablesim.c (dense
+tables), round by round on seeded churn scenarios (SPEC.md)."""
+import numpy as np
+import pytest
+
+from oracle.listsim import ListSim
+
+import scenarios as sc
+
+
+def run_pair(om, n, rounds, sched, peer_mode, fanout=3, quirk=False, seed=0x5EED0001,
+             init_full=False, t_fail=5, t_cleanup=5):
+    cfg = om.default_config(n, peer_mode=om.GH_PEER_RING if peer_mode == "ring" else om.GH_PEER_PULL,
+                            fanout=fanout, detect_mode=int(quirk), seed=seed, t_fail=t_fail,
+                            t_cleanup=t_cleanup)
+    orc = om.Oracle(cfg)
+    if init_full:
+        hb, ts, alive = sc.full_state(n)
+        orc.import_state(hb, ts, alive, 0)
+        ls = ListSim.from_dense(hb, ts, alive, 0, seed=seed, peer_mode=peer_mode, fanout=fanout,
+                                quirk=quirk)
+    else:
+        ls = ListSim(n, seed=seed, peer_mode=peer_mode, fanout=fanout, quirk=quirk)
+    import oracle.listsim as L
+    L.T_FAIL, L.T_CLEANUP = t_fail, t_cleanup
+    try:
+        for r in range(1, rounds + 1):
+            ev = sched.get(r, [])
+            if ev:
+                orc.apply_events(ev)
+                ls.apply_events(ev)
+            s1 = orc.step(1)
+            s2 = ls.step(1)
+            assert s1 == s2, f"round {r}: stats {s1} != {s2}"
+            h1, t1, a1 = orc.export_state()
+            h2, t2, a2 = ls.dense()
+            np.testing.assert_array_equal(a1, a2, err_msg=f"alive r={r}")
+            np.testing.assert_array_equal(h1, h2, err_msg=f"hb r={r}")
+            np.testing.assert_array_equal(*[sc.masked(h1, t1)[1], sc.masked(h2, t2)[1]],
+                                          err_msg=f"ts r={r}")
+            bm = orc.read_failed()
+            failed = [c for c in range(n) if bm[c >> 5] >> (c & 31) & 1]
+            assert failed == ls.last_failed
+            assert list(orc.read_detectors()) == ls.last_detectors
+    finally:
+        L.T_FAIL, L.T_CLEANUP = 5, 5
+    return orc, ls
+
+
+@pytest.mark.parametrize("peer_mode", ["ring", "pull"])
+@pytest.mark.parametrize("quirk", [False, True])
+def test_bootstrap_crash_c1(oracle_mod, peer_mode, quirk):
+    """BASELINE config 1 shape: 10 joins, member 7 crashes at r=30, to r=60."""
+    n = 10
+    sched = sc.bootstrap_schedule(n)
+    sched.setdefault(30, []).append((sc.CRASH, 7))
+    orc, ls = run_pair(oracle_mod, n, 60, sched, peer_mode, quirk=quirk)
+    hb, ts, alive = orc.export_state()
+    assert alive[7] == 0
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("peer_mode", ["ring", "pull"])
+def test_random_churn(oracle_mod, seed, peer_mode):
+    n = 16
+    sched = sc.random_churn(n, 50, seed)
+    run_pair(oracle_mod, n, 50, sched, peer_mode, fanout=2, init_full=True, seed=0x1000 + seed)
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_random_churn_quirk(oracle_mod, seed):
+    n = 14
+    sched = sc.random_churn(n, 40, seed, p_crash=0.08)
+    run_pair(oracle_mod, n, 40, sched, "ring", init_full=True, quirk=True, seed=0x2000 + seed)
+
+
+def test_fast_fail_short_cooldown(oracle_mod):
+    """T_fail/T_cleanup off their defaults (tombstones survive detection)."""
+    n = 12
+    sched = sc.random_churn(n, 40, 9, p_crash=0.1)
+    run_pair(oracle_mod, n, 40, sched, "pull", fanout=3, init_full=True, t_fail=3, t_cleanup=6)
