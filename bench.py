@@ -1,0 +1,177 @@
+"""bench.py — gossip rounds/sec at N=65,536 members (BASELINE.json metric).
+
+One "step" = one synchronous gossip round of the whole simulated cluster
+(SPEC.md §2: REMOVE delivery, <4 guard, own heartbeat, T_fail detection,
+T_cleanup sweep, k=4 Philox-peer max-merge) over the N x N int32 heartbeat and
+timestamp tables resident in HBM (BASELINE config 3, SURVEY.md §8d C3:
+full membership hb=2 ts=0, seed 0x5EED0003).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+N>1 is launched by the driver under torch.distributed.run, one rank per GPU.
+Round 1 runs one independent N=65,536 cluster per GPU ("replicas"; the
+sharded single-cluster path is DESIGN.md's next row), so per-GPU work is fixed
+and value = cluster-rounds/s summed over ranks = total / max-over-ranks time.
+
+The JSON line also carries
+  roofline: the fused round kernel (k_round) — algorithmic bytes per launch
+            4*N^2*(k+4) / its mean duration from HIP events on
+            the engine's stream; peak 8.0 TB/s (MI355X_MICROARCH.md).
+  cpu_baseline: the CPU restatement (oracle/tablesim.c, "port") timed on this
+            host on a bounded sample (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+REPO = pathlib.Path(__file__).resolve().parent
+PKG_DIR = REPO / "p2p-file-system-with-gossip-detect-failure-management_amd"
+sys.path.insert(0, str(PKG_DIR))
+sys.path.insert(0, str(REPO))
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_MEASURED_GBS = 6290.0    # MI355X_MICROARCH.md: 6.29 TB/s float4 copy
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--fanout", type=int, default=4)
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0003)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=2048, help="observer rows in the CPU sample")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    return ap.parse_args()
+
+
+def cpu_baseline(n, fanout, seed, rows, seconds, threads):
+    """Time the C oracle (same semantics) on `rows` observer rows of an
+    N-column table; peers are drawn among the sampled rows."""
+    from oracle import oracle as om
+    om.build()
+    threads = threads or min(16, os.cpu_count() or 1)
+    cfg = om.default_config(n, fanout=fanout, seed=seed)
+    o = om.Oracle(cfg, rows=rows, threads=threads)
+    o.init_full(2, 0, 0)
+    o.step(1)  # first touch
+    done, t0 = 0, time.perf_counter()
+    while True:
+        o.step(1)
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or done >= 50:
+            break
+    o.close()
+    per_round_sample = el / done
+    rounds_per_s = (rows / n) / per_round_sample
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": rounds_per_s, "unit": "rounds/s", "cores": threads, "kind": "port",
+        "sample": f"oracle/tablesim.c (OpenMP, {threads} threads) on {rows} of {n} observer rows x {n} columns, "
+                  f"k={fanout} peers drawn among the sampled rows, {done} rounds in {el:.1f} s, scaled by "
+                  f"rows/N to whole-cluster rounds/s; host CPU: {cpu}",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist  # noqa: F811
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    import gossipsim as gs
+
+    n, k = args.n, args.fanout
+    eng = gs.Engine(gs.default_config(n, fanout=k, seed=args.seed + rank, device=local))
+    eng.init_full(2, 0, 0)
+    if args.warmup:
+        eng.step(args.warmup)
+    eng.set_timing(True)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    eng.sync()
+    t0 = time.perf_counter()
+    st = eng.step(args.steps)  # blocks until the device is done
+    eng.sync()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms, launches = eng.read_timing()
+    eng.close()
+
+    if rank != 0:
+        return
+    total_rounds = args.steps * world
+    value = total_rounds / elapsed
+    b_round = 4.0 * n * n * (k + 4)            # SURVEY.md §8d algorithmic bytes / round
+    b_compulsory = 16.0 * n * n                # each table cell read+written once
+    avg_s = (kern_ms / 1e3) / max(launches, 1)
+    achieved = b_round / avg_s / 1e9
+    line = {
+        "metric": "gossip rounds/sec at N=65,536 members (achieved HBM GB/s, % of peak)",
+        "value": value,
+        "unit": "rounds/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"BASELINE config 3: N={n} members, fanout k={k} Philox pull, full membership "
+                        f"(hb=2, ts=0), T_fail=T_cleanup=5, seed {hex(args.seed)}",
+            "n_members": n, "fanout": k, "global_batch": n, "seq_len": n,
+            "parallelism": "replicas" if world > 1 else "single",
+            "rounds_checked": {"detections": st["detections"], "active_rows": st["active_rows"]},
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": "k_round", "achieved": achieved, "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "bytes_per_launch": b_round, "avg_launch_ms": avg_s * 1e3, "launches": launches,
+            "compulsory_bytes_per_launch": b_compulsory,
+            "compulsory_achieved": b_compulsory / avg_s / 1e9,
+            "frac_of_measured_copy_peak": achieved / HBM_MEASURED_GBS,
+        },
+        "cpu_baseline": None,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(n, k, args.seed, args.cpu_rows, args.cpu_seconds, args.cpu_threads)
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

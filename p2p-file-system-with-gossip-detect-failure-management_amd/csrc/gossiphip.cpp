@@ -1,0 +1,617 @@
+// libgossiphip host side: the C-ABI of include/gossiphip.h over the HIP
+// kernels in round.hip / events.hip / place.hip. One handle = one engine = one
+// gfx950 device, one HIP stream, all tables resident in HBM.
+//
+// Reference interfaces replaced (paths under the reference tree):
+//   InitSlave / InitMaster            slave/slave.go:95, master/master.go:38
+//   HeartBeat round loop              main.go:27-33, slave/slave.go:499-544
+//   GetMsg JOIN/LEAVE/REMOVE          slave/slave.go:207-248
+//   Handle_put_request / Update_metadata / Get_* / Delete_file_info
+//                                     master/master.go:74-259
+// There is no CPU fallback: without a gfx950 device gh_create fails.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "gh_internal.h"
+
+namespace {
+
+struct Engine {
+  gh_config cfg{};
+  int32_t n = 0;
+  int64_t ld = 0;
+  hipStream_t stream = nullptr;
+  GhDev d{};
+  int cur = 0, dcur = 0;
+  int32_t round = 0;
+  std::vector<uint8_t> alive;   // host mirror (source of truth for events)
+  std::vector<gh_event> pending;
+  int32_t* ev_buf = nullptr;    // device scratch for event member lists
+  bool timing = false;
+  double timed_ms = 0.0;
+  int64_t timed_launches = 0;
+  std::vector<hipEvent_t> evs;
+  std::string err;
+  std::vector<void*> allocs;
+};
+
+int set_err(Engine* e, int code, const std::string& msg) {
+  if (e) e->err = msg;
+  return code;
+}
+
+#define HIPCHK(e, call)                                                          \
+  do {                                                                           \
+    hipError_t _st = (call);                                                     \
+    if (_st != hipSuccess)                                                       \
+      return set_err((e), GH_EHIP, std::string(#call) + ": " + hipGetErrorString(_st)); \
+  } while (0)
+
+template <class T>
+int dalloc(Engine* e, T** p, size_t count, int fill_byte) {
+  void* q = nullptr;
+  const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+  if (hipMalloc(&q, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(e, GH_ENOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+  }
+  e->allocs.push_back(q);
+  if (hipMemset(q, fill_byte, bytes) != hipSuccess) return set_err(e, GH_EHIP, "hipMemset failed");
+  *p = static_cast<T*>(q);
+  return GH_OK;
+}
+
+GhRound round_params(const Engine* e, int32_t r) {
+  GhRound p{};
+  p.r = r;
+  p.n = e->n;
+  p.ld = e->ld;
+  p.t_fail = e->cfg.t_fail;
+  p.t_cleanup = e->cfg.t_cleanup;
+  p.min_members = e->cfg.min_members;
+  p.k = e->cfg.fanout;
+  p.seed = e->cfg.seed;
+  p.peer_mode = e->cfg.peer_mode;
+  return p;
+}
+
+int reset_pending_removes(Engine* e) {
+  GhDev& d = e->d;
+  for (int b = 0; b < 2; ++b) {
+    HIPCHK(e, hipMemsetAsync(d.det_cnt[b], 0, sizeof(int32_t) * e->ld, e->stream));
+    HIPCHK(e, hipMemsetAsync(d.det_min[b], 0x7F, sizeof(int32_t) * e->ld, e->stream));
+  }
+  HIPCHK(e, hipMemsetAsync(d.dbits, 0, sizeof(uint32_t) * (e->ld / 32 + 2), e->stream));
+  HIPCHK(e, hipMemsetAsync(d.nd, 0, sizeof(int32_t) * 8, e->stream));
+  HIPCHK(e, hipMemsetAsync(d.det_any, 0, e->n, e->stream));
+  return GH_OK;
+}
+
+int upload_alive(Engine* e) {
+  HIPCHK(e, hipMemcpyAsync(e->d.alive, e->alive.data(), e->n, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+int upload_list(Engine* e, const std::vector<int32_t>& v) {
+  if (v.empty()) return GH_OK;
+  HIPCHK(e, hipMemcpyAsync(e->ev_buf, v.data(), v.size() * sizeof(int32_t), hipMemcpyHostToDevice,
+                           e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+// SPEC.md §5: crashes, then leaves (all leavers stop first), then joins.
+int process_events(Engine* e, int32_t r) {
+  if (e->pending.empty()) return GH_OK;
+  const GhRound p = round_params(e, r);
+  std::vector<gh_event> ev;
+  ev.swap(e->pending);
+  for (const auto& x : ev)
+    if (x.kind == GH_EV_CRASH) e->alive[x.member] = 0;
+  std::vector<int32_t> leavers;
+  for (const auto& x : ev)
+    if (x.kind == GH_EV_LEAVE && e->alive[x.member]) {
+      e->alive[x.member] = 0;
+      leavers.push_back(x.member);
+    }
+  int rc;
+  if ((rc = upload_alive(e))) return rc;
+  if (!leavers.empty()) {
+    if ((rc = upload_list(e, leavers))) return rc;
+    launch_leave(e->d, e->cur, e->ev_buf, (int32_t)leavers.size(), p, e->stream);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  std::vector<int32_t> joiners, fresh;
+  for (const auto& x : ev)
+    if (x.kind == GH_EV_JOIN) {
+      joiners.push_back(x.member);
+      if (!e->alive[x.member]) {
+        fresh.push_back(x.member);
+        e->alive[x.member] = 1;
+      }
+    }
+  if (!fresh.empty()) {
+    if ((rc = upload_list(e, fresh))) return rc;
+    launch_join_reset(e->d, e->cur, e->ev_buf, (int32_t)fresh.size(), p, e->stream);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  if ((rc = upload_alive(e))) return rc;
+  const int32_t I = e->cfg.introducer;
+  if (!joiners.empty() && I >= 0 && I < e->n && e->alive[I]) {
+    if ((rc = upload_list(e, joiners))) return rc;
+    launch_join(e->d, e->cur, e->ev_buf, (int32_t)joiners.size(), I, p, e->stream);
+  }
+  launch_count(e->d, e->cur, p, e->stream);
+  HIPCHK(e, hipGetLastError());
+  return GH_OK;
+}
+
+int ensure_io(Engine* e, int64_t n) {
+  if (n <= e->d.io_cap) return GH_OK;
+  GhDev& d = e->d;
+  const int64_t cap = std::max<int64_t>(n, 1024);
+  const int R = e->cfg.replicas;
+  int rc;
+  if ((rc = dalloc(e, &d.io_a, cap, 0)) || (rc = dalloc(e, &d.io_b, cap * R, 0)) ||
+      (rc = dalloc(e, &d.io_c, cap, 0)) || (rc = dalloc(e, &d.io_d, cap, 0)))
+    return rc;
+  d.io_cap = cap;
+  return GH_OK;
+}
+
+int check_files(Engine* e, const int32_t* files, int64_t n, bool distinct) {
+  if (e->d.fcap <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
+  if (n < 0 || (n > 0 && !files)) return set_err(e, GH_EINVAL, "bad file list");
+  for (int64_t x = 0; x < n; ++x)
+    if (files[x] < 0 || files[x] >= e->d.fcap) return set_err(e, GH_EINVAL, "file id out of range");
+  if (distinct) {
+    std::vector<int32_t> s(files, files + n);
+    std::sort(s.begin(), s.end());
+    if (std::adjacent_find(s.begin(), s.end()) != s.end())
+      return set_err(e, GH_EINVAL, "file ids in one call must be distinct");
+  }
+  return GH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gh_abi_version(void) { return GH_ABI_VERSION; }
+
+void gh_config_default(gh_config* cfg) {
+  if (!cfg) return;
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->n_members = 10;
+  cfg->fanout = 3;
+  cfg->peer_mode = GH_PEER_PULL;
+  cfg->detect_mode = GH_DETECT_CANONICAL;
+  cfg->t_fail = 5;      // PERIOD 5e9 ns / 1 s (slave/slave.go:24, main.go:11)
+  cfg->t_cleanup = 5;   // COOLDOWN (slave/slave.go:25)
+  cfg->min_members = 4; // slave/slave.go:504
+  cfg->replicas = 4;    // master/master.go:131
+  cfg->introducer = 0;
+  cfg->master = 0;
+  cfg->device = 0;
+  cfg->seed = 0x5EED0001ull;
+  cfg->max_files = 0;
+}
+
+const char* gh_last_error(void* h) {
+  return h ? static_cast<Engine*>(h)->err.c_str() : "null handle";
+}
+
+void gh_destroy(void* h) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return;
+  (void)hipSetDevice(e->cfg.device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (auto ev : e->evs) (void)hipEventDestroy(ev);
+  for (void* p : e->allocs) (void)hipFree(p);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int gh_create(const gh_config* cfg, void** handle) {
+  if (!cfg || !handle) return GH_EINVAL;
+  *handle = nullptr;
+  if (cfg->n_members < 1 || cfg->fanout < 1 || cfg->fanout > GH_MAXK || cfg->replicas < 1 ||
+      cfg->replicas > 8 || cfg->min_members < 0 || cfg->max_files < 0 || cfg->max_files > INT32_MAX ||
+      (cfg->peer_mode != GH_PEER_PULL && cfg->peer_mode != GH_PEER_RING) ||
+      (cfg->detect_mode != GH_DETECT_CANONICAL && cfg->detect_mode != GH_DETECT_QUIRK) ||
+      cfg->introducer < 0 || cfg->introducer >= cfg->n_members || cfg->master < 0 ||
+      cfg->master >= cfg->n_members)
+    return GH_EINVAL;
+  if (cfg->detect_mode == GH_DETECT_QUIRK) return GH_EINVAL;  // HIP path: canonical only
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device || cfg->device < 0) {
+    (void)hipGetLastError();
+    return GH_ENODEV;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) return GH_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return GH_ENODEV;
+  if (hipSetDevice(cfg->device) != hipSuccess) return GH_ENODEV;
+
+  Engine* e = new Engine();
+  e->cfg = *cfg;
+  e->n = cfg->n_members;
+  e->ld = ((int64_t)e->n + GH_CHUNK - 1) / GH_CHUNK * GH_CHUNK;
+  e->alive.assign(e->n, 0);
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete e;
+    return GH_EHIP;
+  }
+  GhDev& d = e->d;
+  d.n = e->n;
+  d.ld = e->ld;
+  const int64_t cells = (int64_t)e->n * e->ld;
+  const int64_t nch = e->ld / GH_CHUNK;
+  const int64_t inbox = (int64_t)e->n * std::max(cfg->fanout, 3);
+  int rc = GH_OK;
+  do {
+    if ((rc = dalloc(e, &d.hb[0], cells, 0xFF)) || (rc = dalloc(e, &d.hb[1], cells, 0xFF)) ||
+        (rc = dalloc(e, &d.ts, cells, 0)))
+      break;
+    if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
+        (rc = dalloc(e, &d.det_any, e->n, 0)) || (rc = dalloc(e, &d.cnt, e->n, 0)))
+      break;
+    if ((rc = dalloc(e, &d.det_cnt[0], e->ld, 0)) || (rc = dalloc(e, &d.det_cnt[1], e->ld, 0)) ||
+        (rc = dalloc(e, &d.det_min[0], e->ld, 0x7F)) || (rc = dalloc(e, &d.det_min[1], e->ld, 0x7F)) ||
+        (rc = dalloc(e, &d.dbits, e->ld / 32 + 2, 0)) || (rc = dalloc(e, &d.dlist, 2 * e->ld, 0)) ||
+        (rc = dalloc(e, &d.nd, 8, 0)))
+      break;
+    if ((rc = dalloc(e, &d.part, nch * e->n, 0)) || (rc = dalloc(e, &d.inbox_beg, e->n, 0)) ||
+        (rc = dalloc(e, &d.inbox_cnt, e->n, 0)) || (rc = dalloc(e, &d.inbox_fill, e->n, 0)) ||
+        (rc = dalloc(e, &d.inbox, inbox, 0)) || (rc = dalloc(e, &d.targets, 3 * (int64_t)e->n, 0xFF)) ||
+        (rc = dalloc(e, &d.stats, ST_COUNT, 0)) || (rc = dalloc(e, &e->ev_buf, 2 * (int64_t)e->n + 16, 0)))
+      break;
+    if ((rc = dalloc(e, &d.cand, e->n, 0)) || (rc = dalloc(e, &d.ncand, 4, 0))) break;
+    d.fcap = cfg->max_files;
+    if (d.fcap > 0) {
+      if ((rc = dalloc(e, &d.rep, d.fcap * cfg->replicas, 0xFF)) || (rc = dalloc(e, &d.ver, d.fcap, 0xFF)) ||
+          (rc = dalloc(e, &d.fts, d.fcap, 0)) || (rc = dalloc(e, &d.draws, d.fcap, 0)) ||
+          (rc = dalloc(e, &d.plan, d.fcap, 0)) || (rc = dalloc(e, &d.nplan, 4, 0)))
+        break;
+    }
+  } while (0);
+  if (rc != GH_OK) {
+    std::fprintf(stderr, "gh_create: %s\n", e->err.c_str());
+    gh_destroy(e);
+    return rc;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) {
+    gh_destroy(e);
+    return GH_EHIP;
+  }
+  *handle = e;
+  return GH_OK;
+}
+
+int gh_get_round(void* h, int32_t* round) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || !round) return GH_EINVAL;
+  *round = e->round;
+  return GH_OK;
+}
+
+int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t* alive, int64_t row0,
+                    int64_t n_rows, int32_t round) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  if (row0 < 0 || n_rows < 0 || row0 + n_rows > e->n || (n_rows > 0 && (!hb || !ts || !alive)))
+    return set_err(e, GH_EINVAL, "row range / null buffer");
+  for (int64_t x = 0; x < n_rows * e->n; ++x)
+    if (hb[x] < GH_TOMBSTONE || hb[x] >= GH_FLAG) return set_err(e, GH_ERANGE, "hb value out of range");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  const size_t w = sizeof(int32_t) * e->n, dp = sizeof(int32_t) * e->ld;
+  if (n_rows > 0) {
+    HIPCHK(e, hipMemcpy2DAsync(e->d.hb[e->cur] + row0 * e->ld, dp, hb, w, w, n_rows,
+                               hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpy2DAsync(e->d.ts + row0 * e->ld, dp, ts, w, w, n_rows, hipMemcpyHostToDevice,
+                               e->stream));
+    std::copy(alive, alive + n_rows, e->alive.begin() + row0);
+  }
+  int rc;
+  if ((rc = upload_alive(e))) return rc;
+  e->round = round;
+  e->pending.clear();
+  const GhRound p = round_params(e, round + 1);
+  launch_flags(e->d, e->cur, row0, n_rows, p, e->stream);
+  if ((rc = reset_pending_removes(e))) return rc;
+  launch_count(e->d, e->cur, p, e->stream);
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+int gh_export_state(void* h, int32_t* hb, int32_t* ts, uint8_t* alive, int64_t row0, int64_t n_rows) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  if (row0 < 0 || n_rows < 0 || row0 + n_rows > e->n) return set_err(e, GH_EINVAL, "row range");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  const size_t w = sizeof(int32_t) * e->n, dp = sizeof(int32_t) * e->ld;
+  if (hb && n_rows > 0) {
+    HIPCHK(e, hipMemcpy2DAsync(hb, w, e->d.hb[e->cur] + row0 * e->ld, dp, w, n_rows,
+                               hipMemcpyDeviceToHost, e->stream));
+  }
+  if (ts && n_rows > 0) {
+    HIPCHK(e, hipMemcpy2DAsync(ts, w, e->d.ts + row0 * e->ld, dp, w, n_rows, hipMemcpyDeviceToHost,
+                               e->stream));
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (hb)
+    for (int64_t x = 0; x < n_rows * e->n; ++x)
+      if (hb[x] >= 0) hb[x] &= GH_HBMASK;  // strip the eligibility bit
+  if (alive) std::copy(e->alive.begin() + row0, e->alive.begin() + row0 + n_rows, alive);
+  return GH_OK;
+}
+
+int gh_init_full(void* h, int32_t hb0, int32_t ts0, int32_t round) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  if (hb0 < 0 || hb0 >= GH_FLAG) return set_err(e, GH_ERANGE, "hb0 out of range");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  std::fill(e->alive.begin(), e->alive.end(), 1);
+  int rc;
+  if ((rc = upload_alive(e))) return rc;
+  e->round = round;
+  e->pending.clear();
+  const GhRound p = round_params(e, round + 1);
+  launch_fill(e->d, e->cur, hb0, ts0, p, e->stream);
+  if ((rc = reset_pending_removes(e))) return rc;
+  launch_count(e->d, e->cur, p, e->stream);
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+int gh_apply_events(void* h, const gh_event* ev, int64_t n) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || n < 0 || (n > 0 && !ev)) return GH_EINVAL;
+  for (int64_t x = 0; x < n; ++x) {
+    if (ev[x].kind < GH_EV_JOIN || ev[x].kind > GH_EV_CRASH) return set_err(e, GH_EINVAL, "event kind");
+    if (ev[x].member < 0 || ev[x].member >= e->n) return set_err(e, GH_EINVAL, "event member");
+  }
+  e->pending.insert(e->pending.end(), ev, ev + n);
+  return GH_OK;
+}
+
+int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || rounds < 0) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  HIPCHK(e, hipMemsetAsync(e->d.stats, 0, sizeof(unsigned long long) * ST_COUNT, e->stream));
+  if (e->timing && (int64_t)e->evs.size() < 2 * (int64_t)rounds) {
+    while ((int64_t)e->evs.size() < 2 * (int64_t)rounds) {
+      hipEvent_t ev;
+      HIPCHK(e, hipEventCreate(&ev));
+      e->evs.push_back(ev);
+    }
+  }
+  const int32_t first = e->round + 1;
+  for (int32_t q = 0; q < rounds; ++q) {
+    const int32_t r = e->round + 1;
+    int rc;
+    if ((rc = process_events(e, r))) return rc;
+    const GhRound p = round_params(e, r);
+    launch_active(e->d, e->cur, e->dcur, p, e->stream);
+    if (e->cfg.peer_mode == GH_PEER_PULL)
+      launch_peers_pull(e->d, e->cur, e->dcur, p, e->stream);
+    else
+      launch_ring(e->d, e->cur, e->dcur, p, e->stream);
+    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q], e->stream));
+    launch_round(e->d, e->cur, e->dcur, p, e->stream);
+    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q + 1], e->stream));
+    launch_finish(e->d, e->dcur, p, e->stream);
+    HIPCHK(e, hipGetLastError());
+    e->cur ^= 1;
+    e->dcur ^= 1;
+    e->round = r;
+  }
+  unsigned long long st[ST_COUNT];
+  HIPCHK(e, hipMemcpyAsync(st, e->d.stats, sizeof st, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (e->timing) {
+    for (int32_t q = 0; q < rounds; ++q) {
+      float ms = 0.f;
+      HIPCHK(e, hipEventElapsedTime(&ms, e->evs[2 * q], e->evs[2 * q + 1]));
+      e->timed_ms += ms;
+      e->timed_launches++;
+    }
+  }
+  if (stats) {
+    std::memset(stats, 0, sizeof(*stats));
+    stats->rounds = rounds;
+    stats->last_round = rounds ? e->round : first - 1;
+    stats->detections = (int64_t)st[ST_DETECTIONS];
+    stats->failed_members = (int64_t)st[ST_FAILED];
+    stats->remove_unknown = (int64_t)st[ST_REMOVE_UNKNOWN];
+    stats->ring_empty = (int64_t)st[ST_RING_EMPTY];
+    stats->active_rows = (int64_t)st[ST_ACTIVE_ROWS];
+    stats->merged_cells = (int64_t)st[ST_MERGED];
+    stats->released = (int64_t)st[ST_RELEASED];
+    stats->tombstoned = (int64_t)st[ST_TOMBSTONED];
+  }
+  return GH_OK;
+}
+
+int gh_read_failed(void* h, uint32_t* bitmap, int64_t n_words) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || !bitmap) return GH_EINVAL;
+  const int64_t words = (e->n + 31) / 32;
+  if (n_words < words) return set_err(e, GH_EINVAL, "bitmap too small");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  std::memset(bitmap, 0, n_words * sizeof(uint32_t));
+  HIPCHK(e, hipMemcpyAsync(bitmap, e->d.dbits, words * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+int gh_read_detectors(void* h, int32_t* rows, int64_t cap, int64_t* n_out) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || !n_out || (cap > 0 && !rows)) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  std::vector<uint8_t> any(e->n);
+  HIPCHK(e, hipMemcpyAsync(any.data(), e->d.det_any, e->n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  int64_t k = 0;
+  for (int32_t i = 0; i < e->n; ++i)
+    if (any[i]) {
+      if (k < cap) rows[k] = i;
+      k++;
+    }
+  *n_out = k;
+  return GH_OK;
+}
+
+int gh_lsm(void* h, int32_t observer, int32_t* ids, int32_t* hb, int32_t* ts, int64_t cap, int64_t* n_out) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || !n_out) return GH_EINVAL;
+  if (observer < 0 || observer >= e->n) return set_err(e, GH_EINVAL, "observer");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  std::vector<int32_t> rh(e->n), rt(e->n);
+  HIPCHK(e, hipMemcpyAsync(rh.data(), e->d.hb[e->cur] + (int64_t)observer * e->ld, sizeof(int32_t) * e->n,
+                           hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(rt.data(), e->d.ts + (int64_t)observer * e->ld, sizeof(int32_t) * e->n,
+                           hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  int64_t k = 0;
+  for (int32_t c = 0; c < e->n; ++c)
+    if (rh[c] >= 0) {
+      if (k < cap) {
+        if (ids) ids[k] = c;
+        if (hb) hb[k] = rh[c] & GH_HBMASK;
+        if (ts) ts[k] = rt[c];
+      }
+      k++;
+    }
+  *n_out = k;
+  return GH_OK;
+}
+
+int gh_put(void* h, const int32_t* files, int64_t n, int32_t* replicas, int32_t* versions, int32_t* status) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  int rc;
+  if ((rc = check_files(e, files, n, true))) return rc;
+  if (n == 0) return GH_OK;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  if ((rc = ensure_io(e, n))) return rc;
+  const int R = e->cfg.replicas;
+  HIPCHK(e, hipMemcpyAsync(e->d.io_a, files, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
+  const GhRound p = round_params(e, e->round);
+  launch_candidates(e->d, e->cur, e->cfg.master, p, e->stream);
+  launch_put(e->d, n, R, e->round, e->cfg.seed, e->stream, e->d.hb[e->cur] + (int64_t)e->cfg.master * e->ld,
+             e->n);
+  HIPCHK(e, hipGetLastError());
+  std::vector<int32_t> rep(n * R), ver(n), st(n);
+  HIPCHK(e, hipMemcpyAsync(rep.data(), e->d.io_b, sizeof(int32_t) * n * R, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(ver.data(), e->d.io_c, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(st.data(), e->d.io_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (replicas) std::copy(rep.begin(), rep.end(), replicas);
+  if (versions) std::copy(ver.begin(), ver.end(), versions);
+  if (status) std::copy(st.begin(), st.end(), status);
+  for (int64_t x = 0; x < n; ++x)
+    if (st[x] != GH_OK) return set_err(e, GH_EPLACEMENT_STARVED, "placement starved for some file");
+  return GH_OK;
+}
+
+int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap, int64_t* n_plan) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || !n_plan || (cap > 0 && !plan)) return GH_EINVAL;
+  if (e->d.fcap <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
+  if (observer < 0 || observer >= e->n) return set_err(e, GH_EINVAL, "observer");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  HIPCHK(e, hipMemsetAsync(e->d.nplan, 0, sizeof(int32_t), e->stream));
+  const GhRound p = round_params(e, e->round);
+  launch_candidates(e->d, e->cur, e->cfg.master, p, e->stream);
+  launch_repair(e->d, e->d.hb[e->cur] + (int64_t)observer * e->ld, e->cfg.replicas, e->cfg.seed, e->stream,
+                e->d.hb[e->cur] + (int64_t)e->cfg.master * e->ld, e->n);
+  HIPCHK(e, hipGetLastError());
+  int32_t np = 0;
+  HIPCHK(e, hipMemcpyAsync(&np, e->d.nplan, sizeof np, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  std::vector<gh_plan_entry> all(np);
+  if (np > 0) {
+    HIPCHK(e, hipMemcpyAsync(all.data(), e->d.plan, sizeof(gh_plan_entry) * np, hipMemcpyDeviceToHost,
+                             e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  std::sort(all.begin(), all.end(), [](const gh_plan_entry& a, const gh_plan_entry& b) { return a.file < b.file; });
+  int rc = GH_OK;
+  for (int64_t x = 0; x < np; ++x) {
+    if (x < cap) plan[x] = all[x];
+    if (all[x].status != GH_OK) rc = GH_EPLACEMENT_STARVED;
+  }
+  *n_plan = np;
+  if (rc != GH_OK) set_err(e, rc, "placement starved for some file");
+  return rc;
+}
+
+static int get_or_delete(Engine* e, const int32_t* files, int64_t n, int32_t* replicas, int32_t* versions,
+                         int del) {
+  int rc;
+  if ((rc = check_files(e, files, n, del != 0))) return rc;
+  if (n == 0) return GH_OK;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  if ((rc = ensure_io(e, n))) return rc;
+  const int R = e->cfg.replicas;
+  HIPCHK(e, hipMemcpyAsync(e->d.io_a, files, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
+  launch_get(e->d, n, R, del, e->stream);
+  HIPCHK(e, hipGetLastError());
+  std::vector<int32_t> rep(n * R), ver(n);
+  HIPCHK(e, hipMemcpyAsync(rep.data(), e->d.io_b, sizeof(int32_t) * n * R, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(ver.data(), e->d.io_c, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (replicas) std::copy(rep.begin(), rep.end(), replicas);
+  if (versions) std::copy(ver.begin(), ver.end(), versions);
+  return GH_OK;
+}
+
+int gh_get_files(void* h, const int32_t* files, int64_t n, int32_t* replicas, int32_t* versions) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  return get_or_delete(e, files, n, replicas, versions, 0);
+}
+
+int gh_delete_files(void* h, const int32_t* files, int64_t n, int32_t* old_replicas) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  return get_or_delete(e, files, n, old_replicas, nullptr, 1);
+}
+
+int gh_set_timing(void* h, int32_t enable) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  e->timing = enable != 0;
+  e->timed_ms = 0.0;
+  e->timed_launches = 0;
+  return GH_OK;
+}
+
+int gh_read_timing(void* h, double* total_ms, int64_t* launches) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  if (total_ms) *total_ms = e->timed_ms;
+  if (launches) *launches = e->timed_launches;
+  return GH_OK;
+}
+
+int gh_sync(void* h) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+}  // extern "C"

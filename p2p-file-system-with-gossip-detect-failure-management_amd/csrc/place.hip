@@ -1,0 +1,163 @@
+// Replica placement kernels (SPEC.md §6): the master's Init_replica /
+// Handle_put_request / Update_metadata (master/master.go:74-175) for a batch of
+// files at once, one lane per file, Philox draws keyed by (seed; file, draw).
+#include "gh_internal.h"
+
+namespace {
+
+// Member_list = present members of the master row, ID order
+// (master/master.go:46, slave/slave.go:478). One 1024-thread workgroup.
+__global__ __launch_bounds__(1024) void k_candidates(GhDev d, int cur, int32_t master, GhRound p) {
+  __shared__ int s_sum[1024];
+  const int tid = threadIdx.x;
+  const int32_t* row = d.hb[cur] + (int64_t)master * p.ld;
+  const int per = (p.n + 1023) / 1024;
+  const int b = tid * per, e = min(p.n, b + per);
+  int cnt = 0;
+  for (int c = b; c < e; ++c) cnt += row[c] >= 0;
+  s_sum[tid] = cnt;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = tid >= off ? s_sum[tid - off] : 0;
+    __syncthreads();
+    s_sum[tid] += v;
+    __syncthreads();
+  }
+  int pos = tid ? s_sum[tid - 1] : 0;
+  for (int c = b; c < e; ++c)
+    if (row[c] >= 0) d.cand[pos++] = c;
+  if (tid == 1023) d.ncand[0] = s_sum[1023];
+}
+
+// Init_replica (master/master.go:129-150). nodes[0..len) are kept first; the
+// reference's time-seeded Intn(M-1) becomes Philox word 0 of block
+// (f, draw, PLACE, 0) mapped by multiply-shift, so cand[M-1] is never drawn.
+__device__ int init_replica(const GhDev& d, const int32_t* mrow, int32_t f, int32_t* nodes, int& len,
+                            int R, uint64_t seed, int32_t n) {
+  if (len >= R) return GH_OK;
+  const int M = d.ncand[0];
+  if (M <= 1) return GH_EPLACEMENT_STARVED;  // Intn(<=0) panics
+  const int32_t last = d.cand[M - 1];
+  int in_pool = 0;
+  for (int x = 0; x < len; ++x) {
+    const int32_t a = nodes[x];
+    in_pool += (a >= 0 && a < n && a < last && mrow[a] >= 0);
+  }
+  if ((M - 1) - in_pool < R - len) return GH_EPLACEMENT_STARVED;  // infinite loop
+  uint32_t dr = d.draws[f];
+  uint32_t budget = GH_MAX_DRAWS;
+  int l = len;
+  int32_t tmp[8];
+  for (int x = 0; x < 8; ++x) tmp[x] = x < l ? nodes[x] : -1;
+  while (l < R) {
+    if (budget-- == 0) return GH_EPLACEMENT_STARVED;
+    const uint32_t u = gh_philox_word(seed, (uint32_t)f, dr, GH_TAG_PLACE, 0, 0);
+    dr++;
+    const uint32_t num = (uint32_t)(((uint64_t)u * (uint64_t)(M - 1)) >> 32);
+    const int32_t a = d.cand[num];
+    bool dup = false;
+    for (int x = 0; x < l; ++x) dup |= tmp[x] == a;  // isAddressExist (:137)
+    if (!dup) tmp[l++] = a;
+  }
+  d.draws[f] = dr;
+  for (int x = 0; x < l; ++x) nodes[x] = tmp[x];
+  len = l;
+  return GH_OK;
+}
+
+// put (Handle_put_request, :152-175) for io_a[0..n): out io_b replicas,
+// io_c versions, io_d status.
+__global__ __launch_bounds__(256) void k_put(GhDev d, int64_t n, int32_t R, int32_t now,
+                                             uint64_t seed, const int32_t* mrow, int32_t nm) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n) return;
+  const int32_t f = d.io_a[x];
+  int32_t* rp = d.rep + (int64_t)f * R;
+  int32_t nodes[8];
+  if (d.ver[f] < 0) {  // Update_timestamp: new File_info (:239-245)
+    d.ver[f] = 0;
+    for (int q = 0; q < R; ++q) rp[q] = -1;
+  }
+  d.fts[f] = now;
+  int len = 0;
+  for (int q = 0; q < R; ++q) {
+    nodes[q] = rp[q];
+    len += rp[q] >= 0;
+  }
+  const int st = init_replica(d, mrow, f, nodes, len, R, seed, nm);
+  if (st == GH_OK) {
+    for (int q = 0; q < R; ++q) rp[q] = q < len ? nodes[q] : -1;
+    d.ver[f] += 1;  // :159
+  }
+  for (int q = 0; q < R; ++q) d.io_b[x * R + q] = rp[q];
+  d.io_c[x] = d.ver[f];
+  d.io_d[x] = st;
+}
+
+// Update_metadata (:74-127) with available = observer row's present set.
+__global__ __launch_bounds__(256) void k_repair(GhDev d, const int32_t* orow, int32_t R, uint64_t seed,
+                                                const int32_t* mrow, int32_t nm) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= d.fcap || d.ver[f] < 0) return;
+  int32_t* rp = d.rep + f * R;
+  int32_t working[8];
+  int wl = 0;
+  for (int q = 0; q < R; ++q) {
+    const int32_t a = rp[q];
+    if (a >= 0 && a < nm && orow[a] >= 0) working[wl++] = a;  // :93-99
+  }
+  if (wl >= R) return;  // :104
+  int32_t nodes[8];
+  for (int q = 0; q < 8; ++q) nodes[q] = q < wl ? working[q] : -1;
+  int len = wl;
+  const int st = init_replica(d, mrow, (int32_t)f, nodes, len, R, seed, nm);  // :106-107
+  for (int q = 0; q < R; ++q) rp[q] = q < len ? nodes[q] : -1;
+  const int slot = atomicAdd(d.nplan, 1);
+  gh_plan_entry e;
+  e.file = (int32_t)f;
+  e.node1 = wl > 0 ? working[0] : -1;  // :120 (SPEC D5)
+  e.version = d.ver[f];
+  e.status = st;
+  int nn = 0;
+  for (int q = wl; q < len; ++q) e.new_nodes[nn++] = nodes[q];  // :110-115
+  for (int q = nn; q < 8; ++q) e.new_nodes[q] = -1;
+  e.n_new = nn;
+  d.plan[slot] = e;
+}
+
+// get/ls (:177-212) and delete (:249-259) for io_a[0..n) -> io_b, io_c.
+__global__ __launch_bounds__(256) void k_get(GhDev d, int64_t n, int32_t R, int del) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n) return;
+  const int32_t f = d.io_a[x];
+  const bool has = d.ver[f] >= 0;
+  int32_t* rp = d.rep + (int64_t)f * R;
+  for (int q = 0; q < R; ++q) {
+    d.io_b[x * R + q] = has ? rp[q] : -1;
+    if (del) rp[q] = -1;
+  }
+  d.io_c[x] = d.ver[f];
+  if (del) d.ver[f] = -1;
+}
+
+}  // namespace
+
+void launch_candidates(const GhDev& d, int cur, int32_t master, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_candidates, dim3(1), dim3(1024), 0, s, d, cur, master, p);
+}
+
+void launch_put(const GhDev& d, int64_t n, int32_t R, int32_t now, uint64_t seed, hipStream_t s,
+                const int32_t* mrow, int32_t nm) {
+  hipLaunchKernelGGL(k_put, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, n, R, now, seed,
+                     mrow, nm);
+}
+
+void launch_repair(const GhDev& d, const int32_t* orow, int32_t R, uint64_t seed, hipStream_t s,
+                   const int32_t* mrow, int32_t nm) {
+  hipLaunchKernelGGL(k_repair, dim3((unsigned)((d.fcap + 255) / 256)), dim3(256), 0, s, d, orow, R,
+                     seed, mrow, nm);
+}
+
+void launch_get(const GhDev& d, int64_t n, int32_t R, int del, hipStream_t s) {
+  hipLaunchKernelGGL(k_get, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, n, R, del);
+}

@@ -1,0 +1,438 @@
+// Gossip-round kernels for gfx950 (SPEC.md §2-§3, DESIGN.md "Kernels").
+//
+//   k_active       per row: the <4 guard after REMOVE delivery
+//                  (slave/slave.go:504,511), exact recount only for rows whose
+//                  count could cross the threshold.
+//   k_peers_pull   per receiver: k Philox peers, kept iff the sender is
+//                  active, alive and lists the receiver (slave/slave.go:527-542).
+//   k_ring_*       reference ring topology (slave/slave.go:512-524) + inbox CSR.
+//   k_round        THE HOT KERNEL: one pass over the table applying REMOVE
+//                  delivery, guard, own heartbeat, detection, cleanup and the
+//                  k-peer max-merge (slave/slave.go:276-286,414-497) for a
+//                  64-row x 256-column tile per workgroup.
+//   k_finish       per row/column: reduce the pass's partial counts, build
+//                  the failed-set bitmap D_r for the next round.
+#include <limits.h>
+
+#include "gh_internal.h"
+
+namespace {
+
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
+__device__ __forceinline__ bool dbit(const uint32_t* bits, int64_t c) {
+  return (bits[c >> 5] >> (c & 31)) & 1u;
+}
+
+// Step 1 applies REMOVE(c) at row j unless j is c's only detector
+// (slave/slave.go:344-346: a detector does not message itself).
+__device__ __forceinline__ bool removes_at(int dc, int dm, int j) { return !(dc == 1 && dm == j); }
+
+__global__ __launch_bounds__(256) void k_active(GhDev d, int cur, int dcur, GhRound p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    d.nd[dcur ^ 1] = 0;
+    d.nd[2 + (dcur ^ 1)] = 0;
+  }
+  bool a = false;
+  if (i < p.n) {
+    d.det_any[i] = 0;
+    if (d.alive[i]) {
+      const int c = d.cnt[i];
+      const int nd = d.nd[dcur];
+      if (c < p.min_members) {
+        a = false;
+      } else if (c - nd >= p.min_members) {
+        a = true;
+      } else {
+        const int32_t* row = d.hb[cur] + (int64_t)i * p.ld;
+        const int32_t* dc = d.det_cnt[dcur];
+        const int32_t* dm = d.det_min[dcur];
+        int rem = 0;
+        for (int q = 0; q < nd; ++q) {
+          const int col = d.dlist[(int64_t)dcur * p.ld + q];
+          rem += (row[col] >= 0) && removes_at(dc[col], dm[col], i);
+        }
+        a = (c - rem) >= p.min_members;
+      }
+    }
+    d.active[i] = a;
+  }
+  const unsigned long long m = __ballot(a);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(&d.stats[ST_ACTIVE_ROWS], (unsigned long long)__popcll(m));
+}
+
+__global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, GhRound p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const int beg = i * p.k;
+  int nv = 0;
+  if (d.alive[i] && p.n >= 2) {
+    const bool ib = dbit(d.dbits, i);
+    const int dci = ib ? d.det_cnt[dcur][i] : 0;
+    const int dmi = ib ? d.det_min[dcur][i] : 0;
+    for (int t = 0; t < p.k; ++t) {
+      const uint32_t u = gh_philox_word(p.seed, (uint32_t)i, (uint32_t)p.r, GH_TAG_PEER,
+                                        (uint32_t)(t >> 2), t & 3);
+      const uint32_t q = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
+      const int s = (int)q + ((int)q >= i);
+      if (!d.alive[s] || !d.active[s]) continue;
+      const int32_t v = d.hb[cur][(int64_t)s * p.ld + i];
+      // i must be in s's snapshot list: present, not detected by s this
+      // round (eligibility flag) and not REMOVE'd at s in step 1.
+      if (v < 0 || (v & GH_FLAG)) continue;
+      if (ib && removes_at(dci, dmi, s)) continue;
+      d.inbox[beg + nv++] = s;
+    }
+  }
+  d.inbox_beg[i] = beg;
+  d.inbox_cnt[i] = nv;
+}
+
+// Ring targets: one workgroup per sender row (slave/slave.go:515-524). The
+// snapshot list is the row after steps 1-5 in member-ID order (SPEC D1).
+__global__ __launch_bounds__(256) void k_ring_targets(GhDev d, int cur, int dcur, GhRound p) {
+  __shared__ int s_cnt[256];
+  __shared__ int s_tgt[3];
+  const int sdr = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (!(d.alive[sdr] && d.active[sdr])) {
+    if (tid < 3) d.targets[(int64_t)sdr * 3 + tid] = -1;
+    return;
+  }
+  const int32_t* row = d.hb[cur] + (int64_t)sdr * p.ld;
+  const int per = (p.n + 255) / 256;
+  const int b = tid * per, e = min(p.n, b + per);
+  auto present = [&](int c) -> bool {
+    const int32_t v = row[c];
+    if (v < 0) return false;
+    if ((v & GH_FLAG) && c != sdr) return false;  // detected by the sender this round
+    if (dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], sdr)) return false;
+    return true;
+  };
+  int cnt = 0;
+  for (int c = b; c < e; ++c) cnt += present(c);
+  s_cnt[tid] = cnt;
+  if (tid < 3) s_tgt[tid] = -1;
+  __syncthreads();
+  // exclusive scan (256 entries, one pass by thread 0 is fine: ring mode is
+  // the small-N parity path)
+  __shared__ int s_off[257];
+  __shared__ int s_L, s_idx;
+  if (tid == 0) {
+    int acc = 0;
+    for (int t = 0; t < 256; ++t) {
+      s_off[t] = acc;
+      acc += s_cnt[t];
+    }
+    s_off[256] = acc;
+    s_L = acc;
+    s_idx = -1;
+  }
+  __syncthreads();
+  if (sdr >= b && sdr < e && present(sdr)) {
+    int rank = s_off[tid];
+    for (int c = b; c < sdr; ++c) rank += present(c);
+    s_idx = rank;
+  }
+  __syncthreads();
+  const int L = s_L;
+  if (L == 0) {
+    if (tid == 0) atomicAdd(&d.stats[ST_RING_EMPTY], 1ull);
+    if (tid < 3) d.targets[(int64_t)sdr * 3 + tid] = -1;
+    return;
+  }
+  int want[3] = {s_idx - 1, s_idx + 1, s_idx + 2};
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    int v = want[q] % L;  // C and Go both truncate toward zero
+    if (v < 0) v += L;
+    want[q] = v;
+  }
+  int rank = s_off[tid];
+  for (int c = b; c < e; ++c) {
+    if (!present(c)) continue;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (want[q] == rank) s_tgt[q] = c;
+    rank++;
+  }
+  __syncthreads();
+  if (tid < 3) d.targets[(int64_t)sdr * 3 + tid] = s_tgt[tid];
+}
+
+__global__ __launch_bounds__(256) void k_inbox_count(GhDev d, GhRound p) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= p.n) return;
+  for (int q = 0; q < 3; ++q) {
+    const int t = d.targets[(int64_t)s * 3 + q];
+    if (t >= 0 && d.alive[t]) atomicAdd(&d.inbox_cnt[t], 1);
+  }
+}
+
+// Exclusive scan of inbox_cnt -> inbox_beg; one 1024-thread workgroup.
+__global__ __launch_bounds__(1024) void k_inbox_scan(GhDev d, GhRound p) {
+  __shared__ int s_sum[1024];
+  const int tid = threadIdx.x;
+  const int per = (p.n + 1023) / 1024;
+  const int b = tid * per, e = min(p.n, b + per);
+  int acc = 0;
+  for (int x = b; x < e; ++x) acc += d.inbox_cnt[x];
+  s_sum[tid] = acc;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = tid >= off ? s_sum[tid - off] : 0;
+    __syncthreads();
+    s_sum[tid] += v;
+    __syncthreads();
+  }
+  int run = tid ? s_sum[tid - 1] : 0;
+  for (int x = b; x < e; ++x) {
+    d.inbox_beg[x] = run;
+    d.inbox_fill[x] = 0;
+    run += d.inbox_cnt[x];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_inbox_fill(GhDev d, GhRound p) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= p.n) return;
+  for (int q = 0; q < 3; ++q) {
+    const int t = d.targets[(int64_t)s * 3 + q];
+    if (t >= 0 && d.alive[t]) {
+      const int pos = atomicAdd(&d.inbox_fill[t], 1);
+      d.inbox[d.inbox_beg[t] + pos] = s;
+    }
+  }
+}
+
+// The fused round. Tile = GH_RB rows x GH_CHUNK columns; block index is
+// chunk-major so the concurrently running tiles share one 256-column slice of
+// the table and peer-row segments are re-read from the on-die caches.
+// Each lane owns 4 consecutive columns (16-B loads/stores); a wave owns one
+// row segment at a time. KB = peer loads issued together (4 or 8).
+template <int KB>
+__global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRound p) {
+  __shared__ int s_dcnt[GH_CHUNK];
+  __shared__ int s_dmin[GH_CHUNK];
+  __shared__ uint16_t s_part[GH_RB];
+  __shared__ unsigned long long s_st[ST_COUNT];
+
+  const int nrb = (p.n + GH_RB - 1) / GH_RB;
+  const int chunk = blockIdx.x / nrb;
+  const int rb = blockIdx.x - chunk * nrb;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = uni(tid >> 6);
+  const int64_t c0 = (int64_t)chunk * GH_CHUNK + lane * 4;
+
+  s_dcnt[tid] = 0;
+  s_dmin[tid] = INT_MAX;
+  if (tid < ST_COUNT) s_st[tid] = 0;
+  if (tid < GH_RB) s_part[tid] = 0;
+  __syncthreads();
+
+  const int32_t* __restrict__ hbo = d.hb[cur];
+  int32_t* __restrict__ hbn = d.hb[cur ^ 1];
+  int32_t* __restrict__ tsb = d.ts;
+  const int32_t r = p.r;
+  const int32_t lim_fail = r - p.t_fail;
+  const int32_t lim_clean = r - p.t_cleanup;
+  const int32_t lim_next = r + 1 - p.t_fail;
+
+  // REMOVE bits of this lane's 4 columns (rare: slow path only when set)
+  const uint32_t my4 = (d.dbits[c0 >> 5] >> (c0 & 31)) & 0xFu;
+  int dc[4] = {0, 0, 0, 0}, dm[4] = {0, 0, 0, 0};
+  if (my4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      dc[j] = d.det_cnt[dcur][c0 + j];
+      dm[j] = d.det_min[dcur][c0 + j];
+    }
+  }
+
+  int n_unknown = 0, n_tomb = 0, n_det = 0, n_rel = 0, n_merged = 0;
+
+  for (int rr = wave; rr < GH_RB; rr += 4) {
+    const int i = rb * GH_RB + rr;
+    if (i >= p.n) break;
+    const int64_t off = (int64_t)i * p.ld + c0;
+    const int al = uni(d.alive[i]);
+    const int4 v = *reinterpret_cast<const int4*>(hbo + off);
+    if (!al) {  // crashed rows are frozen: carry hb into the new buffer
+      *reinterpret_cast<int4*>(hbn + off) = v;
+      int cnt = (v.x >= 0) + (v.y >= 0) + (v.z >= 0) + (v.w >= 0);
+      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+      if (lane == 0) s_part[rr] = (uint16_t)cnt;
+      continue;
+    }
+    const int ac = uni(d.active[i]);
+    const int beg = uni(d.inbox_beg[i]);
+    const int cntv = uni(d.inbox_cnt[i]);
+    const int4 t4 = *reinterpret_cast<const int4*>(tsb + off);
+
+    int m[4] = {-1, -1, -1, -1};
+    for (int base = 0; base < cntv; base += KB) {
+      int4 pv[KB];
+      int ps[KB];
+#pragma unroll
+      for (int q = 0; q < KB; ++q) {
+        const int s = (base + q < cntv) ? uni(d.inbox[beg + base + q]) : i;
+        ps[q] = s;
+        pv[q] = *reinterpret_cast<const int4*>(hbo + (int64_t)s * p.ld + c0);
+      }
+#pragma unroll
+      for (int q = 0; q < KB; ++q) {
+        if (base + q >= cntv) break;
+        const int s = ps[q];
+        const int x[4] = {pv[q].x, pv[q].y, pv[q].z, pv[q].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          // sender snapshot: present, not detected by s (flag), +1 on s's diagonal
+          int val = (x[j] >= 0 && !(x[j] & GH_FLAG)) ? x[j] + ((c0 + j) == s) : -1;
+          if (((my4 >> j) & 1u) && removes_at(dc[j], dm[j], s)) val = -1;
+          m[j] = max(m[j], val);
+        }
+      }
+    }
+
+    int xo[4] = {v.x, v.y, v.z, v.w};
+    int to[4] = {t4.x, t4.y, t4.z, t4.w};
+    int npres = 0;
+    bool any_det = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t c = c0 + j;
+      int x = xo[j] >= 0 ? (xo[j] & GH_HBMASK) : xo[j];
+      int t = to[j];
+      // step 1: REMOVE delivery (slave/slave.go:236-240, 276-286)
+      if (((my4 >> j) & 1u) && removes_at(dc[j], dm[j], i)) {
+        if (x >= 0) {
+          x = GH_TOMBSTONE;
+          n_tomb++;
+        } else if (x == GH_ABSENT) {
+          n_unknown++;
+        }
+      }
+      if (!ac) {
+        if (x >= 0) t = r;  // step 2 guard (:505-507)
+      } else {
+        if (c == i) {
+          if (x >= 0) {  // step 3 own heartbeat (:443-448)
+            x += 1;
+            t = r;
+          }
+        } else if (x > 1 && t < lim_fail) {  // step 4 detect (:468-473)
+          x = GH_TOMBSTONE;
+          n_det++;
+          any_det = true;
+          atomicAdd(&s_dcnt[lane * 4 + j], 1);
+          atomicMin(&s_dmin[lane * 4 + j], i);
+        }
+        if (x == GH_TOMBSTONE && t < lim_clean) {  // step 5 clean (:490-492)
+          x = GH_ABSENT;
+          n_rel++;
+        }
+      }
+      if (x >= GH_ABSENT && m[j] > x) {  // step 6 merge (:424-426, :435-437)
+        x = m[j];
+        t = r;
+        n_merged++;
+      }
+      npres += x >= 0;
+      if (x > 1 && c != i && t < lim_next) x |= GH_FLAG;
+      xo[j] = x;
+      to[j] = t;
+    }
+    *reinterpret_cast<int4*>(hbn + off) = make_int4(xo[0], xo[1], xo[2], xo[3]);
+    *reinterpret_cast<int4*>(tsb + off) = make_int4(to[0], to[1], to[2], to[3]);
+    for (int o = 32; o > 0; o >>= 1) npres += __shfl_xor(npres, o);
+    if (lane == 0) s_part[rr] = (uint16_t)npres;
+    if (__any(any_det) && lane == 0) d.det_any[i] = 1;
+  }
+
+  if (n_unknown) atomicAdd(&s_st[ST_REMOVE_UNKNOWN], (unsigned long long)n_unknown);
+  if (n_tomb) atomicAdd(&s_st[ST_TOMBSTONED], (unsigned long long)n_tomb);
+  if (n_det) atomicAdd(&s_st[ST_DETECTIONS], (unsigned long long)n_det);
+  if (n_rel) atomicAdd(&s_st[ST_RELEASED], (unsigned long long)n_rel);
+  if (n_merged) atomicAdd(&s_st[ST_MERGED], (unsigned long long)n_merged);
+  __syncthreads();
+
+  const int row0 = rb * GH_RB;
+  if (tid < GH_RB && row0 + tid < p.n) d.part[(int64_t)chunk * p.n + row0 + tid] = s_part[tid];
+  if (s_dcnt[tid]) {
+    const int64_t c = (int64_t)chunk * GH_CHUNK + tid;
+    atomicAdd(&d.det_cnt[dcur ^ 1][c], s_dcnt[tid]);
+    atomicMin(&d.det_min[dcur ^ 1][c], s_dmin[tid]);
+  }
+  if (tid < ST_COUNT && s_st[tid]) atomicAdd(&d.stats[tid], s_st[tid]);
+}
+
+// Rows: sum the per-chunk partial counts. Columns: bitmap + list of D_r,
+// and reset the consumed D_{r-1} accumulators for reuse in round r+1.
+__global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p, int nchunks) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x < p.n) {
+    int sum = 0;
+    for (int ch = 0; ch < nchunks; ++ch) sum += d.part[(int64_t)ch * p.n + x];
+    d.cnt[x] = sum;
+  }
+  const int dnew = dcur ^ 1;
+  bool has = false;
+  if (x < p.ld) {
+    has = d.det_cnt[dnew][x] > 0;
+    d.det_cnt[dcur][x] = 0;
+    d.det_min[dcur][x] = INT_MAX;
+  }
+  const unsigned long long m = __ballot(has);
+  const int lane = threadIdx.x & 63;
+  if (x - lane < p.ld && lane == 0) {
+    const int64_t w = (x - lane) >> 5;
+    d.dbits[w] = (uint32_t)m;
+    d.dbits[w + 1] = (uint32_t)(m >> 32);
+    if (m) {
+      atomicAdd(&d.nd[dnew], __popcll(m));
+      atomicAdd(&d.stats[ST_FAILED], (unsigned long long)__popcll(m));
+    }
+  }
+  if (has) {
+    // list order is irrelevant: only k_active's recount reads it
+    const int pos = atomicAdd(&d.nd[2 + dnew], 1);
+    d.dlist[(int64_t)dnew * p.ld + pos] = (int32_t)x;
+  }
+}
+
+}  // namespace
+
+void launch_active(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_active, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
+}
+
+void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_peers_pull, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
+}
+
+void launch_ring(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_ring_targets, dim3(p.n), dim3(256), 0, s, d, cur, dcur, p);
+  (void)hipMemsetAsync(d.inbox_cnt, 0, sizeof(int32_t) * p.n, s);
+  hipLaunchKernelGGL(k_inbox_count, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
+  hipLaunchKernelGGL(k_inbox_scan, dim3(1), dim3(1024), 0, s, d, p);
+  hipLaunchKernelGGL(k_inbox_fill, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
+}
+
+void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  const int nrb = (p.n + GH_RB - 1) / GH_RB;
+  const int64_t nchunks = p.ld / GH_CHUNK;
+  const dim3 grid((unsigned)(nrb * nchunks));
+  if (p.peer_mode == GH_PEER_PULL && p.k <= 4)
+    hipLaunchKernelGGL(k_round<4>, grid, dim3(256), 0, s, d, cur, dcur, p);
+  else
+    hipLaunchKernelGGL(k_round<8>, grid, dim3(256), 0, s, d, cur, dcur, p);
+}
+
+void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s) {
+  const int64_t span = p.ld > p.n ? p.ld : p.n;
+  const int nchunks = (int)(p.ld / GH_CHUNK);
+  hipLaunchKernelGGL(k_finish, dim3((unsigned)((span + 255) / 256)), dim3(256), 0, s, d, dcur, p,
+                     nchunks);
+}

@@ -1,0 +1,168 @@
+"""GPU parity: libgossiphip's HIP path (through the C-ABI) against the CPU
+oracle (oracle/tablesim.c), bit for bit — hb, ts, alive, failed set,
+detectors, per-round counters and placement results — on the App. B KATs,
+BASELINE config shapes and seeded churn. Run on a MI355X: pytest -m gpu."""
+import numpy as np
+import pytest
+
+import scenarios as sc
+from kat_util import KATS, kat_config, run_kat
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gs():
+    import gossipsim
+    return gossipsim
+
+
+def compare(eng, orc, r, full=True):
+    h1, t1, a1 = eng.export_state()
+    h2, t2, a2 = orc.export_state()
+    np.testing.assert_array_equal(a1, a2, err_msg=f"alive r={r}")
+    if full:
+        bad = np.argwhere(h1 != h2)
+        assert bad.size == 0, f"hb r={r}: {len(bad)} cells differ, first {bad[:5].tolist()} " \
+                              f"gpu={h1[tuple(bad[0])]} cpu={h2[tuple(bad[0])]}"
+        np.testing.assert_array_equal(t1, t2, err_msg=f"ts r={r}")
+    np.testing.assert_array_equal(eng.read_failed(), orc.read_failed(), err_msg=f"failed r={r}")
+    np.testing.assert_array_equal(eng.read_detectors(), orc.read_detectors(), err_msg=f"detectors r={r}")
+
+
+def run_parity(gs, om, cfg_kw, n, rounds, sched, init=None, threads=8, every=1, files=None):
+    eng = gs.Engine(gs.default_config(n, **cfg_kw))
+    orc = om.Oracle(om.default_config(n, **cfg_kw), threads=threads)
+    if init is not None:
+        hb, ts, alive = init
+        eng.import_state(hb, ts, alive, 0)
+        orc.import_state(hb, ts, alive, 0)
+    for r in range(1, rounds + 1):
+        ev = sched.get(r, [])
+        if ev:
+            eng.apply_events(ev)
+            orc.apply_events(ev)
+        s1, s2 = eng.step(1), orc.step(1)
+        assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
+        if files is not None and r in files:
+            f = np.asarray(files[r], np.int32)
+            a, b = eng.put(f), orc.put(f)
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x, y)
+            for obs in orc.read_detectors()[:2]:
+                assert eng.repair(int(obs)) == orc.repair(int(obs))
+        if r % every == 0 or r == rounds or ev:
+            compare(eng, orc, r)
+    return eng, orc
+
+
+@pytest.mark.parametrize("k", [k for k in KATS if k["detect_mode"] == 0], ids=lambda k: k["name"])
+def test_kats_gpu(gs, k):
+    run_kat(gs.Engine(kat_config(gs, k)), k)
+
+
+@pytest.mark.parametrize("peer_mode", [0, 1])
+def test_c1_bootstrap_crash_places(gs, oracle_mod, peer_mode):
+    """BASELINE config 1: 10 members join one per round, 10 files put at r=20,
+    member 7 crashes at r=30, run to r=60 with repairs."""
+    n = 10
+    sched = sc.bootstrap_schedule(n)
+    sched.setdefault(30, []).append((sc.CRASH, 7))
+    files = {20: list(range(10))}
+    for r in range(31, 61):
+        files[r] = []
+    run_parity(gs, oracle_mod, dict(peer_mode=peer_mode, max_files=16, seed=0x5EED0001), n, 60, sched,
+               files=files)
+
+
+@pytest.mark.parametrize("n,peer_mode,seed", [(16, 0, 1), (16, 1, 2), (64, 0, 3), (64, 1, 4), (300, 0, 5),
+                                              (257, 1, 6)])
+def test_random_churn(gs, oracle_mod, n, peer_mode, seed):
+    sched = sc.random_churn(n, 40, seed, p_crash=0.03, p_leave=0.01, p_join=0.05)
+    run_parity(gs, oracle_mod, dict(peer_mode=peer_mode, fanout=3, seed=0x77 + seed), n, 40, sched,
+               init=sc.full_state(n))
+
+
+@pytest.mark.parametrize("fanout", [1, 4, 5, 8])
+def test_fanouts_short_timeouts(gs, oracle_mod, fanout):
+    n = 200
+    sched = sc.random_churn(n, 30, 11, p_crash=0.05)
+    run_parity(gs, oracle_mod, dict(fanout=fanout, t_fail=3, t_cleanup=7, seed=0x99), n, 30, sched,
+               init=sc.full_state(n))
+
+
+def test_c2_n4096_crash_1pct(gs, oracle_mod):
+    """BASELINE config 2: N=4,096, k=3, full tables (hb=2, ts=0), 1% crash
+    drawn by Philox(0x5EED0002) at r=8, 64 rounds; full-state compare every 8
+    rounds, counters and failed sets every round."""
+    n = 4096
+    sched = {8: [(sc.CRASH, c) for c in sc.crash_ids(n, 0.01, 0x5EED0002)]}
+    eng, orc = run_parity(gs, oracle_mod, dict(fanout=3, seed=0x5EED0002), n, 64, sched,
+                          init=sc.full_state(n), every=8)
+
+
+def test_placement_parity_many_files(gs, oracle_mod):
+    n, F = 512, 20000
+    cfg = dict(max_files=F, seed=0x5EED0005)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg))
+    hb, ts, alive = sc.full_state(n)
+    eng.import_state(hb, ts, alive, 3)
+    orc.import_state(hb, ts, alive, 3)
+    f = np.random.default_rng(0).permutation(F)[: F // 2].astype(np.int32)
+    for x, y in zip(eng.put(f), orc.put(f)):
+        np.testing.assert_array_equal(x, y)
+    # crash 5% and let the failure be detected, then repair from two observers
+    sched = {1: [(sc.CRASH, c) for c in sc.crash_ids(n, 0.05, 0x5EED0005)]}
+    for r in range(1, 12):
+        if r in sched:
+            eng.apply_events(sched[r])
+            orc.apply_events(sched[r])
+        assert eng.step(1) == orc.step(1)
+    for obs in (0, 5):
+        assert eng.repair(obs) == orc.repair(obs)
+    for x, y in zip(eng.get_files(np.arange(F)), orc.get_files(np.arange(F))):
+        np.testing.assert_array_equal(x, y)
+    g = np.arange(0, F, 7, dtype=np.int32)
+    np.testing.assert_array_equal(eng.delete_files(g), orc.delete_files(g))
+    for x, y in zip(eng.put(g[:100]), orc.put(g[:100])):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_starvation_gpu(gs, oracle_mod):
+    n = 8
+    eng = gs.Engine(gs.default_config(n, max_files=4))
+    hb = np.full((n, n), -1, np.int32)
+    hb[0, :4] = 3
+    alive = np.zeros(n, np.uint8)
+    alive[0] = 1
+    eng.import_state(hb, np.zeros((n, n), np.int32), alive, 20)
+    rep, ver, st = eng.put([0])
+    assert st[0] == gs.GH_EPLACEMENT_STARVED and ver[0] == 0
+
+
+def test_n65536_invariants(gs):
+    """BASELINE config 3 scale (N=65,536, k=4, 48 GiB of tables): properties
+    that hold at any size — with no failures every member stays everywhere,
+    the own heartbeat advances by one per round, no cell runs ahead of its
+    owner, nothing is detected; then a 1% crash is detected by every live
+    observer's failed set within T_fail + a few rounds."""
+    n, rounds = 65536, 6
+    eng = gs.Engine(gs.default_config(n, fanout=4, seed=0x5EED0003))
+    eng.init_full(2, 0, 0)
+    st = eng.step(rounds)
+    assert st["detections"] == 0 and st["active_rows"] == n * rounds
+    rows = np.array([0, 1, 4095, 32768, 65535])
+    for i in rows:
+        hb, ts, _ = eng.export_state(int(i), 1)
+        assert hb[0, i] == 2 + rounds
+        assert (hb[0] >= 2).all() and (hb[0] <= 2 + rounds).all()
+        assert (ts[0] <= rounds).all()
+    crashed = sc.crash_ids(n, 0.01, 0x5EED0003)
+    eng.apply_events([(sc.CRASH, c) for c in crashed])
+    seen = set()
+    for _ in range(12):
+        eng.step(1)
+        bm = eng.read_failed()
+        seen |= {c for c in crashed if bm[c >> 5] >> (c & 31) & 1}
+    assert seen == set(crashed)
