@@ -21,6 +21,7 @@
 #define GH_CHUNK 256             // columns per wave row-segment (64 lanes x int4)
 #define GH_RB 64                 // rows per workgroup tile in the round kernel
 #define GH_MAXK 8                // max pull fanout
+#define GH_DLIST_MAX 1024        // |D| above which k_active_exact recounts whole rows
 #define GH_TAG_PEER 0x50454552u
 #define GH_TAG_PLACE 0x504C4143u
 #define GH_MAX_DRAWS (1u << 20)

@@ -44,6 +44,9 @@ __global__ __launch_bounds__(256) void k_active(GhDev d, int cur, int dcur, GhRo
         a = false;
       } else if (c - nd >= p.min_members) {
         a = true;
+      } else if (nd > GH_DLIST_MAX) {
+        a = false;          // decided by k_active_exact's full-row recount
+        d.cnt[i] = -1;      // marks the row uncertain for it
       } else {
         const int32_t* row = d.hb[cur] + (int64_t)i * p.ld;
         const int32_t* dc = d.det_cnt[dcur];
@@ -60,6 +63,33 @@ __global__ __launch_bounds__(256) void k_active(GhDev d, int cur, int dcur, GhRo
   }
   const unsigned long long m = __ballot(a);
   if ((threadIdx.x & 63) == 0 && m) atomicAdd(&d.stats[ST_ACTIVE_ROWS], (unsigned long long)__popcll(m));
+}
+
+// Failure storms (|D| > GH_DLIST_MAX): rows k_active could not decide from
+// the D list get an exact post-REMOVE recount by one wave sweeping the row.
+__global__ __launch_bounds__(256) void k_active_exact(GhDev d, int cur, int dcur, GhRound p) {
+  if (d.nd[dcur] <= GH_DLIST_MAX) return;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= p.n || d.cnt[i] != -1) return;
+  const int32_t* row = d.hb[cur] + (int64_t)i * p.ld;
+  const int32_t* dc = d.det_cnt[dcur];
+  const int32_t* dm = d.det_min[dcur];
+  int cnt = 0;
+  for (int64_t c = lane * 4; c < p.ld; c += 256) {
+    const int4 v = *reinterpret_cast<const int4*>(row + c);
+    const uint32_t b4 = (d.dbits[c >> 5] >> (c & 31)) & 0xFu;
+    const int x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      cnt += x[j] >= 0 && !(((b4 >> j) & 1u) && removes_at(dc[c + j], dm[c + j], i));
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if (lane == 0) {
+    const bool a = cnt >= p.min_members;
+    d.active[i] = a;
+    if (a) atomicAdd(&d.stats[ST_ACTIVE_ROWS], 1ull);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, GhRound p) {
@@ -406,6 +436,7 @@ __global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p, in
 
 void launch_active(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_active, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
+  hipLaunchKernelGGL(k_active_exact, dim3((p.n + 3) / 4), dim3(256), 0, s, d, cur, dcur, p);
 }
 
 void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {

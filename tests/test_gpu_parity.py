@@ -101,6 +101,17 @@ def test_c2_n4096_crash_1pct(gs, oracle_mod):
                           init=sc.full_state(n), every=8)
 
 
+def test_c2_steady_state_crash(gs, oracle_mod):
+    """N=4,096, k=3 in the healthy regime (T_fail = T_cleanup = 12 rounds,
+    above the ~6-round dissemination time): ~55% of cells merge every round;
+    a 1% crash at r=8 is detected and REMOVE'd everywhere."""
+    n = 4096
+    sched = {8: [(sc.CRASH, c) for c in sc.crash_ids(n, 0.01, 0x5EED0012)]}
+    eng, orc = run_parity(gs, oracle_mod, dict(fanout=3, seed=0x5EED0012, t_fail=12, t_cleanup=12), n, 48,
+                          sched, init=sc.full_state(n), every=8)
+    assert eng.step(0)["rounds"] == 0
+
+
 def test_placement_parity_many_files(gs, oracle_mod):
     n, F = 512, 20000
     cfg = dict(max_files=F, seed=0x5EED0005)
@@ -146,12 +157,13 @@ def test_n65536_invariants(gs):
     that hold at any size — with no failures every member stays everywhere,
     the own heartbeat advances by one per round, no cell runs ahead of its
     owner, nothing is detected; then a 1% crash is detected by every live
-    observer's failed set within T_fail + a few rounds."""
-    n, rounds = 65536, 6
-    eng = gs.Engine(gs.default_config(n, fanout=4, seed=0x5EED0003))
+    observer's failed set within T_fail + the dissemination time."""
+    n, rounds = 65536, 12
+    eng = gs.Engine(gs.default_config(n, fanout=4, seed=0x5EED0003, t_fail=16, t_cleanup=16))
     eng.init_full(2, 0, 0)
     st = eng.step(rounds)
     assert st["detections"] == 0 and st["active_rows"] == n * rounds
+    assert st["merged_cells"] > n * n  # the epidemic has reached every cell
     rows = np.array([0, 1, 4095, 32768, 65535])
     for i in rows:
         hb, ts, _ = eng.export_state(int(i), 1)
@@ -161,7 +173,7 @@ def test_n65536_invariants(gs):
     crashed = sc.crash_ids(n, 0.01, 0x5EED0003)
     eng.apply_events([(sc.CRASH, c) for c in crashed])
     seen = set()
-    for _ in range(12):
+    for _ in range(40):
         eng.step(1)
         bm = eng.read_failed()
         seen |= {c for c in crashed if bm[c >> 5] >> (c & 31) & 1}
