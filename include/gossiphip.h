@@ -165,6 +165,12 @@ int gh_get_files(void* h, const int32_t* files, int64_t n, int32_t* replicas,
 int gh_delete_files(void* h, const int32_t* files, int64_t n,
                     int32_t* old_replicas);
 
+/* Tuning knob of the fused round kernel (k_round): lanes per row segment
+ * (64, 32 or 16 -> 256/128/64-column chunks per workgroup tile) and
+ * non-temporal loads/stores on the once-touched streams. Results do not
+ * depend on it; the default is the measured fastest. */
+int gh_set_round_variant(void* h, int32_t seg_lanes, int32_t nontemporal);
+
 /* Device timing of the fused round kernel (HIP events on the engine's
  * stream), for bench.py's roofline: enable, then read the sum of kernel
  * durations (ms) and launch count since enabling. */

@@ -102,8 +102,10 @@ struct GhRound {
 void launch_active(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_ring(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
-void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);
+// seg = lanes per row segment (64, 32, 16 -> 256/128/64-column chunks), nt =
+// non-temporal streams; launch_finish must get the seg its round used.
+void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, int seg, bool nt);
+void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s, int seg);
 void launch_count(const GhDev& d, int cur, const GhRound& p, hipStream_t s);
 void launch_flags(const GhDev& d, int cur, int64_t row0, int64_t nrows, const GhRound& p,
                   hipStream_t s);

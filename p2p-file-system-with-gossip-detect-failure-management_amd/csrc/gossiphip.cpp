@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -33,6 +34,8 @@ struct Engine {
   std::vector<uint8_t> alive;   // host mirror (source of truth for events)
   std::vector<gh_event> pending;
   int32_t* ev_buf = nullptr;    // device scratch for event member lists
+  int seg = 64;          // k_round lanes per row segment (tuning, gh_set_round_variant)
+  bool nt = false;       // k_round non-temporal streams
   bool timing = false;
   double timed_ms = 0.0;
   int64_t timed_launches = 0;
@@ -245,6 +248,9 @@ int gh_create(const gh_config* cfg, void** handle) {
   e->n = cfg->n_members;
   e->ld = ((int64_t)e->n + GH_CHUNK - 1) / GH_CHUNK * GH_CHUNK;
   e->alive.assign(e->n, 0);
+  if (const char* v = std::getenv("GH_ROUND_SEG")) e->seg = std::atoi(v);
+  if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
+  if (e->seg != 64 && e->seg != 32 && e->seg != 16) e->seg = 64;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return GH_EHIP;
@@ -253,7 +259,7 @@ int gh_create(const gh_config* cfg, void** handle) {
   d.n = e->n;
   d.ld = e->ld;
   const int64_t cells = (int64_t)e->n * e->ld;
-  const int64_t nch = e->ld / GH_CHUNK;
+  const int64_t nch = e->ld / 64;  // partial-count chunks at the narrowest variant (seg 16)
   const int64_t inbox = (int64_t)e->n * std::max(cfg->fanout, 3);
   int rc = GH_OK;
   do {
@@ -408,9 +414,9 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     else
       launch_ring(e->d, e->cur, e->dcur, p, e->stream);
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q], e->stream));
-    launch_round(e->d, e->cur, e->dcur, p, e->stream);
+    launch_round(e->d, e->cur, e->dcur, p, e->stream, e->seg, e->nt);
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q + 1], e->stream));
-    launch_finish(e->d, e->dcur, p, e->stream);
+    launch_finish(e->d, e->dcur, p, e->stream, e->seg);
     HIPCHK(e, hipGetLastError());
     e->cur ^= 1;
     e->dcur ^= 1;
@@ -587,6 +593,15 @@ int gh_delete_files(void* h, const int32_t* files, int64_t n, int32_t* old_repli
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
   return get_or_delete(e, files, n, old_replicas, nullptr, 1);
+}
+
+int gh_set_round_variant(void* h, int32_t seg_lanes, int32_t nontemporal) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  if (seg_lanes != 64 && seg_lanes != 32 && seg_lanes != 16) return set_err(e, GH_EINVAL, "seg_lanes");
+  e->seg = seg_lanes;
+  e->nt = nontemporal != 0;
+  return GH_OK;
 }
 
 int gh_set_timing(void* h, int32_t enable) {

@@ -236,15 +236,38 @@ __global__ __launch_bounds__(256) void k_inbox_fill(GhDev d, GhRound p) {
   }
 }
 
-// The fused round. Tile = GH_RB rows x GH_CHUNK columns; block index is
-// chunk-major so the concurrently running tiles share one 256-column slice of
-// the table and peer-row segments are re-read from the on-die caches.
-// Each lane owns 4 consecutive columns (16-B loads/stores); a wave owns one
-// row segment at a time. KB = peer loads issued together (4 or 8).
-template <int KB>
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__device__ __forceinline__ v4i ldv(const int32_t* p) {
+  if constexpr (NT)
+    return __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
+  else
+    return *reinterpret_cast<const v4i*>(p);
+}
+template <bool NT>
+__device__ __forceinline__ void stv(int32_t* p, v4i v) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(p));
+  else
+    *reinterpret_cast<v4i*>(p) = v;
+}
+
+// The fused round. Tile = GH_RB rows x CW columns, CW = 4*SEG; block index is
+// chunk-major so the concurrently running tiles share one CW-column slice of
+// the table and peer-row segments can be re-read from the on-die caches.
+// Each lane owns 4 consecutive columns (16-B loads/stores); SEG lanes cover
+// one row segment, so a wave handles 64/SEG rows per instruction.
+// KB = peer loads issued together (4 or 8). NT = non-temporal hints on the
+// once-touched streams (own ts in/out, new hb out), leaving the cache to the
+// re-read old-hb slice.
+template <int KB, int SEG, bool NT>
 __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRound p) {
-  __shared__ int s_dcnt[GH_CHUNK];
-  __shared__ int s_dmin[GH_CHUNK];
+  constexpr int CW = SEG * 4;
+  constexpr int RPW = 64 / SEG;
+  constexpr int RSTEP = 4 * RPW;
+  __shared__ int s_dcnt[CW];
+  __shared__ int s_dmin[CW];
   __shared__ uint16_t s_part[GH_RB];
   __shared__ unsigned long long s_st[ST_COUNT];
 
@@ -254,10 +277,14 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = uni(tid >> 6);
-  const int64_t c0 = (int64_t)chunk * GH_CHUNK + lane * 4;
+  const int sub = lane / SEG;
+  const int lc = lane % SEG;
+  const int64_t c0 = (int64_t)chunk * CW + lc * 4;
 
-  s_dcnt[tid] = 0;
-  s_dmin[tid] = INT_MAX;
+  for (int t = tid; t < CW; t += 256) {
+    s_dcnt[t] = 0;
+    s_dmin[t] = INT_MAX;
+  }
   if (tid < ST_COUNT) s_st[tid] = 0;
   if (tid < GH_RB) s_part[tid] = 0;
   __syncthreads();
@@ -283,102 +310,130 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
 
   int n_unknown = 0, n_tomb = 0, n_det = 0, n_rel = 0, n_merged = 0;
 
-  for (int rr = wave; rr < GH_RB; rr += 4) {
-    const int i = rb * GH_RB + rr;
-    if (i >= p.n) break;
+  for (int rr0 = wave * RPW; rr0 < GH_RB; rr0 += RSTEP) {
+    const int rr = rr0 + sub;
+    const int i_raw = rb * GH_RB + rr;
+    const bool valid = i_raw < p.n;
+    if (!__any(valid)) break;
+    const int i = valid ? i_raw : p.n - 1;  // in-range row for the loads of idle halves
     const int64_t off = (int64_t)i * p.ld + c0;
-    const int al = uni(d.alive[i]);
-    const int4 v = *reinterpret_cast<const int4*>(hbo + off);
-    if (!al) {  // crashed rows are frozen: carry hb into the new buffer
-      *reinterpret_cast<int4*>(hbn + off) = v;
-      int cnt = (v.x >= 0) + (v.y >= 0) + (v.z >= 0) + (v.w >= 0);
-      for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-      if (lane == 0) s_part[rr] = (uint16_t)cnt;
-      continue;
+    int al, ac, beg, cntv;
+    if constexpr (RPW == 1) {
+      al = uni(d.alive[i]);
+      ac = uni(d.active[i]);
+      beg = uni(d.inbox_beg[i]);
+      cntv = al ? uni(d.inbox_cnt[i]) : 0;
+    } else {
+      al = d.alive[i] && valid;
+      ac = d.active[i];
+      beg = d.inbox_beg[i];
+      cntv = al ? d.inbox_cnt[i] : 0;
     }
-    const int ac = uni(d.active[i]);
-    const int beg = uni(d.inbox_beg[i]);
-    const int cntv = uni(d.inbox_cnt[i]);
-    const int4 t4 = *reinterpret_cast<const int4*>(tsb + off);
+    const v4i v = ldv<false>(hbo + off);  // re-read by peers: keep it cached
+    v4i t4 = {0, 0, 0, 0};
+    if (al) t4 = ldv<NT>(tsb + off);
 
+    int cmax = cntv;
+    if constexpr (RPW > 1) {
+#pragma unroll
+      for (int o = SEG; o < 64; o <<= 1) cmax = max(cmax, __shfl_xor(cmax, o));
+    }
     int m[4] = {-1, -1, -1, -1};
-    for (int base = 0; base < cntv; base += KB) {
-      int4 pv[KB];
+    for (int base = 0; base < cmax; base += KB) {
+      v4i pv[KB];
       int ps[KB];
 #pragma unroll
       for (int q = 0; q < KB; ++q) {
-        const int s = (base + q < cntv) ? uni(d.inbox[beg + base + q]) : i;
+        int s = i;
+        if (base + q < cntv) {
+          if constexpr (RPW == 1)
+            s = uni(d.inbox[beg + base + q]);
+          else
+            s = d.inbox[beg + base + q];
+        }
         ps[q] = s;
-        pv[q] = *reinterpret_cast<const int4*>(hbo + (int64_t)s * p.ld + c0);
+        pv[q] = ldv<false>(hbo + (int64_t)s * p.ld + c0);
       }
 #pragma unroll
       for (int q = 0; q < KB; ++q) {
-        if (base + q >= cntv) break;
+        if (base + q >= cntv) continue;
         const int s = ps[q];
-        const int x[4] = {pv[q].x, pv[q].y, pv[q].z, pv[q].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+          const int x = pv[q][j];
           // sender snapshot: present, not detected by s (flag), +1 on s's diagonal
-          int val = (x[j] >= 0 && !(x[j] & GH_FLAG)) ? x[j] + ((c0 + j) == s) : -1;
+          int val = (x >= 0 && !(x & GH_FLAG)) ? x + ((c0 + j) == s) : -1;
           if (((my4 >> j) & 1u) && removes_at(dc[j], dm[j], s)) val = -1;
           m[j] = max(m[j], val);
         }
       }
     }
 
-    int xo[4] = {v.x, v.y, v.z, v.w};
-    int to[4] = {t4.x, t4.y, t4.z, t4.w};
+    v4i xo = v;
+    v4i to = t4;
     int npres = 0;
     bool any_det = false;
+    if (al) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t c = c0 + j;
-      int x = xo[j] >= 0 ? (xo[j] & GH_HBMASK) : xo[j];
-      int t = to[j];
-      // step 1: REMOVE delivery (slave/slave.go:236-240, 276-286)
-      if (((my4 >> j) & 1u) && removes_at(dc[j], dm[j], i)) {
-        if (x >= 0) {
-          x = GH_TOMBSTONE;
-          n_tomb++;
-        } else if (x == GH_ABSENT) {
-          n_unknown++;
-        }
-      }
-      if (!ac) {
-        if (x >= 0) t = r;  // step 2 guard (:505-507)
-      } else {
-        if (c == i) {
-          if (x >= 0) {  // step 3 own heartbeat (:443-448)
-            x += 1;
-            t = r;
+      for (int j = 0; j < 4; ++j) {
+        const int64_t c = c0 + j;
+        int x = xo[j] >= 0 ? (xo[j] & GH_HBMASK) : xo[j];
+        int t = to[j];
+        // step 1: REMOVE delivery (slave/slave.go:236-240, 276-286)
+        if (((my4 >> j) & 1u) && removes_at(dc[j], dm[j], i)) {
+          if (x >= 0) {
+            x = GH_TOMBSTONE;
+            n_tomb++;
+          } else if (x == GH_ABSENT) {
+            n_unknown++;
           }
-        } else if (x > 1 && t < lim_fail) {  // step 4 detect (:468-473)
-          x = GH_TOMBSTONE;
-          n_det++;
-          any_det = true;
-          atomicAdd(&s_dcnt[lane * 4 + j], 1);
-          atomicMin(&s_dmin[lane * 4 + j], i);
         }
-        if (x == GH_TOMBSTONE && t < lim_clean) {  // step 5 clean (:490-492)
-          x = GH_ABSENT;
-          n_rel++;
+        if (!ac) {
+          if (x >= 0) t = r;  // step 2 guard (:505-507)
+        } else {
+          if (c == i) {
+            if (x >= 0) {  // step 3 own heartbeat (:443-448)
+              x += 1;
+              t = r;
+            }
+          } else if (x > 1 && t < lim_fail) {  // step 4 detect (:468-473)
+            x = GH_TOMBSTONE;
+            n_det++;
+            any_det = true;
+            atomicAdd(&s_dcnt[lc * 4 + j], 1);
+            atomicMin(&s_dmin[lc * 4 + j], i);
+          }
+          if (x == GH_TOMBSTONE && t < lim_clean) {  // step 5 clean (:490-492)
+            x = GH_ABSENT;
+            n_rel++;
+          }
         }
+        if (x >= GH_ABSENT && m[j] > x) {  // step 6 merge (:424-426, :435-437)
+          x = m[j];
+          t = r;
+          n_merged++;
+        }
+        if (x > 1 && c != i && t < lim_next) x |= GH_FLAG;
+        xo[j] = x;
+        to[j] = t;
       }
-      if (x >= GH_ABSENT && m[j] > x) {  // step 6 merge (:424-426, :435-437)
-        x = m[j];
-        t = r;
-        n_merged++;
-      }
-      npres += x >= 0;
-      if (x > 1 && c != i && t < lim_next) x |= GH_FLAG;
-      xo[j] = x;
-      to[j] = t;
     }
-    *reinterpret_cast<int4*>(hbn + off) = make_int4(xo[0], xo[1], xo[2], xo[3]);
-    *reinterpret_cast<int4*>(tsb + off) = make_int4(to[0], to[1], to[2], to[3]);
-    for (int o = 32; o > 0; o >>= 1) npres += __shfl_xor(npres, o);
-    if (lane == 0) s_part[rr] = (uint16_t)npres;
-    if (__any(any_det) && lane == 0) d.det_any[i] = 1;
+    // crashed rows are frozen: their hb is carried into the new buffer as is
+#pragma unroll
+    for (int j = 0; j < 4; ++j) npres += xo[j] >= 0;
+    if (valid) {
+      stv<NT>(hbn + off, xo);
+      if (al) stv<NT>(tsb + off, to);
+    }
+#pragma unroll
+    for (int o = SEG / 2; o > 0; o >>= 1) {
+      npres += __shfl_xor(npres, o);
+      any_det |= __shfl_xor((int)any_det, o) != 0;
+    }
+    if (lc == 0 && valid) {
+      s_part[rr] = (uint16_t)npres;
+      if (any_det) d.det_any[i] = 1;
+    }
   }
 
   if (n_unknown) atomicAdd(&s_st[ST_REMOVE_UNKNOWN], (unsigned long long)n_unknown);
@@ -390,10 +445,12 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
 
   const int row0 = rb * GH_RB;
   if (tid < GH_RB && row0 + tid < p.n) d.part[(int64_t)chunk * p.n + row0 + tid] = s_part[tid];
-  if (s_dcnt[tid]) {
-    const int64_t c = (int64_t)chunk * GH_CHUNK + tid;
-    atomicAdd(&d.det_cnt[dcur ^ 1][c], s_dcnt[tid]);
-    atomicMin(&d.det_min[dcur ^ 1][c], s_dmin[tid]);
+  for (int t = tid; t < CW; t += 256) {
+    if (s_dcnt[t]) {
+      const int64_t c = (int64_t)chunk * CW + t;
+      atomicAdd(&d.det_cnt[dcur ^ 1][c], s_dcnt[t]);
+      atomicMin(&d.det_min[dcur ^ 1][c], s_dmin[t]);
+    }
   }
   if (tid < ST_COUNT && s_st[tid]) atomicAdd(&d.stats[tid], s_st[tid]);
 }
@@ -451,19 +508,36 @@ void launch_ring(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_
   hipLaunchKernelGGL(k_inbox_fill, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
 }
 
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+template <int KB>
+static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, int seg,
+                            bool nt) {
   const int nrb = (p.n + GH_RB - 1) / GH_RB;
-  const int64_t nchunks = p.ld / GH_CHUNK;
-  const dim3 grid((unsigned)(nrb * nchunks));
-  if (p.peer_mode == GH_PEER_PULL && p.k <= 4)
-    hipLaunchKernelGGL(k_round<4>, grid, dim3(256), 0, s, d, cur, dcur, p);
-  else
-    hipLaunchKernelGGL(k_round<8>, grid, dim3(256), 0, s, d, cur, dcur, p);
+  const int64_t nchunks = p.ld / (seg * 4);
+  const dim3 grid((unsigned)(nrb * nchunks)), blk(256);
+#define GH_ROUND_CASE(SEG_)                                                              \
+  if (seg == SEG_) {                                                                     \
+    if (nt)                                                                              \
+      hipLaunchKernelGGL((k_round<KB, SEG_, true>), grid, blk, 0, s, d, cur, dcur, p);  \
+    else                                                                                 \
+      hipLaunchKernelGGL((k_round<KB, SEG_, false>), grid, blk, 0, s, d, cur, dcur, p); \
+    return;                                                                              \
+  }
+  GH_ROUND_CASE(64)
+  GH_ROUND_CASE(32)
+  GH_ROUND_CASE(16)
+#undef GH_ROUND_CASE
 }
 
-void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s) {
+void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, int seg, bool nt) {
+  if (p.peer_mode == GH_PEER_PULL && p.k <= 4)
+    launch_round_kb<4>(d, cur, dcur, p, s, seg, nt);
+  else
+    launch_round_kb<8>(d, cur, dcur, p, s, seg, nt);
+}
+
+void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s, int seg) {
   const int64_t span = p.ld > p.n ? p.ld : p.n;
-  const int nchunks = (int)(p.ld / GH_CHUNK);
+  const int nchunks = (int)(p.ld / (seg * 4));
   hipLaunchKernelGGL(k_finish, dim3((unsigned)((span + 255) / 256)), dim3(256), 0, s, d, dcur, p,
                      nchunks);
 }

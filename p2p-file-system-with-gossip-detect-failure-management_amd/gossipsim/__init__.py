@@ -163,7 +163,10 @@ class Engine:
         self._chk(self.lib.gh_delete_files(self.h, _p(f), len(f), _p(rep)))
         return rep
 
-    # ---- timing ----------------------------------------------------------
+    # ---- tuning / timing -------------------------------------------------
+    def set_round_variant(self, seg_lanes=64, nontemporal=False):
+        self._chk(self.lib.gh_set_round_variant(self.h, seg_lanes, int(nontemporal)))
+
     def set_timing(self, enable=True):
         self._chk(self.lib.gh_set_timing(self.h, int(enable)))
 

@@ -178,3 +178,22 @@ def test_n65536_invariants(gs):
         bm = eng.read_failed()
         seen |= {c for c in crashed if bm[c >> 5] >> (c & 31) & 1}
     assert seen == set(crashed)
+
+
+@pytest.mark.parametrize("seg,nt", [(64, 0), (64, 1), (32, 0), (32, 1), (16, 1)])
+def test_round_variants_identical(gs, oracle_mod, seg, nt):
+    """Every k_round tiling variant gives the oracle's results (tuning knob)."""
+    n = 700
+    sched = sc.random_churn(n, 24, 21, p_crash=0.04, p_leave=0.01, p_join=0.05)
+    eng = gs.Engine(gs.default_config(n, fanout=4, seed=0x31, t_fail=4, t_cleanup=6))
+    eng.set_round_variant(seg, nt)
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, fanout=4, seed=0x31, t_fail=4, t_cleanup=6), threads=8)
+    hb, ts, alive = sc.full_state(n)
+    eng.import_state(hb, ts, alive, 0)
+    orc.import_state(hb, ts, alive, 0)
+    for r in range(1, 25):
+        if r in sched:
+            eng.apply_events(sched[r])
+            orc.apply_events(sched[r])
+        assert eng.step(1) == orc.step(1), r
+    compare(eng, orc, 24)
