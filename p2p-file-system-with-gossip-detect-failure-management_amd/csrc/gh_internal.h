@@ -96,6 +96,10 @@ struct GhRound {
   int32_t k;
   uint64_t seed;
   int32_t peer_mode;
+  int32_t ablate;     // timing-only experiments (results wrong): 1 = every
+                      // peer load reads the own row, 2 = no peer loads. 0 always
+                      // in production (set only through GH_ROUND_ABLATE).
+  int32_t order;      // k_round tile order: 0 chunk-major (default), 1 row-major
 };
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------

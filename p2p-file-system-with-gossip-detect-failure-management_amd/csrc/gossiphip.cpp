@@ -36,6 +36,8 @@ struct Engine {
   int32_t* ev_buf = nullptr;    // device scratch for event member lists
   int seg = 64;          // k_round lanes per row segment (tuning, gh_set_round_variant)
   bool nt = false;       // k_round non-temporal streams
+  int ablate = 0;        // timing-only experiment switch (GH_ROUND_ABLATE), never set in production
+  int order = 0;         // k_round tile order (GH_ROUND_ORDER): 0 chunk-major, 1 row-major
   bool timing = false;
   double timed_ms = 0.0;
   int64_t timed_launches = 0;
@@ -81,6 +83,8 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.k = e->cfg.fanout;
   p.seed = e->cfg.seed;
   p.peer_mode = e->cfg.peer_mode;
+  p.ablate = e->ablate;
+  p.order = e->order;
   return p;
 }
 
@@ -250,6 +254,8 @@ int gh_create(const gh_config* cfg, void** handle) {
   e->alive.assign(e->n, 0);
   if (const char* v = std::getenv("GH_ROUND_SEG")) e->seg = std::atoi(v);
   if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_ROUND_ABLATE")) e->ablate = std::atoi(v);
+  if (const char* v = std::getenv("GH_ROUND_ORDER")) e->order = std::atoi(v) != 0;
   if (e->seg != 64 && e->seg != 32 && e->seg != 16) e->seg = 64;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;

@@ -272,8 +272,15 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   __shared__ unsigned long long s_st[ST_COUNT];
 
   const int nrb = (p.n + GH_RB - 1) / GH_RB;
-  const int chunk = blockIdx.x / nrb;
-  const int rb = blockIdx.x - chunk * nrb;
+  int chunk, rb;
+  if (p.order == 0) {
+    chunk = blockIdx.x / nrb;
+    rb = blockIdx.x - chunk * nrb;
+  } else {
+    const int nch = (int)(p.ld / CW);
+    rb = blockIdx.x / nch;
+    chunk = blockIdx.x - rb * nch;
+  }
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = uni(tid >> 6);
@@ -333,6 +340,7 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     v4i t4 = {0, 0, 0, 0};
     if (al) t4 = ldv<NT>(tsb + off);
 
+    if (p.ablate == 2) cntv = 0;
     int cmax = cntv;
     if constexpr (RPW > 1) {
 #pragma unroll
@@ -352,7 +360,7 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
             s = d.inbox[beg + base + q];
         }
         ps[q] = s;
-        pv[q] = ldv<false>(hbo + (int64_t)s * p.ld + c0);
+        pv[q] = ldv<false>(hbo + (int64_t)(p.ablate == 1 ? i : s) * p.ld + c0);
       }
 #pragma unroll
       for (int q = 0; q < KB; ++q) {
