@@ -70,7 +70,8 @@ typedef struct gh_config {
   int32_t introducer;    /* INTRODUCER_ADDR, slave/slave.go:22 (0)           */
   int32_t master;        /* master row whose list is Member_list (0)        */
   int32_t device;        /* HIP device ordinal                               */
-  int32_t reserved0;
+  int32_t tile_width;    /* HBM layout: members per table tile (32, 64, 128,
+                            256; 0 = default 64), see DESIGN.md             */
   uint64_t seed;         /* Philox key for peers and placement draws         */
   int64_t max_files;     /* file-metadata capacity (0 = no files)            */
   int32_t reserved[8];
@@ -165,11 +166,10 @@ int gh_get_files(void* h, const int32_t* files, int64_t n, int32_t* replicas,
 int gh_delete_files(void* h, const int32_t* files, int64_t n,
                     int32_t* old_replicas);
 
-/* Tuning knob of the fused round kernel (k_round): lanes per row segment
- * (64, 32 or 16 -> 256/128/64-column chunks per workgroup tile) and
- * non-temporal loads/stores on the once-touched streams. Results do not
- * depend on it; the default is the measured fastest. */
-int gh_set_round_variant(void* h, int32_t seg_lanes, int32_t nontemporal);
+/* Tuning knob of the fused round kernel (k_round): non-temporal loads/stores
+ * on the once-touched streams (own ts, new hb). Results do not depend on it;
+ * the default is the measured fastest. */
+int gh_set_round_variant(void* h, int32_t nontemporal);
 
 /* Device timing of the fused round kernel (HIP events on the engine's
  * stream), for bench.py's roofline: enable, then read the sum of kernel

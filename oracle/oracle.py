@@ -29,7 +29,7 @@ class Config(C.Structure):
         ("n_members", C.c_int32), ("fanout", C.c_int32), ("peer_mode", C.c_int32),
         ("detect_mode", C.c_int32), ("t_fail", C.c_int32), ("t_cleanup", C.c_int32),
         ("min_members", C.c_int32), ("replicas", C.c_int32), ("introducer", C.c_int32),
-        ("master", C.c_int32), ("device", C.c_int32), ("reserved0", C.c_int32),
+        ("master", C.c_int32), ("device", C.c_int32), ("tile_width", C.c_int32),
         ("seed", C.c_uint64), ("max_files", C.c_int64), ("reserved", C.c_int32 * 8),
     ]
 

@@ -1,7 +1,9 @@
-// Churn and state-maintenance kernels (SPEC.md §5, §3).
+// Churn and state-maintenance kernels (SPEC.md §5, §3). All tables use the
+// tiled layout of gh_internal.h (gh_cell).
 //   k_count        present count per row (after events / import)
 //   k_flags        recompute the eligibility bit of imported rows
 //   k_fill         synthetic full-membership start (BASELINE configs 2-4)
+//   k_pack/unpack  row-major staging <-> tiled tables (import/export/lsm)
 //   k_leave        LEAVE delivery: slave/slave.go:310-336 -> :232-235
 //   k_join_*       JOIN at the introducer and its full-list broadcast:
 //                  slave/slave.go:224-231, 250-274
@@ -11,15 +13,18 @@
 
 namespace {
 
-// One wave per row: lanes sweep the row 256 columns per step.
+constexpr unsigned kMaxGrid = 65536;
+
+// One wave per row: each lane reads 4 consecutive members (one tile), the
+// wave 256 members per step.
 __global__ __launch_bounds__(256) void k_count(GhDev d, int cur, GhRound p) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= p.n) return;
-  const int32_t* row = d.hb[cur] + (int64_t)i * p.ld;
+  const int32_t* hb = d.hb[cur];
   int cnt = 0;
   for (int64_t c = lane * 4; c < p.ld; c += 256) {
-    const int4 v = *reinterpret_cast<const int4*>(row + c);
+    const int4 v = *reinterpret_cast<const int4*>(hb + gh_cell(d, i, c));
     cnt += (v.x >= 0) + (v.y >= 0) + (v.z >= 0) + (v.w >= 0);
   }
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
@@ -35,33 +40,71 @@ __device__ __forceinline__ int32_t with_flag(int32_t x, int32_t t, int64_t c, in
   return x;
 }
 
+// Storage-order walk over rows [row0, row0+nrows) of every tile.
+struct RowsWalk {
+  int64_t per_tile, total;
+  __device__ RowsWalk(const GhDev& d, int64_t nrows) : per_tile(nrows * d.tw), total(nrows * d.ld) {}
+  // idx -> (row i, member c, tiled offset of cell (i, c))
+  __device__ void at(const GhDev& d, int64_t idx, int64_t row0, int64_t& i, int64_t& c, int64_t& off) const {
+    const int64_t t = idx / per_tile;
+    const int64_t rem = idx - t * per_tile;
+    i = row0 + (rem >> d.lgtw);
+    const int64_t cw = rem & (d.tw - 1);
+    c = (t << d.lgtw) + cw;
+    off = t * d.tstride + (i << d.lgtw) + cw;
+  }
+};
+
 __global__ __launch_bounds__(256) void k_flags(GhDev d, int cur, int64_t row0, int64_t nrows,
                                                GhRound p) {
-  const int64_t total = nrows * p.ld;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+  const RowsWalk w(d, nrows);
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < w.total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = row0 + idx / p.ld;
-    const int64_t c = idx % p.ld;
-    const int64_t off = i * p.ld + c;
+    int64_t i, c, off;
+    w.at(d, idx, row0, i, c, off);
     // p.r is the round about to run: eligible <=> ts < r - T_fail
     d.hb[cur][off] = with_flag(d.hb[cur][off], d.ts[off], c, i, p.r - p.t_fail);
   }
 }
 
-__global__ __launch_bounds__(256) void k_fill(GhDev d, int cur, int32_t hb0, int32_t ts0,
-                                              GhRound p) {
-  const int64_t total = (int64_t)p.n * p.ld;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+__global__ __launch_bounds__(256) void k_fill(GhDev d, int cur, int32_t hb0, int32_t ts0, GhRound p) {
+  const RowsWalk w(d, p.n);
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < w.total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = idx / p.ld;
-    const int64_t c = idx % p.ld;
+    int64_t i, c, off;
+    w.at(d, idx, 0, i, c, off);
     if (c < p.n) {
-      d.hb[cur][idx] = with_flag(hb0, ts0, c, i, p.r - p.t_fail);
-      d.ts[idx] = ts0;
+      d.hb[cur][off] = with_flag(hb0, ts0, c, i, p.r - p.t_fail);
+      d.ts[off] = ts0;
     } else {
-      d.hb[cur][idx] = GH_ABSENT;
-      d.ts[idx] = 0;
+      d.hb[cur][off] = GH_ABSENT;
+      d.ts[off] = 0;
     }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pack(GhDev d, int32_t* dst, const int32_t* src, int64_t row0,
+                                              int64_t nrows) {
+  const RowsWalk w(d, nrows);
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < w.total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t i, c, off;
+    w.at(d, idx, row0, i, c, off);
+    if (c < d.n) dst[off] = src[(i - row0) * d.n + c];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_unpack(GhDev d, int32_t* dst, const int32_t* src, int64_t row0,
+                                                int64_t nrows, int strip) {
+  const RowsWalk w(d, nrows);
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < w.total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t i, c, off;
+    w.at(d, idx, row0, i, c, off);
+    if (c >= d.n) continue;
+    int32_t x = src[off];
+    if (strip && x >= 0) x &= GH_HBMASK;
+    dst[(i - row0) * d.n + c] = x;
   }
 }
 
@@ -75,8 +118,8 @@ __global__ __launch_bounds__(256) void k_leave(GhDev d, int cur, const int32_t* 
     int32_t* hb = d.hb[cur];
     for (int q = 0; q < nl; ++q) {
       const int c = leavers[q];
-      if (c == j || hb[(int64_t)c * p.ld + j] < 0) continue;
-      const int64_t off = (int64_t)j * p.ld + c;
+      if (c == j || hb[gh_cell(d, c, j)] < 0) continue;
+      const int64_t off = gh_cell(d, j, c);
       const int32_t x = hb[off];
       if (x >= 0) {
         hb[off] = GH_TOMBSTONE;
@@ -96,7 +139,7 @@ __global__ __launch_bounds__(256) void k_join_reset(GhDev d, int cur, const int3
   const int64_t total = (int64_t)nr * p.ld;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t off = (int64_t)rows[idx / p.ld] * p.ld + idx % p.ld;
+    const int64_t off = gh_cell(d, rows[idx / p.ld], idx % p.ld);
     d.hb[cur][off] = GH_ABSENT;
     d.ts[off] = 0;
   }
@@ -108,7 +151,7 @@ __global__ void k_join_add(GhDev d, int cur, const int32_t* joiners, int32_t nj,
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   int added = 0;
   for (int q = 0; q < nj; ++q) {
-    const int64_t off = (int64_t)I * p.ld + joiners[q];
+    const int64_t off = gh_cell(d, I, joiners[q]);
     if (d.hb[cur][off] < 0) {
       d.hb[cur][off] = 0;
       d.ts[off] = p.r;
@@ -119,21 +162,20 @@ __global__ void k_join_add(GhDev d, int cur, const int32_t* joiners, int32_t nj,
 }
 
 // The introducer's full list to every alive member of it (:256-272), merged
-// with MergeMemberList's rule at now = r. Grid: rows x 256-column chunks.
+// with MergeMemberList's rule at now = r.
 __global__ __launch_bounds__(256) void k_join_bcast(GhDev d, int cur, int32_t I, GhRound p) {
   if (d.nd[4] == 0) return;
-  const int64_t nchunks = p.ld / GH_CHUNK;
   int32_t* hb = d.hb[cur];
-  const int32_t* rowI = hb + (int64_t)I * p.ld;
+  const RowsWalk w(d, p.n);
   int merged = 0;
-  for (int64_t tile = blockIdx.x; tile < (int64_t)p.n * nchunks; tile += gridDim.x) {
-    const int64_t j = tile / nchunks;
-    const int64_t c = (tile % nchunks) * GH_CHUNK + threadIdx.x;
-    if (!(d.alive[j] && rowI[j] >= 0 && j != I)) continue;
-    const int32_t mv = rowI[c];
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < w.total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    int64_t j, c, off;
+    w.at(d, idx, 0, j, c, off);
+    if (c >= p.n || j == I || !d.alive[j] || hb[gh_cell(d, I, j)] < 0) continue;
+    const int32_t mv = hb[gh_cell(d, I, c)];
     if (mv < 0) continue;
     const int32_t m = mv & GH_HBMASK;
-    const int64_t off = j * p.ld + c;
     const int32_t xr = hb[off];
     const int32_t x = xr >= 0 ? (xr & GH_HBMASK) : xr;
     if (x >= GH_ABSENT && m > x) {
@@ -145,6 +187,10 @@ __global__ __launch_bounds__(256) void k_join_bcast(GhDev d, int cur, int32_t I,
   if (merged) atomicAdd(&d.stats[ST_MERGED], (unsigned long long)merged);
 }
 
+unsigned grid_for(int64_t work) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, kMaxGrid));
+}
+
 }  // namespace
 
 void launch_count(const GhDev& d, int cur, const GhRound& p, hipStream_t s) {
@@ -153,17 +199,26 @@ void launch_count(const GhDev& d, int cur, const GhRound& p, hipStream_t s) {
 
 void launch_flags(const GhDev& d, int cur, int64_t row0, int64_t nrows, const GhRound& p,
                   hipStream_t s) {
-  const int64_t cells = nrows * p.ld;
-  if (cells == 0) return;
-  hipLaunchKernelGGL(k_flags, dim3((unsigned)std::min<int64_t>((cells + 255) / 256, 65536)), dim3(256), 0, s, d, cur, row0,
-                     nrows, p);
+  if (nrows == 0) return;
+  hipLaunchKernelGGL(k_flags, dim3(grid_for(nrows * p.ld)), dim3(256), 0, s, d, cur, row0, nrows, p);
 }
 
-void launch_fill(const GhDev& d, int cur, int32_t hb0, int32_t ts0, const GhRound& p,
+void launch_fill(const GhDev& d, int cur, int32_t hb0, int32_t ts0, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill, dim3(grid_for((int64_t)p.n * p.ld)), dim3(256), 0, s, d, cur, hb0, ts0, p);
+}
+
+void launch_pack(const GhDev& d, int32_t* dst_tiled, const int32_t* src_rows, int64_t row0, int64_t nrows,
                  hipStream_t s) {
-  const int64_t cells = (int64_t)p.n * p.ld;
-  hipLaunchKernelGGL(k_fill, dim3((unsigned)std::min<int64_t>((cells + 255) / 256, 65536)), dim3(256), 0, s, d, cur, hb0,
-                     ts0, p);
+  if (nrows == 0) return;
+  hipLaunchKernelGGL(k_pack, dim3(grid_for(nrows * d.ld)), dim3(256), 0, s, d, dst_tiled, src_rows, row0,
+                     nrows);
+}
+
+void launch_unpack(const GhDev& d, int32_t* dst_rows, const int32_t* src_tiled, int64_t row0, int64_t nrows,
+                   int strip_flag, hipStream_t s) {
+  if (nrows == 0) return;
+  hipLaunchKernelGGL(k_unpack, dim3(grid_for(nrows * d.ld)), dim3(256), 0, s, d, dst_rows, src_tiled, row0,
+                     nrows, strip_flag);
 }
 
 void launch_leave(const GhDev& d, int cur, const int32_t* leavers, int32_t nl, const GhRound& p,
@@ -174,15 +229,12 @@ void launch_leave(const GhDev& d, int cur, const int32_t* leavers, int32_t nl, c
 void launch_join(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, int32_t introducer,
                  const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_join_add, dim3(1), dim3(64), 0, s, d, cur, joiners, nj, introducer, p);
-  const int64_t nchunks = p.ld / GH_CHUNK;
-  hipLaunchKernelGGL(k_join_bcast, dim3((unsigned)std::min<int64_t>(p.n * nchunks, 65536)), dim3(256), 0, s, d, cur,
-                     introducer, p);
+  hipLaunchKernelGGL(k_join_bcast, dim3(grid_for((int64_t)p.n * p.ld)), dim3(256), 0, s, d, cur, introducer,
+                     p);
 }
 
 void launch_join_reset(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p,
                        hipStream_t s) {
-  const int64_t cells = (int64_t)nr * p.ld;
-  if (cells == 0) return;
-  hipLaunchKernelGGL(k_join_reset, dim3((unsigned)std::min<int64_t>((cells + 255) / 256, 65536)), dim3(256), 0, s, d, cur,
-                     rows, nr, p);
+  if (nr == 0) return;
+  hipLaunchKernelGGL(k_join_reset, dim3(grid_for((int64_t)nr * p.ld)), dim3(256), 0, s, d, cur, rows, nr, p);
 }

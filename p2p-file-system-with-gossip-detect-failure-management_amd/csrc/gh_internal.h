@@ -1,27 +1,34 @@
 // Internal definitions shared by libgossiphip's HIP translation units.
+//
 // Device layout (SPEC.md §1/§3, DESIGN.md "Data layout in HBM"):
-//   hb[2][N][ld] int32   double-buffered heartbeat table (row = observer),
-//                        bit 30 of a present cell = next-round detection
-//                        eligibility; -1 absent, -2 tombstone; ld = N rounded
-//                        up to 256 columns (padding cells stay -1).
-//   ts[N][ld]    int32   local-clock tick of each cell, updated in place.
+//   The N x N membership tables are stored in column TILES of TW members:
+//     cell(i, c) = (c / TW) * (N * TW) + i * TW + c % TW
+//   i.e. tile t holds members [t*TW, (t+1)*TW) of every observer row, rows
+//   contiguous. One tile of one table is N*TW*4 bytes (16 MiB at N=65,536,
+//   TW=64): the round kernel sweeps tile by tile, so its own-row streams are
+//   sequential and every peer gather of a tile stays inside that slice.
+//   hb[2]  int32   double-buffered heartbeat table; bit 30 of a present cell =
+//                  next-round detection eligibility; -1 absent, -2 tombstone.
+//   ts     int32   local-clock tick of each cell, updated in place.
+//   Columns are padded to ld = N rounded up to 256 (padding cells stay -1).
 //   per row: alive, active (u8), cnt (present count), det_any (u8),
 //            inbox_beg / inbox_cnt (int32), inbox[] (sender rows).
 //   per column: det_cnt / det_min (x2: pending D_{r-1} and current D_r),
 //            dbits (bitmap of pending D_{r-1}).
-//   part[ld/256][N] uint16  per-(chunk,row) present counts of the last pass.
+//   part[ld/TW][N] uint16  per-(tile,row) present counts of the last pass.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/gossiphip.h"
 
-#define GH_FLAG (1 << 30)       // eligibility bit inside a present hb cell
+#define GH_FLAG (1 << 30)        // eligibility bit inside a present hb cell
 #define GH_HBMASK (GH_FLAG - 1)  // heartbeat value bits
-#define GH_CHUNK 256             // columns per wave row-segment (64 lanes x int4)
+#define GH_PAD 256               // column padding granule (ld % 256 == 0)
 #define GH_RB 64                 // rows per workgroup tile in the round kernel
 #define GH_MAXK 8                // max pull fanout
 #define GH_DLIST_MAX 1024        // |D| above which k_active_exact recounts whole rows
+#define GH_TW_DEFAULT 64         // default tile width (members per tile)
 #define GH_TAG_PEER 0x50454552u
 #define GH_TAG_PLACE 0x504C4143u
 #define GH_MAX_DRAWS (1u << 20)
@@ -63,8 +70,11 @@ __host__ __device__ inline uint32_t gh_philox_word(uint64_t seed, uint32_t a, ui
 }
 
 struct GhDev {
-  int32_t n;        // members
-  int64_t ld;       // row pitch in cells
+  int32_t n;        // members (= observer rows)
+  int64_t ld;       // padded columns (multiple of GH_PAD)
+  int32_t tw;       // tile width (power of two, divides GH_PAD)
+  int32_t lgtw;     // log2(tw)
+  int64_t tstride;  // cells per tile = n * tw
   int32_t *hb[2];   // double buffer
   int32_t *ts;
   uint8_t *alive, *active, *det_any;
@@ -87,6 +97,11 @@ struct GhDev {
   int64_t io_cap;
 };
 
+// Linear index of cell (observer i, member c) in the tiled layout.
+__host__ __device__ __forceinline__ int64_t gh_cell(const GhDev& d, int64_t i, int64_t c) {
+  return (c >> d.lgtw) * d.tstride + (i << d.lgtw) + (c & (d.tw - 1));
+}
+
 // Parameters of one round, passed by value to the kernels.
 struct GhRound {
   int32_t r;          // now
@@ -99,22 +114,25 @@ struct GhRound {
   int32_t ablate;     // timing-only experiments (results wrong): 1 = every
                       // peer load reads the own row, 2 = no peer loads. 0 always
                       // in production (set only through GH_ROUND_ABLATE).
-  int32_t order;      // k_round tile order: 0 chunk-major (default), 1 row-major
 };
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------
 void launch_active(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_ring(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
-// seg = lanes per row segment (64, 32, 16 -> 256/128/64-column chunks), nt =
-// non-temporal streams; launch_finish must get the seg its round used.
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, int seg, bool nt);
-void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s, int seg);
+// nt = non-temporal hints on the once-touched streams of k_round
+void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt);
+void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);
 void launch_count(const GhDev& d, int cur, const GhRound& p, hipStream_t s);
 void launch_flags(const GhDev& d, int cur, int64_t row0, int64_t nrows, const GhRound& p,
                   hipStream_t s);
 void launch_fill(const GhDev& d, int cur, int32_t hb0, int32_t ts0, const GhRound& p,
                  hipStream_t s);
+// row-major staging [nrows][n] <-> tiled tables (import/export/lsm)
+void launch_pack(const GhDev& d, int32_t* dst_tiled, const int32_t* src_rows, int64_t row0,
+                 int64_t nrows, hipStream_t s);
+void launch_unpack(const GhDev& d, int32_t* dst_rows, const int32_t* src_tiled, int64_t row0,
+                   int64_t nrows, int strip_flag, hipStream_t s);
 void launch_leave(const GhDev& d, int cur, const int32_t* leavers, int32_t nl, const GhRound& p,
                   hipStream_t s);
 void launch_join(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, int32_t introducer,
@@ -122,10 +140,9 @@ void launch_join(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, in
 void launch_join_reset(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p,
                        hipStream_t s);
 void launch_candidates(const GhDev& d, int cur, int32_t master, const GhRound& p, hipStream_t s);
-// mrow = the master's row of the current hb buffer, nm = N.
-void launch_put(const GhDev& d, int64_t n, int32_t R, int32_t now, uint64_t seed, hipStream_t s,
-                const int32_t* mrow, int32_t nm);
-// orow = the observer's row (available set).
-void launch_repair(const GhDev& d, const int32_t* orow, int32_t R, uint64_t seed, hipStream_t s,
-                   const int32_t* mrow, int32_t nm);
+// placement reads the master's (and the observer's) row of the current hb
+void launch_put(const GhDev& d, const int32_t* hb, int32_t master, int64_t n, int32_t R, int32_t now,
+                uint64_t seed, hipStream_t s);
+void launch_repair(const GhDev& d, const int32_t* hb, int32_t master, int32_t observer, int32_t R,
+                   uint64_t seed, hipStream_t s);
 void launch_get(const GhDev& d, int64_t n, int32_t R, int del, hipStream_t s);

@@ -34,10 +34,8 @@ struct Engine {
   std::vector<uint8_t> alive;   // host mirror (source of truth for events)
   std::vector<gh_event> pending;
   int32_t* ev_buf = nullptr;    // device scratch for event member lists
-  int seg = 64;          // k_round lanes per row segment (tuning, gh_set_round_variant)
-  bool nt = false;       // k_round non-temporal streams
+  bool nt = true;        // k_round non-temporal streams (gh_set_round_variant)
   int ablate = 0;        // timing-only experiment switch (GH_ROUND_ABLATE), never set in production
-  int order = 0;         // k_round tile order (GH_ROUND_ORDER): 0 chunk-major, 1 row-major
   bool timing = false;
   double timed_ms = 0.0;
   int64_t timed_launches = 0;
@@ -72,6 +70,22 @@ int dalloc(Engine* e, T** p, size_t count, int fill_byte) {
   return GH_OK;
 }
 
+// Row-major device staging for import/export/lsm (the tables are tiled).
+struct Staging {
+  int32_t* p = nullptr;
+  int alloc(Engine* e, int64_t rows) {
+    if (hipMalloc(&p, std::max<size_t>(sizeof(int32_t) * e->n * rows, 16)) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+      return set_err(e, GH_ENOMEM, "staging allocation failed");
+    }
+    return GH_OK;
+  }
+  ~Staging() {
+    if (p) (void)hipFree(p);
+  }
+};
+
 GhRound round_params(const Engine* e, int32_t r) {
   GhRound p{};
   p.r = r;
@@ -84,7 +98,6 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.seed = e->cfg.seed;
   p.peer_mode = e->cfg.peer_mode;
   p.ablate = e->ablate;
-  p.order = e->order;
   return p;
 }
 
@@ -250,13 +263,16 @@ int gh_create(const gh_config* cfg, void** handle) {
   Engine* e = new Engine();
   e->cfg = *cfg;
   e->n = cfg->n_members;
-  e->ld = ((int64_t)e->n + GH_CHUNK - 1) / GH_CHUNK * GH_CHUNK;
+  e->ld = ((int64_t)e->n + GH_PAD - 1) / GH_PAD * GH_PAD;
   e->alive.assign(e->n, 0);
-  if (const char* v = std::getenv("GH_ROUND_SEG")) e->seg = std::atoi(v);
+  int tw = cfg->tile_width ? cfg->tile_width : GH_TW_DEFAULT;
+  if (const char* v = std::getenv("GH_TILE_W")) tw = std::atoi(v);
   if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_ROUND_ABLATE")) e->ablate = std::atoi(v);
-  if (const char* v = std::getenv("GH_ROUND_ORDER")) e->order = std::atoi(v) != 0;
-  if (e->seg != 64 && e->seg != 32 && e->seg != 16) e->seg = 64;
+  if (tw != 32 && tw != 64 && tw != 128 && tw != 256) {
+    delete e;
+    return GH_EINVAL;
+  }
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return GH_EHIP;
@@ -264,8 +280,12 @@ int gh_create(const gh_config* cfg, void** handle) {
   GhDev& d = e->d;
   d.n = e->n;
   d.ld = e->ld;
+  d.tw = tw;
+  d.lgtw = __builtin_ctz((unsigned)tw);
+  d.tstride = (int64_t)e->n * tw;
+  e->cfg.tile_width = tw;
   const int64_t cells = (int64_t)e->n * e->ld;
-  const int64_t nch = e->ld / 64;  // partial-count chunks at the narrowest variant (seg 16)
+  const int64_t nch = e->ld / tw;  // partial counts: one per (tile, row)
   const int64_t inbox = (int64_t)e->n * std::max(cfg->fanout, 3);
   int rc = GH_OK;
   do {
@@ -323,15 +343,20 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
   for (int64_t x = 0; x < n_rows * e->n; ++x)
     if (hb[x] < GH_TOMBSTONE || hb[x] >= GH_FLAG) return set_err(e, GH_ERANGE, "hb value out of range");
   HIPCHK(e, hipSetDevice(e->cfg.device));
-  const size_t w = sizeof(int32_t) * e->n, dp = sizeof(int32_t) * e->ld;
+  int rc;
   if (n_rows > 0) {
-    HIPCHK(e, hipMemcpy2DAsync(e->d.hb[e->cur] + row0 * e->ld, dp, hb, w, w, n_rows,
-                               hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpy2DAsync(e->d.ts + row0 * e->ld, dp, ts, w, w, n_rows, hipMemcpyHostToDevice,
-                               e->stream));
+    // row-major host rows -> device staging -> tiled tables
+    Staging st;
+    if ((rc = st.alloc(e, n_rows))) return rc;
+    const size_t bytes = sizeof(int32_t) * e->n * n_rows;
+    HIPCHK(e, hipMemcpyAsync(st.p, hb, bytes, hipMemcpyHostToDevice, e->stream));
+    launch_pack(e->d, e->d.hb[e->cur], st.p, row0, n_rows, e->stream);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipMemcpyAsync(st.p, ts, bytes, hipMemcpyHostToDevice, e->stream));
+    launch_pack(e->d, e->d.ts, st.p, row0, n_rows, e->stream);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
     std::copy(alive, alive + n_rows, e->alive.begin() + row0);
   }
-  int rc;
   if ((rc = upload_alive(e))) return rc;
   e->round = round;
   e->pending.clear();
@@ -349,19 +374,22 @@ int gh_export_state(void* h, int32_t* hb, int32_t* ts, uint8_t* alive, int64_t r
   if (!e) return GH_EINVAL;
   if (row0 < 0 || n_rows < 0 || row0 + n_rows > e->n) return set_err(e, GH_EINVAL, "row range");
   HIPCHK(e, hipSetDevice(e->cfg.device));
-  const size_t w = sizeof(int32_t) * e->n, dp = sizeof(int32_t) * e->ld;
-  if (hb && n_rows > 0) {
-    HIPCHK(e, hipMemcpy2DAsync(hb, w, e->d.hb[e->cur] + row0 * e->ld, dp, w, n_rows,
-                               hipMemcpyDeviceToHost, e->stream));
+  if (n_rows > 0 && (hb || ts)) {
+    int rc;
+    Staging st;
+    if ((rc = st.alloc(e, n_rows))) return rc;
+    const size_t bytes = sizeof(int32_t) * e->n * n_rows;
+    if (hb) {  // tiled -> row-major staging, eligibility bit stripped
+      launch_unpack(e->d, st.p, e->d.hb[e->cur], row0, n_rows, 1, e->stream);
+      HIPCHK(e, hipMemcpyAsync(hb, st.p, bytes, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+    }
+    if (ts) {
+      launch_unpack(e->d, st.p, e->d.ts, row0, n_rows, 0, e->stream);
+      HIPCHK(e, hipMemcpyAsync(ts, st.p, bytes, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+    }
   }
-  if (ts && n_rows > 0) {
-    HIPCHK(e, hipMemcpy2DAsync(ts, w, e->d.ts + row0 * e->ld, dp, w, n_rows, hipMemcpyDeviceToHost,
-                               e->stream));
-  }
-  HIPCHK(e, hipStreamSynchronize(e->stream));
-  if (hb)
-    for (int64_t x = 0; x < n_rows * e->n; ++x)
-      if (hb[x] >= 0) hb[x] &= GH_HBMASK;  // strip the eligibility bit
   if (alive) std::copy(e->alive.begin() + row0, e->alive.begin() + row0 + n_rows, alive);
   return GH_OK;
 }
@@ -420,9 +448,9 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     else
       launch_ring(e->d, e->cur, e->dcur, p, e->stream);
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q], e->stream));
-    launch_round(e->d, e->cur, e->dcur, p, e->stream, e->seg, e->nt);
+    launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt);
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q + 1], e->stream));
-    launch_finish(e->d, e->dcur, p, e->stream, e->seg);
+    launch_finish(e->d, e->dcur, p, e->stream);
     HIPCHK(e, hipGetLastError());
     e->cur ^= 1;
     e->dcur ^= 1;
@@ -490,17 +518,14 @@ int gh_lsm(void* h, int32_t observer, int32_t* ids, int32_t* hb, int32_t* ts, in
   if (observer < 0 || observer >= e->n) return set_err(e, GH_EINVAL, "observer");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   std::vector<int32_t> rh(e->n), rt(e->n);
-  HIPCHK(e, hipMemcpyAsync(rh.data(), e->d.hb[e->cur] + (int64_t)observer * e->ld, sizeof(int32_t) * e->n,
-                           hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipMemcpyAsync(rt.data(), e->d.ts + (int64_t)observer * e->ld, sizeof(int32_t) * e->n,
-                           hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipStreamSynchronize(e->stream));
+  int rc = gh_export_state(h, rh.data(), rt.data(), nullptr, observer, 1);
+  if (rc != GH_OK) return rc;
   int64_t k = 0;
   for (int32_t c = 0; c < e->n; ++c)
     if (rh[c] >= 0) {
       if (k < cap) {
         if (ids) ids[k] = c;
-        if (hb) hb[k] = rh[c] & GH_HBMASK;
+        if (hb) hb[k] = rh[c];
         if (ts) ts[k] = rt[c];
       }
       k++;
@@ -521,8 +546,7 @@ int gh_put(void* h, const int32_t* files, int64_t n, int32_t* replicas, int32_t*
   HIPCHK(e, hipMemcpyAsync(e->d.io_a, files, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
   const GhRound p = round_params(e, e->round);
   launch_candidates(e->d, e->cur, e->cfg.master, p, e->stream);
-  launch_put(e->d, n, R, e->round, e->cfg.seed, e->stream, e->d.hb[e->cur] + (int64_t)e->cfg.master * e->ld,
-             e->n);
+  launch_put(e->d, e->d.hb[e->cur], e->cfg.master, n, R, e->round, e->cfg.seed, e->stream);
   HIPCHK(e, hipGetLastError());
   std::vector<int32_t> rep(n * R), ver(n), st(n);
   HIPCHK(e, hipMemcpyAsync(rep.data(), e->d.io_b, sizeof(int32_t) * n * R, hipMemcpyDeviceToHost, e->stream));
@@ -546,8 +570,7 @@ int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap, int64
   HIPCHK(e, hipMemsetAsync(e->d.nplan, 0, sizeof(int32_t), e->stream));
   const GhRound p = round_params(e, e->round);
   launch_candidates(e->d, e->cur, e->cfg.master, p, e->stream);
-  launch_repair(e->d, e->d.hb[e->cur] + (int64_t)observer * e->ld, e->cfg.replicas, e->cfg.seed, e->stream,
-                e->d.hb[e->cur] + (int64_t)e->cfg.master * e->ld, e->n);
+  launch_repair(e->d, e->d.hb[e->cur], e->cfg.master, observer, e->cfg.replicas, e->cfg.seed, e->stream);
   HIPCHK(e, hipGetLastError());
   int32_t np = 0;
   HIPCHK(e, hipMemcpyAsync(&np, e->d.nplan, sizeof np, hipMemcpyDeviceToHost, e->stream));
@@ -601,11 +624,9 @@ int gh_delete_files(void* h, const int32_t* files, int64_t n, int32_t* old_repli
   return get_or_delete(e, files, n, old_replicas, nullptr, 1);
 }
 
-int gh_set_round_variant(void* h, int32_t seg_lanes, int32_t nontemporal) {
+int gh_set_round_variant(void* h, int32_t nontemporal) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
-  if (seg_lanes != 64 && seg_lanes != 32 && seg_lanes != 16) return set_err(e, GH_EINVAL, "seg_lanes");
-  e->seg = seg_lanes;
   e->nt = nontemporal != 0;
   return GH_OK;
 }

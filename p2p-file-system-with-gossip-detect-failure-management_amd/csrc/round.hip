@@ -9,7 +9,7 @@
 //   k_round        THE HOT KERNEL: one pass over the table applying REMOVE
 //                  delivery, guard, own heartbeat, detection, cleanup and the
 //                  k-peer max-merge (slave/slave.go:276-286,414-497) for a
-//                  64-row x 256-column tile per workgroup.
+//                  64-row x TW-member tile per workgroup.
 //   k_finish       per row/column: reduce the pass's partial counts, build
 //                  the failed-set bitmap D_r for the next round.
 #include <limits.h>
@@ -48,13 +48,13 @@ __global__ __launch_bounds__(256) void k_active(GhDev d, int cur, int dcur, GhRo
         a = false;          // decided by k_active_exact's full-row recount
         d.cnt[i] = -1;      // marks the row uncertain for it
       } else {
-        const int32_t* row = d.hb[cur] + (int64_t)i * p.ld;
+        const int32_t* hb = d.hb[cur];
         const int32_t* dc = d.det_cnt[dcur];
         const int32_t* dm = d.det_min[dcur];
         int rem = 0;
         for (int q = 0; q < nd; ++q) {
           const int col = d.dlist[(int64_t)dcur * p.ld + q];
-          rem += (row[col] >= 0) && removes_at(dc[col], dm[col], i);
+          rem += (hb[gh_cell(d, i, col)] >= 0) && removes_at(dc[col], dm[col], i);
         }
         a = (c - rem) >= p.min_members;
       }
@@ -72,12 +72,12 @@ __global__ __launch_bounds__(256) void k_active_exact(GhDev d, int cur, int dcur
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= p.n || d.cnt[i] != -1) return;
-  const int32_t* row = d.hb[cur] + (int64_t)i * p.ld;
+  const int32_t* hb = d.hb[cur];
   const int32_t* dc = d.det_cnt[dcur];
   const int32_t* dm = d.det_min[dcur];
   int cnt = 0;
   for (int64_t c = lane * 4; c < p.ld; c += 256) {
-    const int4 v = *reinterpret_cast<const int4*>(row + c);
+    const int4 v = *reinterpret_cast<const int4*>(hb + gh_cell(d, i, c));
     const uint32_t b4 = (d.dbits[c >> 5] >> (c & 31)) & 0xFu;
     const int x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -107,7 +107,7 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
       const uint32_t q = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
       const int s = (int)q + ((int)q >= i);
       if (!d.alive[s] || !d.active[s]) continue;
-      const int32_t v = d.hb[cur][(int64_t)s * p.ld + i];
+      const int32_t v = d.hb[cur][gh_cell(d, s, i)];
       // i must be in s's snapshot list: present, not detected by s this
       // round (eligibility flag) and not REMOVE'd at s in step 1.
       if (v < 0 || (v & GH_FLAG)) continue;
@@ -130,11 +130,11 @@ __global__ __launch_bounds__(256) void k_ring_targets(GhDev d, int cur, int dcur
     if (tid < 3) d.targets[(int64_t)sdr * 3 + tid] = -1;
     return;
   }
-  const int32_t* row = d.hb[cur] + (int64_t)sdr * p.ld;
+  const int32_t* hb = d.hb[cur];
   const int per = (p.n + 255) / 256;
   const int b = tid * per, e = min(p.n, b + per);
   auto present = [&](int c) -> bool {
-    const int32_t v = row[c];
+    const int32_t v = hb[gh_cell(d, sdr, c)];
     if (v < 0) return false;
     if ((v & GH_FLAG) && c != sdr) return false;  // detected by the sender this round
     if (dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], sdr)) return false;
@@ -253,42 +253,37 @@ __device__ __forceinline__ void stv(int32_t* p, v4i v) {
     *reinterpret_cast<v4i*>(p) = v;
 }
 
-// The fused round. Tile = GH_RB rows x CW columns, CW = 4*SEG; block index is
-// chunk-major so the concurrently running tiles share one CW-column slice of
-// the table and peer-row segments can be re-read from the on-die caches.
-// Each lane owns 4 consecutive columns (16-B loads/stores); SEG lanes cover
-// one row segment, so a wave handles 64/SEG rows per instruction.
-// KB = peer loads issued together (4 or 8). NT = non-temporal hints on the
-// once-touched streams (own ts in/out, new hb out), leaving the cache to the
-// re-read old-hb slice.
-template <int KB, int SEG, bool NT>
+// The fused round. Workgroup tile = GH_RB rows x TW members of one table
+// tile; the block index is tile-major so the concurrently running workgroups
+// sweep one tile (a contiguous N*TW*4-byte slice of each table) together:
+// own-row streams are sequential and peer gathers stay in that slice, which
+// the on-die caches hold. Each lane owns 4 consecutive members (16-B
+// loads/stores); SEG = TW/4 lanes cover one row segment, so a wave handles
+// 64/SEG rows per instruction. KB = peer loads issued together (4 or 8).
+// NT = non-temporal hints on the once-touched streams (own ts in/out, new hb
+// out), leaving the caches to the re-read old-hb slice.
+template <int KB, int TW, bool NT>
 __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRound p) {
-  constexpr int CW = SEG * 4;
+  constexpr int SEG = TW / 4;
   constexpr int RPW = 64 / SEG;
   constexpr int RSTEP = 4 * RPW;
-  __shared__ int s_dcnt[CW];
-  __shared__ int s_dmin[CW];
+  __shared__ int s_dcnt[TW];
+  __shared__ int s_dmin[TW];
   __shared__ uint16_t s_part[GH_RB];
   __shared__ unsigned long long s_st[ST_COUNT];
 
   const int nrb = (p.n + GH_RB - 1) / GH_RB;
-  int chunk, rb;
-  if (p.order == 0) {
-    chunk = blockIdx.x / nrb;
-    rb = blockIdx.x - chunk * nrb;
-  } else {
-    const int nch = (int)(p.ld / CW);
-    rb = blockIdx.x / nch;
-    chunk = blockIdx.x - rb * nch;
-  }
+  const int tile = blockIdx.x / nrb;
+  const int rb = blockIdx.x - tile * nrb;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = uni(tid >> 6);
   const int sub = lane / SEG;
   const int lc = lane % SEG;
-  const int64_t c0 = (int64_t)chunk * CW + lc * 4;
+  const int64_t c0 = (int64_t)tile * TW + lc * 4;              // member of this lane's first cell
+  const int64_t tb = (int64_t)tile * ((int64_t)p.n * TW) + lc * 4;  // tile base + lane offset
 
-  for (int t = tid; t < CW; t += 256) {
+  for (int t = tid; t < TW; t += 256) {
     s_dcnt[t] = 0;
     s_dmin[t] = INT_MAX;
   }
@@ -304,7 +299,7 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   const int32_t lim_clean = r - p.t_cleanup;
   const int32_t lim_next = r + 1 - p.t_fail;
 
-  // REMOVE bits of this lane's 4 columns (rare: slow path only when set)
+  // REMOVE bits of this lane's 4 members (rare: slow path only when set)
   const uint32_t my4 = (d.dbits[c0 >> 5] >> (c0 & 31)) & 0xFu;
   int dc[4] = {0, 0, 0, 0}, dm[4] = {0, 0, 0, 0};
   if (my4) {
@@ -322,8 +317,8 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     const int i_raw = rb * GH_RB + rr;
     const bool valid = i_raw < p.n;
     if (!__any(valid)) break;
-    const int i = valid ? i_raw : p.n - 1;  // in-range row for the loads of idle halves
-    const int64_t off = (int64_t)i * p.ld + c0;
+    const int i = valid ? i_raw : p.n - 1;  // in-range row for the loads of idle lanes
+    const int64_t off = tb + (int64_t)i * TW;
     int al, ac, beg, cntv;
     if constexpr (RPW == 1) {
       al = uni(d.alive[i]);
@@ -360,7 +355,7 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
             s = d.inbox[beg + base + q];
         }
         ps[q] = s;
-        pv[q] = ldv<false>(hbo + (int64_t)(p.ablate == 1 ? i : s) * p.ld + c0);
+        pv[q] = ldv<false>(hbo + tb + (int64_t)(p.ablate == 1 ? i : s) * TW);
       }
 #pragma unroll
       for (int q = 0; q < KB; ++q) {
@@ -452,10 +447,10 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   __syncthreads();
 
   const int row0 = rb * GH_RB;
-  if (tid < GH_RB && row0 + tid < p.n) d.part[(int64_t)chunk * p.n + row0 + tid] = s_part[tid];
-  for (int t = tid; t < CW; t += 256) {
+  if (tid < GH_RB && row0 + tid < p.n) d.part[(int64_t)tile * p.n + row0 + tid] = s_part[tid];
+  for (int t = tid; t < TW; t += 256) {
     if (s_dcnt[t]) {
-      const int64_t c = (int64_t)chunk * CW + t;
+      const int64_t c = (int64_t)tile * TW + t;
       atomicAdd(&d.det_cnt[dcur ^ 1][c], s_dcnt[t]);
       atomicMin(&d.det_min[dcur ^ 1][c], s_dmin[t]);
     }
@@ -468,9 +463,16 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
 __global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p, int nchunks) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (x < p.n) {
-    int sum = 0;
-    for (int ch = 0; ch < nchunks; ++ch) sum += d.part[(int64_t)ch * p.n + x];
-    d.cnt[x] = sum;
+    int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    int ch = 0;
+    for (; ch + 4 <= nchunks; ch += 4) {
+      s0 += d.part[(int64_t)ch * p.n + x];
+      s1 += d.part[(int64_t)(ch + 1) * p.n + x];
+      s2 += d.part[(int64_t)(ch + 2) * p.n + x];
+      s3 += d.part[(int64_t)(ch + 3) * p.n + x];
+    }
+    for (; ch < nchunks; ++ch) s0 += d.part[(int64_t)ch * p.n + x];
+    d.cnt[x] = s0 + s1 + s2 + s3;
   }
   const int dnew = dcur ^ 1;
   bool has = false;
@@ -516,36 +518,36 @@ void launch_ring(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_
   hipLaunchKernelGGL(k_inbox_fill, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
 }
 
-template <int KB>
-static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, int seg,
-                            bool nt) {
+template <int KB, int TW>
+static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
   const int nrb = (p.n + GH_RB - 1) / GH_RB;
-  const int64_t nchunks = p.ld / (seg * 4);
-  const dim3 grid((unsigned)(nrb * nchunks)), blk(256);
-#define GH_ROUND_CASE(SEG_)                                                              \
-  if (seg == SEG_) {                                                                     \
-    if (nt)                                                                              \
-      hipLaunchKernelGGL((k_round<KB, SEG_, true>), grid, blk, 0, s, d, cur, dcur, p);  \
-    else                                                                                 \
-      hipLaunchKernelGGL((k_round<KB, SEG_, false>), grid, blk, 0, s, d, cur, dcur, p); \
-    return;                                                                              \
-  }
-  GH_ROUND_CASE(64)
-  GH_ROUND_CASE(32)
-  GH_ROUND_CASE(16)
-#undef GH_ROUND_CASE
-}
-
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, int seg, bool nt) {
-  if (p.peer_mode == GH_PEER_PULL && p.k <= 4)
-    launch_round_kb<4>(d, cur, dcur, p, s, seg, nt);
+  const dim3 grid((unsigned)(nrb * (p.ld / TW))), blk(256);
+  if (nt)
+    hipLaunchKernelGGL((k_round<KB, TW, true>), grid, blk, 0, s, d, cur, dcur, p);
   else
-    launch_round_kb<8>(d, cur, dcur, p, s, seg, nt);
+    hipLaunchKernelGGL((k_round<KB, TW, false>), grid, blk, 0, s, d, cur, dcur, p);
 }
 
-void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s, int seg) {
+template <int KB>
+static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
+  switch (d.tw) {
+    case 32: launch_round_tw<KB, 32>(d, cur, dcur, p, s, nt); break;
+    case 128: launch_round_tw<KB, 128>(d, cur, dcur, p, s, nt); break;
+    case 256: launch_round_tw<KB, 256>(d, cur, dcur, p, s, nt); break;
+    default: launch_round_tw<KB, 64>(d, cur, dcur, p, s, nt); break;
+  }
+}
+
+void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
+  if (p.peer_mode == GH_PEER_PULL && p.k <= 4)
+    launch_round_kb<4>(d, cur, dcur, p, s, nt);
+  else
+    launch_round_kb<8>(d, cur, dcur, p, s, nt);
+}
+
+void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s) {
   const int64_t span = p.ld > p.n ? p.ld : p.n;
-  const int nchunks = (int)(p.ld / (seg * 4));
+  const int nchunks = (int)(p.ld / d.tw);
   hipLaunchKernelGGL(k_finish, dim3((unsigned)((span + 255) / 256)), dim3(256), 0, s, d, dcur, p,
                      nchunks);
 }

@@ -164,8 +164,8 @@ class Engine:
         return rep
 
     # ---- tuning / timing -------------------------------------------------
-    def set_round_variant(self, seg_lanes=64, nontemporal=False):
-        self._chk(self.lib.gh_set_round_variant(self.h, seg_lanes, int(nontemporal)))
+    def set_round_variant(self, nontemporal=True):
+        self._chk(self.lib.gh_set_round_variant(self.h, int(nontemporal)))
 
     def set_timing(self, enable=True):
         self._chk(self.lib.gh_set_timing(self.h, int(enable)))

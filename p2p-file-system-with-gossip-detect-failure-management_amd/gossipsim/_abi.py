@@ -34,7 +34,7 @@ class Config(C.Structure):
         ("n_members", C.c_int32), ("fanout", C.c_int32), ("peer_mode", C.c_int32),
         ("detect_mode", C.c_int32), ("t_fail", C.c_int32), ("t_cleanup", C.c_int32),
         ("min_members", C.c_int32), ("replicas", C.c_int32), ("introducer", C.c_int32),
-        ("master", C.c_int32), ("device", C.c_int32), ("reserved0", C.c_int32),
+        ("master", C.c_int32), ("device", C.c_int32), ("tile_width", C.c_int32),
         ("seed", C.c_uint64), ("max_files", C.c_int64), ("reserved", C.c_int32 * 8),
     ]
 
@@ -79,7 +79,7 @@ SYMBOLS = [
     ("gh_repair", C.c_int, [_vp, _i32, _P(PlanEntry), _i64, _P(_i64)]),
     ("gh_get_files", C.c_int, [_vp, _vp, _i64, _vp, _vp]),
     ("gh_delete_files", C.c_int, [_vp, _vp, _i64, _vp]),
-    ("gh_set_round_variant", C.c_int, [_vp, _i32, _i32]),
+    ("gh_set_round_variant", C.c_int, [_vp, _i32]),
     ("gh_set_timing", C.c_int, [_vp, _i32]),
     ("gh_read_timing", C.c_int, [_vp, _P(C.c_double), _P(_i64)]),
     ("gh_sync", C.c_int, [_vp]),

@@ -180,13 +180,14 @@ def test_n65536_invariants(gs):
     assert seen == set(crashed)
 
 
-@pytest.mark.parametrize("seg,nt", [(64, 0), (64, 1), (32, 0), (32, 1), (16, 1)])
-def test_round_variants_identical(gs, oracle_mod, seg, nt):
-    """Every k_round tiling variant gives the oracle's results (tuning knob)."""
+@pytest.mark.parametrize("tw,nt", [(64, 1), (64, 0), (32, 1), (128, 1), (256, 0), (256, 1)])
+def test_layout_variants_identical(gs, oracle_mod, tw, nt):
+    """Every table tile width and k_round stream policy gives the oracle's
+    results (layout/tuning knobs), including N not a multiple of the tile."""
     n = 700
     sched = sc.random_churn(n, 24, 21, p_crash=0.04, p_leave=0.01, p_join=0.05)
-    eng = gs.Engine(gs.default_config(n, fanout=4, seed=0x31, t_fail=4, t_cleanup=6))
-    eng.set_round_variant(seg, nt)
+    eng = gs.Engine(gs.default_config(n, fanout=4, seed=0x31, t_fail=4, t_cleanup=6, tile_width=tw))
+    eng.set_round_variant(nt)
     orc = oracle_mod.Oracle(oracle_mod.default_config(n, fanout=4, seed=0x31, t_fail=4, t_cleanup=6), threads=8)
     hb, ts, alive = sc.full_state(n)
     eng.import_state(hb, ts, alive, 0)
@@ -197,3 +198,7 @@ def test_round_variants_identical(gs, oracle_mod, seg, nt):
             orc.apply_events(sched[r])
         assert eng.step(1) == orc.step(1), r
     compare(eng, orc, 24)
+    for obs in (0, 3, 699):
+        a, b = eng.lsm(obs), orc.lsm(obs)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)

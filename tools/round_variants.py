@@ -1,7 +1,9 @@
-"""Interleaved A/B of k_round tiling variants on one N=65,536 engine in one
-process (guide §5.4 rule 24): per iteration every variant runs `rounds`
-steady-state rounds; per-variant HIP-event kernel times are collected.
-  python tools/round_variants.py [--n 65536] [--iters 5] [--rounds 3]"""
+"""A/B of k_round layout/stream variants at N=65,536 (steady state). One
+engine per tile width (48 GiB each, up to 4 alive at once), rounds
+interleaved across variants in one process (guide §5.4 rule 24); kernel time
+from HIP events on each engine's stream.
+  python tools/round_variants.py [--n 65536] [--iters 4] [--rounds 3]
+         [--variants 64:1,64:0,128:1,256:1]   (tile_width:nontemporal)"""
 import argparse
 import json
 import pathlib
@@ -15,24 +17,28 @@ import gossipsim as gs  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--n", type=int, default=65536)
 ap.add_argument("--k", type=int, default=4)
-ap.add_argument("--iters", type=int, default=5)
+ap.add_argument("--iters", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=3)
-ap.add_argument("--variants", default="64:0,64:1,32:0,32:1,16:0,16:1")
+ap.add_argument("--variants", default="64:1,64:0,128:1,256:1")
 a = ap.parse_args()
 variants = [tuple(int(x) for x in v.split(":")) for v in a.variants.split(",")]
-eng = gs.Engine(gs.default_config(a.n, fanout=a.k, seed=0x5EED0003, t_fail=16, t_cleanup=16))
-eng.init_full(2, 0, 0)
-eng.step(12)
+engines = {}
+for tw in sorted({v[0] for v in variants}):
+    e = gs.Engine(gs.default_config(a.n, fanout=a.k, seed=0x5EED0003, t_fail=16, t_cleanup=16, tile_width=tw))
+    e.init_full(2, 0, 0)
+    e.step(12)
+    engines[tw] = e
 res = {v: [] for v in variants}
 for it in range(a.iters):
     for v in variants:
-        eng.set_round_variant(*v)
-        eng.set_timing(True)
-        eng.step(a.rounds)
-        ms, k = eng.read_timing()
+        e = engines[v[0]]
+        e.set_round_variant(v[1])
+        e.set_timing(True)
+        e.step(a.rounds)
+        ms, k = e.read_timing()
         res[v].append(ms / k)
     print(f"iter {it}: " + " ".join(f"{v[0]}:{v[1]}={res[v][-1]:.2f}" for v in variants), flush=True)
 bytes_alg = 4.0 * a.n * a.n * (a.k + 4)
-out = {f"seg{v[0]}_nt{v[1]}": {"median_ms": statistics.median(t), "min_ms": min(t),
-                               "alg_GBps": bytes_alg / (statistics.median(t) / 1e3) / 1e9} for v, t in res.items()}
+out = {f"tw{v[0]}_nt{v[1]}": {"median_ms": statistics.median(t), "min_ms": min(t),
+                             "alg_GBps": bytes_alg / (statistics.median(t) / 1e3) / 1e9} for v, t in res.items()}
 print(json.dumps(out, indent=1))
