@@ -166,10 +166,11 @@ int gh_get_files(void* h, const int32_t* files, int64_t n, int32_t* replicas,
 int gh_delete_files(void* h, const int32_t* files, int64_t n,
                     int32_t* old_replicas);
 
-/* Tuning knob of the fused round kernel (k_round): non-temporal loads/stores
- * on the once-touched streams (own ts, new hb). Results do not depend on it;
- * the default is the measured fastest. */
-int gh_set_round_variant(void* h, int32_t nontemporal);
+/* Tuning knobs of the fused round kernel (k_round): non-temporal loads/stores
+ * on the once-touched streams (own ts, new hb) and the XCD-aware block->tile
+ * map. Results do not depend on them; the defaults are the measured fastest
+ * (DESIGN.md). */
+int gh_set_round_variant(void* h, int32_t nontemporal, int32_t xcd_map);
 
 /* Device timing of the fused round kernel (HIP events on the engine's
  * stream), for bench.py's roofline: enable, then read the sum of kernel

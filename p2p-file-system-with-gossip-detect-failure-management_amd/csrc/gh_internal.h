@@ -111,6 +111,7 @@ struct GhRound {
   int32_t k;
   uint64_t seed;
   int32_t peer_mode;
+  int32_t xmap;       // k_round block->tile map: 0 tile-major, 1 XCD-aware
   int32_t ablate;     // timing-only experiments (results wrong): 1 = every
                       // peer load reads the own row, 2 = no peer loads. 0 always
                       // in production (set only through GH_ROUND_ABLATE).

@@ -36,6 +36,7 @@ struct Engine {
   int32_t* ev_buf = nullptr;    // device scratch for event member lists
   bool nt = true;        // k_round non-temporal streams (gh_set_round_variant)
   int ablate = 0;        // timing-only experiment switch (GH_ROUND_ABLATE), never set in production
+  int xmap = 0;          // k_round XCD-aware tile map (gh_set_round_variant)
   bool timing = false;
   double timed_ms = 0.0;
   int64_t timed_launches = 0;
@@ -98,6 +99,7 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.seed = e->cfg.seed;
   p.peer_mode = e->cfg.peer_mode;
   p.ablate = e->ablate;
+  p.xmap = e->xmap;
   return p;
 }
 
@@ -263,16 +265,20 @@ int gh_create(const gh_config* cfg, void** handle) {
   Engine* e = new Engine();
   e->cfg = *cfg;
   e->n = cfg->n_members;
-  e->ld = ((int64_t)e->n + GH_PAD - 1) / GH_PAD * GH_PAD;
   e->alive.assign(e->n, 0);
   int tw = cfg->tile_width ? cfg->tile_width : GH_TW_DEFAULT;
   if (const char* v = std::getenv("GH_TILE_W")) tw = std::atoi(v);
   if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_ROUND_XMAP")) e->xmap = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_ROUND_ABLATE")) e->ablate = std::atoi(v);
-  if (tw != 32 && tw != 64 && tw != 128 && tw != 256) {
+  if (tw != 8 && tw != 16 && tw != 32 && tw != 64 && tw != 128 && tw != 256) {
     delete e;
     return GH_EINVAL;
   }
+  // columns padded so that 8 | (ld / tw): the XCD-aware map gives each of the
+  // 8 XCDs the same number of tiles
+  const int64_t pad = std::max<int64_t>(GH_PAD, 8 * (int64_t)tw);
+  e->ld = ((int64_t)e->n + pad - 1) / pad * pad;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return GH_EHIP;
@@ -624,10 +630,11 @@ int gh_delete_files(void* h, const int32_t* files, int64_t n, int32_t* old_repli
   return get_or_delete(e, files, n, old_replicas, nullptr, 1);
 }
 
-int gh_set_round_variant(void* h, int32_t nontemporal) {
+int gh_set_round_variant(void* h, int32_t nontemporal, int32_t xcd_map) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
   e->nt = nontemporal != 0;
+  e->xmap = xcd_map != 0;
   return GH_OK;
 }
 

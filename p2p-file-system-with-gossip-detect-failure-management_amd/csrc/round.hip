@@ -262,19 +262,38 @@ __device__ __forceinline__ void stv(int32_t* p, v4i v) {
 // 64/SEG rows per instruction. KB = peer loads issued together (4 or 8).
 // NT = non-temporal hints on the once-touched streams (own ts in/out, new hb
 // out), leaving the caches to the re-read old-hb slice.
+// Rows per workgroup tile: GH_RB, or more when a wave step covers more rows
+// (narrow tiles), so all 4 waves have rows.
+template <int TW>
+constexpr int round_rb() {
+  return 1024 / TW > GH_RB ? 1024 / TW : GH_RB;
+}
+
 template <int KB, int TW, bool NT>
 __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRound p) {
   constexpr int SEG = TW / 4;
   constexpr int RPW = 64 / SEG;
   constexpr int RSTEP = 4 * RPW;
+  constexpr int RB = round_rb<TW>();  // rows per workgroup tile
   __shared__ int s_dcnt[TW];
   __shared__ int s_dmin[TW];
-  __shared__ uint16_t s_part[GH_RB];
+  __shared__ uint16_t s_part[RB];
   __shared__ unsigned long long s_st[ST_COUNT];
 
-  const int nrb = (p.n + GH_RB - 1) / GH_RB;
-  const int tile = blockIdx.x / nrb;
-  const int rb = blockIdx.x - tile * nrb;
+  const int nrb = (p.n + RB - 1) / RB;
+  int tile, rb;
+  if (p.xmap) {
+    // XCD-aware: blocks b and b+8 share an XCD (round-robin dispatch, speed
+    // only), so XCD x = b % 8 sweeps tiles x, x+8, ... and its L2 holds the
+    // slice of the tile it is on. Needs (ld / TW) % 8 == 0 (host pads ld).
+    const int x = blockIdx.x & 7;
+    const int j = blockIdx.x >> 3;
+    tile = x + 8 * (j / nrb);
+    rb = j - (j / nrb) * nrb;
+  } else {
+    tile = blockIdx.x / nrb;
+    rb = blockIdx.x - tile * nrb;
+  }
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = uni(tid >> 6);
@@ -288,7 +307,7 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     s_dmin[t] = INT_MAX;
   }
   if (tid < ST_COUNT) s_st[tid] = 0;
-  if (tid < GH_RB) s_part[tid] = 0;
+  if (tid < RB) s_part[tid] = 0;
   __syncthreads();
 
   const int32_t* __restrict__ hbo = d.hb[cur];
@@ -312,9 +331,9 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
 
   int n_unknown = 0, n_tomb = 0, n_det = 0, n_rel = 0, n_merged = 0;
 
-  for (int rr0 = wave * RPW; rr0 < GH_RB; rr0 += RSTEP) {
+  for (int rr0 = wave * RPW; rr0 < RB; rr0 += RSTEP) {
     const int rr = rr0 + sub;
-    const int i_raw = rb * GH_RB + rr;
+    const int i_raw = rb * RB + rr;
     const bool valid = i_raw < p.n;
     if (!__any(valid)) break;
     const int i = valid ? i_raw : p.n - 1;  // in-range row for the loads of idle lanes
@@ -446,8 +465,8 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   if (n_merged) atomicAdd(&s_st[ST_MERGED], (unsigned long long)n_merged);
   __syncthreads();
 
-  const int row0 = rb * GH_RB;
-  if (tid < GH_RB && row0 + tid < p.n) d.part[(int64_t)tile * p.n + row0 + tid] = s_part[tid];
+  const int row0 = rb * RB;
+  if (tid < RB && row0 + tid < p.n) d.part[(int64_t)tile * p.n + row0 + tid] = s_part[tid];
   for (int t = tid; t < TW; t += 256) {
     if (s_dcnt[t]) {
       const int64_t c = (int64_t)tile * TW + t;
@@ -520,7 +539,8 @@ void launch_ring(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_
 
 template <int KB, int TW>
 static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
-  const int nrb = (p.n + GH_RB - 1) / GH_RB;
+  constexpr int RB = round_rb<TW>();
+  const int nrb = (p.n + RB - 1) / RB;
   const dim3 grid((unsigned)(nrb * (p.ld / TW))), blk(256);
   if (nt)
     hipLaunchKernelGGL((k_round<KB, TW, true>), grid, blk, 0, s, d, cur, dcur, p);
@@ -531,6 +551,8 @@ static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p,
 template <int KB>
 static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
   switch (d.tw) {
+    case 8: launch_round_tw<KB, 8>(d, cur, dcur, p, s, nt); break;
+    case 16: launch_round_tw<KB, 16>(d, cur, dcur, p, s, nt); break;
     case 32: launch_round_tw<KB, 32>(d, cur, dcur, p, s, nt); break;
     case 128: launch_round_tw<KB, 128>(d, cur, dcur, p, s, nt); break;
     case 256: launch_round_tw<KB, 256>(d, cur, dcur, p, s, nt); break;

@@ -164,8 +164,8 @@ class Engine:
         return rep
 
     # ---- tuning / timing -------------------------------------------------
-    def set_round_variant(self, nontemporal=True):
-        self._chk(self.lib.gh_set_round_variant(self.h, int(nontemporal)))
+    def set_round_variant(self, nontemporal=True, xcd_map=False):
+        self._chk(self.lib.gh_set_round_variant(self.h, int(nontemporal), int(xcd_map)))
 
     def set_timing(self, enable=True):
         self._chk(self.lib.gh_set_timing(self.h, int(enable)))

@@ -180,14 +180,15 @@ def test_n65536_invariants(gs):
     assert seen == set(crashed)
 
 
-@pytest.mark.parametrize("tw,nt", [(64, 1), (64, 0), (32, 1), (128, 1), (256, 0), (256, 1)])
-def test_layout_variants_identical(gs, oracle_mod, tw, nt):
+@pytest.mark.parametrize("tw,nt,xmap", [(64, 1, 0), (64, 0, 1), (32, 1, 1), (128, 1, 0), (256, 0, 0),
+                                         (256, 1, 1), (16, 1, 1), (8, 1, 1), (16, 0, 0)])
+def test_layout_variants_identical(gs, oracle_mod, tw, nt, xmap):
     """Every table tile width and k_round stream policy gives the oracle's
     results (layout/tuning knobs), including N not a multiple of the tile."""
     n = 700
     sched = sc.random_churn(n, 24, 21, p_crash=0.04, p_leave=0.01, p_join=0.05)
     eng = gs.Engine(gs.default_config(n, fanout=4, seed=0x31, t_fail=4, t_cleanup=6, tile_width=tw))
-    eng.set_round_variant(nt)
+    eng.set_round_variant(nt, xmap)
     orc = oracle_mod.Oracle(oracle_mod.default_config(n, fanout=4, seed=0x31, t_fail=4, t_cleanup=6), threads=8)
     hb, ts, alive = sc.full_state(n)
     eng.import_state(hb, ts, alive, 0)

@@ -3,7 +3,7 @@ engine per tile width (48 GiB each, up to 4 alive at once), rounds
 interleaved across variants in one process (guide §5.4 rule 24); kernel time
 from HIP events on each engine's stream.
   python tools/round_variants.py [--n 65536] [--iters 4] [--rounds 3]
-         [--variants 64:1,64:0,128:1,256:1]   (tile_width:nontemporal)"""
+         [--variants 64:1:0,16:1:1]   (tile_width:nontemporal:xcd_map)"""
 import argparse
 import json
 import pathlib
@@ -19,7 +19,7 @@ ap.add_argument("--n", type=int, default=65536)
 ap.add_argument("--k", type=int, default=4)
 ap.add_argument("--iters", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=3)
-ap.add_argument("--variants", default="64:1,64:0,128:1,256:1")
+ap.add_argument("--variants", default="64:1:0,64:1:1,16:1:1,16:1:0,8:1:1,32:1:1")
 a = ap.parse_args()
 variants = [tuple(int(x) for x in v.split(":")) for v in a.variants.split(",")]
 engines = {}
@@ -32,13 +32,13 @@ res = {v: [] for v in variants}
 for it in range(a.iters):
     for v in variants:
         e = engines[v[0]]
-        e.set_round_variant(v[1])
+        e.set_round_variant(v[1], v[2])
         e.set_timing(True)
         e.step(a.rounds)
         ms, k = e.read_timing()
         res[v].append(ms / k)
-    print(f"iter {it}: " + " ".join(f"{v[0]}:{v[1]}={res[v][-1]:.2f}" for v in variants), flush=True)
+    print(f"iter {it}: " + " ".join(f"{v[0]}:{v[1]}:{v[2]}={res[v][-1]:.2f}" for v in variants), flush=True)
 bytes_alg = 4.0 * a.n * a.n * (a.k + 4)
-out = {f"tw{v[0]}_nt{v[1]}": {"median_ms": statistics.median(t), "min_ms": min(t),
+out = {f"tw{v[0]}_nt{v[1]}_x{v[2]}": {"median_ms": statistics.median(t), "min_ms": min(t),
                              "alg_GBps": bytes_alg / (statistics.median(t) / 1e3) / 1e9} for v, t in res.items()}
 print(json.dumps(out, indent=1))
