@@ -1,0 +1,42 @@
+// Collective transport of the column-sharded engine (DESIGN.md "Multi-GPU").
+//
+// Every per-round exchange of the sharded engine is O(N) and goes through
+// this interface, stream-ordered on the engine's HIP stream:
+//   RCCL   one process per GPU, RCCL (loaded at run time) over xGMI;
+//   LOCAL  ranks are threads of one process (any devices, including G shards
+//          on one GPU, which RCCL does not allow): the parity-test transport
+//          for the sharded code path, built from hipMemcpyPeerAsync + a
+//          reduction kernel + a host barrier.
+// world == 1 needs no transport: both calls degenerate to a device copy.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+
+enum GhDType { GH_DT_U8 = 0, GH_DT_I32 = 1, GH_DT_U64 = 2 };
+enum GhROp { GH_OP_SUM = 0, GH_OP_MAX = 1 };
+
+struct GhComm {
+  int rank = 0, world = 1;
+  std::string err;
+  virtual ~GhComm() {}
+  // recv[x] = op over ranks of send[x], x < count. send may equal recv.
+  virtual int allreduce(const void* send, void* recv, size_t count, GhDType dt, GhROp op,
+                        hipStream_t s) = 0;
+  // recv[r*bytes .. (r+1)*bytes) = rank r's send; send may alias
+  // recv + rank*bytes (in place).
+  virtual int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+};
+
+size_t gh_dtype_size(GhDType dt);
+
+// world == 1 (no transport)
+GhComm* gh_comm_single();
+// RCCL: id = 128-byte ncclUniqueId from gh_comm_rccl_unique_id on rank 0;
+// the caller has selected the rank's device.
+GhComm* gh_comm_rccl(int rank, int world, const uint8_t* id, std::string* err);
+int gh_comm_rccl_unique_id(uint8_t* id, std::string* err);
+// LOCAL: ranks rendezvous on the same key (<= 128 bytes, NUL-terminated)
+GhComm* gh_comm_local(int rank, int world, const uint8_t* key, int device, std::string* err);
