@@ -8,10 +8,12 @@ full membership hb=2 ts=0, seed 0x5EED0003).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
 
-N>1 is launched by the driver under torch.distributed.run, one rank per GPU.
-Round 1 runs one independent N=65,536 cluster per GPU ("replicas"; the
-sharded single-cluster path is DESIGN.md's next row), so per-GPU work is fixed
-and value = cluster-rounds/s summed over ranks = total / max-over-ranks time.
+N>1 is launched by the driver under torch.distributed.run, one rank per GPU:
+the SAME cluster (N=65,536 by default) is column-sharded over the N GPUs
+(DESIGN.md "Multi-GPU"; rank g owns member columns [g*N/G, (g+1)*N/G) of all
+rows, RCCL over xGMI carries the O(N) per-round exchanges), so total work is
+fixed ("scaling": "strong") and value = rounds / max-over-ranks time. The RCCL
+unique id travels from rank 0 over a gloo (CPU) process group.
 
 Timeouts: the reference's PERIOD = COOLDOWN = 5 s at 1 s rounds
 (slave/slave.go:24-25) was sized for ~10 VMs. A heartbeat needs ~log5(N) ~ 7
@@ -105,17 +107,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist  # noqa: F811
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-
     import gossipsim as gs
 
     n, k = args.n, args.fanout
-    eng = gs.Engine(gs.default_config(n, fanout=k, seed=args.seed + rank, device=local,
-                                      t_fail=args.t_fail, t_cleanup=args.t_fail))
+    cfg = gs.default_config(n, fanout=k, seed=args.seed, device=local, t_fail=args.t_fail, t_cleanup=args.t_fail)
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        box = [gs.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        eng = gs.Engine(cfg, rank=rank, world=world, transport=gs.GH_COMM_RCCL, comm_id=box[0])
+    else:
+        eng = gs.Engine(cfg)
+    _, _, _, ncols = eng.shard_info()
     eng.init_full(2, 0, 0)
     if args.warmup:
         eng.step(args.warmup)
@@ -143,10 +148,10 @@ def main():
 
     if rank != 0:
         return
-    total_rounds = args.steps * world
-    value = total_rounds / elapsed
-    b_round = 4.0 * n * n * (k + 4)            # SURVEY.md §8d algorithmic bytes / round
-    b_compulsory = 16.0 * n * n                # each table cell read+written once
+    value = args.steps / elapsed
+    # SURVEY.md §8d algorithmic bytes of one k_round launch (this rank's columns)
+    b_round = 4.0 * n * ncols * (k + 4)
+    b_compulsory = 16.0 * n * ncols            # each table cell read+written once
     avg_s = (kern_ms / 1e3) / max(launches, 1)
     achieved = b_round / avg_s / 1e9
     line = {
@@ -158,7 +163,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
@@ -168,7 +173,8 @@ def main():
                         f"T_fail=T_cleanup={args.t_fail} rounds, seed {hex(args.seed)}",
             "t_fail": args.t_fail,
             "n_members": n, "fanout": k, "global_batch": n, "seq_len": n,
-            "parallelism": "replicas" if world > 1 else "single",
+            "parallelism": f"column-shard x{world} (RCCL)" if world > 1 else "single",
+            "columns_per_gpu": ncols,
             "rounds_checked": {"detections": st["detections"], "active_rows": st["active_rows"]},
         },
         "roofline": {

@@ -166,6 +166,30 @@ int gh_get_files(void* h, const int32_t* files, int64_t n, int32_t* replicas,
 int gh_delete_files(void* h, const int32_t* files, int64_t n,
                     int32_t* old_replicas);
 
+/* ---- multi-GPU: one cluster column-sharded over G ranks ----------------
+ * Rank g holds all N observer rows for member columns [g*ncs, g*ncs+ncol)
+ * (ncs = roundup(ceil(N/G), 32)) of hb (x2) and ts: 12*N*ncs bytes of HBM.
+ * Merge, detection, cleanup and REMOVE delivery of a member happen on its
+ * column's rank; per round the ranks exchange only O(N) vectors (present
+ * counts, pull inboxes or ring positions/targets) by RCCL over xGMI. This
+ * replaces the reference's per-host processes exchanging UDP lists
+ * (slave/slave.go:499-544) for a simulated cluster spread over GPUs.
+ * SPMD contract: every rank calls every gh_* function of a sharded handle
+ * with the same arguments in the same order (most calls are collective);
+ * every rank returns the same (global) results. */
+#define GH_COMM_RCCL 0    /* one process per GPU, RCCL over xGMI              */
+#define GH_COMM_LOCAL 1   /* ranks are threads of one process (any devices)  */
+#define GH_COMM_ID_BYTES 128
+
+/* RCCL unique id for gh_create_sharded (call on rank 0, send to all). */
+int gh_comm_unique_id(uint8_t* id);
+/* comm_id: GH_COMM_RCCL -> the unique id; GH_COMM_LOCAL -> a NUL-terminated
+ * group key shared by the ranks (<= GH_COMM_ID_BYTES). world == 1 needs no
+ * transport (comm_id may be NULL). cfg->device selects the rank's GPU. */
+int gh_create_sharded(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
+                      const uint8_t* comm_id, void** handle);
+int gh_shard_info(void* h, int32_t* rank, int32_t* world, int64_t* col0, int64_t* ncols);
+
 /* Tuning knobs of the fused round kernel (k_round): non-temporal loads/stores
  * on the once-touched streams (own ts, new hb) and the XCD-aware block->tile
  * map. Results do not depend on them; the defaults are the measured fastest

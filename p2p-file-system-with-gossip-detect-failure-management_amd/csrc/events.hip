@@ -1,9 +1,11 @@
 // Churn and state-maintenance kernels (SPEC.md §5, §3). All tables use the
-// tiled layout of gh_internal.h (gh_cell).
-//   k_count        present count per row (after events / import)
+// tiled layout of gh_internal.h (gh_cell) over the shard's local columns.
+//   k_count        local present count per row (after events / import)
 //   k_flags        recompute the eligibility bit of imported rows
 //   k_fill         synthetic full-membership start (BASELINE configs 2-4)
-//   k_pack/unpack  row-major staging <-> tiled tables (import/export/lsm)
+//   k_pack/unpack  host row order <-> tiled local columns (import/export/lsm)
+//   k_rowbits      presence bitmap of some rows over the local columns (the
+//                  rows' lists, gathered across shards by the host)
 //   k_leave        LEAVE delivery: slave/slave.go:310-336 -> :232-235
 //   k_join_*       JOIN at the introducer and its full-list broadcast:
 //                  slave/slave.go:224-231, 250-274
@@ -28,7 +30,7 @@ __global__ __launch_bounds__(256) void k_count(GhDev d, int cur, GhRound p) {
     cnt += (v.x >= 0) + (v.y >= 0) + (v.z >= 0) + (v.w >= 0);
   }
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-  if (lane == 0) d.cnt[i] = cnt;
+  if (lane == 0) d.cntl[i] = cnt;
 }
 
 __device__ __forceinline__ int32_t with_flag(int32_t x, int32_t t, int64_t c, int64_t i,
@@ -40,11 +42,11 @@ __device__ __forceinline__ int32_t with_flag(int32_t x, int32_t t, int64_t c, in
   return x;
 }
 
-// Storage-order walk over rows [row0, row0+nrows) of every tile.
+// Storage-order walk over rows [row0, row0+nrows) of every local tile.
 struct RowsWalk {
   int64_t per_tile, total;
   __device__ RowsWalk(const GhDev& d, int64_t nrows) : per_tile(nrows * d.tw), total(nrows * d.ld) {}
-  // idx -> (row i, member c, tiled offset of cell (i, c))
+  // idx -> (row i, local column c, tiled offset of cell (i, c))
   __device__ void at(const GhDev& d, int64_t idx, int64_t row0, int64_t& i, int64_t& c, int64_t& off) const {
     const int64_t t = idx / per_tile;
     const int64_t rem = idx - t * per_tile;
@@ -63,7 +65,7 @@ __global__ __launch_bounds__(256) void k_flags(GhDev d, int cur, int64_t row0, i
     int64_t i, c, off;
     w.at(d, idx, row0, i, c, off);
     // p.r is the round about to run: eligible <=> ts < r - T_fail
-    d.hb[cur][off] = with_flag(d.hb[cur][off], d.ts[off], c, i, p.r - p.t_fail);
+    d.hb[cur][off] = with_flag(d.hb[cur][off], d.ts[off], d.col0 + c, i, p.r - p.t_fail);
   }
 }
 
@@ -73,8 +75,8 @@ __global__ __launch_bounds__(256) void k_fill(GhDev d, int cur, int32_t hb0, int
        idx += (int64_t)gridDim.x * blockDim.x) {
     int64_t i, c, off;
     w.at(d, idx, 0, i, c, off);
-    if (c < p.n) {
-      d.hb[cur][off] = with_flag(hb0, ts0, c, i, p.r - p.t_fail);
+    if (c < d.ncol) {
+      d.hb[cur][off] = with_flag(hb0, ts0, d.col0 + c, i, p.r - p.t_fail);
       d.ts[off] = ts0;
     } else {
       d.hb[cur][off] = GH_ABSENT;
@@ -90,7 +92,7 @@ __global__ __launch_bounds__(256) void k_pack(GhDev d, int32_t* dst, const int32
        idx += (int64_t)gridDim.x * blockDim.x) {
     int64_t i, c, off;
     w.at(d, idx, row0, i, c, off);
-    if (c < d.n) dst[off] = src[(i - row0) * d.n + c];
+    if (c < d.ncol) dst[off] = src[(i - row0) * d.n + d.col0 + c];
   }
 }
 
@@ -101,15 +103,34 @@ __global__ __launch_bounds__(256) void k_unpack(GhDev d, int32_t* dst, const int
        idx += (int64_t)gridDim.x * blockDim.x) {
     int64_t i, c, off;
     w.at(d, idx, row0, i, c, off);
-    if (c >= d.n) continue;
+    if (c >= d.ncs) continue;
     int32_t x = src[off];
     if (strip && x >= 0) x &= GH_HBMASK;
-    dst[(i - row0) * d.n + c] = x;
+    dst[(i - row0) * d.ncs + c] = x;
+  }
+}
+
+// bit b of word w of row q = local column 32w+b of rows[q] is present
+__global__ __launch_bounds__(256) void k_rowbits(GhDev d, int cur, const int32_t* rows, int32_t nr) {
+  uint32_t* out = d.rbits + (int64_t)d.rank * nr * d.ncsw;
+  const int64_t total = (int64_t)nr * d.ncsw;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(idx / d.ncsw);
+    const int64_t w = idx - (int64_t)q * d.ncsw;
+    const int row = rows[q];
+    uint32_t bits = 0;
+    for (int b = 0; b < 32; ++b) {
+      const int64_t c = w * 32 + b;
+      if (c < d.ncol && d.hb[cur][gh_cell(d, row, c)] >= 0) bits |= 1u << b;
+    }
+    out[idx] = bits;
   }
 }
 
 // LEAVE from each leaver c to every alive member j of c's list (j != c):
-// removeMember(c) at j.
+// removeMember(c) at j. The leavers' lists are the gathered bitmaps rbits
+// [world][nl][ncsw]; cell (j, c) lives on c's shard.
 __global__ __launch_bounds__(256) void k_leave(GhDev d, int cur, const int32_t* leavers, int32_t nl,
                                                GhRound p) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -118,8 +139,10 @@ __global__ __launch_bounds__(256) void k_leave(GhDev d, int cur, const int32_t* 
     int32_t* hb = d.hb[cur];
     for (int q = 0; q < nl; ++q) {
       const int c = leavers[q];
-      if (c == j || hb[gh_cell(d, c, j)] < 0) continue;
-      const int64_t off = gh_cell(d, j, c);
+      const int64_t lc = (int64_t)c - d.col0;
+      if (lc < 0 || lc >= d.ncol) continue;
+      if (c == j || !gh_gbit(d, d.rbits, nl, q, j)) continue;
+      const int64_t off = gh_cell(d, j, lc);
       const int32_t x = hb[off];
       if (x >= 0) {
         hb[off] = GH_TOMBSTONE;
@@ -145,13 +168,16 @@ __global__ __launch_bounds__(256) void k_join_reset(GhDev d, int cur, const int3
   }
 }
 
-// addNewMember at the introducer (slave/slave.go:250-255). nd[4] counts adds.
+// addNewMember at the introducer (slave/slave.go:250-255) for the joiners
+// whose column is local. nd[4] counts this shard's adds.
 __global__ void k_join_add(GhDev d, int cur, const int32_t* joiners, int32_t nj, int32_t I,
                            GhRound p) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   int added = 0;
   for (int q = 0; q < nj; ++q) {
-    const int64_t off = gh_cell(d, I, joiners[q]);
+    const int64_t lc = (int64_t)joiners[q] - d.col0;
+    if (lc < 0 || lc >= d.ncol) continue;
+    const int64_t off = gh_cell(d, I, lc);
     if (d.hb[cur][off] < 0) {
       d.hb[cur][off] = 0;
       d.ts[off] = p.r;
@@ -162,7 +188,8 @@ __global__ void k_join_add(GhDev d, int cur, const int32_t* joiners, int32_t nj,
 }
 
 // The introducer's full list to every alive member of it (:256-272), merged
-// with MergeMemberList's rule at now = r.
+// with MergeMemberList's rule at now = r. nd[4] = adds over all shards;
+// rbits row 0 = the introducer's list after the adds.
 __global__ __launch_bounds__(256) void k_join_bcast(GhDev d, int cur, int32_t I, GhRound p) {
   if (d.nd[4] == 0) return;
   int32_t* hb = d.hb[cur];
@@ -172,7 +199,7 @@ __global__ __launch_bounds__(256) void k_join_bcast(GhDev d, int cur, int32_t I,
        idx += (int64_t)gridDim.x * blockDim.x) {
     int64_t j, c, off;
     w.at(d, idx, 0, j, c, off);
-    if (c >= p.n || j == I || !d.alive[j] || hb[gh_cell(d, I, j)] < 0) continue;
+    if (c >= d.ncol || j == I || !d.alive[j] || !gh_gbit(d, d.rbits, 1, 0, j)) continue;
     const int32_t mv = hb[gh_cell(d, I, c)];
     if (mv < 0) continue;
     const int32_t m = mv & GH_HBMASK;
@@ -221,16 +248,23 @@ void launch_unpack(const GhDev& d, int32_t* dst_rows, const int32_t* src_tiled, 
                      nrows, strip_flag);
 }
 
+void launch_rowbits(const GhDev& d, int cur, const int32_t* rows, int32_t nr, hipStream_t s) {
+  if (nr == 0) return;
+  hipLaunchKernelGGL(k_rowbits, dim3(grid_for((int64_t)nr * d.ncsw)), dim3(256), 0, s, d, cur, rows, nr);
+}
+
 void launch_leave(const GhDev& d, int cur, const int32_t* leavers, int32_t nl, const GhRound& p,
                   hipStream_t s) {
   hipLaunchKernelGGL(k_leave, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, leavers, nl, p);
 }
 
-void launch_join(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, int32_t introducer,
-                 const GhRound& p, hipStream_t s) {
+void launch_join_add(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, int32_t introducer,
+                     const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_join_add, dim3(1), dim3(64), 0, s, d, cur, joiners, nj, introducer, p);
-  hipLaunchKernelGGL(k_join_bcast, dim3(grid_for((int64_t)p.n * p.ld)), dim3(256), 0, s, d, cur, introducer,
-                     p);
+}
+
+void launch_join_bcast(const GhDev& d, int cur, int32_t introducer, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_join_bcast, dim3(grid_for((int64_t)p.n * p.ld)), dim3(256), 0, s, d, cur, introducer, p);
 }
 
 void launch_join_reset(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p,

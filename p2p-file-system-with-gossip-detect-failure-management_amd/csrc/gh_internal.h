@@ -1,20 +1,30 @@
 // Internal definitions shared by libgossiphip's HIP translation units.
 //
+// Column sharding (DESIGN.md "Multi-GPU"): an engine (rank g of world G)
+// holds ALL N observer rows for its member columns
+//   [col0, col0 + ncol),  col0 = g * ncs,  ncs = roundup(ceil(N / G), 32),
+// so merge, detection, cleanup and REMOVE delivery of a column never leave
+// its owner; only O(N) per-row / per-column vectors cross ranks (comm.h).
+// G = 1 is the same code with ncol = N.
+//
 // Device layout (SPEC.md §1/§3, DESIGN.md "Data layout in HBM"):
-//   The N x N membership tables are stored in column TILES of TW members:
-//     cell(i, c) = (c / TW) * (N * TW) + i * TW + c % TW
-//   i.e. tile t holds members [t*TW, (t+1)*TW) of every observer row, rows
-//   contiguous. One tile of one table is N*TW*4 bytes (16 MiB at N=65,536,
-//   TW=64): the round kernel sweeps tile by tile, so its own-row streams are
-//   sequential and every peer gather of a tile stays inside that slice.
+//   The N x ld local membership tables are stored in column TILES of TW
+//   members:
+//     cell(i, c) = (c / TW) * (N * TW) + i * TW + c % TW     (c local)
+//   i.e. tile t holds local members [t*TW, (t+1)*TW) of every observer row,
+//   rows contiguous. One tile of one table is N*TW*4 bytes (16 MiB at
+//   N=65,536, TW=64): the round kernel sweeps tile by tile, so its own-row
+//   streams are sequential and every peer gather of a tile stays inside
+//   that slice.
 //   hb[2]  int32   double-buffered heartbeat table; bit 30 of a present cell =
 //                  next-round detection eligibility; -1 absent, -2 tombstone.
 //   ts     int32   local-clock tick of each cell, updated in place.
-//   Columns are padded to ld = N rounded up to 256 (padding cells stay -1).
-//   per row: alive, active (u8), cnt (present count), det_any (u8),
-//            inbox_beg / inbox_cnt (int32), inbox[] (sender rows).
-//   per column: det_cnt / det_min (x2: pending D_{r-1} and current D_r),
-//            dbits (bitmap of pending D_{r-1}).
+//   Local columns are padded to ld (multiple of 8*TW and 256); padding cells
+//   stay -1.
+//   per row (global): alive, active, und (u8), cntl / cntg (local / global
+//            present count, [N] = |D|), post, det_any, inbox_cnt, inbox[].
+//   per local column: det_cnt / det_min (x2: pending D_{r-1} and current
+//            D_r), dbits (bitmap of pending D_{r-1}), dlist.
 //   part[ld/TW][N] uint16  per-(tile,row) present counts of the last pass.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -27,7 +37,7 @@
 #define GH_PAD 256               // column padding granule (ld % 256 == 0)
 #define GH_RB 64                 // rows per workgroup tile in the round kernel
 #define GH_MAXK 8                // max pull fanout
-#define GH_DLIST_MAX 1024        // |D| above which k_active_exact recounts whole rows
+#define GH_DLIST_MAX 1024        // local |D| above which undecided rows are recounted in full
 #define GH_TW_DEFAULT 64         // default tile width (members per tile)
 #define GH_TAG_PEER 0x50454552u
 #define GH_TAG_PLACE 0x504C4143u
@@ -37,8 +47,8 @@ enum {
   ST_DETECTIONS = 0,
   ST_FAILED,
   ST_REMOVE_UNKNOWN,
-  ST_RING_EMPTY,
-  ST_ACTIVE_ROWS,
+  ST_RING_EMPTY,  // counted by rank 0 only (replicated computation)
+  ST_ACTIVE_ROWS, // counted by rank 0 only
   ST_MERGED,
   ST_RELEASED,
   ST_TOMBSTONED,
@@ -70,23 +80,31 @@ __host__ __device__ inline uint32_t gh_philox_word(uint64_t seed, uint32_t a, ui
 }
 
 struct GhDev {
-  int32_t n;        // members (= observer rows)
-  int64_t ld;       // padded columns (multiple of GH_PAD)
-  int32_t tw;       // tile width (power of two, divides GH_PAD)
+  int32_t n;        // members N (= observer rows = global columns)
+  int64_t ld;       // padded LOCAL columns
+  int32_t tw;       // tile width (power of two)
   int32_t lgtw;     // log2(tw)
   int64_t tstride;  // cells per tile = n * tw
+  int64_t col0;     // global member id of local column 0
+  int32_t ncol;     // valid local columns
+  int32_t ncs;      // columns per rank (multiple of 32): rank g owns [g*ncs, g*ncs + ncol_g)
+  int32_t ncsw;     // ncs / 32 (bitmap words per rank)
+  int32_t rank, world;
   int32_t *hb[2];   // double buffer
   int32_t *ts;
-  uint8_t *alive, *active, *det_any;
-  int32_t *cnt;
+  uint8_t *alive, *active, *det_any, *und;
+  int32_t *cntl, *cntg;  // [n + 8]: per-row present counts (local / allreduced), [n] = |D|
+  int32_t *post;         // [n]: post-REMOVE present counts of undecided rows (allreduced)
   int32_t *det_cnt[2], *det_min[2];
   uint32_t *dbits;
   int32_t *dlist;
-  int32_t *nd;      // [0..1] |D| per parity, [2..3] dlist fill, [4] join adds
+  int32_t *nd;      // [0..1] local |D| per parity, [2..3] dlist fill, [4] join adds
   uint16_t *part;
   int32_t *inbox_beg, *inbox_cnt, *inbox, *inbox_fill, *targets;
+  int32_t *ring;    // ring mode: [world][n][2] (local snapshot count, local position of the sender)
+  uint32_t *rbits;  // gathered presence bitmaps of some rows: [world][nr][ncsw]
   unsigned long long *stats;  // ST_COUNT
-  // files
+  // files (replicated on every rank)
   int64_t fcap;
   int32_t *rep, *ver, *fts;
   uint32_t *draws;
@@ -97,9 +115,16 @@ struct GhDev {
   int64_t io_cap;
 };
 
-// Linear index of cell (observer i, member c) in the tiled layout.
+// Linear index of cell (observer i, LOCAL member column c) in the tiled layout.
 __host__ __device__ __forceinline__ int64_t gh_cell(const GhDev& d, int64_t i, int64_t c) {
   return (c >> d.lgtw) * d.tstride + (i << d.lgtw) + (c & (d.tw - 1));
+}
+
+// Bit of GLOBAL member j in row q of a gathered bitmap [world][nr][ncsw].
+__device__ __forceinline__ bool gh_gbit(const GhDev& d, const uint32_t* bits, int nr, int q, int64_t j) {
+  const int64_t o = j / d.ncs;
+  const int64_t lc = j - o * d.ncs;
+  return (bits[(o * nr + q) * d.ncsw + (lc >> 5)] >> (lc & 31)) & 1u;
 }
 
 // Parameters of one round, passed by value to the kernels.
@@ -118,32 +143,40 @@ struct GhRound {
 };
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------
-void launch_active(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
+// round.hip
+void launch_prep(const GhDev& d, int dcur, hipStream_t s);
+void launch_active_pre(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
+void launch_active_post(const GhDev& d, const GhRound& p, hipStream_t s);
 void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
-void launch_ring(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
+void launch_ring_count(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
+void launch_ring_select(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
+void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
 // nt = non-temporal hints on the once-touched streams of k_round
 void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt);
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);
+// events.hip
 void launch_count(const GhDev& d, int cur, const GhRound& p, hipStream_t s);
 void launch_flags(const GhDev& d, int cur, int64_t row0, int64_t nrows, const GhRound& p,
                   hipStream_t s);
 void launch_fill(const GhDev& d, int cur, int32_t hb0, int32_t ts0, const GhRound& p,
                  hipStream_t s);
-// row-major staging [nrows][n] <-> tiled tables (import/export/lsm)
+// full rows [nrows][n] (host order) -> tiled local columns
 void launch_pack(const GhDev& d, int32_t* dst_tiled, const int32_t* src_rows, int64_t row0,
                  int64_t nrows, hipStream_t s);
+// tiled local columns -> [nrows][ncs] (local column order)
 void launch_unpack(const GhDev& d, int32_t* dst_rows, const int32_t* src_tiled, int64_t row0,
                    int64_t nrows, int strip_flag, hipStream_t s);
+// presence bitmaps of rows[0..nr) over the local columns -> rbits + rank*nr*ncsw
+void launch_rowbits(const GhDev& d, int cur, const int32_t* rows, int32_t nr, hipStream_t s);
 void launch_leave(const GhDev& d, int cur, const int32_t* leavers, int32_t nl, const GhRound& p,
                   hipStream_t s);
-void launch_join(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, int32_t introducer,
-                 const GhRound& p, hipStream_t s);
+void launch_join_add(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, int32_t introducer,
+                     const GhRound& p, hipStream_t s);
+void launch_join_bcast(const GhDev& d, int cur, int32_t introducer, const GhRound& p, hipStream_t s);
 void launch_join_reset(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p,
                        hipStream_t s);
-void launch_candidates(const GhDev& d, int cur, int32_t master, const GhRound& p, hipStream_t s);
-// placement reads the master's (and the observer's) row of the current hb
-void launch_put(const GhDev& d, const int32_t* hb, int32_t master, int64_t n, int32_t R, int32_t now,
-                uint64_t seed, hipStream_t s);
-void launch_repair(const GhDev& d, const int32_t* hb, int32_t master, int32_t observer, int32_t R,
-                   uint64_t seed, hipStream_t s);
+// place.hip (rbits holds the master row [q=0] and, for repair, the observer row [q=1])
+void launch_candidates(const GhDev& d, int32_t nr, hipStream_t s);
+void launch_put(const GhDev& d, int32_t nr, int64_t n, int32_t R, int32_t now, uint64_t seed, hipStream_t s);
+void launch_repair(const GhDev& d, int32_t nr, int32_t R, uint64_t seed, hipStream_t s);
 void launch_get(const GhDev& d, int64_t n, int32_t R, int del, hipStream_t s);

@@ -1,11 +1,15 @@
 // libgossiphip host side: the C-ABI of include/gossiphip.h over the HIP
-// kernels in round.hip / events.hip / place.hip. One handle = one engine = one
-// gfx950 device, one HIP stream, all tables resident in HBM.
+// kernels in round.hip / events.hip / place.hip. One handle = one engine =
+// one gfx950 device, one HIP stream, its tables resident in HBM. A sharded
+// engine (gh_create_sharded) is rank g of G column shards of one cluster;
+// its O(N) per-round exchanges go through comm.h (RCCL, or threads of one
+// process).
 //
 // Reference interfaces replaced (paths under the reference tree):
 //   InitSlave / InitMaster            slave/slave.go:95, master/master.go:38
 //   HeartBeat round loop              main.go:27-33, slave/slave.go:499-544
 //   GetMsg JOIN/LEAVE/REMOVE          slave/slave.go:207-248
+//   UDP list exchange between hosts   slave/slave.go:527-542 (-> comm.h)
 //   Handle_put_request / Update_metadata / Get_* / Delete_file_info
 //                                     master/master.go:74-259
 // There is no CPU fallback: without a gfx950 device gh_create fails.
@@ -13,12 +17,14 @@
 
 #include <algorithm>
 #include <climits>
-#include <cstdlib>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
+#include "comm.h"
 #include "gh_internal.h"
 
 namespace {
@@ -27,6 +33,8 @@ struct Engine {
   gh_config cfg{};
   int32_t n = 0;
   int64_t ld = 0;
+  int rank = 0, world = 1;
+  std::unique_ptr<GhComm> comm;
   hipStream_t stream = nullptr;
   GhDev d{};
   int cur = 0, dcur = 0;
@@ -34,6 +42,8 @@ struct Engine {
   std::vector<uint8_t> alive;   // host mirror (source of truth for events)
   std::vector<gh_event> pending;
   int32_t* ev_buf = nullptr;    // device scratch for event member lists
+  int32_t* rows_buf = nullptr;  // device scratch for a few row ids
+  int64_t rbits_rows = 0;       // rows rbits can hold
   bool nt = true;        // k_round non-temporal streams (gh_set_round_variant)
   int ablate = 0;        // timing-only experiment switch (GH_ROUND_ABLATE), never set in production
   int xmap = 0;          // k_round XCD-aware tile map (gh_set_round_variant)
@@ -57,6 +67,11 @@ int set_err(Engine* e, int code, const std::string& msg) {
       return set_err((e), GH_EHIP, std::string(#call) + ": " + hipGetErrorString(_st)); \
   } while (0)
 
+#define COMMCHK(e, call)                                                          \
+  do {                                                                            \
+    if ((call) != 0) return set_err((e), GH_EHIP, "collective failed: " + (e)->comm->err); \
+  } while (0)
+
 template <class T>
 int dalloc(Engine* e, T** p, size_t count, int fill_byte) {
   void* q = nullptr;
@@ -66,21 +81,28 @@ int dalloc(Engine* e, T** p, size_t count, int fill_byte) {
     return set_err(e, GH_ENOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
   }
   e->allocs.push_back(q);
-  if (hipMemset(q, fill_byte, bytes) != hipSuccess) return set_err(e, GH_EHIP, "hipMemset failed");
+  // on the engine's (non-blocking) stream: a null-stream memset is not
+  // ordered with it and could land after the first kernel writing q
+  if (hipMemsetAsync(q, fill_byte, bytes, e->stream) != hipSuccess)
+    return set_err(e, GH_EHIP, "hipMemsetAsync failed");
   *p = static_cast<T*>(q);
   return GH_OK;
 }
 
-// Row-major device staging for import/export/lsm (the tables are tiled).
+// Device staging buffer for import/export/read-outs.
 struct Staging {
-  int32_t* p = nullptr;
-  int alloc(Engine* e, int64_t rows) {
-    if (hipMalloc(&p, std::max<size_t>(sizeof(int32_t) * e->n * rows, 16)) != hipSuccess) {
+  void* p = nullptr;
+  int alloc(Engine* e, size_t bytes) {
+    if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) {
       (void)hipGetLastError();
       p = nullptr;
       return set_err(e, GH_ENOMEM, "staging allocation failed");
     }
     return GH_OK;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
   }
   ~Staging() {
     if (p) (void)hipFree(p);
@@ -121,11 +143,33 @@ int upload_alive(Engine* e) {
   return GH_OK;
 }
 
-int upload_list(Engine* e, const std::vector<int32_t>& v) {
+int upload(Engine* e, int32_t* dst, const std::vector<int32_t>& v) {
   if (v.empty()) return GH_OK;
-  HIPCHK(e, hipMemcpyAsync(e->ev_buf, v.data(), v.size() * sizeof(int32_t), hipMemcpyHostToDevice,
-                           e->stream));
+  HIPCHK(e, hipMemcpyAsync(dst, v.data(), v.size() * sizeof(int32_t), hipMemcpyHostToDevice, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+// Presence bitmaps of rows[0..nr) (device ids) over ALL members, gathered
+// from every shard into d.rbits [world][nr][ncsw].
+int gather_rows(Engine* e, const int32_t* rows_dev, int32_t nr) {
+  GhDev& d = e->d;
+  if (nr > e->rbits_rows) {
+    uint32_t* nb = nullptr;
+    int rc;
+    if ((rc = dalloc(e, &nb, (size_t)e->world * nr * d.ncsw, 0))) return rc;
+    d.rbits = nb;  // the old buffer stays in allocs until gh_destroy
+    e->rbits_rows = nr;
+  }
+  launch_rowbits(d, e->cur, rows_dev, nr, e->stream);
+  HIPCHK(e, hipGetLastError());
+  const size_t bytes = sizeof(uint32_t) * (size_t)nr * d.ncsw;
+  COMMCHK(e, e->comm->allgather(d.rbits + (size_t)e->rank * nr * d.ncsw, d.rbits, bytes, e->stream));
+  return GH_OK;
+}
+
+int allreduce_i32(Engine* e, int32_t* send, int32_t* recv, size_t count) {
+  COMMCHK(e, e->comm->allreduce(send, recv, count, GH_DT_I32, GH_OP_SUM, e->stream));
   return GH_OK;
 }
 
@@ -146,7 +190,8 @@ int process_events(Engine* e, int32_t r) {
   int rc;
   if ((rc = upload_alive(e))) return rc;
   if (!leavers.empty()) {
-    if ((rc = upload_list(e, leavers))) return rc;
+    if ((rc = upload(e, e->ev_buf, leavers))) return rc;
+    if ((rc = gather_rows(e, e->ev_buf, (int32_t)leavers.size()))) return rc;
     launch_leave(e->d, e->cur, e->ev_buf, (int32_t)leavers.size(), p, e->stream);
     HIPCHK(e, hipStreamSynchronize(e->stream));
   }
@@ -160,15 +205,20 @@ int process_events(Engine* e, int32_t r) {
       }
     }
   if (!fresh.empty()) {
-    if ((rc = upload_list(e, fresh))) return rc;
+    if ((rc = upload(e, e->ev_buf, fresh))) return rc;
     launch_join_reset(e->d, e->cur, e->ev_buf, (int32_t)fresh.size(), p, e->stream);
     HIPCHK(e, hipStreamSynchronize(e->stream));
   }
   if ((rc = upload_alive(e))) return rc;
   const int32_t I = e->cfg.introducer;
   if (!joiners.empty() && I >= 0 && I < e->n && e->alive[I]) {
-    if ((rc = upload_list(e, joiners))) return rc;
-    launch_join(e->d, e->cur, e->ev_buf, (int32_t)joiners.size(), I, p, e->stream);
+    if ((rc = upload(e, e->ev_buf, joiners))) return rc;
+    launch_join_add(e->d, e->cur, e->ev_buf, (int32_t)joiners.size(), I, p, e->stream);
+    HIPCHK(e, hipGetLastError());
+    if ((rc = allreduce_i32(e, e->d.nd + 4, e->d.nd + 4, 1))) return rc;
+    if ((rc = upload(e, e->rows_buf, {I}))) return rc;
+    if ((rc = gather_rows(e, e->rows_buf, 1))) return rc;
+    launch_join_bcast(e->d, e->cur, I, p, e->stream);
   }
   launch_count(e->d, e->cur, p, e->stream);
   HIPCHK(e, hipGetLastError());
@@ -199,6 +249,207 @@ int check_files(Engine* e, const int32_t* files, int64_t n, bool distinct) {
     if (std::adjacent_find(s.begin(), s.end()) != s.end())
       return set_err(e, GH_EINVAL, "file ids in one call must be distinct");
   }
+  return GH_OK;
+}
+
+// Rows [row0, row0+n_rows) of a table (tiled local columns on every shard)
+// -> host row order [n_rows][n].
+int export_table(Engine* e, int32_t* out, const int32_t* table, int64_t row0, int64_t n_rows, int strip) {
+  const GhDev& d = e->d;
+  const size_t chunk = (size_t)n_rows * d.ncs;  // one shard's [n_rows][ncs]
+  Staging st;
+  int rc;
+  if ((rc = st.alloc(e, sizeof(int32_t) * chunk * e->world))) return rc;
+  launch_unpack(d, st.as<int32_t>() + chunk * e->rank, table, row0, n_rows, strip, e->stream);
+  HIPCHK(e, hipGetLastError());
+  COMMCHK(e, e->comm->allgather(st.as<int32_t>() + chunk * e->rank, st.p, sizeof(int32_t) * chunk, e->stream));
+  std::vector<int32_t> host(chunk * e->world);
+  HIPCHK(e, hipMemcpyAsync(host.data(), st.p, sizeof(int32_t) * host.size(), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  for (int g = 0; g < e->world; ++g) {
+    const int64_t c0 = (int64_t)g * d.ncs;
+    const int64_t nc = std::max<int64_t>(0, std::min<int64_t>(d.ncs, e->n - c0));
+    for (int64_t r = 0; r < n_rows && nc > 0; ++r)
+      std::memcpy(out + r * e->n + c0, host.data() + chunk * g + r * d.ncs, sizeof(int32_t) * nc);
+  }
+  return GH_OK;
+}
+
+int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport, const uint8_t* comm_id,
+           void** handle) {
+  if (!cfg || !handle) return GH_EINVAL;
+  *handle = nullptr;
+  if (cfg->n_members < 1 || cfg->fanout < 1 || cfg->fanout > GH_MAXK || cfg->replicas < 1 ||
+      cfg->replicas > 8 || cfg->min_members < 0 || cfg->max_files < 0 || cfg->max_files > INT32_MAX ||
+      (cfg->peer_mode != GH_PEER_PULL && cfg->peer_mode != GH_PEER_RING) ||
+      (cfg->detect_mode != GH_DETECT_CANONICAL && cfg->detect_mode != GH_DETECT_QUIRK) ||
+      cfg->introducer < 0 || cfg->introducer >= cfg->n_members || cfg->master < 0 ||
+      cfg->master >= cfg->n_members)
+    return GH_EINVAL;
+  if (world < 1 || rank < 0 || rank >= world) return GH_EINVAL;
+  if (world > 1 && !comm_id) return GH_EINVAL;
+  if (transport != GH_COMM_RCCL && transport != GH_COMM_LOCAL) return GH_EINVAL;
+  if (cfg->detect_mode == GH_DETECT_QUIRK) return GH_EINVAL;  // HIP path: canonical only (DESIGN.md)
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device || cfg->device < 0) {
+    (void)hipGetLastError();
+    return GH_ENODEV;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) return GH_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return GH_ENODEV;
+  if (hipSetDevice(cfg->device) != hipSuccess) return GH_ENODEV;
+
+  Engine* e = new Engine();
+  e->cfg = *cfg;
+  e->n = cfg->n_members;
+  e->rank = rank;
+  e->world = world;
+  e->alive.assign(e->n, 0);
+  int tw = cfg->tile_width ? cfg->tile_width : GH_TW_DEFAULT;
+  if (const char* v = std::getenv("GH_TILE_W")) tw = std::atoi(v);
+  if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_ROUND_XMAP")) e->xmap = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_ROUND_ABLATE")) e->ablate = std::atoi(v);
+  if (tw != 8 && tw != 16 && tw != 32 && tw != 64 && tw != 128 && tw != 256) {
+    delete e;
+    return GH_EINVAL;
+  }
+  // communicator
+  std::string cerr;
+  GhComm* c = nullptr;
+  if (world == 1 && transport != GH_COMM_RCCL)
+    c = gh_comm_single();
+  else if (world == 1 && !comm_id)
+    c = gh_comm_single();
+  else if (transport == GH_COMM_RCCL)
+    c = gh_comm_rccl(rank, world, comm_id, &cerr);
+  else
+    c = gh_comm_local(rank, world, comm_id, cfg->device, &cerr);
+  if (!c) {
+    std::fprintf(stderr, "gh_create_sharded: %s\n", cerr.c_str());
+    delete e;
+    return GH_EHIP;
+  }
+  c->rank = rank;
+  c->world = world;
+  e->comm.reset(c);
+  // column shard: [rank*ncs, rank*ncs + ncol), padded so that 8 | (ld / tw)
+  // (the XCD-aware map gives each of the 8 XCDs the same number of tiles)
+  const int64_t ncs = ((e->n + world - 1) / world + 31) / 32 * 32;
+  const int64_t col0 = (int64_t)rank * ncs;
+  const int64_t ncol = std::max<int64_t>(0, std::min<int64_t>(ncs, e->n - col0));
+  const int64_t pad = std::max<int64_t>(GH_PAD, 8 * (int64_t)tw);
+  e->ld = (ncs + pad - 1) / pad * pad;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete e;
+    return GH_EHIP;
+  }
+  GhDev& d = e->d;
+  d.n = e->n;
+  d.ld = e->ld;
+  d.tw = tw;
+  d.lgtw = __builtin_ctz((unsigned)tw);
+  d.tstride = (int64_t)e->n * tw;
+  d.col0 = col0;
+  d.ncol = (int32_t)ncol;
+  d.ncs = (int32_t)ncs;
+  d.ncsw = (int32_t)(ncs / 32);
+  d.rank = rank;
+  d.world = world;
+  e->cfg.tile_width = tw;
+  const int64_t cells = (int64_t)e->n * e->ld;
+  const int64_t nch = e->ld / tw;  // partial counts: one per (tile, row)
+  const int64_t slots = (int64_t)world * ncs;  // global rows incl. the last shard's tail
+  const int64_t inbox = std::max<int64_t>(slots * cfg->fanout, 3 * (int64_t)e->n);
+  int rc = GH_OK;
+  do {
+    if ((rc = dalloc(e, &d.hb[0], cells, 0xFF)) || (rc = dalloc(e, &d.hb[1], cells, 0xFF)) ||
+        (rc = dalloc(e, &d.ts, cells, 0)))
+      break;
+    if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
+        (rc = dalloc(e, &d.det_any, e->n, 0)) || (rc = dalloc(e, &d.und, e->n, 0)) ||
+        (rc = dalloc(e, &d.cntl, e->n + 8, 0)) || (rc = dalloc(e, &d.cntg, e->n + 8, 0)) ||
+        (rc = dalloc(e, &d.post, e->n, 0)))
+      break;
+    if ((rc = dalloc(e, &d.det_cnt[0], e->ld, 0)) || (rc = dalloc(e, &d.det_cnt[1], e->ld, 0)) ||
+        (rc = dalloc(e, &d.det_min[0], e->ld, 0x7F)) || (rc = dalloc(e, &d.det_min[1], e->ld, 0x7F)) ||
+        (rc = dalloc(e, &d.dbits, e->ld / 32 + 2, 0)) || (rc = dalloc(e, &d.dlist, 2 * e->ld, 0)) ||
+        (rc = dalloc(e, &d.nd, 8, 0)))
+      break;
+    if ((rc = dalloc(e, &d.part, nch * e->n, 0)) || (rc = dalloc(e, &d.inbox_beg, e->n, 0)) ||
+        (rc = dalloc(e, &d.inbox_cnt, slots, 0)) || (rc = dalloc(e, &d.inbox_fill, e->n, 0)) ||
+        (rc = dalloc(e, &d.inbox, inbox, 0)) || (rc = dalloc(e, &d.targets, 3 * (int64_t)e->n, 0xFF)) ||
+        (rc = dalloc(e, &d.stats, ST_COUNT, 0)) || (rc = dalloc(e, &e->ev_buf, 2 * (int64_t)e->n + 16, 0)) ||
+        (rc = dalloc(e, &e->rows_buf, 16, 0)))
+      break;
+    if (cfg->peer_mode == GH_PEER_RING && (rc = dalloc(e, &d.ring, 2 * (int64_t)world * e->n, 0))) break;
+    if ((rc = dalloc(e, &d.rbits, (size_t)world * 2 * d.ncsw, 0))) break;
+    e->rbits_rows = 2;
+    if ((rc = dalloc(e, &d.cand, e->n, 0)) || (rc = dalloc(e, &d.ncand, 4, 0))) break;
+    d.fcap = cfg->max_files;
+    if (d.fcap > 0) {
+      if ((rc = dalloc(e, &d.rep, d.fcap * cfg->replicas, 0xFF)) || (rc = dalloc(e, &d.ver, d.fcap, 0xFF)) ||
+          (rc = dalloc(e, &d.fts, d.fcap, 0)) || (rc = dalloc(e, &d.draws, d.fcap, 0)) ||
+          (rc = dalloc(e, &d.plan, d.fcap, 0)) || (rc = dalloc(e, &d.nplan, 4, 0)))
+        break;
+    }
+  } while (0);
+  if (rc != GH_OK) {
+    std::fprintf(stderr, "gh_create: %s\n", e->err.c_str());
+    gh_destroy(e);
+    return rc;
+  }
+  if (hipDeviceSynchronize() != hipSuccess) {
+    gh_destroy(e);
+    return GH_EHIP;
+  }
+  *handle = e;
+  return GH_OK;
+}
+
+// Per-round exchange of the global present counts and |D_{r-1}|, then the
+// <4 guard (SPEC §2 step 2) for every row.
+int decide_active(Engine* e, const GhRound& p) {
+  GhDev& d = e->d;
+  launch_prep(d, e->dcur, e->stream);
+  int rc;
+  if ((rc = allreduce_i32(e, d.cntl, d.cntg, (size_t)e->n + 1))) return rc;
+  launch_active_pre(d, e->cur, e->dcur, p, e->stream);
+  HIPCHK(e, hipGetLastError());
+  if (e->world > 1 && (rc = allreduce_i32(e, d.post, d.post, (size_t)e->n))) return rc;
+  launch_active_post(d, p, e->stream);
+  HIPCHK(e, hipGetLastError());
+  return GH_OK;
+}
+
+// Who merges whose snapshot this round: pull inboxes (owner of the
+// receiver's column draws and validates, allgather) or ring targets.
+int build_inboxes(Engine* e, const GhRound& p) {
+  GhDev& d = e->d;
+  if (e->cfg.peer_mode == GH_PEER_PULL) {
+    launch_peers_pull(d, e->cur, e->dcur, p, e->stream);
+    HIPCHK(e, hipGetLastError());
+    if (e->world > 1) {
+      const size_t k = (size_t)e->cfg.fanout;
+      COMMCHK(e, e->comm->allgather(d.inbox + (size_t)e->rank * d.ncs * k, d.inbox,
+                                    sizeof(int32_t) * d.ncs * k, e->stream));
+      COMMCHK(e, e->comm->allgather(d.inbox_cnt + (size_t)e->rank * d.ncs, d.inbox_cnt,
+                                    sizeof(int32_t) * d.ncs, e->stream));
+    }
+    return GH_OK;
+  }
+  launch_ring_count(d, e->cur, e->dcur, p, e->stream);
+  HIPCHK(e, hipGetLastError());
+  if (e->world > 1)
+    COMMCHK(e, e->comm->allgather(d.ring + (size_t)e->rank * e->n * 2, d.ring, sizeof(int32_t) * e->n * 2,
+                                  e->stream));
+  launch_ring_select(d, e->cur, e->dcur, p, e->stream);
+  HIPCHK(e, hipGetLastError());
+  if (e->world > 1)
+    COMMCHK(e, e->comm->allreduce(d.targets, d.targets, 3 * (size_t)e->n, GH_DT_I32, GH_OP_MAX, e->stream));
+  launch_inbox(d, p, e->stream);
+  HIPCHK(e, hipGetLastError());
   return GH_OK;
 }
 
@@ -235,6 +486,7 @@ void gh_destroy(void* h) {
   if (!e) return;
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  e->comm.reset();
   for (auto ev : e->evs) (void)hipEventDestroy(ev);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -242,94 +494,31 @@ void gh_destroy(void* h) {
 }
 
 int gh_create(const gh_config* cfg, void** handle) {
-  if (!cfg || !handle) return GH_EINVAL;
-  *handle = nullptr;
-  if (cfg->n_members < 1 || cfg->fanout < 1 || cfg->fanout > GH_MAXK || cfg->replicas < 1 ||
-      cfg->replicas > 8 || cfg->min_members < 0 || cfg->max_files < 0 || cfg->max_files > INT32_MAX ||
-      (cfg->peer_mode != GH_PEER_PULL && cfg->peer_mode != GH_PEER_RING) ||
-      (cfg->detect_mode != GH_DETECT_CANONICAL && cfg->detect_mode != GH_DETECT_QUIRK) ||
-      cfg->introducer < 0 || cfg->introducer >= cfg->n_members || cfg->master < 0 ||
-      cfg->master >= cfg->n_members)
-    return GH_EINVAL;
-  if (cfg->detect_mode == GH_DETECT_QUIRK) return GH_EINVAL;  // HIP path: canonical only (DESIGN.md)
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device || cfg->device < 0) {
-    (void)hipGetLastError();
-    return GH_ENODEV;
-  }
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) return GH_ENODEV;
-  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return GH_ENODEV;
-  if (hipSetDevice(cfg->device) != hipSuccess) return GH_ENODEV;
+  return create(cfg, 0, 1, GH_COMM_LOCAL, nullptr, handle);
+}
 
-  Engine* e = new Engine();
-  e->cfg = *cfg;
-  e->n = cfg->n_members;
-  e->alive.assign(e->n, 0);
-  int tw = cfg->tile_width ? cfg->tile_width : GH_TW_DEFAULT;
-  if (const char* v = std::getenv("GH_TILE_W")) tw = std::atoi(v);
-  if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
-  if (const char* v = std::getenv("GH_ROUND_XMAP")) e->xmap = std::atoi(v) != 0;
-  if (const char* v = std::getenv("GH_ROUND_ABLATE")) e->ablate = std::atoi(v);
-  if (tw != 8 && tw != 16 && tw != 32 && tw != 64 && tw != 128 && tw != 256) {
-    delete e;
-    return GH_EINVAL;
-  }
-  // columns padded so that 8 | (ld / tw): the XCD-aware map gives each of the
-  // 8 XCDs the same number of tiles
-  const int64_t pad = std::max<int64_t>(GH_PAD, 8 * (int64_t)tw);
-  e->ld = ((int64_t)e->n + pad - 1) / pad * pad;
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
-    delete e;
+int gh_create_sharded(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
+                      const uint8_t* comm_id, void** handle) {
+  return create(cfg, rank, world, transport, comm_id, handle);
+}
+
+int gh_comm_unique_id(uint8_t* id) {
+  if (!id) return GH_EINVAL;
+  std::string err;
+  if (gh_comm_rccl_unique_id(id, &err) != 0) {
+    std::fprintf(stderr, "gh_comm_unique_id: %s\n", err.c_str());
     return GH_EHIP;
   }
-  GhDev& d = e->d;
-  d.n = e->n;
-  d.ld = e->ld;
-  d.tw = tw;
-  d.lgtw = __builtin_ctz((unsigned)tw);
-  d.tstride = (int64_t)e->n * tw;
-  e->cfg.tile_width = tw;
-  const int64_t cells = (int64_t)e->n * e->ld;
-  const int64_t nch = e->ld / tw;  // partial counts: one per (tile, row)
-  const int64_t inbox = (int64_t)e->n * std::max(cfg->fanout, 3);
-  int rc = GH_OK;
-  do {
-    if ((rc = dalloc(e, &d.hb[0], cells, 0xFF)) || (rc = dalloc(e, &d.hb[1], cells, 0xFF)) ||
-        (rc = dalloc(e, &d.ts, cells, 0)))
-      break;
-    if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
-        (rc = dalloc(e, &d.det_any, e->n, 0)) || (rc = dalloc(e, &d.cnt, e->n, 0)))
-      break;
-    if ((rc = dalloc(e, &d.det_cnt[0], e->ld, 0)) || (rc = dalloc(e, &d.det_cnt[1], e->ld, 0)) ||
-        (rc = dalloc(e, &d.det_min[0], e->ld, 0x7F)) || (rc = dalloc(e, &d.det_min[1], e->ld, 0x7F)) ||
-        (rc = dalloc(e, &d.dbits, e->ld / 32 + 2, 0)) || (rc = dalloc(e, &d.dlist, 2 * e->ld, 0)) ||
-        (rc = dalloc(e, &d.nd, 8, 0)))
-      break;
-    if ((rc = dalloc(e, &d.part, nch * e->n, 0)) || (rc = dalloc(e, &d.inbox_beg, e->n, 0)) ||
-        (rc = dalloc(e, &d.inbox_cnt, e->n, 0)) || (rc = dalloc(e, &d.inbox_fill, e->n, 0)) ||
-        (rc = dalloc(e, &d.inbox, inbox, 0)) || (rc = dalloc(e, &d.targets, 3 * (int64_t)e->n, 0xFF)) ||
-        (rc = dalloc(e, &d.stats, ST_COUNT, 0)) || (rc = dalloc(e, &e->ev_buf, 2 * (int64_t)e->n + 16, 0)))
-      break;
-    if ((rc = dalloc(e, &d.cand, e->n, 0)) || (rc = dalloc(e, &d.ncand, 4, 0))) break;
-    d.fcap = cfg->max_files;
-    if (d.fcap > 0) {
-      if ((rc = dalloc(e, &d.rep, d.fcap * cfg->replicas, 0xFF)) || (rc = dalloc(e, &d.ver, d.fcap, 0xFF)) ||
-          (rc = dalloc(e, &d.fts, d.fcap, 0)) || (rc = dalloc(e, &d.draws, d.fcap, 0)) ||
-          (rc = dalloc(e, &d.plan, d.fcap, 0)) || (rc = dalloc(e, &d.nplan, 4, 0)))
-        break;
-    }
-  } while (0);
-  if (rc != GH_OK) {
-    std::fprintf(stderr, "gh_create: %s\n", e->err.c_str());
-    gh_destroy(e);
-    return rc;
-  }
-  if (hipDeviceSynchronize() != hipSuccess) {
-    gh_destroy(e);
-    return GH_EHIP;
-  }
-  *handle = e;
+  return GH_OK;
+}
+
+int gh_shard_info(void* h, int32_t* rank, int32_t* world, int64_t* col0, int64_t* ncols) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  if (rank) *rank = e->rank;
+  if (world) *world = e->world;
+  if (col0) *col0 = e->d.col0;
+  if (ncols) *ncols = e->d.ncol;
   return GH_OK;
 }
 
@@ -351,15 +540,15 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
   HIPCHK(e, hipSetDevice(e->cfg.device));
   int rc;
   if (n_rows > 0) {
-    // row-major host rows -> device staging -> tiled tables
+    // host rows -> device staging -> tiled local columns
     Staging st;
-    if ((rc = st.alloc(e, n_rows))) return rc;
     const size_t bytes = sizeof(int32_t) * e->n * n_rows;
+    if ((rc = st.alloc(e, bytes))) return rc;
     HIPCHK(e, hipMemcpyAsync(st.p, hb, bytes, hipMemcpyHostToDevice, e->stream));
-    launch_pack(e->d, e->d.hb[e->cur], st.p, row0, n_rows, e->stream);
+    launch_pack(e->d, e->d.hb[e->cur], st.as<int32_t>(), row0, n_rows, e->stream);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, hipMemcpyAsync(st.p, ts, bytes, hipMemcpyHostToDevice, e->stream));
-    launch_pack(e->d, e->d.ts, st.p, row0, n_rows, e->stream);
+    launch_pack(e->d, e->d.ts, st.as<int32_t>(), row0, n_rows, e->stream);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     std::copy(alive, alive + n_rows, e->alive.begin() + row0);
   }
@@ -380,22 +569,9 @@ int gh_export_state(void* h, int32_t* hb, int32_t* ts, uint8_t* alive, int64_t r
   if (!e) return GH_EINVAL;
   if (row0 < 0 || n_rows < 0 || row0 + n_rows > e->n) return set_err(e, GH_EINVAL, "row range");
   HIPCHK(e, hipSetDevice(e->cfg.device));
-  if (n_rows > 0 && (hb || ts)) {
-    int rc;
-    Staging st;
-    if ((rc = st.alloc(e, n_rows))) return rc;
-    const size_t bytes = sizeof(int32_t) * e->n * n_rows;
-    if (hb) {  // tiled -> row-major staging, eligibility bit stripped
-      launch_unpack(e->d, st.p, e->d.hb[e->cur], row0, n_rows, 1, e->stream);
-      HIPCHK(e, hipMemcpyAsync(hb, st.p, bytes, hipMemcpyDeviceToHost, e->stream));
-      HIPCHK(e, hipStreamSynchronize(e->stream));
-    }
-    if (ts) {
-      launch_unpack(e->d, st.p, e->d.ts, row0, n_rows, 0, e->stream);
-      HIPCHK(e, hipMemcpyAsync(ts, st.p, bytes, hipMemcpyDeviceToHost, e->stream));
-      HIPCHK(e, hipStreamSynchronize(e->stream));
-    }
-  }
+  int rc;
+  if (n_rows > 0 && hb && (rc = export_table(e, hb, e->d.hb[e->cur], row0, n_rows, 1))) return rc;
+  if (n_rows > 0 && ts && (rc = export_table(e, ts, e->d.ts, row0, n_rows, 0))) return rc;
   if (alive) std::copy(e->alive.begin() + row0, e->alive.begin() + row0 + n_rows, alive);
   return GH_OK;
 }
@@ -448,11 +624,8 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     int rc;
     if ((rc = process_events(e, r))) return rc;
     const GhRound p = round_params(e, r);
-    launch_active(e->d, e->cur, e->dcur, p, e->stream);
-    if (e->cfg.peer_mode == GH_PEER_PULL)
-      launch_peers_pull(e->d, e->cur, e->dcur, p, e->stream);
-    else
-      launch_ring(e->d, e->cur, e->dcur, p, e->stream);
+    if ((rc = decide_active(e, p))) return rc;
+    if ((rc = build_inboxes(e, p))) return rc;
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q], e->stream));
     launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt);
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q + 1], e->stream));
@@ -463,6 +636,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     e->round = r;
   }
   unsigned long long st[ST_COUNT];
+  COMMCHK(e, e->comm->allreduce(e->d.stats, e->d.stats, ST_COUNT, GH_DT_U64, GH_OP_SUM, e->stream));
   HIPCHK(e, hipMemcpyAsync(st, e->d.stats, sizeof st, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   if (e->timing) {
@@ -495,8 +669,14 @@ int gh_read_failed(void* h, uint32_t* bitmap, int64_t n_words) {
   const int64_t words = (e->n + 31) / 32;
   if (n_words < words) return set_err(e, GH_EINVAL, "bitmap too small");
   HIPCHK(e, hipSetDevice(e->cfg.device));
+  const GhDev& d = e->d;
+  Staging st;
+  int rc;
+  if ((rc = st.alloc(e, sizeof(uint32_t) * (size_t)d.ncsw * e->world))) return rc;
+  // shard g's pending D bits cover members [g*ncs, (g+1)*ncs): word-aligned
+  COMMCHK(e, e->comm->allgather(d.dbits, st.p, sizeof(uint32_t) * d.ncsw, e->stream));
   std::memset(bitmap, 0, n_words * sizeof(uint32_t));
-  HIPCHK(e, hipMemcpyAsync(bitmap, e->d.dbits, words * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(bitmap, st.p, words * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   return GH_OK;
 }
@@ -505,8 +685,12 @@ int gh_read_detectors(void* h, int32_t* rows, int64_t cap, int64_t* n_out) {
   Engine* e = static_cast<Engine*>(h);
   if (!e || !n_out || (cap > 0 && !rows)) return GH_EINVAL;
   HIPCHK(e, hipSetDevice(e->cfg.device));
+  Staging st;
+  int rc;
+  if ((rc = st.alloc(e, e->n))) return rc;
+  COMMCHK(e, e->comm->allreduce(e->d.det_any, st.p, e->n, GH_DT_U8, GH_OP_MAX, e->stream));
   std::vector<uint8_t> any(e->n);
-  HIPCHK(e, hipMemcpyAsync(any.data(), e->d.det_any, e->n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(any.data(), st.p, e->n, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   int64_t k = 0;
   for (int32_t i = 0; i < e->n; ++i)
@@ -550,9 +734,10 @@ int gh_put(void* h, const int32_t* files, int64_t n, int32_t* replicas, int32_t*
   if ((rc = ensure_io(e, n))) return rc;
   const int R = e->cfg.replicas;
   HIPCHK(e, hipMemcpyAsync(e->d.io_a, files, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
-  const GhRound p = round_params(e, e->round);
-  launch_candidates(e->d, e->cur, e->cfg.master, p, e->stream);
-  launch_put(e->d, e->d.hb[e->cur], e->cfg.master, n, R, e->round, e->cfg.seed, e->stream);
+  if ((rc = upload(e, e->rows_buf, {e->cfg.master}))) return rc;
+  if ((rc = gather_rows(e, e->rows_buf, 1))) return rc;
+  launch_candidates(e->d, 1, e->stream);
+  launch_put(e->d, 1, n, R, e->round, e->cfg.seed, e->stream);
   HIPCHK(e, hipGetLastError());
   std::vector<int32_t> rep(n * R), ver(n), st(n);
   HIPCHK(e, hipMemcpyAsync(rep.data(), e->d.io_b, sizeof(int32_t) * n * R, hipMemcpyDeviceToHost, e->stream));
@@ -574,9 +759,11 @@ int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap, int64
   if (observer < 0 || observer >= e->n) return set_err(e, GH_EINVAL, "observer");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   HIPCHK(e, hipMemsetAsync(e->d.nplan, 0, sizeof(int32_t), e->stream));
-  const GhRound p = round_params(e, e->round);
-  launch_candidates(e->d, e->cur, e->cfg.master, p, e->stream);
-  launch_repair(e->d, e->d.hb[e->cur], e->cfg.master, observer, e->cfg.replicas, e->cfg.seed, e->stream);
+  int rc;
+  if ((rc = upload(e, e->rows_buf, {e->cfg.master, observer}))) return rc;
+  if ((rc = gather_rows(e, e->rows_buf, 2))) return rc;
+  launch_candidates(e->d, 2, e->stream);
+  launch_repair(e->d, 2, e->cfg.replicas, e->cfg.seed, e->stream);
   HIPCHK(e, hipGetLastError());
   int32_t np = 0;
   HIPCHK(e, hipMemcpyAsync(&np, e->d.nplan, sizeof np, hipMemcpyDeviceToHost, e->stream));
@@ -588,7 +775,7 @@ int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap, int64
     HIPCHK(e, hipStreamSynchronize(e->stream));
   }
   std::sort(all.begin(), all.end(), [](const gh_plan_entry& a, const gh_plan_entry& b) { return a.file < b.file; });
-  int rc = GH_OK;
+  rc = GH_OK;
   for (int64_t x = 0; x < np; ++x) {
     if (x < cap) plan[x] = all[x];
     if (all[x].status != GH_OK) rc = GH_EPLACEMENT_STARVED;

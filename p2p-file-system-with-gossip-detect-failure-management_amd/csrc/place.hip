@@ -1,20 +1,23 @@
 // Replica placement kernels (SPEC.md §6): the master's Init_replica /
 // Handle_put_request / Update_metadata (master/master.go:74-175) for a batch of
 // files at once, one lane per file, Philox draws keyed by (seed; file, draw).
+// The master's list (and, for repair, the observer's) arrives as gathered
+// presence bitmaps in rbits (q = 0 master, q = 1 observer), so the file
+// metadata is replicated on every shard and every shard computes the same
+// placement.
 #include "gh_internal.h"
 
 namespace {
 
 // Member_list = present members of the master row, ID order
 // (master/master.go:46, slave/slave.go:478). One 1024-thread workgroup.
-__global__ __launch_bounds__(1024) void k_candidates(GhDev d, int cur, int32_t master, GhRound p) {
+__global__ __launch_bounds__(1024) void k_candidates(GhDev d, int32_t nr) {
   __shared__ int s_sum[1024];
   const int tid = threadIdx.x;
-  const int32_t* hb = d.hb[cur];
-  const int per = (p.n + 1023) / 1024;
-  const int b = tid * per, e = min(p.n, b + per);
+  const int per = (d.n + 1023) / 1024;
+  const int b = min(d.n, tid * per), e = min(d.n, b + per);
   int cnt = 0;
-  for (int c = b; c < e; ++c) cnt += hb[gh_cell(d, master, c)] >= 0;
+  for (int c = b; c < e; ++c) cnt += gh_gbit(d, d.rbits, nr, 0, c);
   s_sum[tid] = cnt;
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {
@@ -25,15 +28,15 @@ __global__ __launch_bounds__(1024) void k_candidates(GhDev d, int cur, int32_t m
   }
   int pos = tid ? s_sum[tid - 1] : 0;
   for (int c = b; c < e; ++c)
-    if (hb[gh_cell(d, master, c)] >= 0) d.cand[pos++] = c;
+    if (gh_gbit(d, d.rbits, nr, 0, c)) d.cand[pos++] = c;
   if (tid == 1023) d.ncand[0] = s_sum[1023];
 }
 
 // Init_replica (master/master.go:129-150). nodes[0..len) are kept first; the
 // reference's time-seeded Intn(M-1) becomes Philox word 0 of block
 // (f, draw, PLACE, 0) mapped by multiply-shift, so cand[M-1] is never drawn.
-__device__ int init_replica(const GhDev& d, const int32_t* hb, int32_t master, int32_t f, int32_t* nodes,
-                            int& len, int R, uint64_t seed) {
+__device__ int init_replica(const GhDev& d, int32_t nr, int32_t f, int32_t* nodes, int& len, int R,
+                            uint64_t seed) {
   if (len >= R) return GH_OK;
   const int M = d.ncand[0];
   if (M <= 1) return GH_EPLACEMENT_STARVED;  // Intn(<=0) panics
@@ -41,7 +44,7 @@ __device__ int init_replica(const GhDev& d, const int32_t* hb, int32_t master, i
   int in_pool = 0;
   for (int x = 0; x < len; ++x) {
     const int32_t a = nodes[x];
-    in_pool += (a >= 0 && a < d.n && a < last && hb[gh_cell(d, master, a)] >= 0);
+    in_pool += (a >= 0 && a < d.n && a < last && gh_gbit(d, d.rbits, nr, 0, a));
   }
   if ((M - 1) - in_pool < R - len) return GH_EPLACEMENT_STARVED;  // infinite loop
   uint32_t dr = d.draws[f];
@@ -67,8 +70,8 @@ __device__ int init_replica(const GhDev& d, const int32_t* hb, int32_t master, i
 
 // put (Handle_put_request, :152-175) for io_a[0..n): out io_b replicas,
 // io_c versions, io_d status.
-__global__ __launch_bounds__(256) void k_put(GhDev d, const int32_t* hb, int32_t master, int64_t n, int32_t R,
-                                             int32_t now, uint64_t seed) {
+__global__ __launch_bounds__(256) void k_put(GhDev d, int32_t nr, int64_t n, int32_t R, int32_t now,
+                                             uint64_t seed) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (x >= n) return;
   const int32_t f = d.io_a[x];
@@ -84,7 +87,7 @@ __global__ __launch_bounds__(256) void k_put(GhDev d, const int32_t* hb, int32_t
     nodes[q] = rp[q];
     len += rp[q] >= 0;
   }
-  const int st = init_replica(d, hb, master, f, nodes, len, R, seed);
+  const int st = init_replica(d, nr, f, nodes, len, R, seed);
   if (st == GH_OK) {
     for (int q = 0; q < R; ++q) rp[q] = q < len ? nodes[q] : -1;
     d.ver[f] += 1;  // :159
@@ -94,9 +97,9 @@ __global__ __launch_bounds__(256) void k_put(GhDev d, const int32_t* hb, int32_t
   d.io_d[x] = st;
 }
 
-// Update_metadata (:74-127) with available = the observer row's present set.
-__global__ __launch_bounds__(256) void k_repair(GhDev d, const int32_t* hb, int32_t master, int32_t observer,
-                                                int32_t R, uint64_t seed) {
+// Update_metadata (:74-127) with available = the observer row's present set
+// (rbits q = 1).
+__global__ __launch_bounds__(256) void k_repair(GhDev d, int32_t nr, int32_t R, uint64_t seed) {
   const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= d.fcap || d.ver[f] < 0) return;
   int32_t* rp = d.rep + f * R;
@@ -104,13 +107,13 @@ __global__ __launch_bounds__(256) void k_repair(GhDev d, const int32_t* hb, int3
   int wl = 0;
   for (int q = 0; q < R; ++q) {
     const int32_t a = rp[q];
-    if (a >= 0 && a < d.n && hb[gh_cell(d, observer, a)] >= 0) working[wl++] = a;  // :93-99
+    if (a >= 0 && a < d.n && gh_gbit(d, d.rbits, nr, 1, a)) working[wl++] = a;  // :93-99
   }
   if (wl >= R) return;  // :104
   int32_t nodes[8];
   for (int q = 0; q < 8; ++q) nodes[q] = q < wl ? working[q] : -1;
   int len = wl;
-  const int st = init_replica(d, hb, master, (int32_t)f, nodes, len, R, seed);  // :106-107
+  const int st = init_replica(d, nr, (int32_t)f, nodes, len, R, seed);  // :106-107
   for (int q = 0; q < R; ++q) rp[q] = q < len ? nodes[q] : -1;
   const int slot = atomicAdd(d.nplan, 1);
   gh_plan_entry e;
@@ -142,19 +145,16 @@ __global__ __launch_bounds__(256) void k_get(GhDev d, int64_t n, int32_t R, int 
 
 }  // namespace
 
-void launch_candidates(const GhDev& d, int cur, int32_t master, const GhRound& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_candidates, dim3(1), dim3(1024), 0, s, d, cur, master, p);
+void launch_candidates(const GhDev& d, int32_t nr, hipStream_t s) {
+  hipLaunchKernelGGL(k_candidates, dim3(1), dim3(1024), 0, s, d, nr);
 }
 
-void launch_put(const GhDev& d, const int32_t* hb, int32_t master, int64_t n, int32_t R, int32_t now,
-                uint64_t seed, hipStream_t s) {
-  hipLaunchKernelGGL(k_put, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, hb, master, n, R, now, seed);
+void launch_put(const GhDev& d, int32_t nr, int64_t n, int32_t R, int32_t now, uint64_t seed, hipStream_t s) {
+  hipLaunchKernelGGL(k_put, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, nr, n, R, now, seed);
 }
 
-void launch_repair(const GhDev& d, const int32_t* hb, int32_t master, int32_t observer, int32_t R,
-                   uint64_t seed, hipStream_t s) {
-  hipLaunchKernelGGL(k_repair, dim3((unsigned)((d.fcap + 255) / 256)), dim3(256), 0, s, d, hb, master, observer,
-                     R, seed);
+void launch_repair(const GhDev& d, int32_t nr, int32_t R, uint64_t seed, hipStream_t s) {
+  hipLaunchKernelGGL(k_repair, dim3((unsigned)((d.fcap + 255) / 256)), dim3(256), 0, s, d, nr, R, seed);
 }
 
 void launch_get(const GhDev& d, int64_t n, int32_t R, int del, hipStream_t s) {

@@ -1,9 +1,11 @@
 // Gossip-round kernels for gfx950 (SPEC.md §2-§3, DESIGN.md "Kernels").
 //
-//   k_active       per row: the <4 guard after REMOVE delivery
-//                  (slave/slave.go:504,511), exact recount only for rows whose
-//                  count could cross the threshold.
-//   k_peers_pull   per receiver: k Philox peers, kept iff the sender is
+//   k_prep / k_active_pre / k_active_exact / k_active_post
+//                  per row: the <4 guard after REMOVE delivery
+//                  (slave/slave.go:504,511). Rows decided by the global count
+//                  need nothing else; the few undecided rows get an exact
+//                  post-REMOVE count (summed over ranks when sharded).
+//   k_peers_pull   per receiver column: k Philox peers, kept iff the sender is
 //                  active, alive and lists the receiver (slave/slave.go:527-542).
 //   k_ring_*       reference ring topology (slave/slave.go:512-524) + inbox CSR.
 //   k_round        THE HOT KERNEL: one pass over the table applying REMOVE
@@ -12,6 +14,8 @@
 //                  64-row x TW-member tile per workgroup.
 //   k_finish       per row/column: reduce the pass's partial counts, build
 //                  the failed-set bitmap D_r for the next round.
+// Member columns are local to the engine's shard (gh_internal.h); rows,
+// alive/active and the inboxes are global.
 #include <limits.h>
 
 #include "gh_internal.h"
@@ -28,50 +32,59 @@ __device__ __forceinline__ bool dbit(const uint32_t* bits, int64_t c) {
 // (slave/slave.go:344-346: a detector does not message itself).
 __device__ __forceinline__ bool removes_at(int dc, int dm, int j) { return !(dc == 1 && dm == j); }
 
-__global__ __launch_bounds__(256) void k_active(GhDev d, int cur, int dcur, GhRound p) {
+// |D_{r-1}| of this shard next to the local counts, for one allreduce.
+__global__ void k_prep(GhDev d, int dcur) { d.cntl[d.n] = d.nd[dcur]; }
+
+// Decides rows from the global count cntg and global |D| = cntg[n]; an
+// undecided row (|D| could push it under the threshold) gets its exact local
+// post-REMOVE count in post[] (und = 1), or is left to k_active_exact's full
+// recount in failure storms (und = 2).
+__global__ __launch_bounds__(256) void k_active_pre(GhDev d, int cur, int dcur, GhRound p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     d.nd[dcur ^ 1] = 0;
     d.nd[2 + (dcur ^ 1)] = 0;
   }
+  if (i >= p.n) return;
+  d.det_any[i] = 0;
   bool a = false;
-  if (i < p.n) {
-    d.det_any[i] = 0;
-    if (d.alive[i]) {
-      const int c = d.cnt[i];
+  uint8_t u = 0;
+  int32_t post = 0;
+  if (d.alive[i]) {
+    const int c = d.cntg[i];
+    const int ndg = d.cntg[p.n];
+    if (c < p.min_members) {
+      a = false;
+    } else if (c - ndg >= p.min_members) {
+      a = true;
+    } else if (d.nd[dcur] > GH_DLIST_MAX) {
+      u = 2;
+    } else {
+      u = 1;
+      const int32_t* hb = d.hb[cur];
+      const int32_t* dc = d.det_cnt[dcur];
+      const int32_t* dm = d.det_min[dcur];
+      int rem = 0;
       const int nd = d.nd[dcur];
-      if (c < p.min_members) {
-        a = false;
-      } else if (c - nd >= p.min_members) {
-        a = true;
-      } else if (nd > GH_DLIST_MAX) {
-        a = false;          // decided by k_active_exact's full-row recount
-        d.cnt[i] = -1;      // marks the row uncertain for it
-      } else {
-        const int32_t* hb = d.hb[cur];
-        const int32_t* dc = d.det_cnt[dcur];
-        const int32_t* dm = d.det_min[dcur];
-        int rem = 0;
-        for (int q = 0; q < nd; ++q) {
-          const int col = d.dlist[(int64_t)dcur * p.ld + q];
-          rem += (hb[gh_cell(d, i, col)] >= 0) && removes_at(dc[col], dm[col], i);
-        }
-        a = (c - rem) >= p.min_members;
+      for (int q = 0; q < nd; ++q) {
+        const int col = d.dlist[(int64_t)dcur * p.ld + q];
+        rem += (hb[gh_cell(d, i, col)] >= 0) && removes_at(dc[col], dm[col], i);
       }
+      post = d.cntl[i] - rem;
     }
-    d.active[i] = a;
   }
-  const unsigned long long m = __ballot(a);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(&d.stats[ST_ACTIVE_ROWS], (unsigned long long)__popcll(m));
+  d.active[i] = a;
+  d.und[i] = u;
+  d.post[i] = post;
 }
 
-// Failure storms (|D| > GH_DLIST_MAX): rows k_active could not decide from
-// the D list get an exact post-REMOVE recount by one wave sweeping the row.
+// Failure storms (local |D| > GH_DLIST_MAX): one wave recounts each
+// undecided row over the local columns with REMOVE applied.
 __global__ __launch_bounds__(256) void k_active_exact(GhDev d, int cur, int dcur, GhRound p) {
   if (d.nd[dcur] <= GH_DLIST_MAX) return;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (i >= p.n || d.cnt[i] != -1) return;
+  if (i >= p.n || d.und[i] != 2) return;
   const int32_t* hb = d.hb[cur];
   const int32_t* dc = d.det_cnt[dcur];
   const int32_t* dm = d.det_min[dcur];
@@ -85,29 +98,44 @@ __global__ __launch_bounds__(256) void k_active_exact(GhDev d, int cur, int dcur
       cnt += x[j] >= 0 && !(((b4 >> j) & 1u) && removes_at(dc[c + j], dm[c + j], i));
   }
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-  if (lane == 0) {
-    const bool a = cnt >= p.min_members;
-    d.active[i] = a;
-    if (a) atomicAdd(&d.stats[ST_ACTIVE_ROWS], 1ull);
-  }
+  if (lane == 0) d.post[i] = cnt;
 }
 
-__global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, GhRound p) {
+// post[] now holds the global post-REMOVE counts of the undecided rows.
+__global__ __launch_bounds__(256) void k_active_post(GhDev d, GhRound p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.n) return;
-  const int beg = i * p.k;
+  bool a = false;
+  if (i < p.n) {
+    a = d.active[i];
+    if (d.und[i]) {
+      a = d.post[i] >= p.min_members;
+      d.active[i] = a;
+    }
+  }
+  const unsigned long long m = __ballot(a);
+  if (d.rank == 0 && (threadIdx.x & 63) == 0 && m)
+    atomicAdd(&d.stats[ST_ACTIVE_ROWS], (unsigned long long)__popcll(m));
+}
+
+// Receivers are this shard's member columns (their column holds the senders'
+// view of them); the inbox rows of the other shards arrive by allgather.
+__global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, GhRound p) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= d.ncs) return;
+  const int64_t i = d.col0 + t;  // global receiver (>= n in the tail of the last shard)
+  const int64_t beg = i * p.k;
   int nv = 0;
-  if (d.alive[i] && p.n >= 2) {
-    const bool ib = dbit(d.dbits, i);
-    const int dci = ib ? d.det_cnt[dcur][i] : 0;
-    const int dmi = ib ? d.det_min[dcur][i] : 0;
-    for (int t = 0; t < p.k; ++t) {
+  if (t < d.ncol && d.alive[i] && p.n >= 2) {
+    const bool ib = dbit(d.dbits, t);
+    const int dci = ib ? d.det_cnt[dcur][t] : 0;
+    const int dmi = ib ? d.det_min[dcur][t] : 0;
+    for (int q = 0; q < p.k; ++q) {
       const uint32_t u = gh_philox_word(p.seed, (uint32_t)i, (uint32_t)p.r, GH_TAG_PEER,
-                                        (uint32_t)(t >> 2), t & 3);
-      const uint32_t q = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
-      const int s = (int)q + ((int)q >= i);
+                                        (uint32_t)(q >> 2), q & 3);
+      const uint32_t w = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
+      const int s = (int)w + ((int64_t)w >= i);
       if (!d.alive[s] || !d.active[s]) continue;
-      const int32_t v = d.hb[cur][gh_cell(d, s, i)];
+      const int32_t v = d.hb[cur][gh_cell(d, s, t)];
       // i must be in s's snapshot list: present, not detected by s this
       // round (eligibility flag) and not REMOVE'd at s in step 1.
       if (v < 0 || (v & GH_FLAG)) continue;
@@ -115,77 +143,124 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
       d.inbox[beg + nv++] = s;
     }
   }
-  d.inbox_beg[i] = beg;
   d.inbox_cnt[i] = nv;
 }
 
-// Ring targets: one workgroup per sender row (slave/slave.go:515-524). The
-// snapshot list is the row after steps 1-5 in member-ID order (SPEC D1).
-__global__ __launch_bounds__(256) void k_ring_targets(GhDev d, int cur, int dcur, GhRound p) {
-  __shared__ int s_cnt[256];
-  __shared__ int s_tgt[3];
+// Is local column c in sender sdr's snapshot list (after steps 1-5)?
+__device__ __forceinline__ bool snap_present(const GhDev& d, const int32_t* hb, int dcur, int sdr, int64_t c) {
+  const int32_t v = hb[gh_cell(d, sdr, c)];
+  if (v < 0) return false;
+  if ((v & GH_FLAG) && d.col0 + c != sdr) return false;  // detected by the sender this round
+  if (dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], sdr)) return false;
+  return true;
+}
+
+// Block-wide exclusive scan of per-thread counts (256 threads).
+__device__ __forceinline__ int block_excl_scan(int v, int* s_tmp, int* total) {
+  const int tid = threadIdx.x;
+  s_tmp[tid] = v;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const int x = tid >= off ? s_tmp[tid - off] : 0;
+    __syncthreads();
+    s_tmp[tid] += x;
+    __syncthreads();
+  }
+  const int incl = s_tmp[tid];
+  *total = s_tmp[255];
+  __syncthreads();
+  return incl - v;
+}
+
+// Ring mode, part 1 (one workgroup per sender row): the sender's snapshot
+// list restricted to this shard's columns: its length and, when the sender's
+// own column is local, the sender's position in it (SPEC D1 order).
+__global__ __launch_bounds__(256) void k_ring_count(GhDev d, int cur, int dcur, GhRound p) {
+  __shared__ int s_tmp[256];
   const int sdr = blockIdx.x;
   const int tid = threadIdx.x;
+  int32_t* out = d.ring + ((int64_t)d.rank * p.n + sdr) * 2;
   if (!(d.alive[sdr] && d.active[sdr])) {
-    if (tid < 3) d.targets[(int64_t)sdr * 3 + tid] = -1;
+    if (tid == 0) {
+      out[0] = 0;
+      out[1] = -1;
+    }
     return;
   }
   const int32_t* hb = d.hb[cur];
-  const int per = (p.n + 255) / 256;
-  const int b = tid * per, e = min(p.n, b + per);
-  auto present = [&](int c) -> bool {
-    const int32_t v = hb[gh_cell(d, sdr, c)];
-    if (v < 0) return false;
-    if ((v & GH_FLAG) && c != sdr) return false;  // detected by the sender this round
-    if (dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], sdr)) return false;
-    return true;
-  };
+  const int per = (d.ncol + 255) / 256;
+  const int b = min(d.ncol, tid * per), e = min(d.ncol, b + per);
   int cnt = 0;
-  for (int c = b; c < e; ++c) cnt += present(c);
-  s_cnt[tid] = cnt;
+  for (int c = b; c < e; ++c) cnt += snap_present(d, hb, dcur, sdr, c);
+  int total;
+  const int off = block_excl_scan(cnt, s_tmp, &total);
+  const int64_t ls = (int64_t)sdr - d.col0;
+  if (tid == 0) {
+    out[0] = total;
+    if (!(ls >= 0 && ls < d.ncol)) out[1] = -1;
+  }
+  if (ls >= b && ls < e) {
+    int pos = -1;
+    if (snap_present(d, hb, dcur, sdr, ls)) {
+      pos = off;
+      for (int c = b; c < ls; ++c) pos += snap_present(d, hb, dcur, sdr, c);
+    }
+    out[1] = pos;
+  }
+}
+
+// Ring mode, part 2: with every shard's (length, position) gathered, the
+// sender's targets list[(idx-1) mod L], list[(idx+1) mod L], list[(idx+2)
+// mod L] (slave/slave.go:515-524) that fall into this shard's columns; the
+// other shards' targets arrive by allreduce(max).
+__global__ __launch_bounds__(256) void k_ring_select(GhDev d, int cur, int dcur, GhRound p) {
+  __shared__ int s_tmp[256];
+  __shared__ int s_tgt[3];
+  const int sdr = blockIdx.x;
+  const int tid = threadIdx.x;
   if (tid < 3) s_tgt[tid] = -1;
   __syncthreads();
-  // exclusive scan (256 entries, one pass by thread 0 is fine: ring mode is
-  // the small-N parity path)
-  __shared__ int s_off[257];
-  __shared__ int s_L, s_idx;
-  if (tid == 0) {
-    int acc = 0;
-    for (int t = 0; t < 256; ++t) {
-      s_off[t] = acc;
-      acc += s_cnt[t];
+  if (d.alive[sdr] && d.active[sdr]) {
+    int64_t L = 0, before_me = 0, before_owner = 0;
+    const int owner = (int)(sdr / d.ncs);
+    for (int g = 0; g < d.world; ++g) {
+      const int64_t c = d.ring[((int64_t)g * p.n + sdr) * 2];
+      if (g < d.rank) before_me += c;
+      if (g < owner) before_owner += c;
+      L += c;
     }
-    s_off[256] = acc;
-    s_L = acc;
-    s_idx = -1;
-  }
-  __syncthreads();
-  if (sdr >= b && sdr < e && present(sdr)) {
-    int rank = s_off[tid];
-    for (int c = b; c < sdr; ++c) rank += present(c);
-    s_idx = rank;
-  }
-  __syncthreads();
-  const int L = s_L;
-  if (L == 0) {
-    if (tid == 0) atomicAdd(&d.stats[ST_RING_EMPTY], 1ull);
-    if (tid < 3) d.targets[(int64_t)sdr * 3 + tid] = -1;
-    return;
-  }
-  int want[3] = {s_idx - 1, s_idx + 1, s_idx + 2};
+    if (L == 0) {
+      if (tid == 0 && d.rank == 0) atomicAdd(&d.stats[ST_RING_EMPTY], 1ull);  // slave.go:517 div by 0
+    } else {
+      const int64_t lp = d.ring[((int64_t)owner * p.n + sdr) * 2 + 1];
+      const int64_t idx = lp >= 0 ? before_owner + lp : -1;
+      const int64_t mine = d.ring[((int64_t)d.rank * p.n + sdr) * 2];
+      int64_t want[3] = {idx - 1, idx + 1, idx + 2};
+      bool any = false;
 #pragma unroll
-  for (int q = 0; q < 3; ++q) {
-    int v = want[q] % L;  // C and Go both truncate toward zero
-    if (v < 0) v += L;
-    want[q] = v;
-  }
-  int rank = s_off[tid];
-  for (int c = b; c < e; ++c) {
-    if (!present(c)) continue;
+      for (int q = 0; q < 3; ++q) {
+        int64_t v = want[q] % L;  // C and Go both truncate toward zero
+        if (v < 0) v += L;
+        want[q] = v - before_me;  // position inside this shard's part
+        any |= want[q] >= 0 && want[q] < mine;
+      }
+      if (any) {
+        const int32_t* hb = d.hb[cur];
+        const int per = (d.ncol + 255) / 256;
+        const int b = min(d.ncol, tid * per), e = min(d.ncol, b + per);
+        int cnt = 0;
+        for (int c = b; c < e; ++c) cnt += snap_present(d, hb, dcur, sdr, c);
+        int total;
+        int rank = block_excl_scan(cnt, s_tmp, &total);
+        for (int c = b; c < e; ++c) {
+          if (!snap_present(d, hb, dcur, sdr, c)) continue;
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
-      if (want[q] == rank) s_tgt[q] = c;
-    rank++;
+          for (int q = 0; q < 3; ++q)
+            if (want[q] == rank) s_tgt[q] = (int)(d.col0 + c);
+          rank++;
+        }
+      }
+    }
   }
   __syncthreads();
   if (tid < 3) d.targets[(int64_t)sdr * 3 + tid] = s_tgt[tid];
@@ -205,7 +280,7 @@ __global__ __launch_bounds__(1024) void k_inbox_scan(GhDev d, GhRound p) {
   __shared__ int s_sum[1024];
   const int tid = threadIdx.x;
   const int per = (p.n + 1023) / 1024;
-  const int b = tid * per, e = min(p.n, b + per);
+  const int b = min(p.n, tid * per), e = min(p.n, b + per);
   int acc = 0;
   for (int x = b; x < e; ++x) acc += d.inbox_cnt[x];
   s_sum[tid] = acc;
@@ -224,6 +299,8 @@ __global__ __launch_bounds__(1024) void k_inbox_scan(GhDev d, GhRound p) {
   }
 }
 
+// Inbox order is whatever the atomics give: the merge is a max, so only the
+// set of senders matters.
 __global__ __launch_bounds__(256) void k_inbox_fill(GhDev d, GhRound p) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= p.n) return;
@@ -299,7 +376,8 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   const int wave = uni(tid >> 6);
   const int sub = lane / SEG;
   const int lc = lane % SEG;
-  const int64_t c0 = (int64_t)tile * TW + lc * 4;              // member of this lane's first cell
+  const int64_t l0 = (int64_t)tile * TW + lc * 4;               // local column of this lane's first cell
+  const int64_t c0 = d.col0 + l0;                               // its global member id
   const int64_t tb = (int64_t)tile * ((int64_t)p.n * TW) + lc * 4;  // tile base + lane offset
 
   for (int t = tid; t < TW; t += 256) {
@@ -317,15 +395,16 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   const int32_t lim_fail = r - p.t_fail;
   const int32_t lim_clean = r - p.t_cleanup;
   const int32_t lim_next = r + 1 - p.t_fail;
+  const bool pull = p.peer_mode == GH_PEER_PULL;
 
   // REMOVE bits of this lane's 4 members (rare: slow path only when set)
-  const uint32_t my4 = (d.dbits[c0 >> 5] >> (c0 & 31)) & 0xFu;
+  const uint32_t my4 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFu;
   int dc[4] = {0, 0, 0, 0}, dm[4] = {0, 0, 0, 0};
   if (my4) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      dc[j] = d.det_cnt[dcur][c0 + j];
-      dm[j] = d.det_min[dcur][c0 + j];
+      dc[j] = d.det_cnt[dcur][l0 + j];
+      dm[j] = d.det_min[dcur][l0 + j];
     }
   }
 
@@ -342,12 +421,12 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     if constexpr (RPW == 1) {
       al = uni(d.alive[i]);
       ac = uni(d.active[i]);
-      beg = uni(d.inbox_beg[i]);
+      beg = pull ? i * p.k : uni(d.inbox_beg[i]);
       cntv = al ? uni(d.inbox_cnt[i]) : 0;
     } else {
       al = d.alive[i] && valid;
       ac = d.active[i];
-      beg = d.inbox_beg[i];
+      beg = pull ? i * p.k : d.inbox_beg[i];
       cntv = al ? d.inbox_cnt[i] : 0;
     }
     const v4i v = ldv<false>(hbo + off);  // re-read by peers: keep it cached
@@ -477,8 +556,9 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   if (tid < ST_COUNT && s_st[tid]) atomicAdd(&d.stats[tid], s_st[tid]);
 }
 
-// Rows: sum the per-chunk partial counts. Columns: bitmap + list of D_r,
-// and reset the consumed D_{r-1} accumulators for reuse in round r+1.
+// Rows: sum the per-tile partial counts (local present count). Columns:
+// bitmap + list of D_r, and reset the consumed D_{r-1} accumulators for reuse
+// in round r+1.
 __global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p, int nchunks) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (x < p.n) {
@@ -491,7 +571,7 @@ __global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p, in
       s3 += d.part[(int64_t)(ch + 3) * p.n + x];
     }
     for (; ch < nchunks; ++ch) s0 += d.part[(int64_t)ch * p.n + x];
-    d.cnt[x] = s0 + s1 + s2 + s3;
+    d.cntl[x] = s0 + s1 + s2 + s3;
   }
   const int dnew = dcur ^ 1;
   bool has = false;
@@ -512,7 +592,7 @@ __global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p, in
     }
   }
   if (has) {
-    // list order is irrelevant: only k_active's recount reads it
+    // list order is irrelevant: only k_active_pre's recount reads it
     const int pos = atomicAdd(&d.nd[2 + dnew], 1);
     d.dlist[(int64_t)dnew * p.ld + pos] = (int32_t)x;
   }
@@ -520,17 +600,32 @@ __global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p, in
 
 }  // namespace
 
-void launch_active(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_active, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
+void launch_prep(const GhDev& d, int dcur, hipStream_t s) {
+  hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, s, d, dcur);
+}
+
+void launch_active_pre(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_active_pre, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
   hipLaunchKernelGGL(k_active_exact, dim3((p.n + 3) / 4), dim3(256), 0, s, d, cur, dcur, p);
 }
 
-void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_peers_pull, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
+void launch_active_post(const GhDev& d, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_active_post, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
 }
 
-void launch_ring(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_ring_targets, dim3(p.n), dim3(256), 0, s, d, cur, dcur, p);
+void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_peers_pull, dim3((d.ncs + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
+}
+
+void launch_ring_count(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_ring_count, dim3(p.n), dim3(256), 0, s, d, cur, dcur, p);
+}
+
+void launch_ring_select(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_ring_select, dim3(p.n), dim3(256), 0, s, d, cur, dcur, p);
+}
+
+void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
   (void)hipMemsetAsync(d.inbox_cnt, 0, sizeof(int32_t) * p.n, s);
   hipLaunchKernelGGL(k_inbox_count, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
   hipLaunchKernelGGL(k_inbox_scan, dim3(1), dim3(1024), 0, s, d, p);

@@ -6,20 +6,30 @@ slave/slave.go:546-613 (join, leave, lsm, put, get, delete, ls, store) plus
 crash ("CTRL+C", README.md:30) — and the Fail_recover schedule
 (slave/slave.go:1122-1133: a repair pass 8 rounds after a detection).
 
+A cluster can be column-sharded over G GPUs (DESIGN.md "Multi-GPU"): one
+`Engine(cfg, rank, world, GH_COMM_RCCL, comm_unique_id-from-rank-0)` per
+process and GPU, every rank making the same calls (SPMD); or all G shards
+driven from one process by `ShardGroup` (threads, GH_COMM_LOCAL transport, any
+devices including G shards on one GPU: the sharded-path parity harness).
+
 Every call runs on a gfx950 GPU through the HIP kernels; there is no CPU
 fallback. Construction fails with GossipError(GH_ENODEV) without a device.
 """
 from __future__ import annotations
 
 import ctypes as C
+import itertools
+import os
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
 from . import _abi
-from ._abi import (GH_DETECT_CANONICAL, GH_DETECT_QUIRK, GH_EPLACEMENT_STARVED, GH_EV_CRASH,  # noqa: F401
-                   GH_EV_JOIN, GH_EV_LEAVE, GH_OK, GH_PEER_PULL, GH_PEER_RING, Config, PlanEntry)
+from ._abi import (GH_COMM_LOCAL, GH_COMM_RCCL, GH_DETECT_CANONICAL, GH_DETECT_QUIRK,  # noqa: F401
+                   GH_EPLACEMENT_STARVED, GH_EV_CRASH, GH_EV_JOIN, GH_EV_LEAVE, GH_OK, GH_PEER_PULL,
+                   GH_PEER_RING, Config, PlanEntry)
 
-__all__ = ["Engine", "Cluster", "GossipError", "default_config", "Config"]
+__all__ = ["Engine", "ShardGroup", "Cluster", "GossipError", "default_config", "comm_unique_id", "Config"]
 
 
 class GossipError(RuntimeError):
@@ -37,23 +47,51 @@ def default_config(n, **kw) -> Config:
     return cfg
 
 
+def comm_unique_id() -> bytes:
+    """RCCL unique id for a sharded cluster (rank 0 makes it, every rank uses it)."""
+    buf = (C.c_uint8 * _abi.GH_COMM_ID_BYTES)()
+    rc = _abi.load().gh_comm_unique_id(buf)
+    if rc != GH_OK:
+        raise GossipError(rc, "gh_comm_unique_id failed (RCCL missing?)")
+    return bytes(buf)
+
+
 def _p(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
 
 
 class Engine:
-    """One libgossiphip handle: N members' tables resident in HBM."""
+    """One libgossiphip handle: N members' tables resident in HBM, or rank
+    `rank` of `world` column shards of them (then every rank makes the same
+    calls and gets the same results)."""
 
-    def __init__(self, cfg: Config):
+    def __init__(self, cfg: Config, rank: int = 0, world: int = 1, transport: int | None = None,
+                 comm_id: bytes | None = None):
         self.lib = _abi.load()
         self.cfg = cfg
         self.n = cfg.n_members
         self.R = cfg.replicas
+        self.rank, self.world = rank, world
         h = C.c_void_p()
-        rc = self.lib.gh_create(C.byref(cfg), C.byref(h))
+        if world == 1 and comm_id is None:
+            rc = self.lib.gh_create(C.byref(cfg), C.byref(h))
+        else:
+            if comm_id is None or len(comm_id) > _abi.GH_COMM_ID_BYTES:
+                raise ValueError("a sharded engine needs a comm id of <= 128 bytes")
+            buf = (C.c_uint8 * _abi.GH_COMM_ID_BYTES).from_buffer_copy(
+                comm_id.ljust(_abi.GH_COMM_ID_BYTES, b"\0"))
+            tr = GH_COMM_LOCAL if transport is None else transport
+            rc = self.lib.gh_create_sharded(C.byref(cfg), rank, world, tr, buf, C.byref(h))
         if rc != GH_OK:
             raise GossipError(rc, "gh_create failed (a gfx950 device is required; no CPU fallback)")
         self.h = h
+
+    def shard_info(self):
+        """(rank, world, first member column, member columns) of this engine."""
+        r, w = C.c_int32(), C.c_int32()
+        c0, nc = C.c_int64(), C.c_int64()
+        self._chk(self.lib.gh_shard_info(self.h, C.byref(r), C.byref(w), C.byref(c0), C.byref(nc)))
+        return r.value, w.value, c0.value, nc.value
 
     def close(self):
         if getattr(self, "h", None):
@@ -178,6 +216,65 @@ class Engine:
 
     def sync(self):
         self._chk(self.lib.gh_sync(self.h))
+
+
+def _same(a, b):
+    if isinstance(a, np.ndarray):
+        return isinstance(b, np.ndarray) and a.shape == b.shape and np.array_equal(a, b)
+    if isinstance(a, (tuple, list)):
+        return type(a) is type(b) and len(a) == len(b) and all(_same(x, y) for x, y in zip(a, b))
+    if isinstance(a, dict):
+        return isinstance(b, dict) and a.keys() == b.keys() and all(_same(a[k], b[k]) for k in a)
+    return a == b
+
+
+class ShardGroup:
+    """One cluster column-sharded over `world` engines driven from this
+    process, one thread per rank (GH_COMM_LOCAL). Methods mirror Engine's;
+    each call runs on every rank concurrently (the SPMD contract) and
+    returns rank 0's result after checking that every rank agrees."""
+
+    _ids = itertools.count()
+
+    def __init__(self, cfg: Config, world: int, devices=None):
+        self.world = world
+        self.n = cfg.n_members
+        self.cfg = cfg
+        self.pool = ThreadPoolExecutor(max_workers=world)
+        key = f"gossipsim-{os.getpid()}-{next(self._ids)}".encode()
+        devices = devices or [cfg.device] * world
+
+        def make(r):
+            c = Config.from_buffer_copy(cfg)
+            c.device = devices[r]
+            return Engine(c, rank=r, world=world, transport=GH_COMM_LOCAL, comm_id=key)
+
+        self.engines = list(self.pool.map(make, range(world)))
+
+    def run(self, name, *args, **kw):
+        """Every rank's result of Engine.<name>(*args, **kw)."""
+        futs = [self.pool.submit(getattr(e, name), *args, **kw) for e in self.engines]
+        return [f.result() for f in futs]
+
+    def __getattr__(self, name):
+        if name.startswith("_") or not callable(getattr(Engine, name, None)):
+            raise AttributeError(name)
+
+        def call(*args, **kw):
+            res = self.run(name, *args, **kw)
+            for r, x in enumerate(res[1:], 1):
+                if not _same(res[0], x):
+                    raise AssertionError(f"rank {r} disagrees with rank 0 on {name}")
+            return res[0]
+        return call
+
+    @property
+    def round(self):
+        return self.engines[0].round
+
+    def close(self):
+        self.run("close")
+        self.pool.shutdown()
 
 
 class Cluster:

@@ -27,6 +27,8 @@ GH_ABSENT, GH_TOMBSTONE = -1, -2
 GH_PEER_PULL, GH_PEER_RING = 0, 1
 GH_DETECT_CANONICAL, GH_DETECT_QUIRK = 0, 1
 GH_EV_JOIN, GH_EV_LEAVE, GH_EV_CRASH = 1, 2, 3
+GH_COMM_RCCL, GH_COMM_LOCAL = 0, 1
+GH_COMM_ID_BYTES = 128
 
 
 class Config(C.Structure):
@@ -83,6 +85,9 @@ SYMBOLS = [
     ("gh_set_timing", C.c_int, [_vp, _i32]),
     ("gh_read_timing", C.c_int, [_vp, _P(C.c_double), _P(_i64)]),
     ("gh_sync", C.c_int, [_vp]),
+    ("gh_comm_unique_id", C.c_int, [_vp]),
+    ("gh_create_sharded", C.c_int, [_P(Config), _i32, _i32, _i32, _vp, _P(_vp)]),
+    ("gh_shard_info", C.c_int, [_vp, _P(_i32), _P(_i32), _P(_i64), _P(_i64)]),
 ]
 
 _lib = None
