@@ -1,9 +1,10 @@
 // Churn and state-maintenance kernels (SPEC.md §5, §3). All tables use the
 // tiled layout of gh_internal.h (gh_cell) over the shard's local columns.
 //   k_count        local present count per row (after events / import)
-//   k_flags        recompute the eligibility bit of imported rows
 //   k_fill         synthetic full-membership start (BASELINE configs 2-4)
-//   k_pack/unpack  host row order <-> tiled local columns (import/export/lsm)
+//   k_pack/unpack  host (hb, ts) rows <-> encoded tiled local columns
+//                  (import/export/lsm; gh_internal.h "cell encoding")
+//   k_freeze       exact ts of rows that stop (crash / leave) into ts[]
 //   k_rowbits      presence bitmap of some rows over the local columns (the
 //                  rows' lists, gathered across shards by the host)
 //   k_leave        LEAVE delivery: slave/slave.go:310-336 -> :232-235
@@ -33,13 +34,12 @@ __global__ __launch_bounds__(256) void k_count(GhDev d, int cur, GhRound p) {
   if (lane == 0) d.cntl[i] = cnt;
 }
 
-__device__ __forceinline__ int32_t with_flag(int32_t x, int32_t t, int64_t c, int64_t i,
-                                             int32_t lim_next) {
-  if (x >= 0) {
-    x &= GH_HBMASK;
-    if (x > 1 && c != i && t < lim_next) x |= GH_FLAG;
-  }
-  return x;
+// Encoded cell (member cg of row i) for external (hb, ts) in the round r
+// about to run.
+__device__ __forceinline__ int32_t encode(int32_t x, int32_t t, int64_t cg, int64_t i, const GhRound& p) {
+  if (x == GH_ABSENT) return GH_ABSENT;
+  const int a = min(max(p.r - t, 0), GH_AGE_CAP);
+  return x >= 0 ? gh_present(x, a, x > 1 && cg != i && t < p.r - p.t_fail) : gh_tomb(a);
 }
 
 // Storage-order walk over rows [row0, row0+nrows) of every local tile.
@@ -57,18 +57,6 @@ struct RowsWalk {
   }
 };
 
-__global__ __launch_bounds__(256) void k_flags(GhDev d, int cur, int64_t row0, int64_t nrows,
-                                               GhRound p) {
-  const RowsWalk w(d, nrows);
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < w.total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int64_t i, c, off;
-    w.at(d, idx, row0, i, c, off);
-    // p.r is the round about to run: eligible <=> ts < r - T_fail
-    d.hb[cur][off] = with_flag(d.hb[cur][off], d.ts[off], d.col0 + c, i, p.r - p.t_fail);
-  }
-}
-
 __global__ __launch_bounds__(256) void k_fill(GhDev d, int cur, int32_t hb0, int32_t ts0, GhRound p) {
   const RowsWalk w(d, p.n);
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < w.total;
@@ -76,7 +64,7 @@ __global__ __launch_bounds__(256) void k_fill(GhDev d, int cur, int32_t hb0, int
     int64_t i, c, off;
     w.at(d, idx, 0, i, c, off);
     if (c < d.ncol) {
-      d.hb[cur][off] = with_flag(hb0, ts0, d.col0 + c, i, p.r - p.t_fail);
+      d.hb[cur][off] = encode(hb0, ts0, d.col0 + c, i, p);
       d.ts[off] = ts0;
     } else {
       d.hb[cur][off] = GH_ABSENT;
@@ -85,28 +73,51 @@ __global__ __launch_bounds__(256) void k_fill(GhDev d, int cur, int32_t hb0, int
   }
 }
 
-__global__ __launch_bounds__(256) void k_pack(GhDev d, int32_t* dst, const int32_t* src, int64_t row0,
-                                              int64_t nrows) {
+__global__ __launch_bounds__(256) void k_pack(GhDev d, int cur, const int32_t* hb_rows, const int32_t* ts_rows,
+                                              int64_t row0, int64_t nrows, GhRound p) {
   const RowsWalk w(d, nrows);
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < w.total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     int64_t i, c, off;
     w.at(d, idx, row0, i, c, off);
-    if (c < d.ncol) dst[off] = src[(i - row0) * d.n + d.col0 + c];
+    if (c >= d.ncol) continue;
+    const int64_t src = (i - row0) * d.n + d.col0 + c;
+    d.hb[cur][off] = encode(hb_rows[src], ts_rows[src], d.col0 + c, i, p);
+    d.ts[off] = ts_rows[src];
   }
 }
 
-__global__ __launch_bounds__(256) void k_unpack(GhDev d, int32_t* dst, const int32_t* src, int64_t row0,
-                                                int64_t nrows, int strip) {
+// what = 0: external hb; what = 1: exact ts = r - age where the age has it
+// (alive rows, unsaturated), else the kept ts[].
+__global__ __launch_bounds__(256) void k_unpack(GhDev d, int cur, int32_t* dst, int64_t row0, int64_t nrows,
+                                                int what, GhRound p) {
   const RowsWalk w(d, nrows);
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < w.total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     int64_t i, c, off;
     w.at(d, idx, row0, i, c, off);
     if (c >= d.ncs) continue;
-    int32_t x = src[off];
-    if (strip && x >= 0) x &= GH_HBMASK;
+    const int32_t v = d.hb[cur][off];
+    int32_t x;
+    if (what == 0)
+      x = gh_ext(v);
+    else if (v != GH_ABSENT && d.alive[i] && gh_age(v) < GH_AGE_CAP)
+      x = p.r - gh_age(v);
+    else
+      x = d.ts[off];
     dst[(i - row0) * d.ncs + c] = x;
+  }
+}
+
+// A stopped row is frozen (k_round carries it unchanged) while the round
+// counter moves on, so its ages stop meaning anything: keep the exact ts.
+__global__ __launch_bounds__(256) void k_freeze(GhDev d, int cur, const int32_t* rows, int32_t nr, GhRound p) {
+  const int64_t total = (int64_t)nr * d.ncol;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t off = gh_cell(d, rows[idx / d.ncol], idx % d.ncol);
+    const int32_t v = d.hb[cur][off];
+    if (v != GH_ABSENT && gh_age(v) < GH_AGE_CAP) d.ts[off] = p.r - gh_age(v);
   }
 }
 
@@ -145,7 +156,7 @@ __global__ __launch_bounds__(256) void k_leave(GhDev d, int cur, const int32_t* 
       const int64_t off = gh_cell(d, j, lc);
       const int32_t x = hb[off];
       if (x >= 0) {
-        hb[off] = GH_TOMBSTONE;
+        hb[off] = gh_tomb(gh_age(x));  // keeps its ts (slave/slave.go:280)
         tomb++;
       } else if (x == GH_ABSENT) {
         unknown++;
@@ -179,8 +190,7 @@ __global__ void k_join_add(GhDev d, int cur, const int32_t* joiners, int32_t nj,
     if (lc < 0 || lc >= d.ncol) continue;
     const int64_t off = gh_cell(d, I, lc);
     if (d.hb[cur][off] < 0) {
-      d.hb[cur][off] = 0;
-      d.ts[off] = p.r;
+      d.hb[cur][off] = gh_present(0, 0);  // hb 0, ts = now (age 0 in round r)
       added++;
     }
   }
@@ -202,12 +212,10 @@ __global__ __launch_bounds__(256) void k_join_bcast(GhDev d, int cur, int32_t I,
     if (c >= d.ncol || j == I || !d.alive[j] || !gh_gbit(d, d.rbits, 1, 0, j)) continue;
     const int32_t mv = hb[gh_cell(d, I, c)];
     if (mv < 0) continue;
-    const int32_t m = mv & GH_HBMASK;
-    const int32_t xr = hb[off];
-    const int32_t x = xr >= 0 ? (xr & GH_HBMASK) : xr;
+    const int32_t m = gh_hbv(mv);
+    const int32_t x = gh_ext(hb[off]);
     if (x >= GH_ABSENT && m > x) {
-      hb[off] = m;  // ts = now: never eligible next round, so no flag
-      d.ts[off] = p.r;
+      hb[off] = gh_present(m, 0);  // ts = now: not stale next round
       merged++;
     }
   }
@@ -224,28 +232,25 @@ void launch_count(const GhDev& d, int cur, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_count, dim3((p.n + 3) / 4), dim3(256), 0, s, d, cur, p);
 }
 
-void launch_flags(const GhDev& d, int cur, int64_t row0, int64_t nrows, const GhRound& p,
-                  hipStream_t s) {
-  if (nrows == 0) return;
-  hipLaunchKernelGGL(k_flags, dim3(grid_for(nrows * p.ld)), dim3(256), 0, s, d, cur, row0, nrows, p);
-}
-
 void launch_fill(const GhDev& d, int cur, int32_t hb0, int32_t ts0, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_fill, dim3(grid_for((int64_t)p.n * p.ld)), dim3(256), 0, s, d, cur, hb0, ts0, p);
 }
 
-void launch_pack(const GhDev& d, int32_t* dst_tiled, const int32_t* src_rows, int64_t row0, int64_t nrows,
-                 hipStream_t s) {
+void launch_pack(const GhDev& d, int cur, const int32_t* hb_rows, const int32_t* ts_rows, int64_t row0,
+                 int64_t nrows, const GhRound& p, hipStream_t s) {
   if (nrows == 0) return;
-  hipLaunchKernelGGL(k_pack, dim3(grid_for(nrows * d.ld)), dim3(256), 0, s, d, dst_tiled, src_rows, row0,
-                     nrows);
+  hipLaunchKernelGGL(k_pack, dim3(grid_for(nrows * d.ld)), dim3(256), 0, s, d, cur, hb_rows, ts_rows, row0, nrows, p);
 }
 
-void launch_unpack(const GhDev& d, int32_t* dst_rows, const int32_t* src_tiled, int64_t row0, int64_t nrows,
-                   int strip_flag, hipStream_t s) {
+void launch_unpack(const GhDev& d, int cur, int32_t* dst_rows, int64_t row0, int64_t nrows, int what,
+                   const GhRound& p, hipStream_t s) {
   if (nrows == 0) return;
-  hipLaunchKernelGGL(k_unpack, dim3(grid_for(nrows * d.ld)), dim3(256), 0, s, d, dst_rows, src_tiled, row0,
-                     nrows, strip_flag);
+  hipLaunchKernelGGL(k_unpack, dim3(grid_for(nrows * d.ld)), dim3(256), 0, s, d, cur, dst_rows, row0, nrows, what, p);
+}
+
+void launch_freeze(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p, hipStream_t s) {
+  if (nr == 0 || d.ncol == 0) return;
+  hipLaunchKernelGGL(k_freeze, dim3(grid_for((int64_t)nr * d.ncol)), dim3(256), 0, s, d, cur, rows, nr, p);
 }
 
 void launch_rowbits(const GhDev& d, int cur, const int32_t* rows, int32_t nr, hipStream_t s) {

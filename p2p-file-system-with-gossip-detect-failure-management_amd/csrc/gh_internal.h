@@ -16,9 +16,24 @@
 //   N=65,536, TW=64): the round kernel sweeps tile by tile, so its own-row
 //   streams are sequential and every peer gather of a tile stays inside
 //   that slice.
-//   hb[2]  int32   double-buffered heartbeat table; bit 30 of a present cell =
-//                  next-round detection eligibility; -1 absent, -2 tombstone.
-//   ts     int32   local-clock tick of each cell, updated in place.
+//   hb[2]  int32   double-buffered membership table, one word per cell:
+//                    present    0 <= v:  heartbeat in bits 0..22, age in
+//                                        23..29, flag in bit 30
+//                    tombstone  v < -1:  INT_MIN | age << 23
+//                    absent     v == -1
+//                  age = (last completed round + 1) - ts, the cell's age in the
+//                  round about to run, saturating at GH_AGE_CAP. flag = the
+//                  row's process detects the member in that round (SPEC §2
+//                  step 4: hb > 1, member != observer, ts < r - T_fail),
+//                  decided when the cell is written, so neither the row nor
+//                  the peers reading it as a snapshot re-derive it. Every
+//                  decision of a round on ts is a flag test or an age
+//                  comparison: a round reads and writes one table, not two.
+//   ts     int32   exact local-clock tick, kept only where the age cannot give
+//                  it: saturated cells (written when the age reaches the cap),
+//                  absent cells (written on release), rows that stopped
+//                  (written by k_freeze) and imports. export_state decodes
+//                  ts = (round + 1) - age for the other cells.
 //   Local columns are padded to ld (multiple of 8*TW and 256); padding cells
 //   stay -1.
 //   per row (global): alive, active, und (u8), cntl / cntg (local / global
@@ -32,8 +47,10 @@
 
 #include "../../include/gossiphip.h"
 
-#define GH_FLAG (1 << 30)        // eligibility bit inside a present hb cell
-#define GH_HBMASK (GH_FLAG - 1)  // heartbeat value bits
+#define GH_HB_BITS 23
+#define GH_HB_MAX ((1 << GH_HB_BITS) - 1)  // largest heartbeat a cell holds (saturates)
+#define GH_AGE_CAP 127                     // age saturates here; exact ts is then in ts[]
+#define GH_FLAG (1 << 30)                  // detected next round (present cells)
 #define GH_PAD 256               // column padding granule (ld % 256 == 0)
 #define GH_RB 64                 // rows per workgroup tile in the round kernel
 #define GH_MAXK 8                // max pull fanout
@@ -115,9 +132,55 @@ struct GhDev {
   int64_t io_cap;
 };
 
+// ---- cell encoding --------------------------------------------------------
+__host__ __device__ __forceinline__ int gh_age(int32_t v) { return (v >> GH_HB_BITS) & GH_AGE_CAP; }
+__host__ __device__ __forceinline__ int32_t gh_hbv(int32_t v) { return v & GH_HB_MAX; }
+__host__ __device__ __forceinline__ int32_t gh_present(int32_t hb, int age, bool flag = false) {
+  return hb | (age << GH_HB_BITS) | (flag ? GH_FLAG : 0);
+}
+__host__ __device__ __forceinline__ int32_t gh_tomb(int age) {
+  return (int32_t)(0x80000000u | ((uint32_t)age << GH_HB_BITS));
+}
+// age one round later (saturating)
+__host__ __device__ __forceinline__ int gh_inc(int a) { return a < GH_AGE_CAP ? a + 1 : GH_AGE_CAP; }
+// external value (>= 0 heartbeat, -1 absent, -2 tombstone)
+__host__ __device__ __forceinline__ int32_t gh_ext(int32_t v) {
+  return v >= 0 ? gh_hbv(v) : (v == GH_ABSENT ? GH_ABSENT : GH_TOMBSTONE);
+}
+
 // Linear index of cell (observer i, LOCAL member column c) in the tiled layout.
 __host__ __device__ __forceinline__ int64_t gh_cell(const GhDev& d, int64_t i, int64_t c) {
   return (c >> d.lgtw) * d.tstride + (i << d.lgtw) + (c & (d.tw - 1));
+}
+
+// ts < r - T for a present or tombstoned cell (stored v at table offset off)
+// in round r: the age decides, except for a saturated age when T itself
+// reaches the cap (then the exact ts is in d.ts).
+// EXACT = false is the form for T < GH_AGE_CAP (every realistic timeout):
+// pure register arithmetic, no conditional load in the streaming loops.
+template <bool EXACT = true>
+__device__ __forceinline__ bool gh_stale(const GhDev& d, int32_t v, int64_t off, int32_t r, int32_t T) {
+  const int a = gh_age(v);
+  if constexpr (!EXACT) {
+    return a > T;
+  } else {
+    if (a < GH_AGE_CAP || T < GH_AGE_CAP) return a > T;
+    return d.ts[off] < r - T;
+  }
+}
+
+// The flag of a present cell written for round rn (member cg of row i, exact
+// ts: age < cap ? rn - age : ts[off]).
+template <bool EXACT>
+__device__ __forceinline__ bool gh_flag_for(const GhDev& d, int32_t hb, int age, int64_t cg, int64_t i, int64_t off,
+                                           int32_t rn, int32_t t_fail) {
+  if (hb <= 1 || cg == i) return false;
+  if constexpr (!EXACT) {
+    return age > t_fail;
+  } else {
+    if (age < GH_AGE_CAP || t_fail < GH_AGE_CAP) return age > t_fail;
+    return d.ts[off] < rn - t_fail;
+  }
 }
 
 // Bit of GLOBAL member j in row q of a gathered bitmap [world][nr][ncsw].
@@ -137,6 +200,7 @@ struct GhRound {
   uint64_t seed;
   int32_t peer_mode;
   int32_t xmap;       // k_round block->tile map: 0 tile-major, 1 XCD-aware
+  int32_t tpw;        // k_round tiles per workgroup (1, 2, 4, 8)
   int32_t ablate;     // timing-only experiments (results wrong): 1 = every
                       // peer load reads the own row, 2 = no peer loads. 0 always
                       // in production (set only through GH_ROUND_ABLATE).
@@ -156,16 +220,18 @@ void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);
 // events.hip
 void launch_count(const GhDev& d, int cur, const GhRound& p, hipStream_t s);
-void launch_flags(const GhDev& d, int cur, int64_t row0, int64_t nrows, const GhRound& p,
-                  hipStream_t s);
 void launch_fill(const GhDev& d, int cur, int32_t hb0, int32_t ts0, const GhRound& p,
                  hipStream_t s);
-// full rows [nrows][n] (host order) -> tiled local columns
-void launch_pack(const GhDev& d, int32_t* dst_tiled, const int32_t* src_rows, int64_t row0,
-                 int64_t nrows, hipStream_t s);
-// tiled local columns -> [nrows][ncs] (local column order)
-void launch_unpack(const GhDev& d, int32_t* dst_rows, const int32_t* src_tiled, int64_t row0,
-                   int64_t nrows, int strip_flag, hipStream_t s);
+// full host rows (hb, ts: [nrows][n]) -> encoded tiled local columns; p.r is
+// the round about to run
+void launch_pack(const GhDev& d, int cur, const int32_t* hb_rows, const int32_t* ts_rows, int64_t row0,
+                 int64_t nrows, const GhRound& p, hipStream_t s);
+// tiled local columns -> [nrows][ncs] (local column order) of the external hb
+// (what = 0) or the exact ts (what = 1); p.r is the round about to run
+void launch_unpack(const GhDev& d, int cur, int32_t* dst_rows, int64_t row0, int64_t nrows, int what,
+                   const GhRound& p, hipStream_t s);
+// rows that stop (crash / leave): exact ts of their cells into ts[]
+void launch_freeze(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p, hipStream_t s);
 // presence bitmaps of rows[0..nr) over the local columns -> rbits + rank*nr*ncsw
 void launch_rowbits(const GhDev& d, int cur, const int32_t* rows, int32_t nr, hipStream_t s);
 void launch_leave(const GhDev& d, int cur, const int32_t* leavers, int32_t nl, const GhRound& p,

@@ -47,6 +47,7 @@ struct Engine {
   bool nt = true;        // k_round non-temporal streams (gh_set_round_variant)
   int ablate = 0;        // timing-only experiment switch (GH_ROUND_ABLATE), never set in production
   int xmap = 0;          // k_round XCD-aware tile map (gh_set_round_variant)
+  int tpw = 8;           // k_round tiles per workgroup (GH_ROUND_TPW)
   bool timing = false;
   double timed_ms = 0.0;
   int64_t timed_launches = 0;
@@ -122,6 +123,7 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.peer_mode = e->cfg.peer_mode;
   p.ablate = e->ablate;
   p.xmap = e->xmap;
+  p.tpw = e->tpw;
   return p;
 }
 
@@ -179,15 +181,25 @@ int process_events(Engine* e, int32_t r) {
   const GhRound p = round_params(e, r);
   std::vector<gh_event> ev;
   ev.swap(e->pending);
+  std::vector<int32_t> stopped;  // rows that stop running this round
   for (const auto& x : ev)
-    if (x.kind == GH_EV_CRASH) e->alive[x.member] = 0;
+    if (x.kind == GH_EV_CRASH && e->alive[x.member]) {
+      e->alive[x.member] = 0;
+      stopped.push_back(x.member);
+    }
   std::vector<int32_t> leavers;
   for (const auto& x : ev)
     if (x.kind == GH_EV_LEAVE && e->alive[x.member]) {
       e->alive[x.member] = 0;
       leavers.push_back(x.member);
+      stopped.push_back(x.member);
     }
   int rc;
+  if (!stopped.empty()) {
+    if ((rc = upload(e, e->ev_buf, stopped))) return rc;
+    launch_freeze(e->d, e->cur, e->ev_buf, (int32_t)stopped.size(), p, e->stream);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
   if ((rc = upload_alive(e))) return rc;
   if (!leavers.empty()) {
     if ((rc = upload(e, e->ev_buf, leavers))) return rc;
@@ -252,15 +264,16 @@ int check_files(Engine* e, const int32_t* files, int64_t n, bool distinct) {
   return GH_OK;
 }
 
-// Rows [row0, row0+n_rows) of a table (tiled local columns on every shard)
-// -> host row order [n_rows][n].
-int export_table(Engine* e, int32_t* out, const int32_t* table, int64_t row0, int64_t n_rows, int strip) {
+// Rows [row0, row0+n_rows) of the external hb (what = 0) or ts (what = 1),
+// decoded from the tiled local columns of every shard -> host [n_rows][n].
+int export_table(Engine* e, int32_t* out, int what, int64_t row0, int64_t n_rows) {
   const GhDev& d = e->d;
   const size_t chunk = (size_t)n_rows * d.ncs;  // one shard's [n_rows][ncs]
   Staging st;
   int rc;
   if ((rc = st.alloc(e, sizeof(int32_t) * chunk * e->world))) return rc;
-  launch_unpack(d, st.as<int32_t>() + chunk * e->rank, table, row0, n_rows, strip, e->stream);
+  launch_unpack(d, e->cur, st.as<int32_t>() + chunk * e->rank, row0, n_rows, what, round_params(e, e->round + 1),
+                e->stream);
   HIPCHK(e, hipGetLastError());
   COMMCHK(e, e->comm->allgather(st.as<int32_t>() + chunk * e->rank, st.p, sizeof(int32_t) * chunk, e->stream));
   std::vector<int32_t> host(chunk * e->world);
@@ -284,7 +297,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
       (cfg->peer_mode != GH_PEER_PULL && cfg->peer_mode != GH_PEER_RING) ||
       (cfg->detect_mode != GH_DETECT_CANONICAL && cfg->detect_mode != GH_DETECT_QUIRK) ||
       cfg->introducer < 0 || cfg->introducer >= cfg->n_members || cfg->master < 0 ||
-      cfg->master >= cfg->n_members)
+      cfg->master >= cfg->n_members || cfg->t_fail < 0 || cfg->t_cleanup < 0)
     return GH_EINVAL;
   if (world < 1 || rank < 0 || rank >= world) return GH_EINVAL;
   if (world > 1 && !comm_id) return GH_EINVAL;
@@ -311,6 +324,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_ROUND_XMAP")) e->xmap = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_ROUND_ABLATE")) e->ablate = std::atoi(v);
+  if (const char* v = std::getenv("GH_ROUND_TPW")) e->tpw = std::atoi(v);
+  if (e->tpw != 1 && e->tpw != 2 && e->tpw != 4 && e->tpw != 8) e->tpw = 8;
   if (tw != 8 && tw != 16 && tw != 32 && tw != 64 && tw != 128 && tw != 256) {
     delete e;
     return GH_EINVAL;
@@ -535,28 +550,28 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
   if (!e) return GH_EINVAL;
   if (row0 < 0 || n_rows < 0 || row0 + n_rows > e->n || (n_rows > 0 && (!hb || !ts || !alive)))
     return set_err(e, GH_EINVAL, "row range / null buffer");
-  for (int64_t x = 0; x < n_rows * e->n; ++x)
-    if (hb[x] < GH_TOMBSTONE || hb[x] >= GH_FLAG) return set_err(e, GH_ERANGE, "hb value out of range");
+  for (int64_t x = 0; x < n_rows * e->n; ++x) {
+    if (hb[x] < GH_TOMBSTONE || hb[x] > GH_HB_MAX) return set_err(e, GH_ERANGE, "hb value out of range");
+    if (hb[x] != GH_ABSENT && (int64_t)ts[x] > (int64_t)round + 1)
+      return set_err(e, GH_ERANGE, "ts of a listed member after the round being imported");
+  }
   HIPCHK(e, hipSetDevice(e->cfg.device));
   int rc;
+  const GhRound p = round_params(e, round + 1);
   if (n_rows > 0) {
-    // host rows -> device staging -> tiled local columns
-    Staging st;
+    // host rows -> device staging -> encoded tiled local columns
+    Staging sh, st;
     const size_t bytes = sizeof(int32_t) * e->n * n_rows;
-    if ((rc = st.alloc(e, bytes))) return rc;
-    HIPCHK(e, hipMemcpyAsync(st.p, hb, bytes, hipMemcpyHostToDevice, e->stream));
-    launch_pack(e->d, e->d.hb[e->cur], st.as<int32_t>(), row0, n_rows, e->stream);
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if ((rc = sh.alloc(e, bytes)) || (rc = st.alloc(e, bytes))) return rc;
+    HIPCHK(e, hipMemcpyAsync(sh.p, hb, bytes, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(st.p, ts, bytes, hipMemcpyHostToDevice, e->stream));
-    launch_pack(e->d, e->d.ts, st.as<int32_t>(), row0, n_rows, e->stream);
+    launch_pack(e->d, e->cur, sh.as<int32_t>(), st.as<int32_t>(), row0, n_rows, p, e->stream);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     std::copy(alive, alive + n_rows, e->alive.begin() + row0);
   }
   if ((rc = upload_alive(e))) return rc;
   e->round = round;
   e->pending.clear();
-  const GhRound p = round_params(e, round + 1);
-  launch_flags(e->d, e->cur, row0, n_rows, p, e->stream);
   if ((rc = reset_pending_removes(e))) return rc;
   launch_count(e->d, e->cur, p, e->stream);
   HIPCHK(e, hipGetLastError());
@@ -570,8 +585,8 @@ int gh_export_state(void* h, int32_t* hb, int32_t* ts, uint8_t* alive, int64_t r
   if (row0 < 0 || n_rows < 0 || row0 + n_rows > e->n) return set_err(e, GH_EINVAL, "row range");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   int rc;
-  if (n_rows > 0 && hb && (rc = export_table(e, hb, e->d.hb[e->cur], row0, n_rows, 1))) return rc;
-  if (n_rows > 0 && ts && (rc = export_table(e, ts, e->d.ts, row0, n_rows, 0))) return rc;
+  if (n_rows > 0 && hb && (rc = export_table(e, hb, 0, row0, n_rows))) return rc;
+  if (n_rows > 0 && ts && (rc = export_table(e, ts, 1, row0, n_rows))) return rc;
   if (alive) std::copy(e->alive.begin() + row0, e->alive.begin() + row0 + n_rows, alive);
   return GH_OK;
 }
@@ -579,7 +594,8 @@ int gh_export_state(void* h, int32_t* hb, int32_t* ts, uint8_t* alive, int64_t r
 int gh_init_full(void* h, int32_t hb0, int32_t ts0, int32_t round) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
-  if (hb0 < 0 || hb0 >= GH_FLAG) return set_err(e, GH_ERANGE, "hb0 out of range");
+  if (hb0 < 0 || hb0 > GH_HB_MAX) return set_err(e, GH_ERANGE, "hb0 out of range");
+  if ((int64_t)ts0 > (int64_t)round + 1) return set_err(e, GH_ERANGE, "ts0 after the start round");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   std::fill(e->alive.begin(), e->alive.end(), 1);
   int rc;

@@ -135,9 +135,10 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
       const uint32_t w = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
       const int s = (int)w + ((int64_t)w >= i);
       if (!d.alive[s] || !d.active[s]) continue;
-      const int32_t v = d.hb[cur][gh_cell(d, s, t)];
+      const int64_t off = gh_cell(d, s, t);
+      const int32_t v = d.hb[cur][off];
       // i must be in s's snapshot list: present, not detected by s this
-      // round (eligibility flag) and not REMOVE'd at s in step 1.
+      // round and not REMOVE'd at s in step 1.
       if (v < 0 || (v & GH_FLAG)) continue;
       if (ib && removes_at(dci, dmi, s)) continue;
       d.inbox[beg + nv++] = s;
@@ -147,10 +148,12 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
 }
 
 // Is local column c in sender sdr's snapshot list (after steps 1-5)?
-__device__ __forceinline__ bool snap_present(const GhDev& d, const int32_t* hb, int dcur, int sdr, int64_t c) {
-  const int32_t v = hb[gh_cell(d, sdr, c)];
+__device__ __forceinline__ bool snap_present(const GhDev& d, const int32_t* hb, int dcur, int sdr, int64_t c,
+                                             const GhRound& p) {
+  const int64_t off = gh_cell(d, sdr, c);
+  const int32_t v = hb[off];
   if (v < 0) return false;
-  if ((v & GH_FLAG) && d.col0 + c != sdr) return false;  // detected by the sender this round
+  if (v & GH_FLAG) return false;  // detected by the sender this round
   if (dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], sdr)) return false;
   return true;
 }
@@ -191,7 +194,7 @@ __global__ __launch_bounds__(256) void k_ring_count(GhDev d, int cur, int dcur, 
   const int per = (d.ncol + 255) / 256;
   const int b = min(d.ncol, tid * per), e = min(d.ncol, b + per);
   int cnt = 0;
-  for (int c = b; c < e; ++c) cnt += snap_present(d, hb, dcur, sdr, c);
+  for (int c = b; c < e; ++c) cnt += snap_present(d, hb, dcur, sdr, c, p);
   int total;
   const int off = block_excl_scan(cnt, s_tmp, &total);
   const int64_t ls = (int64_t)sdr - d.col0;
@@ -201,9 +204,9 @@ __global__ __launch_bounds__(256) void k_ring_count(GhDev d, int cur, int dcur, 
   }
   if (ls >= b && ls < e) {
     int pos = -1;
-    if (snap_present(d, hb, dcur, sdr, ls)) {
+    if (snap_present(d, hb, dcur, sdr, ls, p)) {
       pos = off;
-      for (int c = b; c < ls; ++c) pos += snap_present(d, hb, dcur, sdr, c);
+      for (int c = b; c < ls; ++c) pos += snap_present(d, hb, dcur, sdr, c, p);
     }
     out[1] = pos;
   }
@@ -249,11 +252,11 @@ __global__ __launch_bounds__(256) void k_ring_select(GhDev d, int cur, int dcur,
         const int per = (d.ncol + 255) / 256;
         const int b = min(d.ncol, tid * per), e = min(d.ncol, b + per);
         int cnt = 0;
-        for (int c = b; c < e; ++c) cnt += snap_present(d, hb, dcur, sdr, c);
+        for (int c = b; c < e; ++c) cnt += snap_present(d, hb, dcur, sdr, c, p);
         int total;
         int rank = block_excl_scan(cnt, s_tmp, &total);
         for (int c = b; c < e; ++c) {
-          if (!snap_present(d, hb, dcur, sdr, c)) continue;
+          if (!snap_present(d, hb, dcur, sdr, c, p)) continue;
 #pragma unroll
           for (int q = 0; q < 3; ++q)
             if (want[q] == rank) s_tgt[q] = (int)(d.col0 + c);
@@ -346,7 +349,7 @@ constexpr int round_rb() {
   return 1024 / TW > GH_RB ? 1024 / TW : GH_RB;
 }
 
-template <int KB, int TW, bool NT>
+template <int KB, int TW, int TPW, bool NT, bool EXACT>
 __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRound p) {
   constexpr int SEG = TW / 4;
   constexpr int RPW = 64 / SEG;
@@ -356,46 +359,76 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   __shared__ int s_dmin[TW];
   __shared__ uint16_t s_part[RB];
   __shared__ unsigned long long s_st[ST_COUNT];
+  // per-row metadata of the workgroup's rows, staged once for its TPW tiles
+  // so that every row iteration issues its own and its peers' loads back to
+  // back: s_meta = alive | active << 1 | inbox count << 2; s_inb = first KB
+  // senders
+  __shared__ int s_meta[RB];
+  __shared__ int s_beg[RB];
+  __shared__ int s_inb[RB * KB];
 
+  // block -> (tile group of TPW consecutive tiles, row block); group-major so
+  // that the running workgroups sweep the same tiles together
   const int nrb = (p.n + RB - 1) / RB;
-  int tile, rb;
-  if (p.xmap) {
+  const int ngroups = (int)(p.ld / TW) / TPW;
+  int group, rb;
+  if (p.xmap && ngroups % 8 == 0) {
     // XCD-aware: blocks b and b+8 share an XCD (round-robin dispatch, speed
-    // only), so XCD x = b % 8 sweeps tiles x, x+8, ... and its L2 holds the
-    // slice of the tile it is on. Needs (ld / TW) % 8 == 0 (host pads ld).
+    // only), so XCD x = b % 8 sweeps groups x, x+8, ... and its L2 holds the
+    // slice it is on.
     const int x = blockIdx.x & 7;
     const int j = blockIdx.x >> 3;
-    tile = x + 8 * (j / nrb);
+    group = x + 8 * (j / nrb);
     rb = j - (j / nrb) * nrb;
   } else {
-    tile = blockIdx.x / nrb;
-    rb = blockIdx.x - tile * nrb;
+    group = blockIdx.x / nrb;
+    rb = blockIdx.x - group * nrb;
   }
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = uni(tid >> 6);
   const int sub = lane / SEG;
   const int lc = lane % SEG;
-  const int64_t l0 = (int64_t)tile * TW + lc * 4;               // local column of this lane's first cell
-  const int64_t c0 = d.col0 + l0;                               // its global member id
-  const int64_t tb = (int64_t)tile * ((int64_t)p.n * TW) + lc * 4;  // tile base + lane offset
 
-  for (int t = tid; t < TW; t += 256) {
-    s_dcnt[t] = 0;
-    s_dmin[t] = INT_MAX;
-  }
   if (tid < ST_COUNT) s_st[tid] = 0;
-  if (tid < RB) s_part[tid] = 0;
+  const bool pull = p.peer_mode == GH_PEER_PULL;
+  for (int t = tid; t < RB; t += 256) {
+    const int i = rb * RB + t;
+    int meta = 0, beg = 0;
+    if (i < p.n) {
+      const int al = d.alive[i];
+      meta = al | (d.active[i] << 1) | ((al ? d.inbox_cnt[i] : 0) << 2);
+      beg = pull ? i * p.k : d.inbox_beg[i];
+    }
+    if (p.ablate == 2) meta &= 3;
+    s_meta[t] = meta;
+    s_beg[t] = beg;
+  }
+  __syncthreads();
+  for (int t = tid; t < RB * KB; t += 256) {
+    const int row = t / KB, q = t - row * KB;
+    s_inb[t] = q < (s_meta[row] >> 2) ? d.inbox[s_beg[row] + q] : 0;
+  }
   __syncthreads();
 
   const int32_t* __restrict__ hbo = d.hb[cur];
   int32_t* __restrict__ hbn = d.hb[cur ^ 1];
   int32_t* __restrict__ tsb = d.ts;
   const int32_t r = p.r;
-  const int32_t lim_fail = r - p.t_fail;
-  const int32_t lim_clean = r - p.t_cleanup;
-  const int32_t lim_next = r + 1 - p.t_fail;
-  const bool pull = p.peer_mode == GH_PEER_PULL;
+  int n_unknown = 0, n_tomb = 0, n_det = 0, n_rel = 0, n_merged = 0;
+
+#pragma unroll 1
+  for (int tt = 0; tt < TPW; ++tt) {
+  const int tile = group * TPW + tt;
+  const int64_t l0 = (int64_t)tile * TW + lc * 4;                   // local column of this lane's first cell
+  const int64_t c0 = d.col0 + l0;                                   // its global member id
+  const int64_t tb = (int64_t)tile * ((int64_t)p.n * TW) + lc * 4;  // tile base + lane offset
+  for (int t = tid; t < TW; t += 256) {
+    s_dcnt[t] = 0;
+    s_dmin[t] = INT_MAX;
+  }
+  for (int t = tid; t < RB; t += 256) s_part[t] = 0;
+  __syncthreads();
 
   // REMOVE bits of this lane's 4 members (rare: slow path only when set)
   const uint32_t my4 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFu;
@@ -408,78 +441,89 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     }
   }
 
-  int n_unknown = 0, n_tomb = 0, n_det = 0, n_rel = 0, n_merged = 0;
-
-  for (int rr0 = wave * RPW; rr0 < RB; rr0 += RSTEP) {
-    const int rr = rr0 + sub;
-    const int i_raw = rb * RB + rr;
-    const bool valid = i_raw < p.n;
-    if (!__any(valid)) break;
-    const int i = valid ? i_raw : p.n - 1;  // in-range row for the loads of idle lanes
-    const int64_t off = tb + (int64_t)i * TW;
-    int al, ac, beg, cntv;
-    if constexpr (RPW == 1) {
-      al = uni(d.alive[i]);
-      ac = uni(d.active[i]);
-      beg = pull ? i * p.k : uni(d.inbox_beg[i]);
-      cntv = al ? uni(d.inbox_cnt[i]) : 0;
-    } else {
-      al = d.alive[i] && valid;
-      ac = d.active[i];
-      beg = pull ? i * p.k : d.inbox_beg[i];
-      cntv = al ? d.inbox_cnt[i] : 0;
+  // One row iteration = RPW rows per wave: the own segment and the first KB
+  // senders' segments are issued together, then merged.
+  struct Rows {
+    v4i v;        // own segment
+    v4i pv[KB];   // first KB senders' segments
+    int ps[KB];   // their row ids
+    int meta, i, rr;
+    bool valid;
+  };
+  auto issue = [&](Rows& L, int it) {
+    L.rr = wave * RPW + it * RSTEP + sub;
+    const int i_raw = rb * RB + L.rr;
+    L.valid = i_raw < p.n;
+    L.i = L.valid ? i_raw : p.n - 1;  // in-range row for the loads of idle lanes
+    const int rs = L.valid ? L.rr : 0;
+    int meta = s_meta[rs];
+    if constexpr (RPW == 1) meta = uni(meta);
+    L.meta = meta;
+    const int cntv = meta >> 2;
+    L.v = ldv<false>(hbo + tb + (int64_t)L.i * TW);  // re-read by peers: keep it cached
+#pragma unroll
+    for (int q = 0; q < KB; ++q) {
+      int s = L.i;
+      if (q < cntv) {
+        s = s_inb[rs * KB + q];
+        if constexpr (RPW == 1) s = uni(s);
+      }
+      L.ps[q] = s;
+      L.pv[q] = ldv<false>(hbo + tb + (int64_t)(p.ablate == 1 ? L.i : s) * TW);
     }
-    const v4i v = ldv<false>(hbo + off);  // re-read by peers: keep it cached
-    v4i t4 = {0, 0, 0, 0};
-    if (al) t4 = ldv<NT>(tsb + off);
+  };
+  auto merge_seg = [&](int m[4], const v4i& x4, int s) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int x = x4[j];
+      // sender snapshot: present and not detected by s (sign and flag
+      // clear), +1 on s's diagonal
+      int val = (x & (int)(0x80000000u | GH_FLAG)) ? -1 : gh_hbv(x) + ((c0 + j) == s);
+      if (((my4 >> j) & 1u) && removes_at(dc[j], dm[j], s)) val = -1;
+      m[j] = max(m[j], val);
+    }
+  };
 
-    if (p.ablate == 2) cntv = 0;
+  constexpr int NIT = RB / RSTEP;
+#pragma unroll 1
+  for (int it = 0; it < NIT; ++it) {
+    Rows L;
+    issue(L, it);
+    const int i = L.i;
+    const int64_t off = tb + (int64_t)i * TW;
+    const int al = (L.meta & 1) && L.valid;
+    const int ac = (L.meta >> 1) & 1;
+    const int cntv = L.meta >> 2;
+
+    int m[4] = {-1, -1, -1, -1};
+#pragma unroll
+    for (int q = 0; q < KB; ++q)
+      if (q < cntv) merge_seg(m, L.pv[q], L.ps[q]);
+    // rare: more senders than KB (ring mode hubs)
     int cmax = cntv;
     if constexpr (RPW > 1) {
 #pragma unroll
       for (int o = SEG; o < 64; o <<= 1) cmax = max(cmax, __shfl_xor(cmax, o));
     }
-    int m[4] = {-1, -1, -1, -1};
-    for (int base = 0; base < cmax; base += KB) {
-      v4i pv[KB];
-      int ps[KB];
-#pragma unroll
-      for (int q = 0; q < KB; ++q) {
-        int s = i;
-        if (base + q < cntv) {
-          if constexpr (RPW == 1)
-            s = uni(d.inbox[beg + base + q]);
-          else
-            s = d.inbox[beg + base + q];
-        }
-        ps[q] = s;
-        pv[q] = ldv<false>(hbo + tb + (int64_t)(p.ablate == 1 ? i : s) * TW);
-      }
-#pragma unroll
-      for (int q = 0; q < KB; ++q) {
-        if (base + q >= cntv) continue;
-        const int s = ps[q];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int x = pv[q][j];
-          // sender snapshot: present, not detected by s (flag), +1 on s's diagonal
-          int val = (x >= 0 && !(x & GH_FLAG)) ? x + ((c0 + j) == s) : -1;
-          if (((my4 >> j) & 1u) && removes_at(dc[j], dm[j], s)) val = -1;
-          m[j] = max(m[j], val);
-        }
+    for (int q = KB; q < cmax; ++q) {
+      if (q < cntv) {
+        const int s = d.inbox[s_beg[L.valid ? L.rr : 0] + q];
+        merge_seg(m, ldv<false>(hbo + tb + (int64_t)s * TW), s);
       }
     }
 
-    v4i xo = v;
-    v4i to = t4;
+    v4i xo = L.v;
     int npres = 0;
     bool any_det = false;
     if (al) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int64_t c = c0 + j;
-        int x = xo[j] >= 0 ? (xo[j] & GH_HBMASK) : xo[j];
-        int t = to[j];
+        const int64_t oj = off + j;
+        const int32_t w = xo[j];
+        int x = gh_ext(w);
+        const int a = gh_age(w);  // meaningful unless absent
+        bool now = false;         // ts := r in this round
         // step 1: REMOVE delivery (slave/slave.go:236-240, 276-286)
         if (((my4 >> j) & 1u) && removes_at(dc[j], dm[j], i)) {
           if (x >= 0) {
@@ -490,62 +534,62 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
           }
         }
         if (!ac) {
-          if (x >= 0) t = r;  // step 2 guard (:505-507)
+          if (x >= 0) now = true;  // step 2 guard (:505-507)
         } else {
           if (c == i) {
             if (x >= 0) {  // step 3 own heartbeat (:443-448)
-              x += 1;
-              t = r;
+              x = min(x + 1, GH_HB_MAX);
+              now = true;
             }
-          } else if (x > 1 && t < lim_fail) {  // step 4 detect (:468-473)
+          } else if (x >= 0 && (w & GH_FLAG)) {  // step 4 detect (:468-473), decided at the last write
             x = GH_TOMBSTONE;
             n_det++;
             any_det = true;
             atomicAdd(&s_dcnt[lc * 4 + j], 1);
             atomicMin(&s_dmin[lc * 4 + j], i);
           }
-          if (x == GH_TOMBSTONE && t < lim_clean) {  // step 5 clean (:490-492)
+          if (x == GH_TOMBSTONE && gh_stale<EXACT>(d, w, oj, r, p.t_cleanup)) {  // step 5 clean (:490-492)
             x = GH_ABSENT;
             n_rel++;
+            if (a < GH_AGE_CAP) tsb[oj] = r - a;  // an absent cell keeps its ts in ts[]
           }
         }
         if (x >= GH_ABSENT && m[j] > x) {  // step 6 merge (:424-426, :435-437)
           x = m[j];
-          t = r;
+          now = true;
           n_merged++;
         }
-        if (x > 1 && c != i && t < lim_next) x |= GH_FLAG;
-        xo[j] = x;
-        to[j] = t;
+        int32_t out = GH_ABSENT;
+        if (x != GH_ABSENT) {
+          int an = 1;  // age in round r+1 of a cell stamped now
+          if (!now) {
+            an = gh_inc(a);
+            if (a == GH_AGE_CAP - 1) tsb[oj] = r + 1 - GH_AGE_CAP;  // saturates: keep the exact ts
+          }
+          out = x >= 0 ? gh_present(x, an, gh_flag_for<EXACT>(d, x, an, c, i, oj, r + 1, p.t_fail)) : gh_tomb(an);
+        }
+        xo[j] = out;
       }
     }
-    // crashed rows are frozen: their hb is carried into the new buffer as is
+    // crashed rows are frozen: their cells are carried into the new buffer as is
 #pragma unroll
     for (int j = 0; j < 4; ++j) npres += xo[j] >= 0;
-    if (valid) {
-      stv<NT>(hbn + off, xo);
-      if (al) stv<NT>(tsb + off, to);
-    }
+    if (L.valid) stv<NT>(hbn + off, xo);
 #pragma unroll
     for (int o = SEG / 2; o > 0; o >>= 1) {
       npres += __shfl_xor(npres, o);
       any_det |= __shfl_xor((int)any_det, o) != 0;
     }
-    if (lc == 0 && valid) {
-      s_part[rr] = (uint16_t)npres;
+    if (lc == 0 && L.valid) {
+      s_part[L.rr] = (uint16_t)npres;
       if (any_det) d.det_any[i] = 1;
     }
   }
 
-  if (n_unknown) atomicAdd(&s_st[ST_REMOVE_UNKNOWN], (unsigned long long)n_unknown);
-  if (n_tomb) atomicAdd(&s_st[ST_TOMBSTONED], (unsigned long long)n_tomb);
-  if (n_det) atomicAdd(&s_st[ST_DETECTIONS], (unsigned long long)n_det);
-  if (n_rel) atomicAdd(&s_st[ST_RELEASED], (unsigned long long)n_rel);
-  if (n_merged) atomicAdd(&s_st[ST_MERGED], (unsigned long long)n_merged);
   __syncthreads();
-
   const int row0 = rb * RB;
-  if (tid < RB && row0 + tid < p.n) d.part[(int64_t)tile * p.n + row0 + tid] = s_part[tid];
+  for (int t = tid; t < RB; t += 256)
+    if (row0 + t < p.n) d.part[(int64_t)tile * p.n + row0 + t] = s_part[t];
   for (int t = tid; t < TW; t += 256) {
     if (s_dcnt[t]) {
       const int64_t c = (int64_t)tile * TW + t;
@@ -553,6 +597,15 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
       atomicMin(&d.det_min[dcur ^ 1][c], s_dmin[t]);
     }
   }
+  __syncthreads();  // s_dcnt / s_part are reused by the next tile
+  }  // tiles
+
+  if (n_unknown) atomicAdd(&s_st[ST_REMOVE_UNKNOWN], (unsigned long long)n_unknown);
+  if (n_tomb) atomicAdd(&s_st[ST_TOMBSTONED], (unsigned long long)n_tomb);
+  if (n_det) atomicAdd(&s_st[ST_DETECTIONS], (unsigned long long)n_det);
+  if (n_rel) atomicAdd(&s_st[ST_RELEASED], (unsigned long long)n_rel);
+  if (n_merged) atomicAdd(&s_st[ST_MERGED], (unsigned long long)n_merged);
+  __syncthreads();
   if (tid < ST_COUNT && s_st[tid]) atomicAdd(&d.stats[tid], s_st[tid]);
 }
 
@@ -632,15 +685,29 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_inbox_fill, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
 }
 
-template <int KB, int TW>
-static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
+template <int KB, int TW, int TPW>
+static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
   constexpr int RB = round_rb<TW>();
   const int nrb = (p.n + RB - 1) / RB;
-  const dim3 grid((unsigned)(nrb * (p.ld / TW))), blk(256);
-  if (nt)
-    hipLaunchKernelGGL((k_round<KB, TW, true>), grid, blk, 0, s, d, cur, dcur, p);
+  const dim3 grid((unsigned)(nrb * (p.ld / TW / TPW))), blk(256);
+  // timeouts at or above the age cap need the exact ts of saturated cells
+  if (p.t_fail >= GH_AGE_CAP || p.t_cleanup >= GH_AGE_CAP)
+    hipLaunchKernelGGL((k_round<KB, TW, TPW, false, true>), grid, blk, 0, s, d, cur, dcur, p);
+  else if (nt)
+    hipLaunchKernelGGL((k_round<KB, TW, TPW, true, false>), grid, blk, 0, s, d, cur, dcur, p);
   else
-    hipLaunchKernelGGL((k_round<KB, TW, false>), grid, blk, 0, s, d, cur, dcur, p);
+    hipLaunchKernelGGL((k_round<KB, TW, TPW, false, false>), grid, blk, 0, s, d, cur, dcur, p);
+}
+
+// tiles per workgroup: ld / TW is a multiple of 8 (host padding)
+template <int KB, int TW>
+static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
+  switch (p.tpw) {
+    case 1: launch_round_tpw<KB, TW, 1>(d, cur, dcur, p, s, nt); break;
+    case 2: launch_round_tpw<KB, TW, 2>(d, cur, dcur, p, s, nt); break;
+    case 8: launch_round_tpw<KB, TW, 8>(d, cur, dcur, p, s, nt); break;
+    default: launch_round_tpw<KB, TW, 4>(d, cur, dcur, p, s, nt); break;
+  }
 }
 
 template <int KB>
