@@ -25,8 +25,13 @@ tests cover both regimes.
 
 The JSON line also carries
   roofline: the fused round kernel (k_round) — algorithmic bytes per launch
-            4*N^2*(k+4) / its mean duration from HIP events on
-            the engine's stream; peak 8.0 TB/s (MI355X_MICROARCH.md).
+            4*N*ncols*(k+2): own hb segment in, k peer segments in, hb out
+            (DESIGN.md "Kernels"; SURVEY.md §8d's 4*N^2*(k+4) also counted a
+            ts stream in and out, which the age-encoded cells no longer move,
+            reported as survey_bytes_per_launch) / its mean duration from HIP
+            events on the engine's stream; peak 8.0 TB/s (MI355X_MICROARCH.md);
+            traffic = HBM-side bytes per launch from the rocprofv3 PMC passes of
+            tools/pmc.sh for this configuration (profiles/, null if none).
   cpu_baseline: the CPU restatement (oracle/tablesim.c, "port") timed on this
             host on a bounded sample (rank 0, N=1 only).
 """
@@ -63,6 +68,21 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
     return ap.parse_args()
+
+
+def pmc_traffic(n, k, world):
+    """HBM-side bytes per k_round launch from the committed PMC summary of
+    the same configuration (tools/pmc.sh -> profiles/*k_round_pmc*.json)."""
+    best = None
+    for f in sorted((REPO / "profiles").glob("*k_round_pmc*.json")):
+        try:
+            d = json.loads(f.read_text())
+        except (OSError, ValueError):
+            continue
+        c = d.get("config", {})
+        if c.get("n") == n and c.get("k") == k and c.get("world", 1) == world and "traffic_bytes" in d:
+            best = {"traffic_bytes": d["traffic_bytes"], "source": f"profiles/{f.name}"}
+    return best
 
 
 def cpu_baseline(n, fanout, seed, rows, seconds, threads, t_fail):
@@ -149,9 +169,11 @@ def main():
     if rank != 0:
         return
     value = args.steps / elapsed
-    # SURVEY.md §8d algorithmic bytes of one k_round launch (this rank's columns)
-    b_round = 4.0 * n * ncols * (k + 4)
-    b_compulsory = 16.0 * n * ncols            # each table cell read+written once
+    # algorithmic bytes of one k_round launch (this rank's columns)
+    b_round = 4.0 * n * ncols * (k + 2)
+    b_survey = 4.0 * n * ncols * (k + 4)       # SURVEY.md §8d (with a ts stream)
+    b_compulsory = 8.0 * n * ncols             # each cell read and written once
+    traffic = pmc_traffic(n, k, world)
     avg_s = (kern_ms / 1e3) / max(launches, 1)
     achieved = b_round / avg_s / 1e9
     line = {
@@ -179,8 +201,11 @@ def main():
         },
         "roofline": {
             "bound": "hbm", "kernel": "k_round", "achieved": achieved, "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-            "bytes_per_launch": b_round, "avg_launch_ms": avg_s * 1e3, "launches": launches,
+            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic["traffic_bytes"] if traffic else None,
+            "traffic_source": traffic["source"] if traffic else None,
+            "bytes_per_launch": b_round, "survey_bytes_per_launch": b_survey,
+            "avg_launch_ms": avg_s * 1e3, "launches": launches,
             "compulsory_bytes_per_launch": b_compulsory,
             "compulsory_achieved": b_compulsory / avg_s / 1e9,
             "frac_of_measured_copy_peak": achieved / HBM_MEASURED_GBS,

@@ -1,5 +1,5 @@
 #!/bin/bash
-# One GPU session: parity tests, bench line, kernel-trace profile, variant A/B.
+# One GPU session: parity tests, bench line, kernel-trace profile, PMC passes.
 # Every GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
 mkdir -p gpurun_out
@@ -7,4 +7,4 @@ export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 &&
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 10 --warmup 4 --no-cpu-baseline > gpurun_out/prof.log 2>&1 &&
-timeout -k 10 300 python -u tools/round_variants.py --iters 3 --rounds 3 --variants ${VARIANTS:-64:1:0,64:1:1,16:1:1,16:1:0,32:1:1,8:1:1} > gpurun_out/variants.log 2>&1
+bash tools/pmc.sh > gpurun_out/pmc.log 2>&1

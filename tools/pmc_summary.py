@@ -1,5 +1,6 @@
 """Per-dispatch averages of the PMC passes of tools/pmc.sh for k_round:
-  python tools/pmc_summary.py gpurun_out/pmc > summary.json"""
+  python tools/pmc_summary.py gpurun_out/pmc [N K] > summary.json
+(N, K = the bench configuration the passes ran, recorded for bench.py)."""
 import csv
 import glob
 import json
@@ -21,4 +22,9 @@ if "WRITE_SIZE" in out:
 if "TCC_HIT_sum" in out and "TCC_MISS_sum" in out:
     h, m = out["TCC_HIT_sum"]["per_dispatch"], out["TCC_MISS_sum"]["per_dispatch"]
     out["l2_hit_rate"] = h / (h + m)
+if "read_bytes_corrected" in out and "write_bytes" in out:
+    out["traffic_bytes"] = out["read_bytes_corrected"] + out["write_bytes"]
+n, k = (int(x) for x in sys.argv[2:4]) if len(sys.argv) >= 4 else (65536, 4)
+out["config"] = {"n": n, "k": k, "world": 1, "command": "python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline"}
+out["algorithmic_bytes"] = 4.0 * n * n * (k + 2)
 print(json.dumps(out, indent=1))
