@@ -120,6 +120,12 @@ struct GhDev {
   int32_t *inbox_beg, *inbox_cnt, *inbox, *inbox_fill, *targets;
   int32_t *ring;    // ring mode: [world][n][2] (local snapshot count, local position of the sender)
   uint32_t *rbits;  // gathered presence bitmaps of some rows: [world][nr][ncsw]
+  // quirk-mode detection (SPEC §4): per-(tile,row) run summaries / prefixes,
+  // per-row totals of every shard, carry-in and last present tile
+  uint8_t *qsum;    // [ld/tw][n]
+  uint8_t *qall;    // [world][n]
+  uint8_t *qcarry;  // [n]: bit0 run state entering this shard, bit1 shard holds the row's last list entry
+  int32_t *qlast;   // [n]: local tile of the row's last present cell (-1 none)
   unsigned long long *stats;  // ST_COUNT
   // files (replicated on every rank)
   int64_t fcap;
@@ -218,6 +224,10 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
 // nt = non-temporal hints on the once-touched streams of k_round
 void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt);
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);
+// quirk-mode detection: summaries + per-row prefix (then allgather qall), and
+// carry-in + flag rewrite of the current table
+void launch_quirk_scan(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
+void launch_quirk_apply(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 // events.hip
 void launch_count(const GhDev& d, int cur, const GhRound& p, hipStream_t s);
 void launch_fill(const GhDev& d, int cur, int32_t hb0, int32_t ts0, const GhRound& p,

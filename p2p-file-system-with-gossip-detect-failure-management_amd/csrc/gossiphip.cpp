@@ -302,7 +302,6 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (world < 1 || rank < 0 || rank >= world) return GH_EINVAL;
   if (world > 1 && !comm_id) return GH_EINVAL;
   if (transport != GH_COMM_RCCL && transport != GH_COMM_LOCAL) return GH_EINVAL;
-  if (cfg->detect_mode == GH_DETECT_QUIRK) return GH_EINVAL;  // HIP path: canonical only
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device || cfg->device < 0) {
     (void)hipGetLastError();
@@ -399,6 +398,10 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &e->rows_buf, 16, 0)))
       break;
     if (cfg->peer_mode == GH_PEER_RING && (rc = dalloc(e, &d.ring, 2 * (int64_t)world * e->n, 0))) break;
+    if (cfg->detect_mode == GH_DETECT_QUIRK &&
+        ((rc = dalloc(e, &d.qsum, nch * e->n, 0)) || (rc = dalloc(e, &d.qall, (int64_t)world * e->n, 0)) ||
+         (rc = dalloc(e, &d.qcarry, e->n, 0)) || (rc = dalloc(e, &d.qlast, e->n, 0))))
+      break;
     if ((rc = dalloc(e, &d.rbits, (size_t)world * 2 * d.ncsw, 0))) break;
     e->rbits_rows = 2;
     if ((rc = dalloc(e, &d.cand, e->n, 0)) || (rc = dalloc(e, &d.ncand, 4, 0))) break;
@@ -434,6 +437,19 @@ int decide_active(Engine* e, const GhRound& p) {
   HIPCHK(e, hipGetLastError());
   if (e->world > 1 && (rc = allreduce_i32(e, d.post, d.post, (size_t)e->n))) return rc;
   launch_active_post(d, p, e->stream);
+  HIPCHK(e, hipGetLastError());
+  return GH_OK;
+}
+
+// Quirk-mode detection (SPEC §4): rewrite this round's detection flags to
+// the reference's range-over-mutated-slice set before anything reads them.
+int quirk_flags(Engine* e, const GhRound& p) {
+  GhDev& d = e->d;
+  launch_quirk_scan(d, e->cur, e->dcur, p, e->stream);
+  HIPCHK(e, hipGetLastError());
+  if (e->world > 1)
+    COMMCHK(e, e->comm->allgather(d.qall + (size_t)e->rank * e->n, d.qall, e->n, e->stream));
+  launch_quirk_apply(d, e->cur, e->dcur, p, e->stream);
   HIPCHK(e, hipGetLastError());
   return GH_OK;
 }
@@ -641,6 +657,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     if ((rc = process_events(e, r))) return rc;
     const GhRound p = round_params(e, r);
     if ((rc = decide_active(e, p))) return rc;
+    if (e->cfg.detect_mode == GH_DETECT_QUIRK && (rc = quirk_flags(e, p))) return rc;
     if ((rc = build_inboxes(e, p))) return rc;
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q], e->stream));
     launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt);

@@ -18,6 +18,8 @@
 // alive/active and the inboxes are global.
 #include <limits.h>
 
+#include <algorithm>
+
 #include "gh_internal.h"
 
 namespace {
@@ -651,7 +653,135 @@ __global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p, in
   }
 }
 
+// ---- quirk-mode detection (SPEC §4, slave/slave.go:464-477 with :283) ----
+// detectfailure ranges over the slice removeMember shifts, so in each run of
+// consecutive candidates (in list order = present cells after REMOVE, member
+// order) only the candidates at even offsets are removed, plus the last list
+// entry if it is a candidate. The pre-pass below rewrites the detection flag
+// of the current table to exactly that set, so k_round (detection) and the
+// peers (a sender's snapshot keeps its skipped candidates) follow it as is.
+//
+// Run state s = parity of the trailing run of candidates before a cell (0 at
+// the start of a row). A stretch of cells maps s to f(s): with a present
+// non-candidate in it f is constant (the parity of the candidates after the
+// last one), else f(s) = s ^ (its candidates & 1). Bits: 0 = has a present
+// non-candidate, 1 = value, 2 = has a present cell.
+__device__ __forceinline__ int q_compose(int a, int b) {  // a, then b
+  return ((a | b) & 5) | ((b & 1) ? (b & 2) : ((a ^ b) & 2));
+}
+__device__ __forceinline__ int q_apply(int f, int s) { return (f & 1) ? ((f >> 1) & 1) : (s ^ ((f >> 1) & 1)); }
+
+// present after REMOVE / candidate (flag) of local cell (i, c)
+__device__ __forceinline__ void q_cell(const GhDev& d, int32_t v, int dcur, int i, int64_t c, bool& pres, bool& cand) {
+  pres = v >= 0 && !(dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], i));
+  cand = pres && (v & GH_FLAG);
+}
+
+// one thread per (tile, row): the tile's summary
+__global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, GhRound p) {
+  const int64_t ntiles = p.ld / d.tw;
+  const int64_t total = ntiles * p.n;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = idx / p.n;
+    const int i = (int)(idx - t * p.n);
+    int f = 0;
+    for (int j = 0; j < d.tw; ++j) {
+      const int64_t c = t * d.tw + j;
+      bool pres, cand;
+      q_cell(d, d.hb[cur][gh_cell(d, i, c)], dcur, i, c, pres, cand);
+      if (pres) f = q_compose(f, cand ? 6 : 5);
+    }
+    d.qsum[idx] = (uint8_t)f;
+  }
+}
+
+// one thread per row: exclusive prefix over the shard's tiles (in place),
+// the shard's total and its last tile holding a present cell
+__global__ __launch_bounds__(256) void k_quirk_prefix(GhDev d, GhRound p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const int64_t ntiles = p.ld / d.tw;
+  int pre = 0, last = -1;
+  for (int64_t t = 0; t < ntiles; ++t) {
+    const int f = d.qsum[t * p.n + i];
+    d.qsum[t * p.n + i] = (uint8_t)pre;
+    if (f & 4) last = (int)t;
+    pre = q_compose(pre, f);
+  }
+  d.qall[(int64_t)d.rank * p.n + i] = (uint8_t)pre;
+  d.qlast[i] = last;
+}
+
+// one thread per row: the run state entering this shard (the shards before
+// it, in member order) and whether the row's last list entry is here
+__global__ __launch_bounds__(256) void k_quirk_carry(GhDev d, GhRound p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  int s = 0;
+  bool later = false;
+  for (int g = 0; g < d.world; ++g) {
+    const int f = d.qall[(int64_t)g * p.n + i];
+    if (g < d.rank) s = q_apply(f, s);
+    if (g > d.rank && (f & 4)) later = true;
+  }
+  const bool mine_last = !later && (d.qall[(int64_t)d.rank * p.n + i] & 4);
+  d.qcarry[i] = (uint8_t)(s | (mine_last ? 2 : 0));
+}
+
+// one thread per (tile, row): walk the tile's cells with the run state and
+// clear the flag of every candidate the reference's loop skips
+__global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur, GhRound p) {
+  const int64_t ntiles = p.ld / d.tw;
+  const int64_t total = ntiles * p.n;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = idx / p.n;
+    const int i = (int)(idx - t * p.n);
+    if (!(d.alive[i] && d.active[i])) continue;  // only active rows detect (and send)
+    const int qc = d.qcarry[i];
+    int s = q_apply(d.qsum[idx], qc & 1);
+    int64_t lastc = -1;
+    if ((qc & 2) && d.qlast[i] == t) {
+      for (int j = 0; j < d.tw; ++j) {
+        const int64_t c = t * d.tw + j;
+        bool pres, cand;
+        q_cell(d, d.hb[cur][gh_cell(d, i, c)], dcur, i, c, pres, cand);
+        if (pres) lastc = c;
+      }
+    }
+    for (int j = 0; j < d.tw; ++j) {
+      const int64_t c = t * d.tw + j;
+      const int64_t off = gh_cell(d, i, c);
+      const int32_t v = d.hb[cur][off];
+      bool pres, cand;
+      q_cell(d, v, dcur, i, c, pres, cand);
+      if (!pres) continue;
+      if (!cand) {
+        s = 0;
+        continue;
+      }
+      if (!(s == 0 || c == lastc)) d.hb[cur][off] = v & ~GH_FLAG;  // skipped this round
+      s ^= 1;
+    }
+  }
+}
+
 }  // namespace
+
+void launch_quirk_scan(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  const int64_t total = (p.ld / d.tw) * p.n;
+  const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_quirk_sum, dim3(grid), dim3(256), 0, s, d, cur, dcur, p);
+  hipLaunchKernelGGL(k_quirk_prefix, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
+}
+
+void launch_quirk_apply(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  const int64_t total = (p.ld / d.tw) * p.n;
+  const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_quirk_carry, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
+  hipLaunchKernelGGL(k_quirk_apply, dim3(grid), dim3(256), 0, s, d, cur, dcur, p);
+}
 
 void launch_prep(const GhDev& d, int dcur, hipStream_t s) {
   hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, s, d, dcur);

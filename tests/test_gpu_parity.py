@@ -56,9 +56,29 @@ def run_parity(gs, om, cfg_kw, n, rounds, sched, init=None, threads=8, every=1, 
     return eng, orc
 
 
-@pytest.mark.parametrize("k", [k for k in KATS if k["detect_mode"] == 0], ids=lambda k: k["name"])
+@pytest.mark.parametrize("k", KATS, ids=lambda k: k["name"])
 def test_kats_gpu(gs, k):
     run_kat(gs.Engine(kat_config(gs, k)), k)
+
+
+@pytest.mark.parametrize("n,peer_mode,t_fail,seed", [(14, 1, 5, 4), (64, 1, 3, 5), (64, 0, 3, 6), (300, 0, 2, 7),
+                                                     (257, 1, 3, 8)])
+def test_quirk_detection_churn(gs, oracle_mod, n, peer_mode, t_fail, seed):
+    """Quirk-mode detection (slave/slave.go:464-477 range over the slice that
+    removeMember shifts): runs of candidates, skipped candidates staying in
+    the senders' snapshots, the last list entry, under crash/leave/join."""
+    sched = sc.random_churn(n, 40, seed, p_crash=0.08, p_leave=0.02, p_join=0.05)
+    run_parity(gs, oracle_mod, dict(peer_mode=peer_mode, fanout=3, seed=0x2000 + seed, detect_mode=1,
+                                    t_fail=t_fail, t_cleanup=t_fail + 2), n, 40, sched, init=sc.full_state(n))
+
+
+def test_quirk_c2_collapse(gs, oracle_mod):
+    """N=4,096 with the reference's 5-round timeouts in quirk mode: the
+    round-6 detection storm with long candidate runs in every row."""
+    n = 4096
+    sched = {8: [(sc.CRASH, c) for c in sc.crash_ids(n, 0.01, 0x5EED0002)]}
+    run_parity(gs, oracle_mod, dict(fanout=3, seed=0x5EED0002, detect_mode=1), n, 12, sched,
+               init=sc.full_state(n), every=3)
 
 
 @pytest.mark.parametrize("peer_mode", [0, 1])

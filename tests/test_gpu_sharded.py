@@ -68,7 +68,7 @@ def test_shard_layout(gs):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("k", [k for k in KATS if k["detect_mode"] == 0], ids=lambda k: k["name"])
+@pytest.mark.parametrize("k", KATS, ids=lambda k: k["name"])
 def test_kats_sharded(gs, k, world):
     grp = gs.ShardGroup(kat_config(gs, k), world)
     try:
@@ -96,6 +96,15 @@ def test_random_churn_sharded(gs, oracle_mod, world, n, peer_mode, seed):
     sched = sc.random_churn(n, 30, seed, p_crash=0.03, p_leave=0.01, p_join=0.05)
     run_group(gs, oracle_mod, world, dict(peer_mode=peer_mode, fanout=3, seed=0x77 + seed), n, 30, sched,
               init=sc.full_state(n))
+
+
+@pytest.mark.parametrize("world,n,peer_mode", [(2, 64, 1), (3, 300, 0), (4, 257, 1)])
+def test_quirk_detection_sharded(gs, oracle_mod, world, n, peer_mode):
+    """Quirk-mode run parity carried across shard boundaries (the runs of
+    candidates continue from one shard's columns into the next)."""
+    sched = sc.random_churn(n, 30, 40 + world, p_crash=0.08, p_leave=0.02, p_join=0.05)
+    run_group(gs, oracle_mod, world, dict(peer_mode=peer_mode, fanout=3, seed=0x3000 + n, detect_mode=1, t_fail=3,
+                                          t_cleanup=5), n, 30, sched, init=sc.full_state(n))
 
 
 @pytest.mark.parametrize("world", [2, 4])
