@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=12)
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--fanout", type=int, default=4)
+    ap.add_argument("--peer-mode", choices=("pull", "ring"), default="pull",
+                    help="pull: k Philox peers (BASELINE configs 2-4); ring: the reference's ring push")
+    ap.add_argument("--detect", choices=("canonical", "quirk"), default="canonical")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0003)
     ap.add_argument("--t-fail", type=int, default=16,
                     help="T_fail = T_cleanup in rounds (reference: 5; see module doc)")
@@ -130,7 +133,9 @@ def main():
     import gossipsim as gs
 
     n, k = args.n, args.fanout
-    cfg = gs.default_config(n, fanout=k, seed=args.seed, device=local, t_fail=args.t_fail, t_cleanup=args.t_fail)
+    cfg = gs.default_config(n, fanout=k, seed=args.seed, device=local, t_fail=args.t_fail, t_cleanup=args.t_fail,
+                            peer_mode=gs.GH_PEER_RING if args.peer_mode == "ring" else gs.GH_PEER_PULL,
+                            detect_mode=gs.GH_DETECT_QUIRK if args.detect == "quirk" else gs.GH_DETECT_CANONICAL)
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -190,7 +195,9 @@ def main():
         "dtype": "int32",
         "data": "synthetic",
         "config": {
-            "workload": f"BASELINE config 3: N={n} members, fanout k={k} Philox pull, full membership "
+            "workload": f"BASELINE config 3: N={n} members, "
+                        + (f"fanout k={k} Philox pull" if args.peer_mode == "pull" else "reference ring push (3 targets)")
+                        + (", quirk detection" if args.detect == "quirk" else "") + ", full membership "
                         f"start (hb=2, ts=0), {args.warmup} warm-up rounds to the steady state, "
                         f"T_fail=T_cleanup={args.t_fail} rounds, seed {hex(args.seed)}",
             "t_fail": args.t_fail,

@@ -119,6 +119,7 @@ struct GhDev {
   uint16_t *part;
   int32_t *inbox_beg, *inbox_cnt, *inbox, *inbox_fill, *targets;
   int32_t *ring;    // ring mode: [world][n][2] (local snapshot count, local position of the sender)
+  uint16_t *rcnt;   // ring mode: [ld/tw][n] snapshot-list members per (tile, sender row)
   uint32_t *rbits;  // gathered presence bitmaps of some rows: [world][nr][ncsw]
   // quirk-mode detection (SPEC §4): per-(tile,row) run summaries / prefixes,
   // per-row totals of every shard, carry-in and last present tile

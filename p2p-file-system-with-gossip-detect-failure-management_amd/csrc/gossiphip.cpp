@@ -397,7 +397,9 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.stats, ST_COUNT, 0)) || (rc = dalloc(e, &e->ev_buf, 2 * (int64_t)e->n + 16, 0)) ||
         (rc = dalloc(e, &e->rows_buf, 16, 0)))
       break;
-    if (cfg->peer_mode == GH_PEER_RING && (rc = dalloc(e, &d.ring, 2 * (int64_t)world * e->n, 0))) break;
+    if (cfg->peer_mode == GH_PEER_RING &&
+        ((rc = dalloc(e, &d.ring, 2 * (int64_t)world * e->n, 0)) || (rc = dalloc(e, &d.rcnt, nch * e->n, 0))))
+      break;
     if (cfg->detect_mode == GH_DETECT_QUIRK &&
         ((rc = dalloc(e, &d.qsum, nch * e->n, 0)) || (rc = dalloc(e, &d.qall, (int64_t)world * e->n, 0)) ||
          (rc = dalloc(e, &d.qcarry, e->n, 0)) || (rc = dalloc(e, &d.qlast, e->n, 0))))

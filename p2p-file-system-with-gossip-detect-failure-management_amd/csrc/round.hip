@@ -7,7 +7,9 @@
 //                  post-REMOVE count (summed over ranks when sharded).
 //   k_peers_pull   per receiver column: k Philox peers, kept iff the sender is
 //                  active, alive and lists the receiver (slave/slave.go:527-542).
-//   k_ring_*       reference ring topology (slave/slave.go:512-524) + inbox CSR.
+//   k_ring_*       reference ring topology (slave/slave.go:512-524): per-(tile,row)
+//                  snapshot counts, positions, targets + inbox CSR.
+//   k_quirk_*      quirk-mode detection pre-pass (SPEC §4).
 //   k_round        THE HOT KERNEL: one pass over the table applying REMOVE
 //                  delivery, guard, own heartbeat, detection, cleanup and the
 //                  k-peer max-merge (slave/slave.go:276-286,414-497) for a
@@ -149,82 +151,120 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
   d.inbox_cnt[i] = nv;
 }
 
-// Is local column c in sender sdr's snapshot list (after steps 1-5)?
-__device__ __forceinline__ bool snap_present(const GhDev& d, const int32_t* hb, int dcur, int sdr, int64_t c,
-                                             const GhRound& p) {
-  const int64_t off = gh_cell(d, sdr, c);
-  const int32_t v = hb[off];
-  if (v < 0) return false;
-  if (v & GH_FLAG) return false;  // detected by the sender this round
-  if (dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], sdr)) return false;
-  return true;
-}
+// ---- segment walks -------------------------------------------------------
+// The helper kernels below read the table the way k_round does: a lane owns
+// 4 consecutive members, SEG = TW/4 lanes cover one row segment of a tile,
+// and consecutive waves take consecutive (tile, row) segments in storage
+// order, so every wave instruction is one contiguous 1 KiB access.
+typedef int v4i __attribute__((ext_vector_type(4)));
 
-// Block-wide exclusive scan of per-thread counts (256 threads).
-__device__ __forceinline__ int block_excl_scan(int v, int* s_tmp, int* total) {
-  const int tid = threadIdx.x;
-  s_tmp[tid] = v;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    const int x = tid >= off ? s_tmp[tid - off] : 0;
-    __syncthreads();
-    s_tmp[tid] += x;
-    __syncthreads();
+template <int TW>
+struct SegWalk {
+  static constexpr int SEG = TW / 4;
+  static constexpr int RPW = 64 / SEG;
+  int lane, sub, lc;
+  int64_t nseg, first, stride;
+  __device__ SegWalk(const GhRound& p) {
+    lane = threadIdx.x & 63;
+    sub = lane / SEG;
+    lc = lane % SEG;
+    nseg = (p.ld / TW) * p.n;
+    first = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * RPW;
+    stride = (((int64_t)gridDim.x * blockDim.x) >> 6) * RPW;
   }
-  const int incl = s_tmp[tid];
-  *total = s_tmp[255];
-  __syncthreads();
-  return incl - v;
+};
+
+// 4-bit REMOVE mask of local columns l0..l0+3 at row i
+__device__ __forceinline__ uint32_t removed4(const GhDev& d, int dcur, int64_t l0, int i) {
+  uint32_t m = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFu;
+  uint32_t out = 0;
+  for (int j = 0; j < 4; ++j)
+    if (((m >> j) & 1u) && removes_at(d.det_cnt[dcur][l0 + j], d.det_min[dcur][l0 + j], i)) out |= 1u << j;
+  return out;
 }
 
-// Ring mode, part 1 (one workgroup per sender row): the sender's snapshot
-// list restricted to this shard's columns: its length and, when the sender's
-// own column is local, the sender's position in it (SPEC D1 order).
+// Ring mode, part 1: per (tile, sender row) the number of members in the
+// sender's snapshot list (present after REMOVE, not detected by it).
+template <int TW>
+__global__ __launch_bounds__(256) void k_ring_tiles(GhDev d, int cur, int dcur, GhRound p) {
+  const SegWalk<TW> w(p);
+  for (int64_t base = w.first; base < w.nseg; base += w.stride) {
+    const int64_t sid = base + w.sub;
+    const bool valid = sid < w.nseg;
+    const int64_t t = valid ? sid / p.n : 0;
+    const int i = valid ? (int)(sid - t * p.n) : 0;
+    const int64_t l0 = t * TW + w.lc * 4;
+    int cnt = 0;
+    if (valid) {
+      const v4i v = *reinterpret_cast<const v4i*>(d.hb[cur] + t * d.tstride + (int64_t)i * TW + w.lc * 4);
+      const uint32_t rm = removed4(d, dcur, l0, i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) cnt += v[j] >= 0 && !(v[j] & GH_FLAG) && !((rm >> j) & 1u);
+    }
+#pragma unroll
+    for (int o = SegWalk<TW>::SEG / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if (valid && w.lc == 0) d.rcnt[sid] = (uint16_t)cnt;
+  }
+}
+
+// The local column of the want-th (0-based) member of sender s's snapshot
+// list inside tile t (scans the tile-row).
+__device__ __forceinline__ int64_t ring_find(const GhDev& d, const int32_t* hb, int dcur, int s, int64_t t, int want) {
+  for (int j = 0; j < d.tw; ++j) {
+    const int64_t c = t * d.tw + j;
+    const int32_t v = hb[gh_cell(d, s, c)];
+    if (v < 0 || (v & GH_FLAG)) continue;
+    if (dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], s)) continue;
+    if (want-- == 0) return c;
+  }
+  return -1;
+}
+
+// Ring mode, part 2 (one thread per sender row): this shard's list length
+// and, when the sender's own column is local, its position in that list.
 __global__ __launch_bounds__(256) void k_ring_count(GhDev d, int cur, int dcur, GhRound p) {
-  __shared__ int s_tmp[256];
-  const int sdr = blockIdx.x;
-  const int tid = threadIdx.x;
+  const int sdr = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sdr >= p.n) return;
   int32_t* out = d.ring + ((int64_t)d.rank * p.n + sdr) * 2;
   if (!(d.alive[sdr] && d.active[sdr])) {
-    if (tid == 0) {
-      out[0] = 0;
-      out[1] = -1;
-    }
+    out[0] = 0;
+    out[1] = -1;
     return;
   }
-  const int32_t* hb = d.hb[cur];
-  const int per = (d.ncol + 255) / 256;
-  const int b = min(d.ncol, tid * per), e = min(d.ncol, b + per);
-  int cnt = 0;
-  for (int c = b; c < e; ++c) cnt += snap_present(d, hb, dcur, sdr, c, p);
-  int total;
-  const int off = block_excl_scan(cnt, s_tmp, &total);
+  const int64_t ntiles = p.ld / d.tw;
   const int64_t ls = (int64_t)sdr - d.col0;
-  if (tid == 0) {
-    out[0] = total;
-    if (!(ls >= 0 && ls < d.ncol)) out[1] = -1;
-  }
-  if (ls >= b && ls < e) {
-    int pos = -1;
-    if (snap_present(d, hb, dcur, sdr, ls, p)) {
-      pos = off;
-      for (int c = b; c < ls; ++c) pos += snap_present(d, hb, dcur, sdr, c, p);
+  const int64_t own_t = (ls >= 0 && ls < d.ncol) ? ls / d.tw : -1;
+  int64_t total = 0, pos = -1;
+  for (int64_t t = 0; t < ntiles; ++t) {
+    if (t == own_t) {
+      const int32_t* hb = d.hb[cur];
+      const int32_t v = hb[gh_cell(d, sdr, ls)];
+      const bool in = v >= 0 && !(v & GH_FLAG) &&
+                      !(dbit(d.dbits, ls) && removes_at(d.det_cnt[dcur][ls], d.det_min[dcur][ls], sdr));
+      if (in) {
+        pos = total;
+        for (int64_t c = t * d.tw; c < ls; ++c) {
+          const int32_t x = hb[gh_cell(d, sdr, c)];
+          pos += x >= 0 && !(x & GH_FLAG) &&
+                 !(dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], sdr));
+        }
+      }
     }
-    out[1] = pos;
+    total += d.rcnt[t * p.n + sdr];
   }
+  out[0] = (int32_t)total;
+  out[1] = (int32_t)pos;
 }
 
-// Ring mode, part 2: with every shard's (length, position) gathered, the
-// sender's targets list[(idx-1) mod L], list[(idx+1) mod L], list[(idx+2)
-// mod L] (slave/slave.go:515-524) that fall into this shard's columns; the
-// other shards' targets arrive by allreduce(max).
+// Ring mode, part 3 (one thread per sender row): with every shard's (length,
+// position) gathered, the sender's targets list[(idx-1) mod L],
+// list[(idx+1) mod L], list[(idx+2) mod L] (slave/slave.go:515-524) that fall
+// into this shard's columns; the other shards' targets arrive by
+// allreduce(max).
 __global__ __launch_bounds__(256) void k_ring_select(GhDev d, int cur, int dcur, GhRound p) {
-  __shared__ int s_tmp[256];
-  __shared__ int s_tgt[3];
-  const int sdr = blockIdx.x;
-  const int tid = threadIdx.x;
-  if (tid < 3) s_tgt[tid] = -1;
-  __syncthreads();
+  const int sdr = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sdr >= p.n) return;
+  int32_t tg[3] = {-1, -1, -1};
   if (d.alive[sdr] && d.active[sdr]) {
     int64_t L = 0, before_me = 0, before_owner = 0;
     const int owner = (int)(sdr / d.ncs);
@@ -235,40 +275,29 @@ __global__ __launch_bounds__(256) void k_ring_select(GhDev d, int cur, int dcur,
       L += c;
     }
     if (L == 0) {
-      if (tid == 0 && d.rank == 0) atomicAdd(&d.stats[ST_RING_EMPTY], 1ull);  // slave.go:517 div by 0
+      if (d.rank == 0) atomicAdd(&d.stats[ST_RING_EMPTY], 1ull);  // slave.go:517 div by 0
     } else {
       const int64_t lp = d.ring[((int64_t)owner * p.n + sdr) * 2 + 1];
       const int64_t idx = lp >= 0 ? before_owner + lp : -1;
       const int64_t mine = d.ring[((int64_t)d.rank * p.n + sdr) * 2];
       int64_t want[3] = {idx - 1, idx + 1, idx + 2};
-      bool any = false;
-#pragma unroll
       for (int q = 0; q < 3; ++q) {
         int64_t v = want[q] % L;  // C and Go both truncate toward zero
         if (v < 0) v += L;
         want[q] = v - before_me;  // position inside this shard's part
-        any |= want[q] >= 0 && want[q] < mine;
       }
-      if (any) {
-        const int32_t* hb = d.hb[cur];
-        const int per = (d.ncol + 255) / 256;
-        const int b = min(d.ncol, tid * per), e = min(d.ncol, b + per);
-        int cnt = 0;
-        for (int c = b; c < e; ++c) cnt += snap_present(d, hb, dcur, sdr, c, p);
-        int total;
-        int rank = block_excl_scan(cnt, s_tmp, &total);
-        for (int c = b; c < e; ++c) {
-          if (!snap_present(d, hb, dcur, sdr, c, p)) continue;
-#pragma unroll
-          for (int q = 0; q < 3; ++q)
-            if (want[q] == rank) s_tgt[q] = (int)(d.col0 + c);
-          rank++;
-        }
+      const int64_t ntiles = p.ld / d.tw;
+      int64_t acc = 0;
+      for (int64_t t = 0; t < ntiles && acc < mine; ++t) {
+        const int64_t c = d.rcnt[t * p.n + sdr];
+        for (int q = 0; q < 3; ++q)
+          if (want[q] >= acc && want[q] < acc + c)
+            tg[q] = (int32_t)(d.col0 + ring_find(d, d.hb[cur], dcur, sdr, t, (int)(want[q] - acc)));
+        acc += c;
       }
     }
   }
-  __syncthreads();
-  if (tid < 3) d.targets[(int64_t)sdr * 3 + tid] = s_tgt[tid];
+  for (int q = 0; q < 3; ++q) d.targets[(int64_t)sdr * 3 + q] = tg[q];
 }
 
 __global__ __launch_bounds__(256) void k_inbox_count(GhDev d, GhRound p) {
@@ -317,8 +346,6 @@ __global__ __launch_bounds__(256) void k_inbox_fill(GhDev d, GhRound p) {
     }
   }
 }
-
-typedef int v4i __attribute__((ext_vector_type(4)));
 
 template <bool NT>
 __device__ __forceinline__ v4i ldv(const int32_t* p) {
@@ -671,28 +698,31 @@ __device__ __forceinline__ int q_compose(int a, int b) {  // a, then b
 }
 __device__ __forceinline__ int q_apply(int f, int s) { return (f & 1) ? ((f >> 1) & 1) : (s ^ ((f >> 1) & 1)); }
 
-// present after REMOVE / candidate (flag) of local cell (i, c)
-__device__ __forceinline__ void q_cell(const GhDev& d, int32_t v, int dcur, int i, int64_t c, bool& pres, bool& cand) {
-  pres = v >= 0 && !(dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], i));
-  cand = pres && (v & GH_FLAG);
-}
-
-// one thread per (tile, row): the tile's summary
+// one segment per (tile, row): the tile's run summary (segmented scan over
+// the SEG lanes, last lane holds the whole tile)
+template <int TW>
 __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, GhRound p) {
-  const int64_t ntiles = p.ld / d.tw;
-  const int64_t total = ntiles * p.n;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = idx / p.n;
-    const int i = (int)(idx - t * p.n);
+  constexpr int SEG = SegWalk<TW>::SEG;
+  const SegWalk<TW> w(p);
+  for (int64_t base = w.first; base < w.nseg; base += w.stride) {
+    const int64_t sid = base + w.sub;
+    const bool valid = sid < w.nseg;
+    const int64_t t = valid ? sid / p.n : 0;
+    const int i = valid ? (int)(sid - t * p.n) : 0;
     int f = 0;
-    for (int j = 0; j < d.tw; ++j) {
-      const int64_t c = t * d.tw + j;
-      bool pres, cand;
-      q_cell(d, d.hb[cur][gh_cell(d, i, c)], dcur, i, c, pres, cand);
-      if (pres) f = q_compose(f, cand ? 6 : 5);
+    if (valid) {
+      const v4i v = *reinterpret_cast<const v4i*>(d.hb[cur] + t * d.tstride + (int64_t)i * TW + w.lc * 4);
+      const uint32_t rm = removed4(d, dcur, t * TW + w.lc * 4, i);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (v[j] >= 0 && !((rm >> j) & 1u)) f = q_compose(f, (v[j] & GH_FLAG) ? 6 : 5);
     }
-    d.qsum[idx] = (uint8_t)f;
+#pragma unroll
+    for (int o = 1; o < SEG; o <<= 1) {
+      const int other = __shfl_up(f, o, SEG);
+      if (w.lc >= o) f = q_compose(other, f);
+    }
+    if (valid && w.lc == SEG - 1) d.qsum[sid] = (uint8_t)f;
   }
 }
 
@@ -729,58 +759,103 @@ __global__ __launch_bounds__(256) void k_quirk_carry(GhDev d, GhRound p) {
   d.qcarry[i] = (uint8_t)(s | (mine_last ? 2 : 0));
 }
 
-// one thread per (tile, row): walk the tile's cells with the run state and
-// clear the flag of every candidate the reference's loop skips
+// one segment per (tile, row) of an active row: each lane gets the run state
+// before its 4 cells (exclusive segmented scan + the tile's carry-in) and
+// clears the flag of every candidate the reference's loop skips
+template <int TW>
 __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur, GhRound p) {
-  const int64_t ntiles = p.ld / d.tw;
-  const int64_t total = ntiles * p.n;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = idx / p.n;
-    const int i = (int)(idx - t * p.n);
-    if (!(d.alive[i] && d.active[i])) continue;  // only active rows detect (and send)
-    const int qc = d.qcarry[i];
-    int s = q_apply(d.qsum[idx], qc & 1);
-    int64_t lastc = -1;
-    if ((qc & 2) && d.qlast[i] == t) {
-      for (int j = 0; j < d.tw; ++j) {
-        const int64_t c = t * d.tw + j;
-        bool pres, cand;
-        q_cell(d, d.hb[cur][gh_cell(d, i, c)], dcur, i, c, pres, cand);
-        if (pres) lastc = c;
-      }
+  constexpr int SEG = SegWalk<TW>::SEG;
+  const SegWalk<TW> w(p);
+  for (int64_t base = w.first; base < w.nseg; base += w.stride) {
+    const int64_t sid = base + w.sub;
+    const int64_t t = sid < w.nseg ? sid / p.n : 0;
+    const int i = sid < w.nseg ? (int)(sid - t * p.n) : 0;
+    const bool valid = sid < w.nseg && d.alive[i] && d.active[i];  // only active rows detect (and send)
+    int32_t* cell = d.hb[cur] + t * d.tstride + (int64_t)i * TW + w.lc * 4;
+    v4i v = {-1, -1, -1, -1};
+    uint32_t rm = 0;
+    if (valid) {
+      v = *reinterpret_cast<const v4i*>(cell);
+      rm = removed4(d, dcur, t * TW + w.lc * 4, i);
     }
-    for (int j = 0; j < d.tw; ++j) {
-      const int64_t c = t * d.tw + j;
-      const int64_t off = gh_cell(d, i, c);
-      const int32_t v = d.hb[cur][off];
-      bool pres, cand;
-      q_cell(d, v, dcur, i, c, pres, cand);
-      if (!pres) continue;
-      if (!cand) {
+    int f = 0, lastj = -1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (v[j] >= 0 && !((rm >> j) & 1u)) {
+        f = q_compose(f, (v[j] & GH_FLAG) ? 6 : 5);
+        lastj = w.lc * 4 + j;
+      }
+    int incl = f;
+#pragma unroll
+    for (int o = 1; o < SEG; o <<= 1) {
+      const int other = __shfl_up(incl, o, SEG);
+      if (w.lc >= o) incl = q_compose(other, incl);
+    }
+    int excl = __shfl_up(incl, 1, SEG);
+    if (w.lc == 0) excl = 0;
+#pragma unroll
+    for (int o = SEG / 2; o > 0; o >>= 1) lastj = max(lastj, __shfl_xor(lastj, o));
+    if (!valid) continue;
+    const int qc = d.qcarry[i];
+    int s = q_apply(excl, q_apply(d.qsum[sid], qc & 1));
+    const int lastc = ((qc & 2) && d.qlast[i] == t) ? lastj : -1;  // the row's last list entry, if here
+    bool changed = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (!(v[j] >= 0 && !((rm >> j) & 1u))) continue;
+      if (!(v[j] & GH_FLAG)) {
         s = 0;
         continue;
       }
-      if (!(s == 0 || c == lastc)) d.hb[cur][off] = v & ~GH_FLAG;  // skipped this round
+      if (!(s == 0 || w.lc * 4 + j == lastc)) {
+        v[j] &= ~GH_FLAG;  // skipped this round
+        changed = true;
+      }
       s ^= 1;
     }
+    if (changed) *reinterpret_cast<v4i*>(cell) = v;
   }
 }
 
 }  // namespace
 
+// d.tw -> template tile width
+#define GH_TW_DISPATCH(F, ...)                  \
+  switch (d.tw) {                              \
+    case 8: F<8>(__VA_ARGS__); break;          \
+    case 16: F<16>(__VA_ARGS__); break;        \
+    case 32: F<32>(__VA_ARGS__); break;        \
+    case 128: F<128>(__VA_ARGS__); break;      \
+    case 256: F<256>(__VA_ARGS__); break;      \
+    default: F<64>(__VA_ARGS__); break;        \
+  }
+
+static unsigned seg_grid(const GhRound& p, int tw) {
+  const int64_t waves = ((p.ld / tw) * p.n + (64 / (tw / 4)) - 1) / (64 / (tw / 4));
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 16384));
+}
+
+template <int TW>
+static void quirk_sum(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_quirk_sum<TW>, dim3(seg_grid(p, TW)), dim3(256), 0, s, d, cur, dcur, p);
+}
+template <int TW>
+static void quirk_apply(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_quirk_apply<TW>, dim3(seg_grid(p, TW)), dim3(256), 0, s, d, cur, dcur, p);
+}
+template <int TW>
+static void ring_tiles(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_ring_tiles<TW>, dim3(seg_grid(p, TW)), dim3(256), 0, s, d, cur, dcur, p);
+}
+
 void launch_quirk_scan(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
-  const int64_t total = (p.ld / d.tw) * p.n;
-  const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 65536);
-  hipLaunchKernelGGL(k_quirk_sum, dim3(grid), dim3(256), 0, s, d, cur, dcur, p);
+  GH_TW_DISPATCH(quirk_sum, d, cur, dcur, p, s)
   hipLaunchKernelGGL(k_quirk_prefix, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
 }
 
 void launch_quirk_apply(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
-  const int64_t total = (p.ld / d.tw) * p.n;
-  const unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 65536);
   hipLaunchKernelGGL(k_quirk_carry, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
-  hipLaunchKernelGGL(k_quirk_apply, dim3(grid), dim3(256), 0, s, d, cur, dcur, p);
+  GH_TW_DISPATCH(quirk_apply, d, cur, dcur, p, s)
 }
 
 void launch_prep(const GhDev& d, int dcur, hipStream_t s) {
@@ -801,11 +876,12 @@ void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
 }
 
 void launch_ring_count(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_ring_count, dim3(p.n), dim3(256), 0, s, d, cur, dcur, p);
+  GH_TW_DISPATCH(ring_tiles, d, cur, dcur, p, s)
+  hipLaunchKernelGGL(k_ring_count, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
 }
 
 void launch_ring_select(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_ring_select, dim3(p.n), dim3(256), 0, s, d, cur, dcur, p);
+  hipLaunchKernelGGL(k_ring_select, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
 }
 
 void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
