@@ -117,8 +117,10 @@ const char* gh_last_error(void* h);
 int gh_abi_version(void);
 
 /* Whole-state transfer (host <-> HBM). Rows [row0, row0+n_rows) of the N x N
- * tables; hb values >= 2^30 are rejected. `round` is the tick of the last
- * completed round; pending REMOVEs are cleared on import. */
+ * tables. `round` is the tick of the last completed round; heartbeats above
+ * 2^23-1 and listed members with ts > round+1 are rejected (GH_ERANGE: the
+ * device keeps a 23-bit heartbeat and the cell's age); pending
+ * REMOVEs are cleared on import. */
 int gh_import_state(void* h, const int32_t* hb, const int32_t* ts,
                     const uint8_t* alive, int64_t row0, int64_t n_rows,
                     int32_t round);
@@ -148,6 +150,16 @@ int gh_read_detectors(void* h, int32_t* rows, int64_t cap, int64_t* n_out);
 /* "lsm" (slave/slave.go:558-561): observer's present members. */
 int gh_lsm(void* h, int32_t observer, int32_t* ids, int32_t* hb, int32_t* ts,
            int64_t cap, int64_t* n_out);
+
+/* MergeMemberList (slave/slave.go:414-440) of one received list into the
+ * observer's row at the engine's current tick (the last completed round):
+ * ids[x] (distinct members) with heartbeats hb[x] >= 0; the remote ts is
+ * ignored (:426, :437). Present members advance when hb is larger, absent
+ * ones are added, tombstoned ones are left alone. A stopped observer does
+ * not receive (GetMsg runs while Alive). *merged = cells changed. Decoding
+ * a reference datagram into (ids, hb) is the host's codec. */
+int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* hb, int64_t n,
+                  int64_t* merged);
 
 /* "put" placement: Handle_put_request (master/master.go:152) for n distinct
  * files. replicas: [n][replicas] (-1 padded), versions [n], status [n]

@@ -101,6 +101,7 @@ def lib():
         L.or_read_failed.argtypes = [vp, vp, i64]
         L.or_read_detectors.argtypes = [vp, vp, i64, P(i64)]
         L.or_lsm.argtypes = [vp, i32, vp, vp, vp, i64, P(i64)]
+        L.or_merge_list.argtypes = [vp, i32, vp, vp, i64, P(i64)]
         L.or_put.argtypes = [vp, vp, i64, vp, vp, vp]
         L.or_repair.argtypes = [vp, i32, P(PlanEntry), i64, P(i64)]
         L.or_get_files.argtypes = [vp, vp, i64, vp, vp]
@@ -204,6 +205,13 @@ class Oracle:
         self._chk(lib().or_lsm(self.h, observer, _p(ids), _p(hb), _p(ts), self.n, C.byref(n)))
         k = n.value
         return ids[:k], hb[:k], ts[:k]
+
+    def merge_list(self, observer, ids, hb):
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        hb = np.ascontiguousarray(hb, dtype=np.int32)
+        n = C.c_int64()
+        self._chk(lib().or_merge_list(self.h, observer, _p(ids), _p(hb), len(ids), C.byref(n)))
+        return n.value
 
     def put(self, files):
         f = np.ascontiguousarray(files, dtype=np.int32)

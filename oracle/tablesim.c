@@ -577,6 +577,27 @@ int or_lsm(void *h, int32_t obs, int32_t *ids, int32_t *hb, int32_t *ts, int64_t
   return GH_OK;
 }
 
+/* MergeMemberList (slave/slave.go:414-440) of an external list into row obs
+ * at the current tick (the last completed round); ids distinct. */
+int or_merge_list(void *h, int32_t obs, const int32_t *ids, const int32_t *hb, int64_t n, int64_t *merged) {
+  ors *s = (ors *)h;
+  if (obs < 0 || obs >= s->rows) return fail(s, GH_EINVAL, "observer");
+  int64_t m = 0;
+  if (s->alive[obs]) {
+    for (int64_t x = 0; x < n; ++x) {
+      int32_t c = ids[x];
+      int32_t v = HB(s, obs, c);
+      if (v >= GH_ABSENT && hb[x] > v) { /* present and lower, or absent and not tombstoned */
+        HB(s, obs, c) = hb[x];
+        TS(s, obs, c) = s->round;
+        m++;
+      }
+    }
+  }
+  *merged = m;
+  return GH_OK;
+}
+
 /* ---------------------------------------------------------------- files */
 
 /* Member_list of the master: present members of the master row, ID order

@@ -222,6 +222,25 @@ __global__ __launch_bounds__(256) void k_join_bcast(GhDev d, int cur, int32_t I,
   if (merged) atomicAdd(&d.stats[ST_MERGED], (unsigned long long)merged);
 }
 
+// MergeMemberList of an external list into row `obs` at tick p.r - 1 (the
+// last completed round): the cell's age in the coming round p.r is 1.
+__global__ __launch_bounds__(256) void k_merge_list(GhDev d, int cur, int32_t obs, const int32_t* ids,
+                                                    const int32_t* hb, int64_t n, GhRound p) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n) return;
+  const int32_t c = ids[x];
+  const int64_t lc = (int64_t)c - d.col0;
+  if (lc < 0 || lc >= d.ncol) return;
+  const int64_t off = gh_cell(d, obs, lc);
+  const int32_t v = d.hb[cur][off];
+  const int32_t cur_hb = gh_ext(v);
+  const int32_t m = hb[x];
+  if (cur_hb >= GH_ABSENT && m > cur_hb) {  // :424-426, :435-438; tombstones blocked (:432-434)
+    d.hb[cur][off] = gh_present(m, 1, gh_flag_for<false>(d, m, 1, c, obs, off, p.r, p.t_fail));
+    atomicAdd(&d.nd[5], 1);
+  }
+}
+
 unsigned grid_for(int64_t work) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, kMaxGrid));
 }
@@ -276,4 +295,10 @@ void launch_join_reset(const GhDev& d, int cur, const int32_t* rows, int32_t nr,
                        hipStream_t s) {
   if (nr == 0) return;
   hipLaunchKernelGGL(k_join_reset, dim3(grid_for((int64_t)nr * p.ld)), dim3(256), 0, s, d, cur, rows, nr, p);
+}
+
+void launch_merge_list(const GhDev& d, int cur, int32_t obs, const int32_t* ids, const int32_t* hb, int64_t n,
+                       const GhRound& p, hipStream_t s) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(k_merge_list, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, cur, obs, ids, hb, n, p);
 }

@@ -115,7 +115,7 @@ struct GhDev {
   int32_t *det_cnt[2], *det_min[2];
   uint32_t *dbits;
   int32_t *dlist;
-  int32_t *nd;      // [0..1] local |D| per parity, [2..3] dlist fill, [4] join adds
+  int32_t *nd;      // [0..1] local |D| per parity, [2..3] dlist fill, [4] join adds, [5] list merges
   uint16_t *part;
   int32_t *inbox_beg, *inbox_cnt, *inbox, *inbox_fill, *targets;
   int32_t *ring;    // ring mode: [world][n][2] (local snapshot count, local position of the sender)
@@ -250,6 +250,9 @@ void launch_leave(const GhDev& d, int cur, const int32_t* leavers, int32_t nl, c
 void launch_join_add(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, int32_t introducer,
                      const GhRound& p, hipStream_t s);
 void launch_join_bcast(const GhDev& d, int cur, int32_t introducer, const GhRound& p, hipStream_t s);
+// MergeMemberList of an external list into one row (nd[5] counts merges)
+void launch_merge_list(const GhDev& d, int cur, int32_t obs, const int32_t* ids, const int32_t* hb, int64_t n,
+                       const GhRound& p, hipStream_t s);
 void launch_join_reset(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p,
                        hipStream_t s);
 // place.hip (rbits holds the master row [q=0] and, for repair, the observer row [q=1])

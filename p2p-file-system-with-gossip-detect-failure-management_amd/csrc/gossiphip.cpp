@@ -759,6 +759,40 @@ int gh_lsm(void* h, int32_t observer, int32_t* ids, int32_t* hb, int32_t* ts, in
   return GH_OK;
 }
 
+int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* hb, int64_t n, int64_t* merged) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || n < 0 || (n > 0 && (!ids || !hb))) return GH_EINVAL;
+  if (observer < 0 || observer >= e->n) return set_err(e, GH_EINVAL, "observer");
+  {
+    std::vector<int32_t> s(ids, ids + n);
+    for (int64_t x = 0; x < n; ++x) {
+      if (ids[x] < 0 || ids[x] >= e->n) return set_err(e, GH_EINVAL, "member id out of range");
+      if (hb[x] < 0 || hb[x] > GH_HB_MAX) return set_err(e, GH_ERANGE, "heartbeat out of range");
+    }
+    std::sort(s.begin(), s.end());
+    if (std::adjacent_find(s.begin(), s.end()) != s.end()) return set_err(e, GH_EINVAL, "member ids must be distinct");
+  }
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  int32_t cnt = 0;
+  if (n > 0 && e->alive[observer]) {  // GetMsg runs only while Alive (slave/slave.go:208)
+    Staging st;
+    int rc;
+    if ((rc = st.alloc(e, sizeof(int32_t) * 2 * n))) return rc;
+    HIPCHK(e, hipMemcpyAsync(st.p, ids, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(st.as<int32_t>() + n, hb, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemsetAsync(e->d.nd + 5, 0, sizeof(int32_t), e->stream));
+    const GhRound p = round_params(e, e->round + 1);
+    launch_merge_list(e->d, e->cur, observer, st.as<int32_t>(), st.as<int32_t>() + n, n, p, e->stream);
+    HIPCHK(e, hipGetLastError());
+    if ((rc = allreduce_i32(e, e->d.nd + 5, e->d.nd + 5, 1))) return rc;
+    launch_count(e->d, e->cur, p, e->stream);  // presence changed: refresh the row counts
+    HIPCHK(e, hipMemcpyAsync(&cnt, e->d.nd + 5, sizeof cnt, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  if (merged) *merged = cnt;
+  return GH_OK;
+}
+
 int gh_put(void* h, const int32_t* files, int64_t n, int32_t* replicas, int32_t* versions, int32_t* status) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;

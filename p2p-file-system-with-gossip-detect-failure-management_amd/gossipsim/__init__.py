@@ -24,7 +24,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-from . import _abi
+from . import _abi, codec
 from ._abi import (GH_COMM_LOCAL, GH_COMM_RCCL, GH_DETECT_CANONICAL, GH_DETECT_QUIRK,  # noqa: F401
                    GH_EPLACEMENT_STARVED, GH_EV_CRASH, GH_EV_JOIN, GH_EV_LEAVE, GH_OK, GH_PEER_PULL,
                    GH_PEER_RING, Config, PlanEntry)
@@ -170,6 +170,15 @@ class Engine:
         k = n.value
         return ids[:k], hb[:k], ts[:k]
 
+    def merge_list(self, observer, ids, hb):
+        """MergeMemberList (slave/slave.go:414-440) of a received list into
+        `observer`'s row now; returns the number of cells changed."""
+        ids = np.ascontiguousarray(ids, dtype=np.int32)
+        hb = np.ascontiguousarray(hb, dtype=np.int32)
+        n = C.c_int64()
+        self._chk(self.lib.gh_merge_list(self.h, observer, _p(ids), _p(hb), len(ids), C.byref(n)))
+        return n.value
+
     # ---- files -----------------------------------------------------------
     def put(self, files):
         f = np.ascontiguousarray(files, dtype=np.int32)
@@ -283,10 +292,13 @@ class Cluster:
     a failure in round r triggers Update_metadata with its own list as
     `available` at round r + repair_delay (slave/slave.go:1122-1133)."""
 
-    def __init__(self, n, repair_delay=8, **cfg_kw):
+    def __init__(self, n, repair_delay=8, addresses=None, **cfg_kw):
         self.engine = Engine(default_config(n, **cfg_kw))
         self.n = n
         self.repair_delay = repair_delay
+        # member id <-> address (the reference's identity, slave/slave.go:145-159)
+        self.addresses = list(addresses) if addresses is not None else [f"10.0.{i >> 8}.{i & 255}" for i in range(n)]
+        self.ids = {a: i for i, a in enumerate(self.addresses)}
         self.scheduled: dict[int, list[int]] = {}
         self.plans: list[tuple[int, int, tuple]] = []  # (round, observer, plan)
 
@@ -303,6 +315,29 @@ class Cluster:
     def lsm(self, member):
         ids, hb, ts = self.engine.lsm(member)
         return list(zip(ids.tolist(), hb.tolist(), ts.tolist()))
+
+    # wire format of the gossip datagrams (slave/slave.go:365-385, 527-542)
+    def datagram(self, member) -> bytes:
+        """What `member` sends its ring neighbours: its list, encoded. The
+        update time is the member's local tick (the reference sends UnixNano,
+        which receivers ignore, :426, :437)."""
+        return codec.encode((self.addresses[i], hb, ts) for i, hb, ts in self.lsm(member))
+
+    def receive(self, member, datagram: bytes):
+        """GetMsg's gossip branch (:241-245) at `member`: decode (raises
+        codec.DecodePanic where the reference's goroutine would panic), then
+        MergeMemberList. Returns the number of cells changed. Addresses must
+        be cluster members; the first entry of a repeated address is the one
+        MergeMemberList compares (GetIndex, :396-403)."""
+        entries = codec.decode(datagram)
+        seen, ids, hbs = set(), [], []
+        for addr, hb, _ in entries:
+            if addr in seen:
+                continue
+            seen.add(addr)
+            ids.append(self.ids[addr])
+            hbs.append(hb)
+        return self.engine.merge_list(member, ids, hbs)
 
     def put(self, files):
         return self.engine.put(files)

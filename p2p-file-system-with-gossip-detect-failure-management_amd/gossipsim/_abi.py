@@ -77,6 +77,7 @@ SYMBOLS = [
     ("gh_read_failed", C.c_int, [_vp, _vp, _i64]),
     ("gh_read_detectors", C.c_int, [_vp, _vp, _i64, _P(_i64)]),
     ("gh_lsm", C.c_int, [_vp, _i32, _vp, _vp, _vp, _i64, _P(_i64)]),
+    ("gh_merge_list", C.c_int, [_vp, _i32, _vp, _vp, _i64, _P(_i64)]),
     ("gh_put", C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     ("gh_repair", C.c_int, [_vp, _i32, _P(PlanEntry), _i64, _P(_i64)]),
     ("gh_get_files", C.c_int, [_vp, _vp, _i64, _vp, _vp]),

@@ -223,3 +223,52 @@ def test_layout_variants_identical(gs, oracle_mod, tw, nt, xmap):
         a, b = eng.lsm(obs), orc.lsm(obs)
         for x, y in zip(a, b):
             np.testing.assert_array_equal(x, y)
+
+
+def test_merge_list_external_datagrams(gs, oracle_mod):
+    """Reference datagrams (gossipsim.codec, slave/slave.go:365-385) merged
+    into members' rows between rounds (GetMsg -> decode -> MergeMemberList,
+    :241-245) through gh_merge_list, then more rounds: bit-exact vs the
+    oracle. Lists carry raised, equal, lower and tombstoned entries."""
+    from gossipsim import codec
+    n = 48
+    cfg = dict(fanout=3, seed=0x4D, t_fail=4, t_cleanup=6)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg))
+    init = sc.full_state(n)
+    eng.import_state(*init, 0)
+    orc.import_state(*init, 0)
+    sched = sc.random_churn(n, 20, 17, p_crash=0.05, p_leave=0.02, p_join=0.05)
+    addr = [f"10.1.0.{i}" for i in range(n)]
+    rng = np.random.default_rng(5)
+    for r in range(1, 21):
+        if r in sched:
+            eng.apply_events(sched[r])
+            orc.apply_events(sched[r])
+        assert eng.step(1) == orc.step(1), r
+        for _ in range(3):
+            src, dst = (int(x) for x in rng.integers(0, n, 2))
+            ids, hb, ts = orc.lsm(src)
+            if len(ids) == 0:  # empty lists are never sent (HeartBeat's <4 guard); decode would panic
+                continue
+            hb = hb + rng.integers(-2, 4, len(hb)).clip(-hb)  # some raised, some lowered
+            dg = codec.encode((addr[i], int(h), int(t)) for i, h, t in zip(ids, hb, ts))
+            got = codec.decode(dg, read_buf=1 << 20)
+            ids2 = [addr.index(a) for a, _, _ in got]
+            hb2 = [h for _, h, _ in got]
+            assert eng.merge_list(dst, ids2, hb2) == orc.merge_list(dst, ids2, hb2)
+        compare(eng, orc, r)
+
+
+def test_cluster_datagram_roundtrip(gs):
+    """Cluster.datagram/receive: a member's list in the reference's wire
+    format merged at another member (10 VMs, config 1 shape)."""
+    cl = gs.Cluster(10, max_files=16)
+    for m in range(10):
+        cl.join(m)
+        cl.tick()
+    cl.tick(3)
+    dg = cl.datagram(3)
+    assert dg.count(b"<#ENTRY#>") == len(cl.lsm(3)) - 1 and len(dg) <= 1024
+    assert cl.receive(5, dg) >= 0
+    assert {i for i, _, _ in cl.lsm(5)} >= {i for i, _, _ in cl.lsm(3)}

@@ -201,3 +201,26 @@ def test_n65536_sharded_matches_single(gs):
         for x, y in zip(eng.export_state(i, 1), rg):
             np.testing.assert_array_equal(x, y)
     eng.close()
+
+
+def test_merge_list_sharded(gs, oracle_mod):
+    """gh_merge_list over 3 shards: each shard merges the members of its
+    columns; counts summed over ranks."""
+    n = 150
+    cfg = dict(fanout=3, seed=0x4E)
+    grp = gs.ShardGroup(gs.default_config(n, **cfg), 3)
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg))
+    try:
+        init = sc.full_state(n)
+        grp.import_state(*init, 0)
+        orc.import_state(*init, 0)
+        rng = np.random.default_rng(9)
+        for r in range(1, 9):
+            assert grp.step(1) == orc.step(1)
+            ids = rng.permutation(n)[:60].astype(np.int32)
+            hb = rng.integers(0, 3 * r + 4, 60).astype(np.int32)
+            obs = int(rng.integers(0, n))
+            assert grp.merge_list(obs, ids, hb) == orc.merge_list(obs, ids, hb)
+            compare(grp, orc, r)
+    finally:
+        grp.close()
