@@ -167,6 +167,11 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
  * starved. */
 int gh_put(void* h, const int32_t* files, int64_t n, int32_t* replicas,
            int32_t* versions, int32_t* status);
+/* If_file_updated_recent (master/master.go:214-229) for n files: conflict[x]
+ * = 1 if the file exists and was put less than `window` rounds ago (the
+ * reference's 60 s write-write window at 1 s rounds: window = 60). The put
+ * path asks for confirmation on a conflict (server/server.go:79-114). */
+int gh_put_conflicts(void* h, const int32_t* files, int64_t n, int32_t window, uint8_t* conflict);
 /* Update_metadata (master/master.go:74) with available = observer's list;
  * plan entries in file order. *n_plan = number of entries (<= cap written). */
 int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap,

@@ -104,6 +104,7 @@ def lib():
         L.or_merge_list.argtypes = [vp, i32, vp, vp, i64, P(i64)]
         L.or_put.argtypes = [vp, vp, i64, vp, vp, vp]
         L.or_repair.argtypes = [vp, i32, P(PlanEntry), i64, P(i64)]
+        L.or_put_conflicts.argtypes = [vp, vp, i64, i32, vp]
         L.or_get_files.argtypes = [vp, vp, i64, vp, vp]
         L.or_delete_files.argtypes = [vp, vp, i64, vp]
         L.or_philox.argtypes = [vp, vp, vp]
@@ -220,6 +221,12 @@ class Oracle:
         st = np.zeros(len(f), np.int32)
         self._chk(lib().or_put(self.h, _p(f), len(f), _p(rep), _p(ver), _p(st)), ok=(0, GH_EPLACEMENT_STARVED))
         return rep, ver, st
+
+    def put_conflicts(self, files, window=60):
+        f = np.ascontiguousarray(files, dtype=np.int32)
+        out = np.zeros(len(f), np.uint8)
+        self._chk(lib().or_put_conflicts(self.h, _p(f), len(f), window, _p(out)))
+        return out
 
     def repair(self, observer, cap=None):
         cap = cap if cap is not None else max(int(self.cfg.max_files), 1)

@@ -684,6 +684,17 @@ int or_put(void *h, const int32_t *files, int64_t n, int32_t *replicas, int32_t 
   return rc;
 }
 
+/* If_file_updated_recent (master/master.go:214-229): now - ts < 60 s. */
+int or_put_conflicts(void *h, const int32_t *files, int64_t n, int32_t window, uint8_t *conflict) {
+  ors *s = (ors *)h;
+  for (int64_t x = 0; x < n; ++x) {
+    int32_t f = files[x];
+    if (f < 0 || f >= s->fcap) return fail(s, GH_EINVAL, "file id");
+    conflict[x] = s->ver[f] >= 0 && (int64_t)s->round - s->fts[f] < window;
+  }
+  return GH_OK;
+}
+
 int or_repair(void *h, int32_t observer, gh_plan_entry *plan, int64_t cap, int64_t *n_plan) {
   ors *s = (ors *)h;
   if (observer < 0 || observer >= s->rows) return fail(s, GH_EINVAL, "observer");

@@ -260,3 +260,4 @@ void launch_candidates(const GhDev& d, int32_t nr, hipStream_t s);
 void launch_put(const GhDev& d, int32_t nr, int64_t n, int32_t R, int32_t now, uint64_t seed, hipStream_t s);
 void launch_repair(const GhDev& d, int32_t nr, int32_t R, uint64_t seed, hipStream_t s);
 void launch_get(const GhDev& d, int64_t n, int32_t R, int del, hipStream_t s);
+void launch_conflicts(const GhDev& d, int64_t n, int32_t now, int32_t window, hipStream_t s);

@@ -821,6 +821,24 @@ int gh_put(void* h, const int32_t* files, int64_t n, int32_t* replicas, int32_t*
   return GH_OK;
 }
 
+int gh_put_conflicts(void* h, const int32_t* files, int64_t n, int32_t window, uint8_t* conflict) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || (n > 0 && !conflict)) return GH_EINVAL;
+  int rc;
+  if ((rc = check_files(e, files, n, false))) return rc;
+  if (n == 0) return GH_OK;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  if ((rc = ensure_io(e, n))) return rc;
+  HIPCHK(e, hipMemcpyAsync(e->d.io_a, files, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
+  launch_conflicts(e->d, n, e->round, window, e->stream);
+  HIPCHK(e, hipGetLastError());
+  std::vector<int32_t> out(n);
+  HIPCHK(e, hipMemcpyAsync(out.data(), e->d.io_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  for (int64_t x = 0; x < n; ++x) conflict[x] = (uint8_t)out[x];
+  return GH_OK;
+}
+
 int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap, int64_t* n_plan) {
   Engine* e = static_cast<Engine*>(h);
   if (!e || !n_plan || (cap > 0 && !plan)) return GH_EINVAL;

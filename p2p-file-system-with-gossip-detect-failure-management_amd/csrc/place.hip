@@ -143,7 +143,19 @@ __global__ __launch_bounds__(256) void k_get(GhDev d, int64_t n, int32_t R, int 
   if (del) d.ver[f] = -1;
 }
 
+// If_file_updated_recent (:214-229) for io_a[0..n) -> io_d (0/1).
+__global__ __launch_bounds__(256) void k_conflicts(GhDev d, int64_t n, int32_t now, int32_t window) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= n) return;
+  const int32_t f = d.io_a[x];
+  d.io_d[x] = d.ver[f] >= 0 && (int64_t)now - d.fts[f] < window;
+}
+
 }  // namespace
+
+void launch_conflicts(const GhDev& d, int64_t n, int32_t now, int32_t window, hipStream_t s) {
+  hipLaunchKernelGGL(k_conflicts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d, n, now, window);
+}
 
 void launch_candidates(const GhDev& d, int32_t nr, hipStream_t s) {
   hipLaunchKernelGGL(k_candidates, dim3(1), dim3(1024), 0, s, d, nr);

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes as C
 import itertools
+from collections import namedtuple
 import os
 from concurrent.futures import ThreadPoolExecutor
 
@@ -189,6 +190,19 @@ class Engine:
                   ok=(GH_OK, GH_EPLACEMENT_STARVED))
         return rep, ver, st
 
+    def put_conflicts(self, files, window=60):
+        """If_file_updated_recent (master/master.go:214-229): 1 where the
+        file was put less than `window` rounds (60 s at 1 s rounds) ago."""
+        f = np.ascontiguousarray(files, dtype=np.int32)
+        out = np.zeros(len(f), np.uint8)
+        self._chk(self.lib.gh_put_conflicts(self.h, _p(f), len(f), window, _p(out)))
+        return out
+
+    def alive(self):
+        a = np.empty(self.n, np.uint8)
+        self._chk(self.lib.gh_export_state(self.h, None, None, _p(a), 0, self.n))
+        return a
+
     def repair(self, observer, cap=None):
         cap = cap if cap is not None else max(int(self.cfg.max_files), 1)
         plan = (PlanEntry * cap)()
@@ -286,6 +300,10 @@ class ShardGroup:
         self.pool.shutdown()
 
 
+PutResult = namedtuple("PutResult", "file put_or_not replicas version status acks quorum_met")
+GetResult = namedtuple("GetResult", "file replicas version acks quorum_met")
+
+
 class Cluster:
     """The reference's per-node commands over one Engine (member IDs stand in
     for the VM addresses). Repairs follow Fail_recover: every row that detects
@@ -339,13 +357,60 @@ class Cluster:
             hbs.append(hb)
         return self.engine.merge_list(member, ids, hbs)
 
-    def put(self, files):
-        return self.engine.put(files)
+    # SDFS ops (slave/slave.go:661-928 over master/master.go:74-259)
+    WRITE_WINDOW = 60  # If_file_updated_recent: 60 s (master/master.go:225) at 1 s rounds
+
+    @staticmethod
+    def quorum(n_replicas):
+        """cal_quorum_num (slave/slave.go:717-722): int(math.Ceil(float64((n+1)/2)))
+        with Go's integer division inside: 1, 1, 2, 2, 3 for n = 1..5."""
+        return (n_replicas + 1) // 2
+
+    def put(self, files, confirm=()):
+        """put for each file (slave/slave.go:668 -> Get_put_info,
+        server/server.go:74-121): a file put less than WRITE_WINDOW rounds ago
+        is a write-write conflict and goes ahead only if the requester
+        confirms (file in `confirm`, the interactive "yes"); otherwise
+        Handle_put_request places it and bumps the version. acks = replicas
+        whose process is alive; the reference waits for
+        quorum(len(replicas)) of them (:698-714, forever if they never come).
+        Returns PutResult per file, in input order."""
+        files = [int(f) for f in files]
+        conf = set(int(f) for f in confirm)
+        clash = self.engine.put_conflicts(files, self.WRITE_WINDOW) if files else []
+        go = [f for f, c in zip(files, clash) if not c or f in conf]
+        placed = {}
+        if go:
+            rep, ver, st = self.engine.put(go)
+            alive = self.engine.alive()
+            for x, f in enumerate(go):
+                r = [int(a) for a in rep[x] if a >= 0]
+                placed[f] = (r, int(ver[x]), int(st[x]), sum(int(alive[a]) for a in r))
+        out = []
+        for f in files:
+            if f not in placed:
+                out.append(PutResult(f, False, [], -1, GH_OK, 0, False))
+                continue
+            r, v, st, acks = placed[f]
+            out.append(PutResult(f, True, r, v, st, acks, st == GH_OK and acks >= self.quorum(len(r))))
+        return out
 
     def get(self, files):
-        return self.engine.get_files(files)
+        """get (slave/slave.go:815-890): the master's replica list and
+        version (-1: "No File Found"), and whether a read quorum of replicas
+        is alive to answer."""
+        rep, ver = self.engine.get_files(files)
+        alive = self.engine.alive()
+        out = []
+        for x, f in enumerate(files):
+            r = [int(a) for a in rep[x] if a >= 0]
+            acks = sum(int(alive[a]) for a in r)
+            out.append(GetResult(int(f), r, int(ver[x]), acks, int(ver[x]) >= 0 and acks >= self.quorum(len(r))))
+        return out
 
-    ls = get
+    def ls(self, files):
+        """ls (slave/slave.go:892-917): replica list and version per file."""
+        return self.engine.get_files(files)
 
     def delete(self, files):
         return self.engine.delete_files(files)

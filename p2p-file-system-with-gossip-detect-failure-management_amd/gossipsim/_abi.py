@@ -79,6 +79,7 @@ SYMBOLS = [
     ("gh_lsm", C.c_int, [_vp, _i32, _vp, _vp, _vp, _i64, _P(_i64)]),
     ("gh_merge_list", C.c_int, [_vp, _i32, _vp, _vp, _i64, _P(_i64)]),
     ("gh_put", C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
+    ("gh_put_conflicts", C.c_int, [_vp, _vp, _i64, _i32, _vp]),
     ("gh_repair", C.c_int, [_vp, _i32, _P(PlanEntry), _i64, _P(_i64)]),
     ("gh_get_files", C.c_int, [_vp, _vp, _i64, _vp, _vp]),
     ("gh_delete_files", C.c_int, [_vp, _vp, _i64, _vp]),

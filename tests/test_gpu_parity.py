@@ -272,3 +272,41 @@ def test_cluster_datagram_roundtrip(gs):
     assert dg.count(b"<#ENTRY#>") == len(cl.lsm(3)) - 1 and len(dg) <= 1024
     assert cl.receive(5, dg) >= 0
     assert {i for i, _, _ in cl.lsm(5)} >= {i for i, _, _ in cl.lsm(3)}
+
+
+def test_put_conflicts_and_cluster_ops(gs, oracle_mod):
+    """The write-write window on the GPU against the oracle for 3,000 files
+    put at different rounds, and Cluster.put/get: conflicts go ahead only
+    when confirmed; acks count live replicas against the quorum."""
+    n, F = 64, 3000
+    cfg = dict(max_files=F, seed=0x5EED0006)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg))
+    init = sc.full_state(n)
+    eng.import_state(*init, 0)
+    orc.import_state(*init, 0)
+    rng = np.random.default_rng(1)
+    for r in range(1, 80):
+        assert eng.step(1) == orc.step(1)
+        if r % 7 == 0:
+            f = rng.permutation(F)[:200].astype(np.int32)
+            for x, y in zip(eng.put(f), orc.put(f)):
+                np.testing.assert_array_equal(x, y)
+        if r % 13 == 0:
+            f = np.arange(F, dtype=np.int32)
+            np.testing.assert_array_equal(eng.put_conflicts(f), orc.put_conflicts(f))
+    eng.close()
+
+    cl = gs.Cluster(10, max_files=8)
+    for m in range(10):
+        cl.join(m)
+        cl.tick()
+    res = cl.put([0, 1])
+    assert all(p.put_or_not and p.version == 1 and p.quorum_met for p in res)
+    again = cl.put([0, 1], confirm=[1])  # file 0 clashes (0 rounds ago), 1 is confirmed
+    assert (again[0].put_or_not, again[1].put_or_not, again[1].version) == (False, True, 2)
+    for a in res[1].replicas[:3]:
+        cl.crash(a)
+    cl.tick()
+    g = cl.get([1, 5])[0]
+    assert g.acks == 1 and g.quorum_met is False and cl.get([5])[0].version == -1
