@@ -310,3 +310,54 @@ def test_put_conflicts_and_cluster_ops(gs, oracle_mod):
     cl.tick()
     g = cl.get([1, 5])[0]
     assert g.acks == 1 and g.quorum_met is False and cl.get([5])[0].version == -1
+
+
+def c5_run(eng, orc, n, F, rounds=32):
+    """BASELINE config 5 shape at 1-GPU scale: 2^20 files placed, then waves
+    at r=4/8/12 (join 1% new IDs, leave 1%, crash 1%), and every detecting
+    row's repair pass 8 rounds after its detection (Fail_recover,
+    slave/slave.go:1122-1133; here the first two detectors per round)."""
+    files = np.arange(F, dtype=np.int32)
+    for lo in range(0, F, 1 << 18):
+        for x, y in zip(eng.put(files[lo:lo + (1 << 18)]), orc.put(files[lo:lo + (1 << 18)])):
+            np.testing.assert_array_equal(x, y)
+    newcomers = list(range(n - n // 100, n))
+    rng = np.random.default_rng(55)
+    pool = [c for c in range(1, n - n // 100)]
+    rng.shuffle(pool)
+    waves = {4: [(sc.JOIN, c) for c in newcomers],
+             8: [(sc.LEAVE, c) for c in pool[: n // 100]],
+             12: [(sc.CRASH, c) for c in pool[n // 100: 2 * (n // 100)]]}
+    due = {}
+    plans = 0
+    for r in range(1, rounds + 1):
+        if r in waves:
+            eng.apply_events(waves[r])
+            orc.apply_events(waves[r])
+        assert eng.step(1) == orc.step(1), r
+        det = list(orc.read_detectors())
+        np.testing.assert_array_equal(eng.read_detectors(), det)
+        if det:
+            due.setdefault(r + 8, []).extend(int(x) for x in det[:2])
+        for obs in due.pop(r, []):
+            p1, p2 = eng.repair(obs), orc.repair(obs)
+            assert p1 == p2, (r, obs)
+            plans += len(p1)
+    for lo in range(0, F, 1 << 18):
+        for x, y in zip(eng.get_files(files[lo:lo + (1 << 18)]), orc.get_files(files[lo:lo + (1 << 18)])):
+            np.testing.assert_array_equal(x, y)
+    return plans
+
+
+def test_c5_churn_rereplication_1m_files(gs, oracle_mod):
+    n, F = 2048, 1 << 20
+    cfg = dict(fanout=4, seed=0x5EED0005, max_files=F, t_fail=8, t_cleanup=8)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    hb, ts, alive = sc.full_state(n)
+    alive[n - n // 100:] = 0
+    hb[:, n - n // 100:] = -1
+    hb[n - n // 100:, :] = -1
+    eng.import_state(hb, ts, alive, 0)
+    orc.import_state(hb, ts, alive, 0)
+    assert c5_run(eng, orc, n, F) > 0

@@ -224,3 +224,23 @@ def test_merge_list_sharded(gs, oracle_mod):
             compare(grp, orc, r)
     finally:
         grp.close()
+
+
+def test_c5_churn_rereplication_sharded(gs, oracle_mod):
+    """Config 5 shape (2^20 files, join/leave/crash waves, repairs at
+    detection + 8) over 2 shards."""
+    from test_gpu_parity import c5_run
+    n, F = 1024, 1 << 20
+    cfg = dict(fanout=4, seed=0x5EED0015, max_files=F, t_fail=8, t_cleanup=8)
+    grp = gs.ShardGroup(gs.default_config(n, **cfg), 2)
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    try:
+        hb, ts, alive = sc.full_state(n)
+        alive[n - n // 100:] = 0
+        hb[:, n - n // 100:] = -1
+        hb[n - n // 100:, :] = -1
+        grp.import_state(hb, ts, alive, 0)
+        orc.import_state(hb, ts, alive, 0)
+        assert c5_run(grp, orc, n, F) > 0
+    finally:
+        grp.close()
