@@ -16,7 +16,7 @@
 //   N=65,536, TW=64): the round kernel sweeps tile by tile, so its own-row
 //   streams are sequential and every peer gather of a tile stays inside
 //   that slice.
-//   hb[2]  int32   double-buffered membership table, one word per cell:
+//   Each cell has one 32-bit meaning (the "wide" encoding):
 //                    present    0 <= v:  heartbeat in bits 0..22, age in
 //                                        23..29, flag in bit 30
 //                    tombstone  v < -1:  INT_MIN | age << 23
@@ -29,11 +29,26 @@
 //                  the peers reading it as a snapshot re-derive it. Every
 //                  decision of a round on ts is a flag test or an age
 //                  comparison: a round reads and writes one table, not two.
-//   ts     int32   exact local-clock tick, kept only where the age cannot give
-//                  it: saturated cells (written when the age reaches the cap),
-//                  absent cells (written on release), rows that stopped
-//                  (written by k_freeze) and imports. export_state decodes
-//                  ts = (round + 1) - age for the other cells.
+//   hn[2]  uint16  double-buffered NARROW table, where the round streams: a
+//                  heartbeat is stored as an offset from a per-column base
+//                  (base[buf][c]):
+//                    present    H<<15 | off<<5 | age   off 0..1022, H = flag
+//                    tombstone  0xFFE0 | age           age 0..30
+//                    absent     0xFFFF
+//                  Visible (present, unflagged) cells are the non-negative
+//                  int16 values and compare like their heartbeats, so a
+//                  snapshot merge is a packed 16-bit max.
+//   hw[2]  int32   the wide encoding, for (tile, row) segments that a narrow
+//                  cell cannot hold (heartbeat outside [base, base+1022],
+//                  saturated tombstone) and for stopped rows (kept wide and
+//                  identical in both buffers: the round never touches them).
+//                  Every narrow cell of such a segment holds GH_N_WIDE, a code
+//                  no narrow cell has, so any reader finds the segment's
+//                  encoding from the cell it reads.
+//   base[2] int32  per local column: base of buf's narrow cells. The round
+//                  sets base[next][c] = (member c's own heartbeat) - GH_BASE_LAG
+//                  (k_base), so every view of c within GH_BASE_LAG rounds of
+//                  its own counter is narrow.
 //   Local columns are padded to ld (multiple of 8*TW and 256); padding cells
 //   stay -1.
 //   per row (global): alive, active, und (u8), cntl / cntg (local / global
@@ -49,7 +64,12 @@
 
 #define GH_HB_BITS 23
 #define GH_HB_MAX ((1 << GH_HB_BITS) - 1)  // largest heartbeat a cell holds (saturates)
-#define GH_AGE_CAP 127                     // age saturates here; exact ts is then in ts[]
+#define GH_AGE_CAP 31                      // age saturates here; exact ts is then in ts[]
+#define GH_N_ABSENT 0xFFFFu                // narrow absent
+#define GH_N_TOMB 0xFFE0u                  // narrow tombstone | age
+#define GH_N_WIDE 0x7FFFu                  // narrow cell of a wide segment
+#define GH_N_OFFMAX 1022                   // largest narrow heartbeat offset
+#define GH_BASE_LAG 1000                   // base = own heartbeat - GH_BASE_LAG
 #define GH_FLAG (1 << 30)                  // detected next round (present cells)
 #define GH_PAD 256               // column padding granule (ld % 256 == 0)
 #define GH_RB 64                 // rows per workgroup tile in the round kernel
@@ -107,7 +127,13 @@ struct GhDev {
   int32_t ncs;      // columns per rank (multiple of 32): rank g owns [g*ncs, g*ncs + ncol_g)
   int32_t ncsw;     // ncs / 32 (bitmap words per rank)
   int32_t rank, world;
-  int32_t *hb[2];   // double buffer
+  int64_t ntiles;   // ld / tw
+  uint16_t *hn[2];  // narrow double buffer
+  int32_t *hw[2];   // wide double buffer
+  int32_t *base[2]; // [ld] narrow base per buffer
+  int32_t *colq;    // [ld] scratch: per local column event index / merged value
+  int64_t *slow;    // [ntiles * n] round: segments for k_round_slow, tile << 32 | row
+  int32_t *slow_n;  // their count
   int32_t *ts;
   uint8_t *alive, *active, *det_any, *und;
   int32_t *cntl, *cntg;  // [n + 8]: per-row present counts (local / allreduced), [n] = |D|
@@ -140,7 +166,7 @@ struct GhDev {
 };
 
 // ---- cell encoding --------------------------------------------------------
-__host__ __device__ __forceinline__ int gh_age(int32_t v) { return (v >> GH_HB_BITS) & GH_AGE_CAP; }
+__host__ __device__ __forceinline__ int gh_age(int32_t v) { return (v >> GH_HB_BITS) & 0x7F; }
 __host__ __device__ __forceinline__ int32_t gh_hbv(int32_t v) { return v & GH_HB_MAX; }
 __host__ __device__ __forceinline__ int32_t gh_present(int32_t hb, int age, bool flag = false) {
   return hb | (age << GH_HB_BITS) | (flag ? GH_FLAG : 0);
@@ -158,6 +184,64 @@ __host__ __device__ __forceinline__ int32_t gh_ext(int32_t v) {
 // Linear index of cell (observer i, LOCAL member column c) in the tiled layout.
 __host__ __device__ __forceinline__ int64_t gh_cell(const GhDev& d, int64_t i, int64_t c) {
   return (c >> d.lgtw) * d.tstride + (i << d.lgtw) + (c & (d.tw - 1));
+}
+
+// ---- narrow <-> wide --------------------------------------------------
+__host__ __device__ __forceinline__ int32_t gh_dec16(uint32_t x, int32_t base) {
+  if (x == GH_N_ABSENT) return GH_ABSENT;
+  const int a = x & 31, f = (x >> 5) & 1023;
+  if (f == 1023) return gh_tomb(a);
+  return gh_present(base + f, a, (x >> 15) != 0);
+}
+// narrow code of wide value v; fit &= it has one
+__host__ __device__ __forceinline__ uint32_t gh_enc16(int32_t v, int32_t base, bool& fit) {
+  if (v == GH_ABSENT) return GH_N_ABSENT;
+  const int a = gh_age(v);
+  if (v < 0) {
+    fit &= a < 31;
+    return GH_N_TOMB | (a & 31);
+  }
+  const int64_t off = (int64_t)gh_hbv(v) - base;
+  fit &= off >= 0 && off <= GH_N_OFFMAX && a <= 31;
+  return ((v & GH_FLAG) ? 0x8000u : 0u) | ((uint32_t)(off & 1023) << 5) | (uint32_t)(a & 31);
+}
+
+// Cell (i, local c) of buffer buf, wide encoding.
+__device__ __forceinline__ int32_t gh_get(const GhDev& d, int buf, int64_t i, int64_t c) {
+  const int64_t off = gh_cell(d, i, c);
+  const uint32_t x = d.hn[buf][off];
+  return x == GH_N_WIDE ? d.hw[buf][off] : gh_dec16(x, d.base[buf][c]);
+}
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+// Cells (i, c..c+3) of buffer buf (c % 4 == 0), wide encoding.
+__device__ __forceinline__ v4i gh_load4(const GhDev& d, int buf, int64_t i, int64_t c) {
+  const int64_t off = gh_cell(d, i, c);
+  const uint2 x = *reinterpret_cast<const uint2*>(d.hn[buf] + off);
+  if ((x.x & 0xFFFFu) == GH_N_WIDE) return *reinterpret_cast<const v4i*>(d.hw[buf] + off);
+  const v4i b = *reinterpret_cast<const v4i*>(d.base[buf] + c);
+  v4i v;
+  v.x = gh_dec16(x.x & 0xFFFFu, b.x);
+  v.y = gh_dec16(x.x >> 16, b.y);
+  v.z = gh_dec16(x.y & 0xFFFFu, b.z);
+  v.w = gh_dec16(x.y >> 16, b.w);
+  return v;
+}
+// Stores cells (i, c..c+3) in the segment's current encoding; only for
+// changes a narrow cell can always hold (flag toggles of present cells).
+__device__ __forceinline__ void gh_store4(const GhDev& d, int buf, int64_t i, int64_t c, v4i v) {
+  const int64_t off = gh_cell(d, i, c);
+  uint2* np = reinterpret_cast<uint2*>(d.hn[buf] + off);
+  if (((*np).x & 0xFFFFu) == GH_N_WIDE) {
+    *reinterpret_cast<v4i*>(d.hw[buf] + off) = v;
+    return;
+  }
+  const v4i b = *reinterpret_cast<const v4i*>(d.base[buf] + c);
+  bool fit = true;
+  uint2 x;
+  x.x = gh_enc16(v.x, b.x, fit) | (gh_enc16(v.y, b.y, fit) << 16);
+  x.y = gh_enc16(v.z, b.z, fit) | (gh_enc16(v.w, b.w, fit) << 16);
+  *np = x;
 }
 
 // ts < r - T for a present or tombstoned cell (stored v at table offset off)
@@ -208,6 +292,7 @@ struct GhRound {
   int32_t peer_mode;
   int32_t xmap;       // k_round block->tile map: 0 tile-major, 1 XCD-aware
   int32_t tpw;        // k_round tiles per workgroup (1, 2, 4, 8)
+  int32_t exact;      // T_fail or T_cleanup >= GH_AGE_CAP: every cell by the slow rule (exact ts)
   int32_t ablate;     // timing-only experiments (results wrong): 1 = every
                       // peer load reads the own row, 2 = no peer loads. 0 always
                       // in production (set only through GH_ROUND_ABLATE).
@@ -225,6 +310,8 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
 // nt = non-temporal hints on the once-touched streams of k_round
 void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt);
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);
+// base[cur ^ 1] from buffer cur (member c's own heartbeat - GH_BASE_LAG)
+void launch_base(const GhDev& d, int cur, const GhRound& p, hipStream_t s);
 // quirk-mode detection: summaries + per-row prefix (then allgather qall), and
 // carry-in + flag rewrite of the current table
 void launch_quirk_scan(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
@@ -241,12 +328,15 @@ void launch_pack(const GhDev& d, int cur, const int32_t* hb_rows, const int32_t*
 // (what = 0) or the exact ts (what = 1); p.r is the round about to run
 void launch_unpack(const GhDev& d, int cur, int32_t* dst_rows, int64_t row0, int64_t nrows, int what,
                    const GhRound& p, hipStream_t s);
-// rows that stop (crash / leave): exact ts of their cells into ts[]
+// rows that stop (crash / leave): exact ts of their cells into ts[], rows
+// stored wide in both buffers
 void launch_freeze(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p, hipStream_t s);
 // presence bitmaps of rows[0..nr) over the local columns -> rbits + rank*nr*ncsw
 void launch_rowbits(const GhDev& d, int cur, const int32_t* rows, int32_t nr, hipStream_t s);
-void launch_leave(const GhDev& d, int cur, const int32_t* leavers, int32_t nl, const GhRound& p,
-                  hipStream_t s);
+// leavers[0..nl) (global ids); tiles[0..ntl): the distinct local tiles of
+// the local ones
+void launch_leave(const GhDev& d, int cur, const int32_t* leavers, const int32_t* tiles, int32_t ntl, int32_t nl,
+                  const GhRound& p, hipStream_t s);
 void launch_join_add(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, int32_t introducer,
                      const GhRound& p, hipStream_t s);
 void launch_join_bcast(const GhDev& d, int cur, int32_t introducer, const GhRound& p, hipStream_t s);

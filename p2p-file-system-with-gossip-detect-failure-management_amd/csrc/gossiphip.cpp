@@ -124,6 +124,7 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.ablate = e->ablate;
   p.xmap = e->xmap;
   p.tpw = e->tpw;
+  p.exact = e->cfg.t_fail >= GH_AGE_CAP || e->cfg.t_cleanup >= GH_AGE_CAP;
   return p;
 }
 
@@ -202,9 +203,20 @@ int process_events(Engine* e, int32_t r) {
   }
   if ((rc = upload_alive(e))) return rc;
   if (!leavers.empty()) {
-    if ((rc = upload(e, e->ev_buf, leavers))) return rc;
+    // the distinct local tiles holding a leaver's column
+    std::vector<int32_t> tiles;
+    for (int32_t c : leavers) {
+      const int64_t lc = (int64_t)c - e->d.col0;
+      if (lc >= 0 && lc < e->d.ncol) tiles.push_back((int32_t)(lc / e->d.tw));
+    }
+    std::sort(tiles.begin(), tiles.end());
+    tiles.erase(std::unique(tiles.begin(), tiles.end()), tiles.end());
+    std::vector<int32_t> buf(leavers);
+    buf.insert(buf.end(), tiles.begin(), tiles.end());
+    if ((rc = upload(e, e->ev_buf, buf))) return rc;
     if ((rc = gather_rows(e, e->ev_buf, (int32_t)leavers.size()))) return rc;
-    launch_leave(e->d, e->cur, e->ev_buf, (int32_t)leavers.size(), p, e->stream);
+    launch_leave(e->d, e->cur, e->ev_buf, e->ev_buf + leavers.size(), (int32_t)tiles.size(),
+                 (int32_t)leavers.size(), p, e->stream);
     HIPCHK(e, hipStreamSynchronize(e->stream));
   }
   std::vector<int32_t> joiners, fresh;
@@ -365,6 +377,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   d.tw = tw;
   d.lgtw = __builtin_ctz((unsigned)tw);
   d.tstride = (int64_t)e->n * tw;
+  d.ntiles = e->ld / tw;
   d.col0 = col0;
   d.ncol = (int32_t)ncol;
   d.ncs = (int32_t)ncs;
@@ -378,8 +391,11 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   const int64_t inbox = std::max<int64_t>(slots * cfg->fanout, 3 * (int64_t)e->n);
   int rc = GH_OK;
   do {
-    if ((rc = dalloc(e, &d.hb[0], cells, 0xFF)) || (rc = dalloc(e, &d.hb[1], cells, 0xFF)) ||
-        (rc = dalloc(e, &d.ts, cells, 0)))
+    if ((rc = dalloc(e, &d.hn[0], cells, 0xFF)) || (rc = dalloc(e, &d.hn[1], cells, 0xFF)) ||
+        (rc = dalloc(e, &d.hw[0], cells, 0xFF)) || (rc = dalloc(e, &d.hw[1], cells, 0xFF)) ||
+        (rc = dalloc(e, &d.base[0], e->ld, 0)) || (rc = dalloc(e, &d.base[1], e->ld, 0)) ||
+        (rc = dalloc(e, &d.colq, e->ld, 0)) || (rc = dalloc(e, &d.ts, cells, 0)) ||
+        (rc = dalloc(e, &d.slow, (size_t)(e->ld / tw) * e->n, 0)) || (rc = dalloc(e, &d.slow_n, 4, 0)))
       break;
     if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
         (rc = dalloc(e, &d.det_any, e->n, 0)) || (rc = dalloc(e, &d.und, e->n, 0)) ||
@@ -586,6 +602,16 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
     launch_pack(e->d, e->cur, sh.as<int32_t>(), st.as<int32_t>(), row0, n_rows, p, e->stream);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     std::copy(alive, alive + n_rows, e->alive.begin() + row0);
+    // stopped rows are kept wide in both buffers (the round skips them)
+    std::vector<int32_t> stopped;
+    for (int64_t x = 0; x < n_rows; ++x)
+      if (!alive[x]) stopped.push_back((int32_t)(row0 + x));
+    for (size_t b = 0; b < stopped.size(); b += (size_t)e->n) {
+      const std::vector<int32_t> part(stopped.begin() + b, stopped.begin() + std::min(stopped.size(), b + e->n));
+      if ((rc = upload(e, e->ev_buf, part))) return rc;
+      launch_freeze(e->d, e->cur, e->ev_buf, (int32_t)part.size(), p, e->stream);
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+    }
   }
   if ((rc = upload_alive(e))) return rc;
   e->round = round;
@@ -661,6 +687,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     if ((rc = decide_active(e, p))) return rc;
     if (e->cfg.detect_mode == GH_DETECT_QUIRK && (rc = quirk_flags(e, p))) return rc;
     if ((rc = build_inboxes(e, p))) return rc;
+    launch_base(e->d, e->cur, p, e->stream);
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q], e->stream));
     launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt);
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q + 1], e->stream));

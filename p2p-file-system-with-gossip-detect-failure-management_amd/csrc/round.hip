@@ -65,14 +65,13 @@ __global__ __launch_bounds__(256) void k_active_pre(GhDev d, int cur, int dcur, 
       u = 2;
     } else {
       u = 1;
-      const int32_t* hb = d.hb[cur];
       const int32_t* dc = d.det_cnt[dcur];
       const int32_t* dm = d.det_min[dcur];
       int rem = 0;
       const int nd = d.nd[dcur];
       for (int q = 0; q < nd; ++q) {
         const int col = d.dlist[(int64_t)dcur * p.ld + q];
-        rem += (hb[gh_cell(d, i, col)] >= 0) && removes_at(dc[col], dm[col], i);
+        rem += (gh_get(d, cur, i, col) >= 0) && removes_at(dc[col], dm[col], i);
       }
       post = d.cntl[i] - rem;
     }
@@ -89,12 +88,11 @@ __global__ __launch_bounds__(256) void k_active_exact(GhDev d, int cur, int dcur
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= p.n || d.und[i] != 2) return;
-  const int32_t* hb = d.hb[cur];
   const int32_t* dc = d.det_cnt[dcur];
   const int32_t* dm = d.det_min[dcur];
   int cnt = 0;
   for (int64_t c = lane * 4; c < p.ld; c += 256) {
-    const int4 v = *reinterpret_cast<const int4*>(hb + gh_cell(d, i, c));
+    const v4i v = gh_load4(d, cur, i, c);
     const uint32_t b4 = (d.dbits[c >> 5] >> (c & 31)) & 0xFu;
     const int x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -139,8 +137,7 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
       const uint32_t w = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
       const int s = (int)w + ((int64_t)w >= i);
       if (!d.alive[s] || !d.active[s]) continue;
-      const int64_t off = gh_cell(d, s, t);
-      const int32_t v = d.hb[cur][off];
+      const int32_t v = gh_get(d, cur, s, t);
       // i must be in s's snapshot list: present, not detected by s this
       // round and not REMOVE'd at s in step 1.
       if (v < 0 || (v & GH_FLAG)) continue;
@@ -156,8 +153,6 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
 // 4 consecutive members, SEG = TW/4 lanes cover one row segment of a tile,
 // and consecutive waves take consecutive (tile, row) segments in storage
 // order, so every wave instruction is one contiguous 1 KiB access.
-typedef int v4i __attribute__((ext_vector_type(4)));
-
 template <int TW>
 struct SegWalk {
   static constexpr int SEG = TW / 4;
@@ -196,7 +191,7 @@ __global__ __launch_bounds__(256) void k_ring_tiles(GhDev d, int cur, int dcur, 
     const int64_t l0 = t * TW + w.lc * 4;
     int cnt = 0;
     if (valid) {
-      const v4i v = *reinterpret_cast<const v4i*>(d.hb[cur] + t * d.tstride + (int64_t)i * TW + w.lc * 4);
+      const v4i v = gh_load4(d, cur, i, l0);
       const uint32_t rm = removed4(d, dcur, l0, i);
 #pragma unroll
       for (int j = 0; j < 4; ++j) cnt += v[j] >= 0 && !(v[j] & GH_FLAG) && !((rm >> j) & 1u);
@@ -209,10 +204,10 @@ __global__ __launch_bounds__(256) void k_ring_tiles(GhDev d, int cur, int dcur, 
 
 // The local column of the want-th (0-based) member of sender s's snapshot
 // list inside tile t (scans the tile-row).
-__device__ __forceinline__ int64_t ring_find(const GhDev& d, const int32_t* hb, int dcur, int s, int64_t t, int want) {
+__device__ __forceinline__ int64_t ring_find(const GhDev& d, int cur, int dcur, int s, int64_t t, int want) {
   for (int j = 0; j < d.tw; ++j) {
     const int64_t c = t * d.tw + j;
-    const int32_t v = hb[gh_cell(d, s, c)];
+    const int32_t v = gh_get(d, cur, s, c);
     if (v < 0 || (v & GH_FLAG)) continue;
     if (dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], s)) continue;
     if (want-- == 0) return c;
@@ -237,14 +232,13 @@ __global__ __launch_bounds__(256) void k_ring_count(GhDev d, int cur, int dcur, 
   int64_t total = 0, pos = -1;
   for (int64_t t = 0; t < ntiles; ++t) {
     if (t == own_t) {
-      const int32_t* hb = d.hb[cur];
-      const int32_t v = hb[gh_cell(d, sdr, ls)];
+      const int32_t v = gh_get(d, cur, sdr, ls);
       const bool in = v >= 0 && !(v & GH_FLAG) &&
                       !(dbit(d.dbits, ls) && removes_at(d.det_cnt[dcur][ls], d.det_min[dcur][ls], sdr));
       if (in) {
         pos = total;
         for (int64_t c = t * d.tw; c < ls; ++c) {
-          const int32_t x = hb[gh_cell(d, sdr, c)];
+          const int32_t x = gh_get(d, cur, sdr, c);
           pos += x >= 0 && !(x & GH_FLAG) &&
                  !(dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], sdr));
         }
@@ -292,7 +286,7 @@ __global__ __launch_bounds__(256) void k_ring_select(GhDev d, int cur, int dcur,
         const int64_t c = d.rcnt[t * p.n + sdr];
         for (int q = 0; q < 3; ++q)
           if (want[q] >= acc && want[q] < acc + c)
-            tg[q] = (int32_t)(d.col0 + ring_find(d, d.hb[cur], dcur, sdr, t, (int)(want[q] - acc)));
+            tg[q] = (int32_t)(d.col0 + ring_find(d, cur, dcur, sdr, t, (int)(want[q] - acc)));
         acc += c;
       }
     }
@@ -347,53 +341,95 @@ __global__ __launch_bounds__(256) void k_inbox_fill(GhDev d, GhRound p) {
   }
 }
 
+// ---- packed 16-bit (two narrow cells per dword) ------------------------
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 as_s(uint32_t x) { return __builtin_bit_cast(s16x2, x); }
+__device__ __forceinline__ u16x2 as_us(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t as_u(s16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t as_u(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
+  return as_u(__builtin_elementwise_max(as_s(a), as_s(b)));
+}
+__device__ __forceinline__ uint32_t pk_subs_i16(uint32_t a, uint32_t b) {  // saturating a - b
+  return as_u(__builtin_elementwise_sub_sat(as_s(a), as_s(b)));
+}
+__device__ __forceinline__ uint32_t pk_adds_u16(uint32_t a, uint32_t b) {  // saturating a + b
+  return as_u(__builtin_elementwise_add_sat(as_us(a), as_us(b)));
+}
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) { return as_u(as_us(a) + as_us(b)); }
+__device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) { return as_u(as_us(a) - as_us(b)); }
+__device__ __forceinline__ uint32_t pk_sra15(uint32_t a) { return as_u(as_s(a) >> (short)15); }  // 0xFFFF per negative half
+
 template <bool NT>
-__device__ __forceinline__ v4i ldv(const int32_t* p) {
+__device__ __forceinline__ v4u ldn(const uint16_t* p) {
   if constexpr (NT)
-    return __builtin_nontemporal_load(reinterpret_cast<const v4i*>(p));
+    return __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
   else
-    return *reinterpret_cast<const v4i*>(p);
+    return *reinterpret_cast<const v4u*>(p);
 }
 template <bool NT>
-__device__ __forceinline__ void stv(int32_t* p, v4i v) {
+__device__ __forceinline__ void stn(uint16_t* p, v4u v) {
   if constexpr (NT)
-    __builtin_nontemporal_store(v, reinterpret_cast<v4i*>(p));
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
   else
-    *reinterpret_cast<v4i*>(p) = v;
+    *reinterpret_cast<v4u*>(p) = v;
 }
 
-// The fused round. Workgroup tile = GH_RB rows x TW members of one table
+// base[cur ^ 1]: member c's own heartbeat in buffer cur - GH_BASE_LAG, so the
+// round's output (its views of c lag the counter) is narrow; kept when the
+// member is not present in its own row.
+__global__ __launch_bounds__(256) void k_base(GhDev d, int cur, GhRound p) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0) *d.slow_n = 0;
+  if (c >= p.ld) return;
+  int32_t b = d.base[cur][c];
+  const int64_t cg = d.col0 + c;
+  if (c < d.ncol && cg < p.n) {
+    const int32_t v = gh_get(d, cur, cg, c);
+    if (v >= 0) b = gh_hbv(v) - GH_BASE_LAG;
+  }
+  d.base[cur ^ 1][c] = b;
+}
+
+// The round, fast part. Workgroup tile = RB rows x TW members of one table
 // tile; the block index is tile-major so the concurrently running workgroups
-// sweep one tile (a contiguous N*TW*4-byte slice of each table) together:
-// own-row streams are sequential and peer gathers stay in that slice, which
-// the on-die caches hold. Each lane owns 4 consecutive members (16-B
-// loads/stores); SEG = TW/4 lanes cover one row segment, so a wave handles
-// 64/SEG rows per instruction. KB = peer loads issued together (4 or 8).
-// NT = non-temporal hints on the once-touched streams (own ts in/out, new hb
-// out), leaving the caches to the re-read old-hb slice.
-// Rows per workgroup tile: GH_RB, or more when a wave step covers more rows
-// (narrow tiles), so all 4 waves have rows.
+// sweep one tile (a contiguous N*TW*2-byte slice of each narrow table)
+// together: own-row streams are sequential and peer gathers stay in that
+// slice, which the on-die caches hold. Each lane owns 8 consecutive members
+// (one 16-B load of narrow cells); SEG = TW/8 lanes cover one row segment,
+// so a wave handles 64/SEG rows per instruction. KB = peer loads issued
+// together (4 or 8). NT = non-temporal hint on the once-written stream.
+//
+// A lane is on the fast path when the row is alive and active, no member of
+// the lane is REMOVE'd, the row's own member is not in the lane, the lane's
+// own cells are visible-present (age < 30) or absent, and every sender's
+// segment is narrow without the sender's own member in the lane. Then the
+// round reduces to packed 16-bit arithmetic on pairs of cells: merged = a
+// sender's heartbeat exceeds the own one (max); age 1 if merged, else +1;
+// rebase onto the next buffer's base; flag = hb > 1 and age > T_fail.
+// A segment whose lanes are all on the fast path and whose results stay
+// narrow is written here; every other segment of an alive row goes to the
+// slow list (k_round_slow, the reference's rule cell by cell). Stopped rows
+// are not written (wide and identical in both buffers).
 template <int TW>
 constexpr int round_rb() {
-  return 1024 / TW > GH_RB ? 1024 / TW : GH_RB;
+  return 2048 / TW > GH_RB ? 2048 / TW : GH_RB;
 }
 
-template <int KB, int TW, int TPW, bool NT, bool EXACT>
+template <int KB, int TW, int TPW, bool NT>
 __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRound p) {
-  constexpr int SEG = TW / 4;
+  constexpr int CPL = 8;
+  constexpr int SEG = TW / CPL;
   constexpr int RPW = 64 / SEG;
   constexpr int RSTEP = 4 * RPW;
   constexpr int RB = round_rb<TW>();  // rows per workgroup tile
-  __shared__ int s_dcnt[TW];
-  __shared__ int s_dmin[TW];
   __shared__ uint16_t s_part[RB];
-  __shared__ unsigned long long s_st[ST_COUNT];
-  // per-row metadata of the workgroup's rows, staged once for its TPW tiles
-  // so that every row iteration issues its own and its peers' loads back to
-  // back: s_meta = alive | active << 1 | inbox count << 2; s_inb = first KB
-  // senders
+  __shared__ unsigned long long s_merged;
+  // per-row metadata of the workgroup's rows, staged once for its TPW tiles:
+  // s_meta = alive | active << 1 | inbox count << 2; s_inb = first KB senders
   __shared__ int s_meta[RB];
-  __shared__ int s_beg[RB];
   __shared__ int s_inb[RB * KB];
 
   // block -> (tile group of TPW consecutive tiles, row block); group-major so
@@ -418,143 +454,214 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   const int wave = uni(tid >> 6);
   const int sub = lane / SEG;
   const int lc = lane % SEG;
+  const unsigned long long gmask = (SEG == 64 ? ~0ull : ((1ull << SEG) - 1)) << (sub * SEG);
 
-  if (tid < ST_COUNT) s_st[tid] = 0;
+  if (tid == 0) s_merged = 0;
   const bool pull = p.peer_mode == GH_PEER_PULL;
-  for (int t = tid; t < RB; t += 256) {
-    const int i = rb * RB + t;
-    int meta = 0, beg = 0;
-    if (i < p.n) {
-      const int al = d.alive[i];
-      meta = al | (d.active[i] << 1) | ((al ? d.inbox_cnt[i] : 0) << 2);
-      beg = pull ? i * p.k : d.inbox_beg[i];
-    }
-    if (p.ablate == 2) meta &= 3;
-    s_meta[t] = meta;
-    s_beg[t] = beg;
-  }
-  __syncthreads();
   for (int t = tid; t < RB * KB; t += 256) {
     const int row = t / KB, q = t - row * KB;
-    s_inb[t] = q < (s_meta[row] >> 2) ? d.inbox[s_beg[row] + q] : 0;
+    const int i = rb * RB + row;
+    int meta = 0, sv = 0;
+    if (i < p.n) {
+      const int al = d.alive[i];
+      const int cnt = al ? d.inbox_cnt[i] : 0;
+      meta = al | (d.active[i] << 1) | (cnt << 2);
+      if (q < cnt) sv = d.inbox[(pull ? i * p.k : d.inbox_beg[i]) + q];
+    }
+    if (q == 0) s_meta[row] = meta;
+    s_inb[t] = sv;
   }
   __syncthreads();
 
-  const int32_t* __restrict__ hbo = d.hb[cur];
-  int32_t* __restrict__ hbn = d.hb[cur ^ 1];
-  int32_t* __restrict__ tsb = d.ts;
-  const int32_t r = p.r;
-  int n_unknown = 0, n_tomb = 0, n_det = 0, n_rel = 0, n_merged = 0;
+  const uint16_t* __restrict__ hno = d.hn[cur];
+  uint16_t* __restrict__ hnn = d.hn[cur ^ 1];
+  const int32_t* __restrict__ bo = d.base[cur];
+  const int32_t* __restrict__ bn = d.base[cur ^ 1];
+  uint32_t n_mrg16 = 0;  // merges x 16
 
 #pragma unroll 1
   for (int tt = 0; tt < TPW; ++tt) {
   const int tile = group * TPW + tt;
-  const int64_t l0 = (int64_t)tile * TW + lc * 4;                   // local column of this lane's first cell
-  const int64_t c0 = d.col0 + l0;                                   // its global member id
-  const int64_t tb = (int64_t)tile * ((int64_t)p.n * TW) + lc * 4;  // tile base + lane offset
-  for (int t = tid; t < TW; t += 256) {
-    s_dcnt[t] = 0;
-    s_dmin[t] = INT_MAX;
-  }
+  const int64_t l0 = (int64_t)tile * TW + lc * CPL;                   // local column of this lane's first cell
+  const int c0 = (int)(d.col0 + l0);                                  // its global member id
+  const int64_t tb = (int64_t)tile * ((int64_t)p.n * TW) + lc * CPL;  // tile base + lane offset
   for (int t = tid; t < RB; t += 256) s_part[t] = 0;
-  __syncthreads();
 
-  // REMOVE bits of this lane's 4 members (rare: slow path only when set)
-  const uint32_t my4 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFu;
-  int dc[4] = {0, 0, 0, 0}, dm[4] = {0, 0, 0, 0};
-  if (my4) {
+  // per pair of the lane's columns: the rebase (base_next - base_cur) << 5,
+  // and the flag threshold "hb > 1" as a code bound; a base jump beyond 1023
+  // or a REMOVE'd member sends the lane to the slow list
+  const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
+  uint32_t d5[4], t5[4];
+  bool jump = false;
+  {
+    const v4i ba0 = *reinterpret_cast<const v4i*>(bo + l0), ba1 = *reinterpret_cast<const v4i*>(bo + l0 + 4);
+    const v4i bb0 = *reinterpret_cast<const v4i*>(bn + l0), bb1 = *reinterpret_cast<const v4i*>(bn + l0 + 4);
+    const int32_t ba[8] = {ba0.x, ba0.y, ba0.z, ba0.w, ba1.x, ba1.y, ba1.z, ba1.w};
+    const int32_t bb[8] = {bb0.x, bb0.y, bb0.z, bb0.w, bb1.x, bb1.y, bb1.z, bb1.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      dc[j] = d.det_cnt[dcur][l0 + j];
-      dm[j] = d.det_min[dcur][l0 + j];
+      uint32_t dd = 0, th = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t delta = (int64_t)bb[2 * j + h] - ba[2 * j + h];
+        jump |= delta > 1023 || delta < -1023;
+        dd |= ((uint32_t)(delta << 5) & 0xFFFFu) << (16 * h);
+        const int64_t thr = 1 - (int64_t)bb[2 * j + h];
+        const uint32_t tc = thr < 0 ? 0xFFFFu : thr > 1023 ? 0x7FFFu : (uint32_t)((thr << 5) | 31);
+        th |= tc << (16 * h);
+      }
+      d5[j] = dd;
+      t5[j] = th;
     }
   }
-
-  // One row iteration = RPW rows per wave: the own segment and the first KB
-  // senders' segments are issued together, then merged.
-  struct Rows {
-    v4i v;        // own segment
-    v4i pv[KB];   // first KB senders' segments
-    int ps[KB];   // their row ids
-    int meta, i, rr;
-    bool valid;
-  };
-  auto issue = [&](Rows& L, int it) {
-    L.rr = wave * RPW + it * RSTEP + sub;
-    const int i_raw = rb * RB + L.rr;
-    L.valid = i_raw < p.n;
-    L.i = L.valid ? i_raw : p.n - 1;  // in-range row for the loads of idle lanes
-    const int rs = L.valid ? L.rr : 0;
-    int meta = s_meta[rs];
-    if constexpr (RPW == 1) meta = uni(meta);
-    L.meta = meta;
-    const int cntv = meta >> 2;
-    L.v = ldv<false>(hbo + tb + (int64_t)L.i * TW);  // re-read by peers: keep it cached
-#pragma unroll
-    for (int q = 0; q < KB; ++q) {
-      int s = L.i;
-      if (q < cntv) {
-        s = s_inb[rs * KB + q];
-        if constexpr (RPW == 1) s = uni(s);
-      }
-      L.ps[q] = s;
-      L.pv[q] = ldv<false>(hbo + tb + (int64_t)(p.ablate == 1 ? L.i : s) * TW);
-    }
-  };
-  auto merge_seg = [&](int m[4], const v4i& x4, int s) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int x = x4[j];
-      // sender snapshot: present and not detected by s (sign and flag
-      // clear), +1 on s's diagonal
-      int val = (x & (int)(0x80000000u | GH_FLAG)) ? -1 : gh_hbv(x) + ((c0 + j) == s);
-      if (((my4 >> j) & 1u) && removes_at(dc[j], dm[j], s)) val = -1;
-      m[j] = max(m[j], val);
-    }
-  };
+  const uint32_t tfp = (uint32_t)min(p.t_fail, 31) * 0x10001u;
+  const bool lane_ok = !p.exact && !jump && my8 == 0;
+  __syncthreads();
 
   constexpr int NIT = RB / RSTEP;
 #pragma unroll 1
   for (int it = 0; it < NIT; ++it) {
-    Rows L;
-    issue(L, it);
-    const int i = L.i;
+    const int rr = wave * RPW + it * RSTEP + sub;
+    const int i_raw = rb * RB + rr;
+    const bool valid = i_raw < p.n;
+    const int i = valid ? i_raw : p.n - 1;  // in-range row for the loads of idle lanes
+    const int rs = valid ? rr : 0;
+    int meta = s_meta[rs];
+    if constexpr (RPW == 1) meta = uni(meta);
+    const bool al = (meta & 1) && valid;
+    const int cntv = meta >> 2;
     const int64_t off = tb + (int64_t)i * TW;
-    const int al = (L.meta & 1) && L.valid;
-    const int ac = (L.meta >> 1) & 1;
-    const int cntv = L.meta >> 2;
 
-    int m[4] = {-1, -1, -1, -1};
+    // own segment and the first KB senders' segments, issued together;
+    // slots q >= cntv hold the own row, a no-op under the max
+    const v4u w = ldn<false>(hno + off);  // re-read by peers: keep it cached
+    v4u pv[KB];
+    bool bad = !((meta >> 1) & 1) || cntv > KB || (unsigned)(i - c0) < 8u;
 #pragma unroll
-    for (int q = 0; q < KB; ++q)
-      if (q < cntv) merge_seg(m, L.pv[q], L.ps[q]);
-    // rare: more senders than KB (ring mode hubs)
-    int cmax = cntv;
-    if constexpr (RPW > 1) {
-#pragma unroll
-      for (int o = SEG; o < 64; o <<= 1) cmax = max(cmax, __shfl_xor(cmax, o));
-    }
-    for (int q = KB; q < cmax; ++q) {
+    for (int q = 0; q < KB; ++q) {
+      int s = i;
       if (q < cntv) {
-        const int s = d.inbox[s_beg[L.valid ? L.rr : 0] + q];
-        merge_seg(m, ldv<false>(hbo + tb + (int64_t)s * TW), s);
+        s = s_inb[rs * KB + q];
+        if constexpr (RPW == 1) s = uni(s);
+        bad |= (unsigned)(s - c0) < 8u;
+      }
+      pv[q] = ldn<false>(hno + tb + (int64_t)s * TW);
+    }
+#pragma unroll
+    for (int q = 0; q < KB; ++q) bad |= q < cntv && (pv[q][0] & 0xFFFFu) == GH_N_WIDE;
+
+    v4u o;
+    uint32_t spec = 0, facc = 0, mcnt = 0, pcnt = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t m = pv[0][j];
+#pragma unroll
+      for (int q = 1; q < KB; ++q) m = pk_max_i16(m, pv[q][j]);
+      const uint32_t x = w[j];
+      const uint32_t hx = pk_sra15(x);
+      // own cells other than visible (age < 30) or absent: flagged,
+      // tombstone, wide marker (x + 1 keeps bit 15), age 30/31
+      spec |= (pk_add_u16(x, 0x00010001u) & 0x80008000u) | ((((x & 0x001F001Fu) + 0x00020002u) & ~hx) & 0x00200020u);
+      const uint32_t wc = x | 0x001F001Fu;                       // own heartbeat key (absent: -1)
+      const uint32_t mm = pk_sra15(pk_subs_i16(wc, m));          // merged: a sender's heartbeat is larger
+      const uint32_t nm = pk_adds_u16(x, 0x00010001u);           // not merged: age + 1 (absent stays)
+      const uint32_t mv = (m & 0x7FE07FE0u) | 0x00010001u;       // merged: its heartbeat, age 1
+      uint32_t y = (mv & mm) | (nm & ~mm);
+      const uint32_t hy = pk_sra15(y);                           // absent halves
+      y = pk_sub_u16(y, d5[j] & ~hy);                            // rebase present halves
+      facc |= (y | pk_add_u16(y, 0x00200020u)) & ~hy;            // offset left [0, 1022]
+      const uint32_t c1 = pk_subs_i16(tfp, y & 0x001F001Fu);     // age > T_fail
+      const uint32_t c2 = pk_subs_i16(t5[j], y);                 // hb > 1
+      y |= c1 & c2 & ~hy & 0x80008000u;
+      o[j] = y;
+      mcnt += __builtin_popcount(mm);
+      pcnt += __builtin_popcount(~hy);
+    }
+    const bool ok = lane_ok && !bad && spec == 0 && (facc & 0x80008000u) == 0;
+    const bool seg_ok = (__ballot(al && !ok) & gmask) == 0;
+    int npres = 0;
+    if (al) {
+      if (seg_ok) {
+        stn<NT>(hnn + off, o);
+        npres = (int)(pcnt >> 4);
+        n_mrg16 += mcnt;
+      } else if (lc == 0) {
+        d.slow[atomicAdd(d.slow_n, 1)] = ((int64_t)tile << 32) | (uint32_t)i;
       }
     }
-
-    v4i xo = L.v;
-    int npres = 0;
-    bool any_det = false;
-    if (al) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int64_t c = c0 + j;
-        const int64_t oj = off + j;
-        const int32_t w = xo[j];
-        int x = gh_ext(w);
-        const int a = gh_age(w);  // meaningful unless absent
-        bool now = false;         // ts := r in this round
+    for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) npres += __shfl_xor(npres, o2);
+    if (lc == 0 && valid) s_part[rr] = (uint16_t)npres;
+  }
+
+  __syncthreads();
+  const int row0 = rb * RB;
+  for (int t = tid; t < RB; t += 256)
+    if (row0 + t < p.n) d.part[(int64_t)tile * p.n + row0 + t] = s_part[t];
+  }  // tiles
+
+  if (n_mrg16) atomicAdd(&s_merged, (unsigned long long)(n_mrg16 >> 4));
+  __syncthreads();
+  if (tid == 0 && s_merged) atomicAdd(&d.stats[ST_MERGED], s_merged);
+}
+
+// The round, slow part: the segments k_round listed, the reference's rule
+// cell by cell on wide values (slave/slave.go:276-286, 414-497; SPEC §2
+// steps 1-6). G = min(TW, 64) lanes per segment, TW / G cells per lane.
+// Reads buffer cur and writes only the listed segments of cur ^ 1.
+template <int TW, bool EXACT>
+__global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, GhRound p) {
+  constexpr int G = TW < 64 ? TW : 64;
+  constexpr int CPL = TW / G;
+  constexpr int SPW = 64 / G;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / G, lg = lane % G;
+  const unsigned long long gmask = (G == 64 ? ~0ull : ((1ull << G) - 1)) << (sub * G);
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t nseg = *d.slow_n;
+  const bool pull = p.peer_mode == GH_PEER_PULL;
+  const int32_t r = p.r;
+  const int32_t* bn = d.base[cur ^ 1];
+  int32_t* tsb = d.ts;
+  int n_unknown = 0, n_tomb = 0, n_det = 0, n_rel = 0, n_merged = 0;
+  for (int64_t s0 = wave * SPW; s0 < nseg; s0 += nw * SPW) {
+    const int64_t sid = s0 + sub;
+    const bool valid = sid < nseg;
+    const int64_t e = valid ? d.slow[sid] : 0;
+    const int64_t tile = e >> 32;
+    const int i = (int)(e & 0xFFFFFFFF);
+    const bool ac = valid && d.active[i];
+    const int cnt = valid ? d.inbox_cnt[i] : 0;
+    const int64_t beg = pull ? (int64_t)i * p.k : (valid ? d.inbox_beg[i] : 0);
+    int32_t v[CPL];
+    bool fit = true, any_det = false;
+    int npres = 0;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int64_t lcol = tile * TW + lg + k * G;
+      const int64_t c = d.col0 + lcol;
+      const int64_t oj = gh_cell(d, i, lcol);
+      int32_t out = GH_ABSENT;
+      if (valid) {
+        const bool rmb = dbit(d.dbits, lcol);
+        const int dc = rmb ? d.det_cnt[dcur][lcol] : 0, dm = rmb ? d.det_min[dcur][lcol] : 0;
+        int m = -1;
+        for (int q = 0; q < cnt; ++q) {
+          const int s = d.inbox[beg + q];
+          const int32_t X = gh_get(d, cur, s, lcol);
+          // sender snapshot: present and not detected by s (sign and flag
+          // clear), +1 on s's diagonal, not REMOVE'd at s
+          int val = (X & (int)(0x80000000u | GH_FLAG)) ? -1 : gh_hbv(X) + (c == s);
+          if (rmb && removes_at(dc, dm, s)) val = -1;
+          m = max(m, val);
+        }
+        const int32_t wv = gh_get(d, cur, i, lcol);
+        int x = gh_ext(wv);
+        const int a = gh_age(wv);  // meaningful unless absent
+        bool now = false;          // ts := r in this round
         // step 1: REMOVE delivery (slave/slave.go:236-240, 276-286)
-        if (((my4 >> j) & 1u) && removes_at(dc[j], dm[j], i)) {
+        if (rmb && removes_at(dc, dm, i)) {
           if (x >= 0) {
             x = GH_TOMBSTONE;
             n_tomb++;
@@ -570,25 +677,24 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
               x = min(x + 1, GH_HB_MAX);
               now = true;
             }
-          } else if (x >= 0 && (w & GH_FLAG)) {  // step 4 detect (:468-473), decided at the last write
+          } else if (x >= 0 && (wv & GH_FLAG)) {  // step 4 detect (:468-473), decided at the last write
             x = GH_TOMBSTONE;
             n_det++;
             any_det = true;
-            atomicAdd(&s_dcnt[lc * 4 + j], 1);
-            atomicMin(&s_dmin[lc * 4 + j], i);
+            atomicAdd(&d.det_cnt[dcur ^ 1][lcol], 1);
+            atomicMin(&d.det_min[dcur ^ 1][lcol], i);
           }
-          if (x == GH_TOMBSTONE && gh_stale<EXACT>(d, w, oj, r, p.t_cleanup)) {  // step 5 clean (:490-492)
+          if (x == GH_TOMBSTONE && gh_stale<EXACT>(d, wv, oj, r, p.t_cleanup)) {  // step 5 clean (:490-492)
             x = GH_ABSENT;
             n_rel++;
             if (a < GH_AGE_CAP) tsb[oj] = r - a;  // an absent cell keeps its ts in ts[]
           }
         }
-        if (x >= GH_ABSENT && m[j] > x) {  // step 6 merge (:424-426, :435-437)
-          x = m[j];
+        if (x >= GH_ABSENT && m > x) {  // step 6 merge (:424-426, :435-437)
+          x = m;
           now = true;
           n_merged++;
         }
-        int32_t out = GH_ABSENT;
         if (x != GH_ABSENT) {
           int an = 1;  // age in round r+1 of a cell stamped now
           if (!now) {
@@ -597,45 +703,40 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
           }
           out = x >= 0 ? gh_present(x, an, gh_flag_for<EXACT>(d, x, an, c, i, oj, r + 1, p.t_fail)) : gh_tomb(an);
         }
-        xo[j] = out;
+        npres += out >= 0;
+        gh_enc16(out, bn[lcol], fit);
+      }
+      v[k] = out;
+    }
+    const bool narrow = (__ballot(!fit) & gmask) == 0;
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) {
+      npres += __shfl_xor(npres, o, G);
+      any_det |= __shfl_xor((int)any_det, o, G) != 0;
+    }
+    if (!valid) continue;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int64_t lcol = tile * TW + lg + k * G;
+      const int64_t oj = gh_cell(d, i, lcol);
+      if (narrow) {
+        bool f = true;
+        d.hn[cur ^ 1][oj] = (uint16_t)gh_enc16(v[k], bn[lcol], f);
+      } else {
+        d.hw[cur ^ 1][oj] = v[k];
+        d.hn[cur ^ 1][oj] = (uint16_t)GH_N_WIDE;
       }
     }
-    // crashed rows are frozen: their cells are carried into the new buffer as is
-#pragma unroll
-    for (int j = 0; j < 4; ++j) npres += xo[j] >= 0;
-    if (L.valid) stv<NT>(hbn + off, xo);
-#pragma unroll
-    for (int o = SEG / 2; o > 0; o >>= 1) {
-      npres += __shfl_xor(npres, o);
-      any_det |= __shfl_xor((int)any_det, o) != 0;
-    }
-    if (lc == 0 && L.valid) {
-      s_part[L.rr] = (uint16_t)npres;
+    if (lg == 0) {
+      d.part[tile * p.n + i] = (uint16_t)npres;
       if (any_det) d.det_any[i] = 1;
     }
   }
-
-  __syncthreads();
-  const int row0 = rb * RB;
-  for (int t = tid; t < RB; t += 256)
-    if (row0 + t < p.n) d.part[(int64_t)tile * p.n + row0 + t] = s_part[t];
-  for (int t = tid; t < TW; t += 256) {
-    if (s_dcnt[t]) {
-      const int64_t c = (int64_t)tile * TW + t;
-      atomicAdd(&d.det_cnt[dcur ^ 1][c], s_dcnt[t]);
-      atomicMin(&d.det_min[dcur ^ 1][c], s_dmin[t]);
-    }
-  }
-  __syncthreads();  // s_dcnt / s_part are reused by the next tile
-  }  // tiles
-
-  if (n_unknown) atomicAdd(&s_st[ST_REMOVE_UNKNOWN], (unsigned long long)n_unknown);
-  if (n_tomb) atomicAdd(&s_st[ST_TOMBSTONED], (unsigned long long)n_tomb);
-  if (n_det) atomicAdd(&s_st[ST_DETECTIONS], (unsigned long long)n_det);
-  if (n_rel) atomicAdd(&s_st[ST_RELEASED], (unsigned long long)n_rel);
-  if (n_merged) atomicAdd(&s_st[ST_MERGED], (unsigned long long)n_merged);
-  __syncthreads();
-  if (tid < ST_COUNT && s_st[tid]) atomicAdd(&d.stats[tid], s_st[tid]);
+  if (n_unknown) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], (unsigned long long)n_unknown);
+  if (n_tomb) atomicAdd(&d.stats[ST_TOMBSTONED], (unsigned long long)n_tomb);
+  if (n_det) atomicAdd(&d.stats[ST_DETECTIONS], (unsigned long long)n_det);
+  if (n_rel) atomicAdd(&d.stats[ST_RELEASED], (unsigned long long)n_rel);
+  if (n_merged) atomicAdd(&d.stats[ST_MERGED], (unsigned long long)n_merged);
 }
 
 // Rows: sum the per-tile partial counts (local present count). Columns:
@@ -711,7 +812,7 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
     const int i = valid ? (int)(sid - t * p.n) : 0;
     int f = 0;
     if (valid) {
-      const v4i v = *reinterpret_cast<const v4i*>(d.hb[cur] + t * d.tstride + (int64_t)i * TW + w.lc * 4);
+      const v4i v = gh_load4(d, cur, i, t * TW + w.lc * 4);
       const uint32_t rm = removed4(d, dcur, t * TW + w.lc * 4, i);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -771,11 +872,10 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
     const int64_t t = sid < w.nseg ? sid / p.n : 0;
     const int i = sid < w.nseg ? (int)(sid - t * p.n) : 0;
     const bool valid = sid < w.nseg && d.alive[i] && d.active[i];  // only active rows detect (and send)
-    int32_t* cell = d.hb[cur] + t * d.tstride + (int64_t)i * TW + w.lc * 4;
     v4i v = {-1, -1, -1, -1};
     uint32_t rm = 0;
     if (valid) {
-      v = *reinterpret_cast<const v4i*>(cell);
+      v = gh_load4(d, cur, i, t * TW + w.lc * 4);
       rm = removed4(d, dcur, t * TW + w.lc * 4, i);
     }
     int f = 0, lastj = -1;
@@ -813,7 +913,7 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
       }
       s ^= 1;
     }
-    if (changed) *reinterpret_cast<v4i*>(cell) = v;
+    if (changed) gh_store4(d, cur, i, t * TW + w.lc * 4, v);
   }
 }
 
@@ -896,13 +996,15 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
   constexpr int RB = round_rb<TW>();
   const int nrb = (p.n + RB - 1) / RB;
   const dim3 grid((unsigned)(nrb * (p.ld / TW / TPW))), blk(256);
-  // timeouts at or above the age cap need the exact ts of saturated cells
-  if (p.t_fail >= GH_AGE_CAP || p.t_cleanup >= GH_AGE_CAP)
-    hipLaunchKernelGGL((k_round<KB, TW, TPW, false, true>), grid, blk, 0, s, d, cur, dcur, p);
-  else if (nt)
-    hipLaunchKernelGGL((k_round<KB, TW, TPW, true, false>), grid, blk, 0, s, d, cur, dcur, p);
+  if (nt)
+    hipLaunchKernelGGL((k_round<KB, TW, TPW, true>), grid, blk, 0, s, d, cur, dcur, p);
   else
-    hipLaunchKernelGGL((k_round<KB, TW, TPW, false, false>), grid, blk, 0, s, d, cur, dcur, p);
+    hipLaunchKernelGGL((k_round<KB, TW, TPW, false>), grid, blk, 0, s, d, cur, dcur, p);
+  // timeouts at or above the age cap need the exact ts of saturated cells
+  if (p.exact)
+    hipLaunchKernelGGL((k_round_slow<TW, true>), dim3(2048), blk, 0, s, d, cur, dcur, p);
+  else
+    hipLaunchKernelGGL((k_round_slow<TW, false>), dim3(2048), blk, 0, s, d, cur, dcur, p);
 }
 
 // tiles per workgroup: ld / TW is a multiple of 8 (host padding)
@@ -933,6 +1035,10 @@ void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream
     launch_round_kb<4>(d, cur, dcur, p, s, nt);
   else
     launch_round_kb<8>(d, cur, dcur, p, s, nt);
+}
+
+void launch_base(const GhDev& d, int cur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_base, dim3((unsigned)((p.ld + 255) / 256)), dim3(256), 0, s, d, cur, p);
 }
 
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s) {
