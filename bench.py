@@ -24,12 +24,13 @@ healthy steady state with T_fail = T_cleanup = 16 rounds (--t-fail). Parity
 tests cover both regimes.
 
 The JSON line also carries
-  roofline: the fused round kernel (k_round) — algorithmic bytes per launch
-            4*N*ncols*(k+2): own hb segment in, k peer segments in, hb out
-            (DESIGN.md "Kernels"; SURVEY.md §8d's 4*N^2*(k+4) also counted a
-            ts stream in and out, which the age-encoded cells no longer move,
-            reported as survey_bytes_per_launch) / its mean duration from HIP
-            events on the engine's stream; peak 8.0 TB/s (MI355X_MICROARCH.md);
+  roofline: the round kernel (k_round) — algorithmic bytes per launch
+            2*N*ncols*(k+2): own segment in, k peer segments in, own segment
+            out, 2-byte narrow cells (DESIGN.md "Kernels"; SURVEY.md §8d's
+            4*N^2*(k+4) counted int32 hb and ts streams, which the narrow
+            age-encoded cells no longer move, reported as
+            survey_bytes_per_launch) / its mean duration from HIP events on
+            the engine's stream; peak 8.0 TB/s (MI355X_MICROARCH.md);
             traffic = HBM-side bytes per launch from the rocprofv3 PMC passes of
             tools/pmc.sh for this configuration (profiles/, null if none).
   cpu_baseline: the CPU restatement (oracle/tablesim.c, "port") timed on this
@@ -83,7 +84,8 @@ def pmc_traffic(n, k, world):
         except (OSError, ValueError):
             continue
         c = d.get("config", {})
-        if c.get("n") == n and c.get("k") == k and c.get("world", 1) == world and "traffic_bytes" in d:
+        if (c.get("n") == n and c.get("k") == k and c.get("world", 1) == world and c.get("cell_bytes", 4) == 2
+                and "traffic_bytes" in d):
             best = {"traffic_bytes": d["traffic_bytes"], "source": f"profiles/{f.name}"}
     return best
 
@@ -175,9 +177,9 @@ def main():
         return
     value = args.steps / elapsed
     # algorithmic bytes of one k_round launch (this rank's columns)
-    b_round = 4.0 * n * ncols * (k + 2)
-    b_survey = 4.0 * n * ncols * (k + 4)       # SURVEY.md §8d (with a ts stream)
-    b_compulsory = 8.0 * n * ncols             # each cell read and written once
+    b_round = 2.0 * n * ncols * (k + 2)        # narrow cells: own in + out, k peers in
+    b_survey = 4.0 * n * ncols * (k + 4)       # SURVEY.md §8d (int32 hb + a ts stream)
+    b_compulsory = 4.0 * n * ncols             # each narrow cell read and written once
     traffic = pmc_traffic(n, k, world)
     avg_s = (kern_ms / 1e3) / max(launches, 1)
     achieved = b_round / avg_s / 1e9
@@ -192,7 +194,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "int32",
+        "dtype": "int16",
         "data": "synthetic",
         "config": {
             "workload": f"BASELINE config 3: N={n} members, "

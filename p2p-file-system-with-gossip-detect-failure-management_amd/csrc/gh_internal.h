@@ -309,6 +309,8 @@ void launch_ring_select(const GhDev& d, int cur, int dcur, const GhRound& p, hip
 void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
 // nt = non-temporal hints on the once-touched streams of k_round
 void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt);
+// the segments k_round listed, by the per-cell rule (after launch_round)
+void launch_round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);
 // base[cur ^ 1] from buffer cur (member c's own heartbeat - GH_BASE_LAG)
 void launch_base(const GhDev& d, int cur, const GhRound& p, hipStream_t s);

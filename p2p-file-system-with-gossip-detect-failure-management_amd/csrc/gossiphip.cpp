@@ -691,6 +691,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q], e->stream));
     launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt);
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q + 1], e->stream));
+    launch_round_slow(e->d, e->cur, e->dcur, p, e->stream);
     launch_finish(e->d, e->dcur, p, e->stream);
     HIPCHK(e, hipGetLastError());
     e->cur ^= 1;

@@ -403,12 +403,13 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, GhRound p) {
 // together (4 or 8). NT = non-temporal hint on the once-written stream.
 //
 // A lane is on the fast path when the row is alive and active, no member of
-// the lane is REMOVE'd, the row's own member is not in the lane, the lane's
-// own cells are visible-present (age < 30) or absent, and every sender's
-// segment is narrow without the sender's own member in the lane. Then the
-// round reduces to packed 16-bit arithmetic on pairs of cells: merged = a
-// sender's heartbeat exceeds the own one (max); age 1 if merged, else +1;
-// rebase onto the next buffer's base; flag = hb > 1 and age > T_fail.
+// the lane is REMOVE'd, the lane's own cells are visible-present (age < 30)
+// or absent, and every sender's segment is narrow. Then the round reduces to
+// packed 16-bit arithmetic on pairs of cells: merged = a sender's heartbeat
+// exceeds the own one (max); age 1 if merged, else +1; rebase onto the next
+// buffer's base; flag = hb > 1 and age > T_fail. The two diagonals are
+// fix-ups around it: a sender's own member carries hb + 1 in its snapshot,
+// the row's own member gets hb + 1 and a fresh stamp and is never flagged.
 // A segment whose lanes are all on the fast path and whose results stay
 // narrow is written here; every other segment of an alive row goes to the
 // slow list (k_round_slow, the reference's rule cell by cell). Stopped rows
@@ -534,21 +535,51 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
 
     // own segment and the first KB senders' segments, issued together;
     // slots q >= cntv hold the own row, a no-op under the max
-    const v4u w = ldn<false>(hno + off);  // re-read by peers: keep it cached
+    v4u w = ldn<false>(hno + off);  // re-read by peers: keep it cached
     v4u pv[KB];
-    bool bad = !((meta >> 1) & 1) || cntv > KB || (unsigned)(i - c0) < 8u;
+    int ps[KB];
+    bool bad = !((meta >> 1) & 1) || cntv > KB;
 #pragma unroll
     for (int q = 0; q < KB; ++q) {
       int s = i;
       if (q < cntv) {
         s = s_inb[rs * KB + q];
         if constexpr (RPW == 1) s = uni(s);
-        bad |= (unsigned)(s - c0) < 8u;
       }
+      ps[q] = s;
       pv[q] = ldn<false>(hno + tb + (int64_t)s * TW);
     }
 #pragma unroll
     for (int q = 0; q < KB; ++q) bad |= q < cntv && (pv[q][0] & 0xFFFFu) == GH_N_WIDE;
+    // A sender's own member in the lane: its snapshot carries hb + 1 there
+    // (the sender's heartbeat of this round).
+#pragma unroll
+    for (int q = 0; q < KB; ++q) {
+      const int js = ps[q] - c0;
+      if (q < cntv && (unsigned)js < 8u) {
+        const int sh = 16 * (js & 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (j == (js >> 1) && ((pv[q][j] >> sh) & 0x8000u) == 0) pv[q][j] += 0x20u << sh;
+      }
+    }
+    // The row's own member in the lane (step 3, :443-448): hb + 1 with a
+    // fresh stamp (age 0, so age 1 after the round's +1), never flagged.
+    // An own cell that is not visible, or at the heartbeat cap, is slow.
+    const int jd = i - c0;
+    const bool own_in = (unsigned)jd < 8u;
+    if (own_in) {
+      const int sh = 16 * (jd & 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j == (jd >> 1)) {
+          const uint32_t hv = (w[j] >> sh) & 0xFFFFu;
+          if (hv >= 0x8000u || (int64_t)bo[l0 + jd] + (hv >> 5) >= GH_HB_MAX)
+            bad = true;
+          else
+            w[j] = (w[j] & ~(0x1Fu << sh)) + (0x20u << sh);
+        }
+    }
 
     v4u o;
     uint32_t spec = 0, facc = 0, mcnt = 0, pcnt = 0;
@@ -576,6 +607,11 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
       o[j] = y;
       mcnt += __builtin_popcount(mm);
       pcnt += __builtin_popcount(~hy);
+    }
+    if (own_in) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j == (jd >> 1)) o[j] &= ~(0x8000u << (16 * (jd & 1)));
     }
     const bool ok = lane_ok && !bad && spec == 0 && (facc & 0x80008000u) == 0;
     const bool seg_ok = (__ballot(al && !ok) & gmask) == 0;
@@ -1000,12 +1036,17 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
     hipLaunchKernelGGL((k_round<KB, TW, TPW, true>), grid, blk, 0, s, d, cur, dcur, p);
   else
     hipLaunchKernelGGL((k_round<KB, TW, TPW, false>), grid, blk, 0, s, d, cur, dcur, p);
+}
+
+template <int TW>
+static void round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
   // timeouts at or above the age cap need the exact ts of saturated cells
   if (p.exact)
-    hipLaunchKernelGGL((k_round_slow<TW, true>), dim3(2048), blk, 0, s, d, cur, dcur, p);
+    hipLaunchKernelGGL((k_round_slow<TW, true>), dim3(2048), dim3(256), 0, s, d, cur, dcur, p);
   else
-    hipLaunchKernelGGL((k_round_slow<TW, false>), dim3(2048), blk, 0, s, d, cur, dcur, p);
+    hipLaunchKernelGGL((k_round_slow<TW, false>), dim3(2048), dim3(256), 0, s, d, cur, dcur, p);
 }
+
 
 // tiles per workgroup: ld / TW is a multiple of 8 (host padding)
 template <int KB, int TW>
@@ -1046,4 +1087,8 @@ void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s) {
   const int nchunks = (int)(p.ld / d.tw);
   hipLaunchKernelGGL(k_finish, dim3((unsigned)((span + 255) / 256)), dim3(256), 0, s, d, dcur, p,
                      nchunks);
+}
+
+void launch_round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  GH_TW_DISPATCH(round_slow, d, cur, dcur, p, s)
 }

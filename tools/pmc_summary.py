@@ -11,7 +11,7 @@ root = sys.argv[1]
 acc = defaultdict(list)
 for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
     for row in csv.DictReader(open(f)):
-        if "k_round" not in row.get("Kernel_Name", ""):
+        if "::k_round<" not in row.get("Kernel_Name", ""):  # the fast kernel, not k_round_slow
             continue
         acc[row["Counter_Name"]].append(float(row["Counter_Value"]))
 out = {k: {"per_dispatch": sum(v) / len(v), "dispatches": len(v)} for k, v in acc.items()}
@@ -25,6 +25,7 @@ if "TCC_HIT_sum" in out and "TCC_MISS_sum" in out:
 if "read_bytes_corrected" in out and "write_bytes" in out:
     out["traffic_bytes"] = out["read_bytes_corrected"] + out["write_bytes"]
 n, k = (int(x) for x in sys.argv[2:4]) if len(sys.argv) >= 4 else (65536, 4)
-out["config"] = {"n": n, "k": k, "world": 1, "command": "python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline"}
-out["algorithmic_bytes"] = 4.0 * n * n * (k + 2)
+out["config"] = {"n": n, "k": k, "world": 1, "cell_bytes": 2,
+                 "command": "python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline"}
+out["algorithmic_bytes"] = 2.0 * n * n * (k + 2)  # narrow cells: own in + out, k peers in
 print(json.dumps(out, indent=1))
