@@ -218,6 +218,10 @@ def main():
             "compulsory_bytes_per_launch": b_compulsory,
             "compulsory_achieved": b_compulsory / avg_s / 1e9,
             "frac_of_measured_copy_peak": achieved / HBM_MEASURED_GBS,
+            # the measured HBM-side bytes over the same duration: above 1 the
+            # algorithmic frac counts sender re-reads the on-die caches serve
+            "traffic_achieved": traffic["traffic_bytes"] / avg_s / 1e9 if traffic else None,
+            "traffic_frac": traffic["traffic_bytes"] / avg_s / 1e9 / HBM_PEAK_GBS if traffic else None,
         },
         "cpu_baseline": None,
     }

@@ -72,7 +72,9 @@
 #define GH_BASE_LAG 1000                   // base = own heartbeat - GH_BASE_LAG
 #define GH_FLAG (1 << 30)                  // detected next round (present cells)
 #define GH_PAD 256               // column padding granule (ld % 256 == 0)
-#define GH_RB 64                 // rows per workgroup tile in the round kernel
+#ifndef GH_WG_CELLS
+#define GH_WG_CELLS 16384        // round kernel: cells per workgroup tile (rows = GH_WG_CELLS / TW)
+#endif
 #define GH_MAXK 8                // max pull fanout
 #define GH_DLIST_MAX 1024        // local |D| above which undecided rows are recounted in full
 #define GH_TW_DEFAULT 64         // default tile width (members per tile)

@@ -46,8 +46,8 @@ struct Engine {
   int64_t rbits_rows = 0;       // rows rbits can hold
   bool nt = true;        // k_round non-temporal streams (gh_set_round_variant)
   int ablate = 0;        // timing-only experiment switch (GH_ROUND_ABLATE), never set in production
-  int xmap = 0;          // k_round XCD-aware tile map (gh_set_round_variant)
-  int tpw = 8;           // k_round tiles per workgroup (GH_ROUND_TPW)
+  int xmap = 1;          // k_round XCD-aware tile map (gh_set_round_variant)
+  int tpw = 1;           // k_round tiles per workgroup (GH_ROUND_TPW)
   bool timing = false;
   double timed_ms = 0.0;
   int64_t timed_launches = 0;
@@ -336,11 +336,11 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (const char* v = std::getenv("GH_ROUND_XMAP")) e->xmap = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_ROUND_ABLATE")) e->ablate = std::atoi(v);
   if (const char* v = std::getenv("GH_ROUND_TPW")) e->tpw = std::atoi(v);
-  if (e->tpw != 1 && e->tpw != 2 && e->tpw != 4 && e->tpw != 8) e->tpw = 8;
   if (tw != 8 && tw != 16 && tw != 32 && tw != 64 && tw != 128 && tw != 256) {
     delete e;
     return GH_EINVAL;
   }
+  if (e->tpw != 1 && e->tpw != 2 && e->tpw != 4 && e->tpw != 8) e->tpw = 1;
   // communicator
   std::string cerr;
   GhComm* c = nullptr;

@@ -414,9 +414,13 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, GhRound p) {
 // narrow is written here; every other segment of an alive row goes to the
 // slow list (k_round_slow, the reference's rule cell by cell). Stopped rows
 // are not written (wide and identical in both buffers).
+// Rows per workgroup tile: GH_WG_CELLS / TW within [64, 1024] (a tall,
+// one-tile block: at TW = 64, 256 rows; measured best per width),
+// and at least one wave step of 4 waves.
 template <int TW>
 constexpr int round_rb() {
-  return 2048 / TW > GH_RB ? 2048 / TW : GH_RB;
+  constexpr int rb = GH_WG_CELLS / TW < 64 ? 64 : GH_WG_CELLS / TW > 1024 ? 1024 : GH_WG_CELLS / TW;
+  return rb < 2048 / TW ? 2048 / TW : rb;
 }
 
 template <int KB, int TW, int TPW, bool NT>

@@ -1,0 +1,15 @@
+#!/bin/bash
+# k_round workgroup-shape sweep: RB (rows per workgroup, build-time GH_RB:
+# lib/libgossiphip_rb<RB>.so) x tile width x tiles per workgroup.
+# LIBS="libgossiphip libgossiphip_rb128" CONFIGS="tw:tpw ..."
+set -o pipefail
+mkdir -p gpurun_out
+for lib in ${LIBS:-libgossiphip}; do
+ for cfg in ${CONFIGS:-128:1 128:2 256:1}; do
+  IFS=: read -r tw tpw <<< "$cfg"
+  out=gpurun_out/rb_${lib}_${tw}_${tpw}.json
+  GOSSIPHIP_LIB=p2p-file-system-with-gossip-detect-failure-management_amd/lib/$lib.so GH_TILE_W=$tw GH_ROUND_TPW=$tpw \
+    timeout -k 10 120 python -u bench.py --steps 6 --warmup 4 --no-cpu-baseline > $out 2>/dev/null || exit 1
+  python -c "import json; d=json.load(open('$out')); print('$lib tw=$tw tpw=$tpw', round(d['roofline']['avg_launch_ms'],3), 'ms')"
+ done
+done
