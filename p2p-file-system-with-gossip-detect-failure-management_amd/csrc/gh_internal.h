@@ -295,9 +295,6 @@ struct GhRound {
   int32_t xmap;       // k_round block->tile map: 0 tile-major, 1 XCD-aware
   int32_t tpw;        // k_round tiles per workgroup (1, 2, 4, 8)
   int32_t exact;      // T_fail or T_cleanup >= GH_AGE_CAP: every cell by the slow rule (exact ts)
-  int32_t ablate;     // timing-only experiments (results wrong): 1 = every
-                      // peer load reads the own row, 2 = no peer loads. 0 always
-                      // in production (set only through GH_ROUND_ABLATE).
 };
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------

@@ -45,7 +45,6 @@ struct Engine {
   int32_t* rows_buf = nullptr;  // device scratch for a few row ids
   int64_t rbits_rows = 0;       // rows rbits can hold
   bool nt = true;        // k_round non-temporal streams (gh_set_round_variant)
-  int ablate = 0;        // timing-only experiment switch (GH_ROUND_ABLATE), never set in production
   int xmap = 1;          // k_round XCD-aware tile map (gh_set_round_variant)
   int tpw = 1;           // k_round tiles per workgroup (GH_ROUND_TPW)
   bool timing = false;
@@ -121,7 +120,6 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.k = e->cfg.fanout;
   p.seed = e->cfg.seed;
   p.peer_mode = e->cfg.peer_mode;
-  p.ablate = e->ablate;
   p.xmap = e->xmap;
   p.tpw = e->tpw;
   p.exact = e->cfg.t_fail >= GH_AGE_CAP || e->cfg.t_cleanup >= GH_AGE_CAP;
@@ -334,7 +332,6 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (const char* v = std::getenv("GH_TILE_W")) tw = std::atoi(v);
   if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_ROUND_XMAP")) e->xmap = std::atoi(v) != 0;
-  if (const char* v = std::getenv("GH_ROUND_ABLATE")) e->ablate = std::atoi(v);
   if (const char* v = std::getenv("GH_ROUND_TPW")) e->tpw = std::atoi(v);
   if (tw != 8 && tw != 16 && tw != 32 && tw != 64 && tw != 128 && tw != 256) {
     delete e;

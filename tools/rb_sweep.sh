@@ -1,7 +1,9 @@
 #!/bin/bash
-# k_round workgroup-shape sweep: RB (rows per workgroup, build-time GH_RB:
-# lib/libgossiphip_rb<RB>.so) x tile width x tiles per workgroup.
-# LIBS="libgossiphip libgossiphip_rb128" CONFIGS="tw:tpw ..."
+# k_round workgroup-shape sweep. Rows per workgroup = GH_WG_CELLS / TW is a
+# build-time constant: build variants lib/libgossiphip_<name>.so with
+# -DGH_WG_CELLS=<cells> (all csrc sources), then compare them over tile width
+# x tiles per workgroup:
+#   LIBS="libgossiphip libgossiphip_c32k" CONFIGS="tw:tpw ..." bash tools/rb_sweep.sh
 set -o pipefail
 mkdir -p gpurun_out
 for lib in ${LIBS:-libgossiphip}; do
