@@ -229,21 +229,52 @@ __device__ __forceinline__ v4i gh_load4(const GhDev& d, int buf, int64_t i, int6
   v.w = gh_dec16(x.y >> 16, b.w);
   return v;
 }
-// Stores cells (i, c..c+3) in the segment's current encoding; only for
-// changes a narrow cell can always hold (flag toggles of present cells).
-__device__ __forceinline__ void gh_store4(const GhDev& d, int buf, int64_t i, int64_t c, v4i v) {
+// Presence and flag bits of cells (i, c..c+7) of buffer buf (c % 8 == 0):
+// bit j = present, bit 8 + j = present and flagged. Narrow codes answer
+// directly (no base).
+__device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, int64_t c) {
   const int64_t off = gh_cell(d, i, c);
-  uint2* np = reinterpret_cast<uint2*>(d.hn[buf] + off);
-  if (((*np).x & 0xFFFFu) == GH_N_WIDE) {
-    *reinterpret_cast<v4i*>(d.hw[buf] + off) = v;
+  const uint4 x = *reinterpret_cast<const uint4*>(d.hn[buf] + off);
+  uint32_t out = 0;
+  if ((x.x & 0xFFFFu) == GH_N_WIDE) {
+    const v4i a = *reinterpret_cast<const v4i*>(d.hw[buf] + off);
+    const v4i b = *reinterpret_cast<const v4i*>(d.hw[buf] + off + 4);
+    const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (v[j] >= 0) out |= (1u << j) | ((v[j] & GH_FLAG) ? 1u << (8 + j) : 0u);
+  } else {
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t h = (w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+      if (h < GH_N_TOMB) out |= (1u << j) | (h >= 0x8000u ? 1u << (8 + j) : 0u);
+    }
+  }
+  return out;
+}
+// Clears the flag of present cells (i, c + j) for the bits j of m (c % 8 == 0).
+__device__ __forceinline__ void gh_clearflags8(const GhDev& d, int buf, int64_t i, int64_t c, uint32_t m) {
+  const int64_t off = gh_cell(d, i, c);
+  uint4* np = reinterpret_cast<uint4*>(d.hn[buf] + off);
+  uint4 x = *np;
+  if ((x.x & 0xFFFFu) == GH_N_WIDE) {
+    v4i* wp = reinterpret_cast<v4i*>(d.hw[buf] + off);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      v4i v = wp[h];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((m >> (4 * h + j)) & 1u) v[j] &= ~GH_FLAG;
+      wp[h] = v;
+    }
     return;
   }
-  const v4i b = *reinterpret_cast<const v4i*>(d.base[buf] + c);
-  bool fit = true;
-  uint2 x;
-  x.x = gh_enc16(v.x, b.x, fit) | (gh_enc16(v.y, b.y, fit) << 16);
-  x.y = gh_enc16(v.z, b.z, fit) | (gh_enc16(v.w, b.w, fit) << 16);
-  *np = x;
+  uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if ((m >> j) & 1u) w[j >> 1] &= ~(0x8000u << (16 * (j & 1)));
+  *np = uint4{w[0], w[1], w[2], w[3]};
 }
 
 // ts < r - T for a present or tombstoned cell (stored v at table offset off)

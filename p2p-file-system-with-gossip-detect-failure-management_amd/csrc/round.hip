@@ -150,12 +150,13 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
 
 // ---- segment walks -------------------------------------------------------
 // The helper kernels below read the table the way k_round does: a lane owns
-// 4 consecutive members, SEG = TW/4 lanes cover one row segment of a tile,
-// and consecutive waves take consecutive (tile, row) segments in storage
-// order, so every wave instruction is one contiguous 1 KiB access.
+// 8 consecutive members (16 B of narrow cells), SEG = TW/8 lanes cover one
+// row segment of a tile, and consecutive waves take consecutive (tile, row)
+// segments in storage order, so every wave instruction is one contiguous
+// 1 KiB access.
 template <int TW>
 struct SegWalk {
-  static constexpr int SEG = TW / 4;
+  static constexpr int SEG = TW / 8;
   static constexpr int RPW = 64 / SEG;
   int lane, sub, lc;
   int64_t nseg, first, stride;
@@ -169,11 +170,11 @@ struct SegWalk {
   }
 };
 
-// 4-bit REMOVE mask of local columns l0..l0+3 at row i
-__device__ __forceinline__ uint32_t removed4(const GhDev& d, int dcur, int64_t l0, int i) {
-  uint32_t m = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFu;
+// 8-bit REMOVE mask of local columns l0..l0+7 at row i (l0 % 8 == 0)
+__device__ __forceinline__ uint32_t removed8(const GhDev& d, int dcur, int64_t l0, int i) {
+  uint32_t m = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
   uint32_t out = 0;
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < 8; ++j)
     if (((m >> j) & 1u) && removes_at(d.det_cnt[dcur][l0 + j], d.det_min[dcur][l0 + j], i)) out |= 1u << j;
   return out;
 }
@@ -188,13 +189,12 @@ __global__ __launch_bounds__(256) void k_ring_tiles(GhDev d, int cur, int dcur, 
     const bool valid = sid < w.nseg;
     const int64_t t = valid ? sid / p.n : 0;
     const int i = valid ? (int)(sid - t * p.n) : 0;
-    const int64_t l0 = t * TW + w.lc * 4;
+    const int64_t l0 = t * TW + w.lc * 8;
     int cnt = 0;
     if (valid) {
-      const v4i v = gh_load4(d, cur, i, l0);
-      const uint32_t rm = removed4(d, dcur, l0, i);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) cnt += v[j] >= 0 && !(v[j] & GH_FLAG) && !((rm >> j) & 1u);
+      const uint32_t pf = gh_pf8(d, cur, i, l0);
+      const uint32_t rm = removed8(d, dcur, l0, i);
+      cnt = __builtin_popcount(pf & ~(pf >> 8) & ~rm & 0xFFu);  // present, not flagged, not REMOVE'd
     }
 #pragma unroll
     for (int o = SegWalk<TW>::SEG / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
@@ -432,6 +432,9 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   constexpr int RB = round_rb<TW>();  // rows per workgroup tile
   __shared__ uint16_t s_part[RB];
   __shared__ unsigned long long s_merged;
+  // this tile's segments for the slow list, appended with one global atomic
+  __shared__ int s_nslow, s_slowbase;
+  __shared__ int s_slow[RB];
   // per-row metadata of the workgroup's rows, staged once for its TPW tiles:
   // s_meta = alive | active << 1 | inbox count << 2; s_inb = first KB senders
   __shared__ int s_meta[RB];
@@ -491,6 +494,7 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   const int c0 = (int)(d.col0 + l0);                                  // its global member id
   const int64_t tb = (int64_t)tile * ((int64_t)p.n * TW) + lc * CPL;  // tile base + lane offset
   for (int t = tid; t < RB; t += 256) s_part[t] = 0;
+  if (tid == 0) s_nslow = 0;
 
   // per pair of the lane's columns: the rebase (base_next - base_cur) << 5,
   // and the flag threshold "hb > 1" as a code bound; a base jump beyond 1023
@@ -626,7 +630,7 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
         npres = (int)(pcnt >> 4);
         n_mrg16 += mcnt;
       } else if (lc == 0) {
-        d.slow[atomicAdd(d.slow_n, 1)] = ((int64_t)tile << 32) | (uint32_t)i;
+        s_slow[atomicAdd(&s_nslow, 1)] = i;
       }
     }
 #pragma unroll
@@ -638,6 +642,10 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   const int row0 = rb * RB;
   for (int t = tid; t < RB; t += 256)
     if (row0 + t < p.n) d.part[(int64_t)tile * p.n + row0 + t] = s_part[t];
+  if (tid == 0 && s_nslow) s_slowbase = atomicAdd(d.slow_n, s_nslow);
+  __syncthreads();
+  for (int t = tid; t < s_nslow; t += 256) d.slow[s_slowbase + t] = ((int64_t)tile << 32) | (uint32_t)s_slow[t];
+  __syncthreads();  // s_nslow / s_slow are reused by the next tile
   }  // tiles
 
   if (n_mrg16) atomicAdd(&s_merged, (unsigned long long)(n_mrg16 >> 4));
@@ -645,63 +653,97 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   if (tid == 0 && s_merged) atomicAdd(&d.stats[ST_MERGED], s_merged);
 }
 
+// 8 wide values of the row segment cells [off, off + 8) whose narrow codes are
+// x: decoded against base[l0 ..], or read from hw for a wide segment.
+__device__ __forceinline__ void wide8(const int32_t* hw, const int32_t* base, int64_t off, int64_t l0, const v4u& x,
+                                      int32_t out[8]) {
+  if ((x[0] & 0xFFFFu) == GH_N_WIDE) {
+    const v4i a = *reinterpret_cast<const v4i*>(hw + off);
+    const v4i b = *reinterpret_cast<const v4i*>(hw + off + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      out[j] = a[j];
+      out[4 + j] = b[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = gh_dec16((x[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, base[l0 + j]);
+  }
+}
+
 // The round, slow part: the segments k_round listed, the reference's rule
 // cell by cell on wide values (slave/slave.go:276-286, 414-497; SPEC §2
-// steps 1-6). G = min(TW, 64) lanes per segment, TW / G cells per lane.
-// Reads buffer cur and writes only the listed segments of cur ^ 1.
+// steps 1-6), with k_round's lane shape (8 consecutive members per lane, SEG
+// lanes per segment, 16-B loads). Reads buffer cur and writes only the
+// listed segments of cur ^ 1. In failure storms most segments come here.
 template <int TW, bool EXACT>
 __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, GhRound p) {
-  constexpr int G = TW < 64 ? TW : 64;
-  constexpr int CPL = TW / G;
-  constexpr int SPW = 64 / G;
+  constexpr int CPL = 8;
+  constexpr int SEG = TW / CPL;
+  constexpr int RPW = 64 / SEG;
   const int lane = threadIdx.x & 63;
-  const int sub = lane / G, lg = lane % G;
-  const unsigned long long gmask = (G == 64 ? ~0ull : ((1ull << G) - 1)) << (sub * G);
+  const int sub = lane / SEG, lc = lane % SEG;
+  const unsigned long long gmask = (SEG == 64 ? ~0ull : ((1ull << SEG) - 1)) << (sub * SEG);
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int64_t nseg = *d.slow_n;
   const bool pull = p.peer_mode == GH_PEER_PULL;
   const int32_t r = p.r;
-  const int32_t* bn = d.base[cur ^ 1];
-  int32_t* tsb = d.ts;
+  const uint16_t* __restrict__ hno = d.hn[cur];
+  uint16_t* __restrict__ hnn = d.hn[cur ^ 1];
+  const int32_t* __restrict__ hwo = d.hw[cur];
+  int32_t* __restrict__ hwn = d.hw[cur ^ 1];
+  const int32_t* __restrict__ bo = d.base[cur];
+  const int32_t* __restrict__ bn = d.base[cur ^ 1];
+  int32_t* __restrict__ tsb = d.ts;
   int n_unknown = 0, n_tomb = 0, n_det = 0, n_rel = 0, n_merged = 0;
-  for (int64_t s0 = wave * SPW; s0 < nseg; s0 += nw * SPW) {
+  for (int64_t s0 = wave * RPW; s0 < nseg; s0 += nw * RPW) {
     const int64_t sid = s0 + sub;
     const bool valid = sid < nseg;
-    const int64_t e = valid ? d.slow[sid] : 0;
+    const int64_t e = d.slow[valid ? sid : s0];
     const int64_t tile = e >> 32;
     const int i = (int)(e & 0xFFFFFFFF);
-    const bool ac = valid && d.active[i];
-    const int cnt = valid ? d.inbox_cnt[i] : 0;
-    const int64_t beg = pull ? (int64_t)i * p.k : (valid ? d.inbox_beg[i] : 0);
-    int32_t v[CPL];
+    const int64_t l0 = tile * TW + lc * CPL;
+    const int c0 = (int)(d.col0 + l0);
+    const int64_t tb = tile * d.tstride + lc * CPL;
+    const int64_t off = tb + (int64_t)i * TW;
+    const bool ac = d.active[i];
+    const int cnt = d.inbox_cnt[i];
+    const int64_t beg = pull ? (int64_t)i * p.k : d.inbox_beg[i];
+    const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
     bool fit = true, any_det = false;
     int npres = 0;
+    int32_t o32[8];
+    v4u o = {0u, 0u, 0u, 0u};
+    if (valid) {
+      int32_t A[8], X[8];
+      wide8(hwo, bo, off, l0, ldn<false>(hno + off), A);
+      int m[8];
 #pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-      const int64_t lcol = tile * TW + lg + k * G;
-      const int64_t c = d.col0 + lcol;
-      const int64_t oj = gh_cell(d, i, lcol);
-      int32_t out = GH_ABSENT;
-      if (valid) {
-        const bool rmb = dbit(d.dbits, lcol);
-        const int dc = rmb ? d.det_cnt[dcur][lcol] : 0, dm = rmb ? d.det_min[dcur][lcol] : 0;
-        int m = -1;
-        for (int q = 0; q < cnt; ++q) {
-          const int s = d.inbox[beg + q];
-          const int32_t X = gh_get(d, cur, s, lcol);
+      for (int j = 0; j < 8; ++j) m[j] = -1;
+      for (int q = 0; q < cnt; ++q) {
+        const int s = d.inbox[beg + q];
+        const int64_t so = tb + (int64_t)s * TW;
+        wide8(hwo, bo, so, l0, ldn<false>(hno + so), X);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
           // sender snapshot: present and not detected by s (sign and flag
           // clear), +1 on s's diagonal, not REMOVE'd at s
-          int val = (X & (int)(0x80000000u | GH_FLAG)) ? -1 : gh_hbv(X) + (c == s);
-          if (rmb && removes_at(dc, dm, s)) val = -1;
-          m = max(m, val);
+          int val = (X[j] & (int)(0x80000000u | GH_FLAG)) ? -1 : gh_hbv(X[j]) + ((c0 + j) == s);
+          if (((my8 >> j) & 1u) && removes_at(d.det_cnt[dcur][l0 + j], d.det_min[dcur][l0 + j], s)) val = -1;
+          m[j] = max(m[j], val);
         }
-        const int32_t wv = gh_get(d, cur, i, lcol);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t c = c0 + j;
+        const int64_t oj = off + j;
+        const int32_t wv = A[j];
         int x = gh_ext(wv);
         const int a = gh_age(wv);  // meaningful unless absent
         bool now = false;          // ts := r in this round
         // step 1: REMOVE delivery (slave/slave.go:236-240, 276-286)
-        if (rmb && removes_at(dc, dm, i)) {
+        if (((my8 >> j) & 1u) && removes_at(d.det_cnt[dcur][l0 + j], d.det_min[dcur][l0 + j], i)) {
           if (x >= 0) {
             x = GH_TOMBSTONE;
             n_tomb++;
@@ -721,8 +763,8 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
             x = GH_TOMBSTONE;
             n_det++;
             any_det = true;
-            atomicAdd(&d.det_cnt[dcur ^ 1][lcol], 1);
-            atomicMin(&d.det_min[dcur ^ 1][lcol], i);
+            atomicAdd(&d.det_cnt[dcur ^ 1][l0 + j], 1);
+            atomicMin(&d.det_min[dcur ^ 1][l0 + j], i);
           }
           if (x == GH_TOMBSTONE && gh_stale<EXACT>(d, wv, oj, r, p.t_cleanup)) {  // step 5 clean (:490-492)
             x = GH_ABSENT;
@@ -730,11 +772,12 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
             if (a < GH_AGE_CAP) tsb[oj] = r - a;  // an absent cell keeps its ts in ts[]
           }
         }
-        if (x >= GH_ABSENT && m > x) {  // step 6 merge (:424-426, :435-437)
-          x = m;
+        if (x >= GH_ABSENT && m[j] > x) {  // step 6 merge (:424-426, :435-437)
+          x = m[j];
           now = true;
           n_merged++;
         }
+        int32_t out = GH_ABSENT;
         if (x != GH_ABSENT) {
           int an = 1;  // age in round r+1 of a cell stamped now
           if (!now) {
@@ -743,31 +786,29 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
           }
           out = x >= 0 ? gh_present(x, an, gh_flag_for<EXACT>(d, x, an, c, i, oj, r + 1, p.t_fail)) : gh_tomb(an);
         }
+        o32[j] = out;
         npres += out >= 0;
-        gh_enc16(out, bn[lcol], fit);
+        o[j >> 1] |= gh_enc16(out, bn[l0 + j], fit) << (16 * (j & 1));
       }
-      v[k] = out;
     }
-    const bool narrow = (__ballot(!fit) & gmask) == 0;
-#pragma unroll
-    for (int o = G / 2; o > 0; o >>= 1) {
-      npres += __shfl_xor(npres, o, G);
-      any_det |= __shfl_xor((int)any_det, o, G) != 0;
-    }
-    if (!valid) continue;
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-      const int64_t lcol = tile * TW + lg + k * G;
-      const int64_t oj = gh_cell(d, i, lcol);
+    // a segment is narrow iff every lane of it has narrow codes
+    const bool narrow = (__ballot(valid && !fit) & gmask) == 0;
+    if (valid) {
       if (narrow) {
-        bool f = true;
-        d.hn[cur ^ 1][oj] = (uint16_t)gh_enc16(v[k], bn[lcol], f);
+        stn<false>(hnn + off, o);
       } else {
-        d.hw[cur ^ 1][oj] = v[k];
-        d.hn[cur ^ 1][oj] = (uint16_t)GH_N_WIDE;
+        *reinterpret_cast<v4i*>(hwn + off) = v4i{o32[0], o32[1], o32[2], o32[3]};
+        *reinterpret_cast<v4i*>(hwn + off + 4) = v4i{o32[4], o32[5], o32[6], o32[7]};
+        const uint32_t wm = GH_N_WIDE | (GH_N_WIDE << 16);
+        stn<false>(hnn + off, v4u{wm, wm, wm, wm});
       }
     }
-    if (lg == 0) {
+#pragma unroll
+    for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) {
+      npres += __shfl_xor(npres, o2);
+      any_det |= __shfl_xor((int)any_det, o2) != 0;
+    }
+    if (lc == 0 && valid) {
       d.part[tile * p.n + i] = (uint16_t)npres;
       if (any_det) d.det_any[i] = 1;
     }
@@ -852,11 +893,11 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
     const int i = valid ? (int)(sid - t * p.n) : 0;
     int f = 0;
     if (valid) {
-      const v4i v = gh_load4(d, cur, i, t * TW + w.lc * 4);
-      const uint32_t rm = removed4(d, dcur, t * TW + w.lc * 4, i);
+      const uint32_t pf = gh_pf8(d, cur, i, t * TW + w.lc * 8);
+      const uint32_t rm = removed8(d, dcur, t * TW + w.lc * 8, i);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (v[j] >= 0 && !((rm >> j) & 1u)) f = q_compose(f, (v[j] & GH_FLAG) ? 6 : 5);
+      for (int j = 0; j < 8; ++j)
+        if (((pf >> j) & 1u) && !((rm >> j) & 1u)) f = q_compose(f, ((pf >> (8 + j)) & 1u) ? 6 : 5);
     }
 #pragma unroll
     for (int o = 1; o < SEG; o <<= 1) {
@@ -912,18 +953,17 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
     const int64_t t = sid < w.nseg ? sid / p.n : 0;
     const int i = sid < w.nseg ? (int)(sid - t * p.n) : 0;
     const bool valid = sid < w.nseg && d.alive[i] && d.active[i];  // only active rows detect (and send)
-    v4i v = {-1, -1, -1, -1};
-    uint32_t rm = 0;
+    uint32_t pf = 0, rm = 0;
     if (valid) {
-      v = gh_load4(d, cur, i, t * TW + w.lc * 4);
-      rm = removed4(d, dcur, t * TW + w.lc * 4, i);
+      pf = gh_pf8(d, cur, i, t * TW + w.lc * 8);
+      rm = removed8(d, dcur, t * TW + w.lc * 8, i);
     }
     int f = 0, lastj = -1;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (v[j] >= 0 && !((rm >> j) & 1u)) {
-        f = q_compose(f, (v[j] & GH_FLAG) ? 6 : 5);
-        lastj = w.lc * 4 + j;
+    for (int j = 0; j < 8; ++j)
+      if (((pf >> j) & 1u) && !((rm >> j) & 1u)) {
+        f = q_compose(f, ((pf >> (8 + j)) & 1u) ? 6 : 5);
+        lastj = w.lc * 8 + j;
       }
     int incl = f;
 #pragma unroll
@@ -939,21 +979,18 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
     const int qc = d.qcarry[i];
     int s = q_apply(excl, q_apply(d.qsum[sid], qc & 1));
     const int lastc = ((qc & 2) && d.qlast[i] == t) ? lastj : -1;  // the row's last list entry, if here
-    bool changed = false;
+    uint32_t clear = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (!(v[j] >= 0 && !((rm >> j) & 1u))) continue;
-      if (!(v[j] & GH_FLAG)) {
+    for (int j = 0; j < 8; ++j) {
+      if (!(((pf >> j) & 1u) && !((rm >> j) & 1u))) continue;
+      if (!((pf >> (8 + j)) & 1u)) {
         s = 0;
         continue;
       }
-      if (!(s == 0 || w.lc * 4 + j == lastc)) {
-        v[j] &= ~GH_FLAG;  // skipped this round
-        changed = true;
-      }
+      if (!(s == 0 || w.lc * 8 + j == lastc)) clear |= 1u << j;  // skipped this round
       s ^= 1;
     }
-    if (changed) gh_store4(d, cur, i, t * TW + w.lc * 4, v);
+    if (clear) gh_clearflags8(d, cur, i, t * TW + w.lc * 8, clear);
   }
 }
 
@@ -971,7 +1008,7 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
   }
 
 static unsigned seg_grid(const GhRound& p, int tw) {
-  const int64_t waves = ((p.ld / tw) * p.n + (64 / (tw / 4)) - 1) / (64 / (tw / 4));
+  const int64_t waves = ((p.ld / tw) * p.n + (64 / (tw / 8)) - 1) / (64 / (tw / 8));
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>((waves + 3) / 4, 16384));
 }
 
