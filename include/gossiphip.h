@@ -207,10 +207,15 @@ int gh_create_sharded(const gh_config* cfg, int32_t rank, int32_t world, int32_t
                       const uint8_t* comm_id, void** handle);
 int gh_shard_info(void* h, int32_t* rank, int32_t* world, int64_t* col0, int64_t* ncols);
 
-/* Tuning knobs of the fused round kernel (k_round): non-temporal loads/stores
- * on the once-touched streams (own ts, new hb) and the XCD-aware block->tile
- * map. Results do not depend on them; the defaults are the measured fastest
- * (DESIGN.md). */
+/* Table encoding of this engine's shard (diagnostic; DESIGN.md "Data layout"):
+ * (tile, row) segments of the current table held in the wide 32-bit encoding
+ * (stopped rows included), and segments the last round ran through the
+ * per-cell rule (k_round_slow). No reference counterpart. */
+int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments);
+
+/* Tuning knobs of the round kernel (k_round): non-temporal stores of the new
+ * table and the XCD-aware block->tile map. Results do not depend on them;
+ * the defaults (both on) are the measured fastest. */
 int gh_set_round_variant(void* h, int32_t nontemporal, int32_t xcd_map);
 
 /* Device timing of the fused round kernel (HIP events on the engine's

@@ -295,6 +295,19 @@ __global__ __launch_bounds__(256) void k_rowbits(GhDev d, int cur, const int32_t
   }
 }
 
+// wide segments of buffer buf (first narrow cell = GH_N_WIDE) -> *out
+__global__ __launch_bounds__(256) void k_count_wide(GhDev d, int buf, unsigned long long* out) {
+  const int64_t total = d.ntiles * d.n;
+  unsigned long long cnt = 0;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = idx / d.n, i = idx - t * d.n;
+    cnt += d.hn[buf][t * d.tstride + i * d.tw] == GH_N_WIDE;
+  }
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(out, cnt);
+}
+
 // base[buf][c] = v for every local column
 __global__ void k_setbase(GhDev d, int buf, int32_t v) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -357,6 +370,11 @@ void launch_freeze(const GhDev& d, int cur, const int32_t* rows, int32_t nr, con
   if (nr == 0) return;
   hipLaunchKernelGGL(k_freeze, dim3(grid_for((int64_t)nr * d.ld)), dim3(256), 0, s, d, cur, rows, nr, p);
   hipLaunchKernelGGL(k_freeze_mark, dim3(grid_for((int64_t)nr * d.ld)), dim3(256), 0, s, d, rows, nr);
+}
+
+void launch_count_wide(const GhDev& d, int buf, unsigned long long* out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, sizeof(unsigned long long), s);
+  hipLaunchKernelGGL(k_count_wide, dim3(grid_for(d.ntiles * d.n)), dim3(256), 0, s, d, buf, out);
 }
 
 void launch_rowbits(const GhDev& d, int cur, const int32_t* rows, int32_t nr, hipStream_t s) {

@@ -363,6 +363,8 @@ void launch_unpack(const GhDev& d, int cur, int32_t* dst_rows, int64_t row0, int
 // rows that stop (crash / leave): exact ts of their cells into ts[], rows
 // stored wide in both buffers
 void launch_freeze(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p, hipStream_t s);
+// number of wide segments of buffer buf -> *out (device)
+void launch_count_wide(const GhDev& d, int buf, unsigned long long* out, hipStream_t s);
 // presence bitmaps of rows[0..nr) over the local columns -> rbits + rank*nr*ncsw
 void launch_rowbits(const GhDev& d, int cur, const int32_t* rows, int32_t nr, hipStream_t s);
 // leavers[0..nl) (global ids); tiles[0..ntl): the distinct local tiles of

@@ -568,6 +568,25 @@ int gh_shard_info(void* h, int32_t* rank, int32_t* world, int64_t* col0, int64_t
   return GH_OK;
 }
 
+int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  Staging st;
+  int rc;
+  if ((rc = st.alloc(e, sizeof(unsigned long long)))) return rc;
+  launch_count_wide(e->d, e->cur, st.as<unsigned long long>(), e->stream);
+  HIPCHK(e, hipGetLastError());
+  unsigned long long w = 0;
+  int32_t sl = 0;
+  HIPCHK(e, hipMemcpyAsync(&w, st.p, sizeof w, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(&sl, e->d.slow_n, sizeof sl, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (wide_segments) *wide_segments = (int64_t)w;
+  if (slow_segments) *slow_segments = sl;
+  return GH_OK;
+}
+
 int gh_get_round(void* h, int32_t* round) {
   Engine* e = static_cast<Engine*>(h);
   if (!e || !round) return GH_EINVAL;

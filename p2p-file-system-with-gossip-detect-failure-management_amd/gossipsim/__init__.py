@@ -94,6 +94,13 @@ class Engine:
         self._chk(self.lib.gh_shard_info(self.h, C.byref(r), C.byref(w), C.byref(c0), C.byref(nc)))
         return r.value, w.value, c0.value, nc.value
 
+    def encoding_info(self):
+        """(wide segments of the current table, segments the last round ran
+        by the per-cell rule) of this engine's shard (diagnostic)."""
+        w, sl = C.c_int64(), C.c_int64()
+        self._chk(self.lib.gh_encoding_info(self.h, C.byref(w), C.byref(sl)))
+        return w.value, sl.value
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.gh_destroy(self.h)
