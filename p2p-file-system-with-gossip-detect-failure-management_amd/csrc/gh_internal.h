@@ -52,10 +52,12 @@
 //   Local columns are padded to ld (multiple of 8*TW and 256); padding cells
 //   stay -1.
 //   per row (global): alive, active, und (u8), cntl / cntg (local / global
-//            present count, [N] = |D|), post, det_any, inbox_cnt, inbox[].
+//            present count, [N] = |D|; the rounds keep cntl current by
+//            per-segment deltas), post, det_any, inboxes: pull mode
+//            inbox[i*(k+1)] = count, then the senders; ring mode inbox_cnt,
+//            inbox_beg into inbox.
 //   per local column: det_cnt / det_min (x2: pending D_{r-1} and current
 //            D_r), dbits (bitmap of pending D_{r-1}), dlist.
-//   part[ld/TW][N] uint16  per-(tile,row) present counts of the last pass.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -144,7 +146,6 @@ struct GhDev {
   uint32_t *dbits;
   int32_t *dlist;
   int32_t *nd;      // [0..1] local |D| per parity, [2..3] dlist fill, [4] join adds, [5] list merges
-  uint16_t *part;
   int32_t *inbox_beg, *inbox_cnt, *inbox, *inbox_fill, *targets;
   int32_t *ring;    // ring mode: [world][n][2] (local snapshot count, local position of the sender)
   uint16_t *rcnt;   // ring mode: [ld/tw][n] snapshot-list members per (tile, sender row)
@@ -314,6 +315,16 @@ __device__ __forceinline__ bool gh_gbit(const GhDev& d, const uint32_t* bits, in
   return (bits[(o * nr + q) * d.ncsw + (lc >> 5)] >> (lc & 31)) & 1u;
 }
 
+// Receiver i's inbox: sender count and the offset of the first sender in
+// d.inbox (pull: count in slot 0 of a (k+1)-int row, so a shard's receivers
+// are one contiguous slice for the allgather; ring: CSR).
+__device__ __forceinline__ int gh_in_cnt(const GhDev& d, bool pull, int k, int64_t i) {
+  return pull ? d.inbox[i * (k + 1)] : d.inbox_cnt[i];
+}
+__device__ __forceinline__ int64_t gh_in_beg(const GhDev& d, bool pull, int k, int64_t i) {
+  return pull ? i * (k + 1) + 1 : (int64_t)d.inbox_beg[i];
+}
+
 // Parameters of one round, passed by value to the kernels.
 struct GhRound {
   int32_t r;          // now
@@ -330,7 +341,6 @@ struct GhRound {
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------
 // round.hip
-void launch_prep(const GhDev& d, int dcur, hipStream_t s);
 void launch_active_pre(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_active_post(const GhDev& d, const GhRound& p, hipStream_t s);
 void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
@@ -342,8 +352,9 @@ void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream
 // the segments k_round listed, by the per-cell rule (after launch_round)
 void launch_round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);
-// base[cur ^ 1] from buffer cur (member c's own heartbeat - GH_BASE_LAG)
-void launch_base(const GhDev& d, int cur, const GhRound& p, hipStream_t s);
+// base[cur ^ 1] from buffer cur (member c's own heartbeat - GH_BASE_LAG),
+// |D_{r-1}| next to the local counts, empty slow list
+void launch_base(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 // quirk-mode detection: summaries + per-row prefix (then allgather qall), and
 // carry-in + flag rewrite of the current table
 void launch_quirk_scan(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);

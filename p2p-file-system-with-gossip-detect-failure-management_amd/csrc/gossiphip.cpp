@@ -383,9 +383,9 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   d.world = world;
   e->cfg.tile_width = tw;
   const int64_t cells = (int64_t)e->n * e->ld;
-  const int64_t nch = e->ld / tw;  // partial counts: one per (tile, row)
+  const int64_t nch = e->ld / tw;  // tiles: per-(tile, row) ring / quirk summaries
   const int64_t slots = (int64_t)world * ncs;  // global rows incl. the last shard's tail
-  const int64_t inbox = std::max<int64_t>(slots * cfg->fanout, 3 * (int64_t)e->n);
+  const int64_t inbox = std::max<int64_t>(slots * (cfg->fanout + 1), 3 * (int64_t)e->n);
   int rc = GH_OK;
   do {
     if ((rc = dalloc(e, &d.hn[0], cells, 0xFF)) || (rc = dalloc(e, &d.hn[1], cells, 0xFF)) ||
@@ -404,7 +404,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.dbits, e->ld / 32 + 2, 0)) || (rc = dalloc(e, &d.dlist, 2 * e->ld, 0)) ||
         (rc = dalloc(e, &d.nd, 8, 0)))
       break;
-    if ((rc = dalloc(e, &d.part, nch * e->n, 0)) || (rc = dalloc(e, &d.inbox_beg, e->n, 0)) ||
+    if ((rc = dalloc(e, &d.inbox_beg, e->n, 0)) ||
         (rc = dalloc(e, &d.inbox_cnt, slots, 0)) || (rc = dalloc(e, &d.inbox_fill, e->n, 0)) ||
         (rc = dalloc(e, &d.inbox, inbox, 0)) || (rc = dalloc(e, &d.targets, 3 * (int64_t)e->n, 0xFF)) ||
         (rc = dalloc(e, &d.stats, ST_COUNT, 0)) || (rc = dalloc(e, &e->ev_buf, 2 * (int64_t)e->n + 16, 0)) ||
@@ -445,7 +445,6 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
 // <4 guard (SPEC §2 step 2) for every row.
 int decide_active(Engine* e, const GhRound& p) {
   GhDev& d = e->d;
-  launch_prep(d, e->dcur, e->stream);
   int rc;
   if ((rc = allreduce_i32(e, d.cntl, d.cntg, (size_t)e->n + 1))) return rc;
   launch_active_pre(d, e->cur, e->dcur, p, e->stream);
@@ -477,11 +476,9 @@ int build_inboxes(Engine* e, const GhRound& p) {
     launch_peers_pull(d, e->cur, e->dcur, p, e->stream);
     HIPCHK(e, hipGetLastError());
     if (e->world > 1) {
-      const size_t k = (size_t)e->cfg.fanout;
-      COMMCHK(e, e->comm->allgather(d.inbox + (size_t)e->rank * d.ncs * k, d.inbox,
-                                    sizeof(int32_t) * d.ncs * k, e->stream));
-      COMMCHK(e, e->comm->allgather(d.inbox_cnt + (size_t)e->rank * d.ncs, d.inbox_cnt,
-                                    sizeof(int32_t) * d.ncs, e->stream));
+      const size_t row = (size_t)e->cfg.fanout + 1;  // count + senders per receiver
+      COMMCHK(e, e->comm->allgather(d.inbox + (size_t)e->rank * d.ncs * row, d.inbox,
+                                    sizeof(int32_t) * d.ncs * row, e->stream));
     }
     return GH_OK;
   }
@@ -700,10 +697,10 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     int rc;
     if ((rc = process_events(e, r))) return rc;
     const GhRound p = round_params(e, r);
+    launch_base(e->d, e->cur, e->dcur, p, e->stream);
     if ((rc = decide_active(e, p))) return rc;
     if (e->cfg.detect_mode == GH_DETECT_QUIRK && (rc = quirk_flags(e, p))) return rc;
     if ((rc = build_inboxes(e, p))) return rc;
-    launch_base(e->d, e->cur, p, e->stream);
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q], e->stream));
     launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt);
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[2 * q + 1], e->stream));

@@ -1,6 +1,7 @@
 // Gossip-round kernels for gfx950 (SPEC.md §2-§3, DESIGN.md "Kernels").
 //
-//   k_prep / k_active_pre / k_active_exact / k_active_post
+//   k_base         next buffer's column bases, |D_{r-1}| for the count allreduce
+//   k_active_pre / k_active_exact / k_active_post
 //                  per row: the <4 guard after REMOVE delivery
 //                  (slave/slave.go:504,511). Rows decided by the global count
 //                  need nothing else; the few undecided rows get an exact
@@ -10,12 +11,15 @@
 //   k_ring_*       reference ring topology (slave/slave.go:512-524): per-(tile,row)
 //                  snapshot counts, positions, targets + inbox CSR.
 //   k_quirk_*      quirk-mode detection pre-pass (SPEC §4).
-//   k_round        THE HOT KERNEL: one pass over the table applying REMOVE
-//                  delivery, guard, own heartbeat, detection, cleanup and the
-//                  k-peer max-merge (slave/slave.go:276-286,414-497) for a
-//                  64-row x TW-member tile per workgroup.
-//   k_finish       per row/column: reduce the pass's partial counts, build
-//                  the failed-set bitmap D_r for the next round.
+//   k_round        THE HOT KERNEL: one pass over the narrow table, packed
+//                  16-bit: k-peer max-merge, own heartbeat, aging, next-round
+//                  flag (slave/slave.go:414-497) for a 256-row x 64-member
+//                  tile per workgroup; lists the segments needing the
+//                  per-cell rule.
+//   k_round_slow   those segments: REMOVE delivery, guard, detection,
+//                  cleanup and merge cell by cell (slave/slave.go:276-286,
+//                  414-497) on wide values.
+//   k_finish       per column: the failed-set bitmap D_r for the next round.
 // Member columns are local to the engine's shard (gh_internal.h); rows,
 // alive/active and the inboxes are global.
 #include <limits.h>
@@ -35,9 +39,6 @@ __device__ __forceinline__ bool dbit(const uint32_t* bits, int64_t c) {
 // Step 1 applies REMOVE(c) at row j unless j is c's only detector
 // (slave/slave.go:344-346: a detector does not message itself).
 __device__ __forceinline__ bool removes_at(int dc, int dm, int j) { return !(dc == 1 && dm == j); }
-
-// |D_{r-1}| of this shard next to the local counts, for one allreduce.
-__global__ void k_prep(GhDev d, int dcur) { d.cntl[d.n] = d.nd[dcur]; }
 
 // Decides rows from the global count cntg and global |D| = cntg[n]; an
 // undecided row (|D| could push it under the threshold) gets its exact local
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= d.ncs) return;
   const int64_t i = d.col0 + t;  // global receiver (>= n in the tail of the last shard)
-  const int64_t beg = i * p.k;
+  const int64_t beg = i * (p.k + 1) + 1;
   int nv = 0;
   if (t < d.ncol && d.alive[i] && p.n >= 2) {
     const bool ib = dbit(d.dbits, t);
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
       d.inbox[beg + nv++] = s;
     }
   }
-  d.inbox_cnt[i] = nv;
+  d.inbox[beg - 1] = nv;
 }
 
 // ---- segment walks -------------------------------------------------------
@@ -380,9 +381,12 @@ __device__ __forceinline__ void stn(uint16_t* p, v4u v) {
 // base[cur ^ 1]: member c's own heartbeat in buffer cur - GH_BASE_LAG, so the
 // round's output (its views of c lag the counter) is narrow; kept when the
 // member is not present in its own row.
-__global__ __launch_bounds__(256) void k_base(GhDev d, int cur, GhRound p) {
+__global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRound p) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0) *d.slow_n = 0;
+  if (c == 0) {
+    *d.slow_n = 0;
+    d.cntl[d.n] = d.nd[dcur];  // |D_{r-1}| of this shard next to the local counts, for one allreduce
+  }
   if (c >= p.ld) return;
   int32_t b = d.base[cur][c];
   const int64_t cg = d.col0 + c;
@@ -430,7 +434,6 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   constexpr int RPW = 64 / SEG;
   constexpr int RSTEP = 4 * RPW;
   constexpr int RB = round_rb<TW>();  // rows per workgroup tile
-  __shared__ uint16_t s_part[RB];
   __shared__ unsigned long long s_merged;
   // this tile's segments for the slow list, appended with one global atomic
   __shared__ int s_nslow, s_slowbase;
@@ -472,9 +475,9 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     int meta = 0, sv = 0;
     if (i < p.n) {
       const int al = d.alive[i];
-      const int cnt = al ? d.inbox_cnt[i] : 0;
+      const int cnt = al ? gh_in_cnt(d, pull, p.k, i) : 0;
       meta = al | (d.active[i] << 1) | (cnt << 2);
-      if (q < cnt) sv = d.inbox[(pull ? i * p.k : d.inbox_beg[i]) + q];
+      if (q < cnt) sv = d.inbox[gh_in_beg(d, pull, p.k, i) + q];
     }
     if (q == 0) s_meta[row] = meta;
     s_inb[t] = sv;
@@ -493,7 +496,6 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   const int64_t l0 = (int64_t)tile * TW + lc * CPL;                   // local column of this lane's first cell
   const int c0 = (int)(d.col0 + l0);                                  // its global member id
   const int64_t tb = (int64_t)tile * ((int64_t)p.n * TW) + lc * CPL;  // tile base + lane offset
-  for (int t = tid; t < RB; t += 256) s_part[t] = 0;
   if (tid == 0) s_nslow = 0;
 
   // per pair of the lane's columns: the rebase (base_next - base_cur) << 5,
@@ -590,7 +592,7 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     }
 
     v4u o;
-    uint32_t spec = 0, facc = 0, mcnt = 0, pcnt = 0;
+    uint32_t spec = 0, facc = 0, mcnt = 0, pcnt = 0, bcnt = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       uint32_t m = pv[0][j];
@@ -598,6 +600,7 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
       for (int q = 1; q < KB; ++q) m = pk_max_i16(m, pv[q][j]);
       const uint32_t x = w[j];
       const uint32_t hx = pk_sra15(x);
+      bcnt += __builtin_popcount(~hx);  // present before (fast lanes: visible or absent)
       // own cells other than visible (age < 30) or absent: flagged,
       // tombstone, wide marker (x + 1 keeps bit 15), age 30/31
       spec |= (pk_add_u16(x, 0x00010001u) & 0x80008000u) | ((((x & 0x001F001Fu) + 0x00020002u) & ~hx) & 0x00200020u);
@@ -623,25 +626,22 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     }
     const bool ok = lane_ok && !bad && spec == 0 && (facc & 0x80008000u) == 0;
     const bool seg_ok = (__ballot(al && !ok) & gmask) == 0;
-    int npres = 0;
+    int dpres = 0;  // present after - present before
     if (al) {
       if (seg_ok) {
         stn<NT>(hnn + off, o);
-        npres = (int)(pcnt >> 4);
+        dpres = ((int)pcnt - (int)bcnt) >> 4;
         n_mrg16 += mcnt;
       } else if (lc == 0) {
         s_slow[atomicAdd(&s_nslow, 1)] = i;
       }
     }
 #pragma unroll
-    for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) npres += __shfl_xor(npres, o2);
-    if (lc == 0 && valid) s_part[rr] = (uint16_t)npres;
+    for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) dpres += __shfl_xor(dpres, o2);
+    if (lc == 0 && dpres) atomicAdd(&d.cntl[i], dpres);
   }
 
   __syncthreads();
-  const int row0 = rb * RB;
-  for (int t = tid; t < RB; t += 256)
-    if (row0 + t < p.n) d.part[(int64_t)tile * p.n + row0 + t] = s_part[t];
   if (tid == 0 && s_nslow) s_slowbase = atomicAdd(d.slow_n, s_nslow);
   __syncthreads();
   for (int t = tid; t < s_nslow; t += 256) d.slow[s_slowbase + t] = ((int64_t)tile << 32) | (uint32_t)s_slow[t];
@@ -708,11 +708,11 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
     const int64_t tb = tile * d.tstride + lc * CPL;
     const int64_t off = tb + (int64_t)i * TW;
     const bool ac = d.active[i];
-    const int cnt = d.inbox_cnt[i];
-    const int64_t beg = pull ? (int64_t)i * p.k : d.inbox_beg[i];
+    const int cnt = gh_in_cnt(d, pull, p.k, i);
+    const int64_t beg = gh_in_beg(d, pull, p.k, i);
     const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
     bool fit = true, any_det = false;
-    int npres = 0;
+    int dpres = 0;  // present after - present before
     int32_t o32[8];
     v4u o = {0u, 0u, 0u, 0u};
     if (valid) {
@@ -787,7 +787,7 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
           out = x >= 0 ? gh_present(x, an, gh_flag_for<EXACT>(d, x, an, c, i, oj, r + 1, p.t_fail)) : gh_tomb(an);
         }
         o32[j] = out;
-        npres += out >= 0;
+        dpres += (out >= 0) - (wv >= 0);
         o[j >> 1] |= gh_enc16(out, bn[l0 + j], fit) << (16 * (j & 1));
       }
     }
@@ -805,11 +805,11 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
     }
 #pragma unroll
     for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) {
-      npres += __shfl_xor(npres, o2);
+      dpres += __shfl_xor(dpres, o2);
       any_det |= __shfl_xor((int)any_det, o2) != 0;
     }
     if (lc == 0 && valid) {
-      d.part[tile * p.n + i] = (uint16_t)npres;
+      if (dpres) atomicAdd(&d.cntl[i], dpres);
       if (any_det) d.det_any[i] = 1;
     }
   }
@@ -820,23 +820,11 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
   if (n_merged) atomicAdd(&d.stats[ST_MERGED], (unsigned long long)n_merged);
 }
 
-// Rows: sum the per-tile partial counts (local present count). Columns:
-// bitmap + list of D_r, and reset the consumed D_{r-1} accumulators for reuse
-// in round r+1.
-__global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p, int nchunks) {
+// Columns: bitmap + list of D_r, and reset the consumed D_{r-1}
+// accumulators for reuse in round r+1 (the rows' counts are kept current by
+// the round kernels).
+__global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (x < p.n) {
-    int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    int ch = 0;
-    for (; ch + 4 <= nchunks; ch += 4) {
-      s0 += d.part[(int64_t)ch * p.n + x];
-      s1 += d.part[(int64_t)(ch + 1) * p.n + x];
-      s2 += d.part[(int64_t)(ch + 2) * p.n + x];
-      s3 += d.part[(int64_t)(ch + 3) * p.n + x];
-    }
-    for (; ch < nchunks; ++ch) s0 += d.part[(int64_t)ch * p.n + x];
-    d.cntl[x] = s0 + s1 + s2 + s3;
-  }
   const int dnew = dcur ^ 1;
   bool has = false;
   if (x < p.ld) {
@@ -1035,10 +1023,6 @@ void launch_quirk_apply(const GhDev& d, int cur, int dcur, const GhRound& p, hip
   GH_TW_DISPATCH(quirk_apply, d, cur, dcur, p, s)
 }
 
-void launch_prep(const GhDev& d, int dcur, hipStream_t s) {
-  hipLaunchKernelGGL(k_prep, dim3(1), dim3(1), 0, s, d, dcur);
-}
-
 void launch_active_pre(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_active_pre, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
   hipLaunchKernelGGL(k_active_exact, dim3((p.n + 3) / 4), dim3(256), 0, s, d, cur, dcur, p);
@@ -1119,15 +1103,12 @@ void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream
     launch_round_kb<8>(d, cur, dcur, p, s, nt);
 }
 
-void launch_base(const GhDev& d, int cur, const GhRound& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_base, dim3((unsigned)((p.ld + 255) / 256)), dim3(256), 0, s, d, cur, p);
+void launch_base(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_base, dim3((unsigned)((p.ld + 255) / 256)), dim3(256), 0, s, d, cur, dcur, p);
 }
 
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s) {
-  const int64_t span = p.ld > p.n ? p.ld : p.n;
-  const int nchunks = (int)(p.ld / d.tw);
-  hipLaunchKernelGGL(k_finish, dim3((unsigned)((span + 255) / 256)), dim3(256), 0, s, d, dcur, p,
-                     nchunks);
+  hipLaunchKernelGGL(k_finish, dim3((unsigned)((p.ld + 255) / 256)), dim3(256), 0, s, d, dcur, p);
 }
 
 void launch_round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
