@@ -209,9 +209,12 @@ int gh_shard_info(void* h, int32_t* rank, int32_t* world, int64_t* col0, int64_t
 
 /* Table encoding of this engine's shard (diagnostic; DESIGN.md "Data layout"):
  * (tile, row) segments of the current table held in the wide 32-bit encoding
- * (stopped rows included), and segments the last round ran through the
- * per-cell rule (k_round_slow). No reference counterpart. */
-int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments);
+ * (stopped rows included); segments the last round ran through the per-cell
+ * rule (k_round_slow); the round kernel variant of the last round (0 lean,
+ * 1 storm) and its storm measure. Any output may be NULL. No reference
+ * counterpart. */
+int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, int32_t* storm_mode,
+                     int64_t* storm_segments);
 
 /* Tuning knobs of the round kernel (k_round): non-temporal stores of the new
  * table and the XCD-aware block->tile map. Results do not depend on them;

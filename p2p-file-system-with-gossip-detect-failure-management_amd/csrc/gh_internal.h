@@ -138,6 +138,8 @@ struct GhDev {
   int32_t *colq;    // [ld] scratch: per local column event index / merged value
   int64_t *slow;    // [ntiles * n] round: segments for k_round_slow, tile << 32 | row
   int32_t *slow_n;  // their count
+  int32_t *mode;    // k_round variant of the round: 0 lean, 1 storm (k_base)
+  int32_t *nstorm;  // storm variant: segments holding flagged or tombstoned cells
   int32_t *ts;
   uint8_t *alive, *active, *det_any, *und;
   int32_t *cntl, *cntg;  // [n + 8]: per-row present counts (local / allreduced), [n] = |D|

@@ -392,7 +392,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.hw[0], cells, 0xFF)) || (rc = dalloc(e, &d.hw[1], cells, 0xFF)) ||
         (rc = dalloc(e, &d.base[0], e->ld, 0)) || (rc = dalloc(e, &d.base[1], e->ld, 0)) ||
         (rc = dalloc(e, &d.colq, e->ld, 0)) || (rc = dalloc(e, &d.ts, cells, 0)) ||
-        (rc = dalloc(e, &d.slow, (size_t)(e->ld / tw) * e->n, 0)) || (rc = dalloc(e, &d.slow_n, 4, 0)))
+        (rc = dalloc(e, &d.slow, (size_t)(e->ld / tw) * e->n, 0)) || (rc = dalloc(e, &d.slow_n, 4, 0)) ||
+        (rc = dalloc(e, &d.mode, 4, 0)) || (rc = dalloc(e, &d.nstorm, 4, 0)))
       break;
     if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
         (rc = dalloc(e, &d.det_any, e->n, 0)) || (rc = dalloc(e, &d.und, e->n, 0)) ||
@@ -565,7 +566,8 @@ int gh_shard_info(void* h, int32_t* rank, int32_t* world, int64_t* col0, int64_t
   return GH_OK;
 }
 
-int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments) {
+int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, int32_t* storm_mode,
+                     int64_t* storm_segments) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
   HIPCHK(e, hipSetDevice(e->cfg.device));
@@ -575,12 +577,16 @@ int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments) {
   launch_count_wide(e->d, e->cur, st.as<unsigned long long>(), e->stream);
   HIPCHK(e, hipGetLastError());
   unsigned long long w = 0;
-  int32_t sl = 0;
+  int32_t sl = 0, mode = 0, ns = 0;
   HIPCHK(e, hipMemcpyAsync(&w, st.p, sizeof w, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipMemcpyAsync(&sl, e->d.slow_n, sizeof sl, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(&mode, e->d.mode, sizeof mode, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(&ns, e->d.nstorm, sizeof ns, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   if (wide_segments) *wide_segments = (int64_t)w;
   if (slow_segments) *slow_segments = sl;
+  if (storm_mode) *storm_mode = mode;
+  if (storm_segments) *storm_segments = ns;
   return GH_OK;
 }
 

@@ -362,6 +362,17 @@ __device__ __forceinline__ uint32_t pk_adds_u16(uint32_t a, uint32_t b) {  // sa
 __device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) { return as_u(as_us(a) + as_us(b)); }
 __device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) { return as_u(as_us(a) - as_us(b)); }
 __device__ __forceinline__ uint32_t pk_sra15(uint32_t a) { return as_u(as_s(a) >> (short)15); }  // 0xFFFF per negative half
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+  return as_u(__builtin_elementwise_min(as_us(a), as_us(b)));
+}
+// 0xFFFF in each half that is zero
+__device__ __forceinline__ uint32_t pk_zero_mask(uint32_t a) {
+  return pk_sub_u16(pk_min_u16(a, 0x00010001u), 0x00010001u);
+}
+// bits (2j, 2j+1) of the 8-bit lane mask from the halves of pair j's mask
+__device__ __forceinline__ uint32_t pair_bits(uint32_t m, int j) {
+  return ((m & 1u) | ((m >> 15) & 2u)) << (2 * j);
+}
 
 template <bool NT>
 __device__ __forceinline__ v4u ldn(const uint16_t* p) {
@@ -384,7 +395,15 @@ __device__ __forceinline__ void stn(uint16_t* p, v4u v) {
 __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRound p) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0) {
+    // k_round variant of this round: the storm one when more than 1/32 of
+    // the segments of the last round went to the slow list or hold cells
+    // that need the per-cell rule in the lean variant (flagged, tombstone,
+    // guard rows); flags are set one round ahead, so a detection wave is
+    // seen the round before it happens
+    const int64_t measure = (int64_t)*d.nstorm + *d.slow_n;
+    *d.mode = measure * 32 > d.ntiles * (int64_t)d.n;
     *d.slow_n = 0;
+    *d.nstorm = 0;
     d.cntl[d.n] = d.nd[dcur];  // |D_{r-1}| of this shard next to the local counts, for one allreduce
   }
   if (c >= p.ld) return;
@@ -427,14 +446,27 @@ constexpr int round_rb() {
   return rb < 2048 / TW ? 2048 / TW : rb;
 }
 
-template <int KB, int TW, int TPW, bool NT>
+template <int KB, int TW, int TPW, bool NT, bool STORM>
 __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRound p) {
+  if (*d.mode != (int)STORM) return;  // the other variant runs this round (k_base)
   constexpr int CPL = 8;
   constexpr int SEG = TW / CPL;
   constexpr int RPW = 64 / SEG;
   constexpr int RSTEP = 4 * RPW;
   constexpr int RB = round_rb<TW>();  // rows per workgroup tile
-  __shared__ unsigned long long s_merged;
+  __shared__ unsigned long long s_merged, s_det, s_rel, s_storm, s_tomb, s_unk;
+  // this tile's per-pair constants: rebase (base_next - base_cur) << 5
+  // (0x8000: jump beyond 1023, no present cell stays narrow) and the code
+  // bound of "hb > 1"
+  __shared__ uint32_t s_d5[TW / 2];
+  __shared__ uint32_t s_t5[TW / 2];
+  // REMOVE of D_{r-1} per pair: 0xFFFF halves for columns with >= 2
+  // detectors (every row removes them); s_rm1: a column with one detector
+  __shared__ uint32_t s_rm[TW / 2];
+  __shared__ uint32_t s_rm1[TW / 2];
+  // this tile's detections per column (count, first detector)
+  __shared__ int s_dcnt[TW];
+  __shared__ int s_dmin[TW];
   // this tile's segments for the slow list, appended with one global atomic
   __shared__ int s_nslow, s_slowbase;
   __shared__ int s_slow[RB];
@@ -467,7 +499,7 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   const int lc = lane % SEG;
   const unsigned long long gmask = (SEG == 64 ? ~0ull : ((1ull << SEG) - 1)) << (sub * SEG);
 
-  if (tid == 0) s_merged = 0;
+  if (tid == 0) s_merged = s_det = s_rel = s_storm = s_tomb = s_unk = 0;
   const bool pull = p.peer_mode == GH_PEER_PULL;
   for (int t = tid; t < RB * KB; t += 256) {
     const int row = t / KB, q = t - row * KB;
@@ -488,7 +520,11 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   uint16_t* __restrict__ hnn = d.hn[cur ^ 1];
   const int32_t* __restrict__ bo = d.base[cur];
   const int32_t* __restrict__ bn = d.base[cur ^ 1];
+  const int32_t r = p.r;
   uint32_t n_mrg16 = 0;  // merges x 16
+  int n_det = 0, n_rel = 0;
+  int n_tomb = 0, n_unk = 0;  // REMOVE: tombstoned / unknown member
+  int32_t* __restrict__ tsb = d.ts;
 
 #pragma unroll 1
   for (int tt = 0; tt < TPW; ++tt) {
@@ -497,37 +533,48 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   const int c0 = (int)(d.col0 + l0);                                  // its global member id
   const int64_t tb = (int64_t)tile * ((int64_t)p.n * TW) + lc * CPL;  // tile base + lane offset
   if (tid == 0) s_nslow = 0;
+  for (int t = tid; t < TW; t += 256) {
+    s_dcnt[t] = 0;
+    s_dmin[t] = INT_MAX;
+  }
 
-  // per pair of the lane's columns: the rebase (base_next - base_cur) << 5,
-  // and the flag threshold "hb > 1" as a code bound; a base jump beyond 1023
-  // or a REMOVE'd member sends the lane to the slow list
+  // REMOVE'd members in the lane: its segments go to the slow list
   const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
-  uint32_t d5[4], t5[4];
-  bool jump = false;
-  {
-    const v4i ba0 = *reinterpret_cast<const v4i*>(bo + l0), ba1 = *reinterpret_cast<const v4i*>(bo + l0 + 4);
-    const v4i bb0 = *reinterpret_cast<const v4i*>(bn + l0), bb1 = *reinterpret_cast<const v4i*>(bn + l0 + 4);
-    const int32_t ba[8] = {ba0.x, ba0.y, ba0.z, ba0.w, ba1.x, ba1.y, ba1.z, ba1.w};
-    const int32_t bb[8] = {bb0.x, bb0.y, bb0.z, bb0.w, bb1.x, bb1.y, bb1.z, bb1.w};
+  for (int pp = tid; pp < TW / 2; pp += 256) {
+    uint32_t dd = 0, th = 0, rmm = 0, rm1 = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint32_t dd = 0, th = 0;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int64_t delta = (int64_t)bb[2 * j + h] - ba[2 * j + h];
-        jump |= delta > 1023 || delta < -1023;
-        dd |= ((uint32_t)(delta << 5) & 0xFFFFu) << (16 * h);
-        const int64_t thr = 1 - (int64_t)bb[2 * j + h];
-        const uint32_t tc = thr < 0 ? 0xFFFFu : thr > 1023 ? 0x7FFFu : (uint32_t)((thr << 5) | 31);
-        th |= tc << (16 * h);
+    for (int h = 0; h < 2; ++h) {
+      const int64_t c = (int64_t)tile * TW + 2 * pp + h;
+      if (dbit(d.dbits, c)) {
+        if (d.det_cnt[dcur][c] == 1)
+          rm1 = 1;
+        else
+          rmm |= 0xFFFFu << (16 * h);
       }
-      d5[j] = dd;
-      t5[j] = th;
+      const int64_t delta = (int64_t)bn[c] - bo[c];
+      const uint32_t d5h = (delta > 1023 || delta < -1023) ? 0x8000u : ((uint32_t)(delta << 5) & 0xFFFFu);
+      const int64_t thr = 1 - (int64_t)bn[c];
+      const uint32_t tc = thr < 0 ? 0xFFFFu : thr > 1023 ? 0x7FFFu : (uint32_t)((thr << 5) | 31);
+      dd |= d5h << (16 * h);
+      th |= tc << (16 * h);
     }
+    s_d5[pp] = dd;
+    s_t5[pp] = th;
+    s_rm[pp] = rmm;
+    s_rm1[pp] = rm1;
   }
   const uint32_t tfp = (uint32_t)min(p.t_fail, 31) * 0x10001u;
-  const bool lane_ok = !p.exact && !jump && my8 == 0;
+  const uint32_t tcp = (uint32_t)min(p.t_cleanup, 31) * 0x10001u;
   __syncthreads();
+  // lean: no REMOVE in the lane; storm: REMOVE applied in the packed path
+  // unless a column has a single detector (that row keeps the member)
+  bool lane_ok = !p.exact;
+  if constexpr (STORM) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lane_ok &= s_rm1[lc * 4 + j] == 0;
+  } else {
+    lane_ok &= my8 == 0;
+  }
 
   constexpr int NIT = RB / RSTEP;
 #pragma unroll 1
@@ -548,7 +595,8 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     v4u w = ldn<false>(hno + off);  // re-read by peers: keep it cached
     v4u pv[KB];
     int ps[KB];
-    bool bad = !((meta >> 1) & 1) || cntv > KB;
+    const bool act = (meta >> 1) & 1;  // else the row is under the <4 guard (step 2)
+    bool bad = (!STORM && !act) || cntv > KB;
 #pragma unroll
     for (int q = 0; q < KB; ++q) {
       int s = i;
@@ -559,6 +607,7 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
       ps[q] = s;
       pv[q] = ldn<false>(hno + tb + (int64_t)s * TW);
     }
+    bad |= (w[0] & 0xFFFFu) == GH_N_WIDE;  // own segment wide
 #pragma unroll
     for (int q = 0; q < KB; ++q) bad |= q < cntv && (pv[q][0] & 0xFFFFu) == GH_N_WIDE;
     // A sender's own member in the lane: its snapshot carries hb + 1 there
@@ -578,13 +627,14 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     // An own cell that is not visible, or at the heartbeat cap, is slow.
     const int jd = i - c0;
     const bool own_in = (unsigned)jd < 8u;
-    if (own_in) {
+    if (own_in && act) {
       const int sh = 16 * (jd & 1);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (j == (jd >> 1)) {
           const uint32_t hv = (w[j] >> sh) & 0xFFFFu;
-          if (hv >= 0x8000u || (int64_t)bo[l0 + jd] + (hv >> 5) >= GH_HB_MAX)
+          if (hv >= 0x8000u || (int64_t)bo[l0 + jd] + (hv >> 5) >= GH_HB_MAX ||
+              (STORM && ((s_rm[lc * 4 + j] >> sh) & 1u)))
             bad = true;
           else
             w[j] = (w[j] & ~(0x1Fu << sh)) + (0x20u << sh);
@@ -592,56 +642,134 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     }
 
     v4u o;
-    uint32_t spec = 0, facc = 0, mcnt = 0, pcnt = 0, bcnt = 0;
+    // acc: bit 5/21 = a special own cell (age >= 30, wide marker), bit 15/31
+    // = a result outside the narrow window; ev: detected or released cells
+    uint32_t acc = 0, detb = 0, relb = 0, stb = 0, mcnt = 0, tomb16 = 0, unk16 = 0;
+    uint32_t fo = 0;  // flagged results: next round's detections
+    const v4u d5 = *reinterpret_cast<const v4u*>(&s_d5[lc * 4]);
+    const v4u t5 = *reinterpret_cast<const v4u*>(&s_t5[lc * 4]);
+    v4u rmv = {0u, 0u, 0u, 0u};
+    if constexpr (STORM) rmv = *reinterpret_cast<const v4u*>(&s_rm[lc * 4]);
+    int dp16 = 0;  // (present after - present before) x 16
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      uint32_t m = pv[0][j];
+      const uint32_t rmj = rmv[j];  // REMOVE'd columns: not in any sender's snapshot
+      uint32_t m = pv[0][j] | rmj;
 #pragma unroll
-      for (int q = 1; q < KB; ++q) m = pk_max_i16(m, pv[q][j]);
+      for (int q = 1; q < KB; ++q) m = pk_max_i16(m, pv[q][j] | rmj);
       const uint32_t x = w[j];
-      const uint32_t hx = pk_sra15(x);
-      bcnt += __builtin_popcount(~hx);  // present before (fast lanes: visible or absent)
-      // own cells other than visible (age < 30) or absent: flagged,
-      // tombstone, wide marker (x + 1 keeps bit 15), age 30/31
-      spec |= (pk_add_u16(x, 0x00010001u) & 0x80008000u) | ((((x & 0x001F001Fu) + 0x00020002u) & ~hx) & 0x00200020u);
-      const uint32_t wc = x | 0x001F001Fu;                       // own heartbeat key (absent: -1)
-      const uint32_t mm = pk_sra15(pk_subs_i16(wc, m));          // merged: a sender's heartbeat is larger
-      const uint32_t nm = pk_adds_u16(x, 0x00010001u);           // not merged: age + 1 (absent stays)
-      const uint32_t mv = (m & 0x7FE07FE0u) | 0x00010001u;       // merged: its heartbeat, age 1
-      uint32_t y = (mv & mm) | (nm & ~mm);
-      const uint32_t hy = pk_sra15(y);                           // absent halves
-      y = pk_sub_u16(y, d5[j] & ~hy);                            // rebase present halves
-      facc |= (y | pk_add_u16(y, 0x00200020u)) & ~hy;            // offset left [0, 1022]
-      const uint32_t c1 = pk_subs_i16(tfp, y & 0x001F001Fu);     // age > T_fail
-      const uint32_t c2 = pk_subs_i16(t5[j], y);                 // hb > 1
-      y |= c1 & c2 & ~hy & 0x80008000u;
+      uint32_t mm, y0, pre;  // merged mask, value if not merged, present-before mask
+      if constexpr (!STORM) {
+        // own cells other than visible (age < 30) or absent go to the slow
+        // list: flagged, tombstone, wide marker (x + 1 keeps bit 15), age 30/31
+        const uint32_t hx = pk_sra15(x);
+        acc |= (pk_add_u16(x, 0x00010001u) & 0x80008000u) | ((((x & 0x001F001Fu) + 0x00020002u) & ~hx) & 0x00200020u);
+        mm = pk_sra15(pk_subs_i16(x | 0x001F001Fu, m));     // merged: a sender's heartbeat is larger
+        y0 = pk_adds_u16(x, 0x00010001u);                   // not merged: age + 1 (absent stays)
+        pre = ~hx;
+      } else {
+        // cell classes: (x | 31) + 1 is 0 for a tombstone or absent cell, has
+        // bit 15 for a flagged present one and not for a visible one
+        const uint32_t actm = act ? 0xFFFFFFFFu : 0u;
+        const uint32_t z = pk_add_u16(x | 0x001F001Fu, 0x00010001u);
+        const uint32_t ta0 = pk_zero_mask(z);                  // tombstone or absent
+        const uint32_t ab = pk_zero_mask(pk_add_u16(x, 0x00010001u));  // absent
+        // step 1 REMOVE: a present cell becomes a tombstone of its age
+        tomb16 += __builtin_popcount(rmj & ~ta0);
+        unk16 += __builtin_popcount(rmj & ab);
+        const uint32_t xr = x | (rmj & 0xFFE0FFE0u);
+        const uint32_t fl0 = pk_sra15(z) & ~rmj;               // flagged present
+        const uint32_t ta = ta0 | rmj;                         // tombstone or absent
+        const uint32_t fl = fl0 & actm;                        // detected now (step 4, active rows)
+        const uint32_t ag = x & 0x001F001Fu;
+        const uint32_t st = pk_sra15(pk_subs_i16(tcp, ag)) & actm;  // age > T_cleanup (step 5, active rows)
+        const uint32_t rel = (ta | fl) & st;                   // absent after step 5 (released, or absent)
+        const uint32_t keep = (ta | fl) & ~st & ~(ab & ~actm); // tombstone next round
+        const uint32_t nowm = ~ta & ~actm;                     // guard rows: present cells stamped now
+        acc |= (ag + 0x00020002u) & ~ab & ~nowm & 0x00200020u; // age >= 30 (saturation) or wide marker
+        const uint32_t key = ((xr & ~(nowm & 0x80008000u)) | 0x001F001Fu) | rel;  // heartbeat key (absent: -1)
+        mm = pk_sra15(pk_subs_i16(key, m)) & ~keep;            // merged (step 6)
+        // not merged: age + 1 (a detected cell becomes a tombstone of its
+        // age), released cells absent, absent stays absent; guard rows'
+        // present cells age 1
+        const uint32_t yact = pk_adds_u16(xr | (fl & 0xFFE0FFE0u), 0x00010001u) | rel;
+        y0 = (((xr & 0x7FE07FE0u) | 0x00010001u) & nowm) | (yact & ~nowm);
+        pre = ~ta0;
+        stb |= ((fl0 | ta) & ~ab) | ~actm;                     // what the lean variant lists
+        detb |= pair_bits(fl, j);
+        relb |= pair_bits(rel & ~ab, j);
+      }
+      const uint32_t mv = (m & 0x7FE07FE0u) | 0x00010001u;   // merged: its heartbeat, age 1
+      uint32_t y = (mv & mm) | (y0 & ~mm);
+      const uint32_t hy = pk_sra15(y);                       // tombstone or absent halves
+      y = pk_sub_u16(y, d5[j] & ~hy);                        // rebase present halves
+      acc |= (y | pk_add_u16(y, 0x00200020u)) & ~hy & 0x80008000u;  // offset left [0, 1022]
+      const uint32_t c1 = pk_subs_i16(tfp, y & 0x001F001Fu); // age > T_fail
+      const uint32_t c2 = pk_subs_i16(t5[j], y);             // hb > 1
+      const uint32_t flo = c1 & c2 & ~hy & 0x80008000u;
+      y |= flo;
+      fo |= flo;
       o[j] = y;
       mcnt += __builtin_popcount(mm);
-      pcnt += __builtin_popcount(~hy);
+      dp16 += __builtin_popcount(~hy) - __builtin_popcount(pre);
     }
-    if (own_in) {
+    if (own_in) {  // the own member is never detected: no flag on a present own cell
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (j == (jd >> 1)) o[j] &= ~(0x8000u << (16 * (jd & 1)));
+        if (j == (jd >> 1) && ((o[j] >> (16 * (jd & 1))) & 0xFFFFu) < GH_N_TOMB) o[j] &= ~(0x8000u << (16 * (jd & 1)));
     }
-    const bool ok = lane_ok && !bad && spec == 0 && (facc & 0x80008000u) == 0;
+    const bool ok = lane_ok && !bad && acc == 0;
     const bool seg_ok = (__ballot(al && !ok) & gmask) == 0;
     int dpres = 0;  // present after - present before
+    bool any_det = false;
     if (al) {
       if (seg_ok) {
         stn<NT>(hnn + off, o);
-        dpres = ((int)pcnt - (int)bcnt) >> 4;
+        dpres = dp16 >> 4;
         n_mrg16 += mcnt;
+        if constexpr (STORM) {
+          n_tomb += (int)(tomb16 >> 4);
+          n_unk += (int)(unk16 >> 4);
+        }
+        if (STORM && (detb | relb)) {  // storms: detections (per column) and released cells' ts
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            if ((detb >> j) & 1u) {
+              atomicAdd(&s_dcnt[lc * CPL + j], 1);
+              atomicMin(&s_dmin[lc * CPL + j], i);
+            }
+            if ((relb >> j) & 1u) tsb[off + j] = r - (int)((w[j >> 1] >> (16 * (j & 1))) & 31u);
+          }
+          n_det += __builtin_popcount(detb);
+          n_rel += __builtin_popcount(relb);
+          any_det = detb != 0;
+        }
       } else if (lc == 0) {
         s_slow[atomicAdd(&s_nslow, 1)] = i;
       }
     }
 #pragma unroll
-    for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) dpres += __shfl_xor(dpres, o2);
-    if (lc == 0 && dpres) atomicAdd(&d.cntl[i], dpres);
+    for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) {
+      dpres += __shfl_xor(dpres, o2);
+      any_det |= __shfl_xor((int)any_det, o2) != 0;
+    }
+    if (lc == 0) {
+      if (dpres) atomicAdd(&d.cntl[i], dpres);
+      if (any_det) d.det_any[i] = 1;
+    }
+    // storm measure: committed segments that hold (storm variant) or will
+    // hold next round (flagged results) cells the lean variant cannot take
+    if (al && seg_ok && (__ballot(stb != 0 || fo != 0) & gmask) != 0 && lc == 0) atomicAdd(&s_storm, 1ull);
   }
 
   __syncthreads();
+  for (int t = tid; t < TW; t += 256) {
+    if (s_dcnt[t]) {
+      const int64_t c = (int64_t)tile * TW + t;
+      atomicAdd(&d.det_cnt[dcur ^ 1][c], s_dcnt[t]);
+      atomicMin(&d.det_min[dcur ^ 1][c], s_dmin[t]);
+    }
+  }
   if (tid == 0 && s_nslow) s_slowbase = atomicAdd(d.slow_n, s_nslow);
   __syncthreads();
   for (int t = tid; t < s_nslow; t += 256) d.slow[s_slowbase + t] = ((int64_t)tile << 32) | (uint32_t)s_slow[t];
@@ -649,8 +777,19 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
   }  // tiles
 
   if (n_mrg16) atomicAdd(&s_merged, (unsigned long long)(n_mrg16 >> 4));
+  if (n_det) atomicAdd(&s_det, (unsigned long long)n_det);
+  if (n_rel) atomicAdd(&s_rel, (unsigned long long)n_rel);
+  if (n_tomb) atomicAdd(&s_tomb, (unsigned long long)n_tomb);
+  if (n_unk) atomicAdd(&s_unk, (unsigned long long)n_unk);
   __syncthreads();
-  if (tid == 0 && s_merged) atomicAdd(&d.stats[ST_MERGED], s_merged);
+  if (tid == 0) {
+    if (s_merged) atomicAdd(&d.stats[ST_MERGED], s_merged);
+    if (s_det) atomicAdd(&d.stats[ST_DETECTIONS], s_det);
+    if (s_rel) atomicAdd(&d.stats[ST_RELEASED], s_rel);
+    if (s_storm) atomicAdd(d.nstorm, (int)s_storm);
+    if (s_tomb) atomicAdd(&d.stats[ST_TOMBSTONED], s_tomb);
+    if (s_unk) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], s_unk);
+  }
 }
 
 // 8 wide values of the row segment cells [off, off + 8) whose narrow codes are
@@ -1057,10 +1196,14 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
   constexpr int RB = round_rb<TW>();
   const int nrb = (p.n + RB - 1) / RB;
   const dim3 grid((unsigned)(nrb * (p.ld / TW / TPW))), blk(256);
-  if (nt)
-    hipLaunchKernelGGL((k_round<KB, TW, TPW, true>), grid, blk, 0, s, d, cur, dcur, p);
-  else
-    hipLaunchKernelGGL((k_round<KB, TW, TPW, false>), grid, blk, 0, s, d, cur, dcur, p);
+  // both variants; the one k_base did not select returns at once
+  if (nt) {
+    hipLaunchKernelGGL((k_round<KB, TW, TPW, true, false>), grid, blk, 0, s, d, cur, dcur, p);
+    hipLaunchKernelGGL((k_round<KB, TW, TPW, true, true>), grid, blk, 0, s, d, cur, dcur, p);
+  } else {
+    hipLaunchKernelGGL((k_round<KB, TW, TPW, false, false>), grid, blk, 0, s, d, cur, dcur, p);
+    hipLaunchKernelGGL((k_round<KB, TW, TPW, false, true>), grid, blk, 0, s, d, cur, dcur, p);
+  }
 }
 
 template <int TW>

@@ -94,12 +94,15 @@ class Engine:
         self._chk(self.lib.gh_shard_info(self.h, C.byref(r), C.byref(w), C.byref(c0), C.byref(nc)))
         return r.value, w.value, c0.value, nc.value
 
-    def encoding_info(self):
+    def encoding_info(self, full=False):
         """(wide segments of the current table, segments the last round ran
-        by the per-cell rule) of this engine's shard (diagnostic)."""
-        w, sl = C.c_int64(), C.c_int64()
-        self._chk(self.lib.gh_encoding_info(self.h, C.byref(w), C.byref(sl)))
-        return w.value, sl.value
+        by the per-cell rule) of this engine's shard; full=True adds the last
+        round's kernel variant (0 lean, 1 storm) and its storm measure
+        (diagnostic)."""
+        w, sl, ns = C.c_int64(), C.c_int64(), C.c_int64()
+        mode = C.c_int32()
+        self._chk(self.lib.gh_encoding_info(self.h, C.byref(w), C.byref(sl), C.byref(mode), C.byref(ns)))
+        return (w.value, sl.value, mode.value, ns.value) if full else (w.value, sl.value)
 
     def close(self):
         if getattr(self, "h", None):

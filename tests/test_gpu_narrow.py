@@ -144,3 +144,30 @@ def test_steady_state_stays_narrow(gs):
     eng.step(6)
     assert eng.encoding_info() == (0, 0)
     eng.close()
+
+
+@pytest.mark.parametrize("peer_mode", [0, 1])
+def test_storm_variant_collapse(gs, oracle_mod, peer_mode):
+    """A failure storm and the collapse under the <4 guard (BASELINE config
+    2's regime, T_fail=5 at N=4,096): the storm variant of the round kernel
+    (detections, REMOVE, releases and guard rows in the packed path) runs and
+    matches the oracle every round."""
+    n = 4096
+    cfg = dict(peer_mode=peer_mode, fanout=3, seed=0x9700 + peer_mode, t_fail=5, t_cleanup=5)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    init = sc.full_state(n)
+    eng.import_state(*init, 0)
+    orc.import_state(*init, 0)
+    sched = {4: [(sc.CRASH, c) for c in sc.crash_ids(n, 0.01, 0x9701)]}
+    storm_rounds = 0
+    for r in range(1, 17):
+        if r in sched:
+            eng.apply_events(sched[r])
+            orc.apply_events(sched[r])
+        assert eng.step(1) == orc.step(1), r
+        storm_rounds += eng.encoding_info(full=True)[2]
+        if r % 4 == 0 or r > 5:
+            compare(eng, orc, r)
+    eng.close()
+    assert storm_rounds > 0
