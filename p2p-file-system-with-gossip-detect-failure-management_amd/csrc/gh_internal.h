@@ -350,7 +350,9 @@ void launch_ring_count(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
 void launch_ring_select(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
 // nt = non-temporal hints on the once-touched streams of k_round
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt);
+// storm: the storm variant (else the lean one); both are launched every
+// round and only the one k_base selected runs
+void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm);
 // the segments k_round listed, by the per-cell rule (after launch_round)
 void launch_round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);

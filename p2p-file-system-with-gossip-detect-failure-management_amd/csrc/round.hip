@@ -1192,18 +1192,19 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
 }
 
 template <int KB, int TW, int TPW>
-static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
+static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm) {
   constexpr int RB = round_rb<TW>();
   const int nrb = (p.n + RB - 1) / RB;
   const dim3 grid((unsigned)(nrb * (p.ld / TW / TPW))), blk(256);
-  // both variants; the one k_base did not select returns at once
-  if (nt) {
-    hipLaunchKernelGGL((k_round<KB, TW, TPW, true, false>), grid, blk, 0, s, d, cur, dcur, p);
+  // the one k_base did not select returns at once
+  if (nt && storm)
     hipLaunchKernelGGL((k_round<KB, TW, TPW, true, true>), grid, blk, 0, s, d, cur, dcur, p);
-  } else {
-    hipLaunchKernelGGL((k_round<KB, TW, TPW, false, false>), grid, blk, 0, s, d, cur, dcur, p);
+  else if (nt)
+    hipLaunchKernelGGL((k_round<KB, TW, TPW, true, false>), grid, blk, 0, s, d, cur, dcur, p);
+  else if (storm)
     hipLaunchKernelGGL((k_round<KB, TW, TPW, false, true>), grid, blk, 0, s, d, cur, dcur, p);
-  }
+  else
+    hipLaunchKernelGGL((k_round<KB, TW, TPW, false, false>), grid, blk, 0, s, d, cur, dcur, p);
 }
 
 template <int TW>
@@ -1218,32 +1219,32 @@ static void round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
 
 // tiles per workgroup: ld / TW is a multiple of 8 (host padding)
 template <int KB, int TW>
-static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
+static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm) {
   switch (p.tpw) {
-    case 1: launch_round_tpw<KB, TW, 1>(d, cur, dcur, p, s, nt); break;
-    case 2: launch_round_tpw<KB, TW, 2>(d, cur, dcur, p, s, nt); break;
-    case 8: launch_round_tpw<KB, TW, 8>(d, cur, dcur, p, s, nt); break;
-    default: launch_round_tpw<KB, TW, 4>(d, cur, dcur, p, s, nt); break;
+    case 1: launch_round_tpw<KB, TW, 1>(d, cur, dcur, p, s, nt, storm); break;
+    case 2: launch_round_tpw<KB, TW, 2>(d, cur, dcur, p, s, nt, storm); break;
+    case 8: launch_round_tpw<KB, TW, 8>(d, cur, dcur, p, s, nt, storm); break;
+    default: launch_round_tpw<KB, TW, 4>(d, cur, dcur, p, s, nt, storm); break;
   }
 }
 
 template <int KB>
-static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
+static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm) {
   switch (d.tw) {
-    case 8: launch_round_tw<KB, 8>(d, cur, dcur, p, s, nt); break;
-    case 16: launch_round_tw<KB, 16>(d, cur, dcur, p, s, nt); break;
-    case 32: launch_round_tw<KB, 32>(d, cur, dcur, p, s, nt); break;
-    case 128: launch_round_tw<KB, 128>(d, cur, dcur, p, s, nt); break;
-    case 256: launch_round_tw<KB, 256>(d, cur, dcur, p, s, nt); break;
-    default: launch_round_tw<KB, 64>(d, cur, dcur, p, s, nt); break;
+    case 8: launch_round_tw<KB, 8>(d, cur, dcur, p, s, nt, storm); break;
+    case 16: launch_round_tw<KB, 16>(d, cur, dcur, p, s, nt, storm); break;
+    case 32: launch_round_tw<KB, 32>(d, cur, dcur, p, s, nt, storm); break;
+    case 128: launch_round_tw<KB, 128>(d, cur, dcur, p, s, nt, storm); break;
+    case 256: launch_round_tw<KB, 256>(d, cur, dcur, p, s, nt, storm); break;
+    default: launch_round_tw<KB, 64>(d, cur, dcur, p, s, nt, storm); break;
   }
 }
 
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt) {
+void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm) {
   if (p.peer_mode == GH_PEER_PULL && p.k <= 4)
-    launch_round_kb<4>(d, cur, dcur, p, s, nt);
+    launch_round_kb<4>(d, cur, dcur, p, s, nt, storm);
   else
-    launch_round_kb<8>(d, cur, dcur, p, s, nt);
+    launch_round_kb<8>(d, cur, dcur, p, s, nt, storm);
 }
 
 void launch_base(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
