@@ -1006,6 +1006,15 @@ __device__ __forceinline__ int q_compose(int a, int b) {  // a, then b
   return ((a | b) & 5) | ((b & 1) ? (b & 2) : ((a ^ b) & 2));
 }
 __device__ __forceinline__ int q_apply(int f, int s) { return (f & 1) ? ((f >> 1) & 1) : (s ^ ((f >> 1) & 1)); }
+// The composed map of 8 consecutive cells with list members P and candidates
+// F (F within P), in closed form: with a non-candidate in the stretch, the
+// parity of the candidates after the last one; else the parity of all.
+__device__ __forceinline__ int q_summary8(uint32_t P, uint32_t F) {
+  if (!P) return 0;
+  const uint32_t B = P & ~F;
+  if (B) return 5 | ((__builtin_popcount(F >> (32 - __builtin_clz(B))) & 1) << 1);
+  return 4 | ((__builtin_popcount(F) & 1) << 1);
+}
 
 // one segment per (tile, row): the tile's run summary (segmented scan over
 // the SEG lanes, last lane holds the whole tile)
@@ -1021,10 +1030,8 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
     int f = 0;
     if (valid) {
       const uint32_t pf = gh_pf8(d, cur, i, t * TW + w.lc * 8);
-      const uint32_t rm = removed8(d, dcur, t * TW + w.lc * 8, i);
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (((pf >> j) & 1u) && !((rm >> j) & 1u)) f = q_compose(f, ((pf >> (8 + j)) & 1u) ? 6 : 5);
+      const uint32_t P = pf & ~removed8(d, dcur, t * TW + w.lc * 8, i) & 0xFFu;
+      f = q_summary8(P, (pf >> 8) & P);
     }
 #pragma unroll
     for (int o = 1; o < SEG; o <<= 1) {
@@ -1085,13 +1092,9 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
       pf = gh_pf8(d, cur, i, t * TW + w.lc * 8);
       rm = removed8(d, dcur, t * TW + w.lc * 8, i);
     }
-    int f = 0, lastj = -1;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (((pf >> j) & 1u) && !((rm >> j) & 1u)) {
-        f = q_compose(f, ((pf >> (8 + j)) & 1u) ? 6 : 5);
-        lastj = w.lc * 8 + j;
-      }
+    const uint32_t P = pf & ~rm & 0xFFu, F = (pf >> 8) & P;  // list members, candidates
+    const int f = q_summary8(P, F);
+    int lastj = P ? w.lc * 8 + 31 - __builtin_clz(P) : -1;
     int incl = f;
 #pragma unroll
     for (int o = 1; o < SEG; o <<= 1) {
@@ -1109,8 +1112,8 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
     uint32_t clear = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if (!(((pf >> j) & 1u) && !((rm >> j) & 1u))) continue;
-      if (!((pf >> (8 + j)) & 1u)) {
+      if (!((P >> j) & 1u)) continue;
+      if (!((F >> j) & 1u)) {
         s = 0;
         continue;
       }
