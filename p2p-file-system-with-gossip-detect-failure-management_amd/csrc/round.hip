@@ -447,8 +447,8 @@ constexpr int round_rb() {
 }
 
 template <int KB, int TW, int TPW, bool NT, bool STORM>
-__global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRound p) {
-  if (*d.mode != (int)STORM) return;  // the other variant runs this round (k_base)
+__device__ __forceinline__ void round_block(const GhDev& d, const int cur, const int dcur, const GhRound& p,
+                                            const int bid) {
   constexpr int CPL = 8;
   constexpr int SEG = TW / CPL;
   constexpr int RPW = 64 / SEG;
@@ -484,13 +484,13 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     // XCD-aware: blocks b and b+8 share an XCD (round-robin dispatch, speed
     // only), so XCD x = b % 8 sweeps groups x, x+8, ... and its L2 holds the
     // slice it is on.
-    const int x = blockIdx.x & 7;
-    const int j = blockIdx.x >> 3;
+    const int x = bid & 7;
+    const int j = bid >> 3;
     group = x + 8 * (j / nrb);
     rb = j - (j / nrb) * nrb;
   } else {
-    group = blockIdx.x / nrb;
-    rb = blockIdx.x - group * nrb;
+    group = bid / nrb;
+    rb = bid - group * nrb;
   }
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -789,6 +789,24 @@ __global__ __launch_bounds__(256) void k_round(GhDev d, int cur, int dcur, GhRou
     if (s_storm) atomicAdd(d.nstorm, (int)s_storm);
     if (s_tomb) atomicAdd(&d.stats[ST_TOMBSTONED], s_tomb);
     if (s_unk) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], s_unk);
+  }
+}
+
+// Both variants are launched every round; the one k_base did not select
+// returns at once. The storm variant runs 1/8 of the workgroups, each taking
+// blocks a multiple of 8 apart (same XCD), so idle it is a small dispatch.
+template <int KB, int TW, int TPW, bool NT, bool STORM>
+__global__ __launch_bounds__(256, (STORM && TW >= 32) ? 4 : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
+  if (*d.mode != (int)STORM) return;
+  if constexpr (STORM) {
+    constexpr int RB = round_rb<TW>();
+    const int nblk = ((p.n + RB - 1) / RB) * ((int)(p.ld / TW) / TPW);
+    for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
+      round_block<KB, TW, TPW, NT, STORM>(d, cur, dcur, p, b);
+      __syncthreads();  // LDS of this block before the next
+    }
+  } else {
+    round_block<KB, TW, TPW, NT, STORM>(d, cur, dcur, p, blockIdx.x);
   }
 }
 
@@ -1198,7 +1216,8 @@ template <int KB, int TW, int TPW>
 static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm) {
   constexpr int RB = round_rb<TW>();
   const int nrb = (p.n + RB - 1) / RB;
-  const dim3 grid((unsigned)(nrb * (p.ld / TW / TPW))), blk(256);
+  const int64_t nblk = (int64_t)nrb * (p.ld / TW / TPW);
+  const dim3 grid((unsigned)(storm ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
   // the one k_base did not select returns at once
   if (nt && storm)
     hipLaunchKernelGGL((k_round<KB, TW, TPW, true, true>), grid, blk, 0, s, d, cur, dcur, p);

@@ -1,5 +1,5 @@
 """A/B of k_round layout/stream variants at N=65,536 (steady state). One
-engine per tile width (48 GiB each, up to 4 alive at once), rounds
+engine per tile width (64 GiB each at N=65,536, up to 3 alive at once), rounds
 interleaved across variants in one process (guide §5.4 rule 24); kernel time
 from HIP events on each engine's stream.
   python tools/round_variants.py [--n 65536] [--iters 4] [--rounds 3]
