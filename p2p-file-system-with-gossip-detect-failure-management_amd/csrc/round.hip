@@ -1102,14 +1102,18 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
   const SegWalk<TW> w(p);
   for (int64_t base = w.first; base < w.nseg; base += w.stride) {
     const int64_t sid = base + w.sub;
-    const int64_t t = sid < w.nseg ? sid / p.n : 0;
-    const int i = sid < w.nseg ? (int)(sid - t * p.n) : 0;
-    const bool valid = sid < w.nseg && d.alive[i] && d.active[i];  // only active rows detect (and send)
-    uint32_t pf = 0, rm = 0;
-    if (valid) {
-      pf = gh_pf8(d, cur, i, t * TW + w.lc * 8);
-      rm = removed8(d, dcur, t * TW + w.lc * 8, i);
-    }
+    const bool inr = sid < w.nseg;
+    const int64_t t = inr ? sid / p.n : 0;
+    const int i = inr ? (int)(sid - t * p.n) : 0;
+    // the segment and the row's state are independent loads: issue them
+    // together, decide validity after
+    const uint32_t pf0 = gh_pf8(d, cur, i, t * TW + w.lc * 8);
+    const uint32_t rm0 = removed8(d, dcur, t * TW + w.lc * 8, i);
+    const int qc = d.qcarry[i];
+    const int qs = d.qsum[inr ? sid : 0];
+    const int ql = d.qlast[i];
+    const bool valid = inr && d.alive[i] && d.active[i];  // only active rows detect (and send)
+    const uint32_t pf = valid ? pf0 : 0u, rm = valid ? rm0 : 0u;
     const uint32_t P = pf & ~rm & 0xFFu, F = (pf >> 8) & P;  // list members, candidates
     const int f = q_summary8(P, F);
     int lastj = P ? w.lc * 8 + 31 - __builtin_clz(P) : -1;
@@ -1124,9 +1128,8 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
 #pragma unroll
     for (int o = SEG / 2; o > 0; o >>= 1) lastj = max(lastj, __shfl_xor(lastj, o));
     if (!valid) continue;
-    const int qc = d.qcarry[i];
-    int s = q_apply(excl, q_apply(d.qsum[sid], qc & 1));
-    const int lastc = ((qc & 2) && d.qlast[i] == t) ? lastj : -1;  // the row's last list entry, if here
+    int s = q_apply(excl, q_apply(qs, qc & 1));
+    const int lastc = ((qc & 2) && ql == t) ? lastj : -1;  // the row's last list entry, if here
     uint32_t clear = 0;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
