@@ -18,7 +18,7 @@ namespace {
 
 constexpr unsigned kMaxGrid = 65536;
 
-// One wave per row: each lane reads 4 consecutive members (one tile), the
+// One wave per row: each lane reads 4 consecutive members (gh_load4), the
 // wave 256 members per step.
 __global__ __launch_bounds__(256) void k_count(GhDev d, int cur, GhRound p) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);

@@ -12,7 +12,7 @@
 //   members:
 //     cell(i, c) = (c / TW) * (N * TW) + i * TW + c % TW     (c local)
 //   i.e. tile t holds local members [t*TW, (t+1)*TW) of every observer row,
-//   rows contiguous. One tile of one table is N*TW*4 bytes (16 MiB at
+//   rows contiguous. One tile of the narrow table is N*TW*2 bytes (8 MiB at
 //   N=65,536, TW=64): the round kernel sweeps tile by tile, so its own-row
 //   streams are sequential and every peer gather of a tile stays inside
 //   that slice.
