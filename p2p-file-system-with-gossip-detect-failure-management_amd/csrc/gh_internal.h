@@ -140,6 +140,7 @@ struct GhDev {
   int32_t *slow_n;  // their count
   int32_t *mode;    // k_round variant of the round: 0 lean, 1 storm (k_base)
   int32_t *nstorm;  // storm variant: segments holding flagged or tombstoned cells
+  int32_t *nflag;   // [2]: segments written into buffer b holding flagged cells (quirk pre-pass gate)
   int32_t *ts;
   uint8_t *alive, *active, *det_any, *und;
   int32_t *cntl, *cntg;  // [n + 8]: per-row present counts (local / allreduced), [n] = |D|
@@ -339,6 +340,8 @@ struct GhRound {
   int32_t xmap;       // k_round block->tile map: 0 tile-major, 1 XCD-aware
   int32_t tpw;        // k_round tiles per workgroup (1, 2, 4, 8)
   int32_t exact;      // T_fail or T_cleanup >= GH_AGE_CAP: every cell by the slow rule (exact ts)
+  int32_t qgate;      // quirk pre-pass: 1 = return at once when nflag[qcur] == 0 (no candidate anywhere)
+  int32_t qcur;       // the buffer the pre-pass rewrites
 };
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------

@@ -48,6 +48,9 @@ struct Engine {
   int xmap = 1;          // k_round XCD-aware tile map (gh_set_round_variant)
   int tpw = 1;           // k_round tiles per workgroup (GH_ROUND_TPW)
   bool timing = false;
+  // the current table may hold flags no round kernel counted (import, fill,
+  // events, list merges): the next quirk pre-pass runs ungated
+  bool qforce = true;
   double timed_ms = 0.0;
   int64_t timed_launches = 0;
   std::vector<hipEvent_t> evs;
@@ -177,6 +180,7 @@ int allreduce_i32(Engine* e, int32_t* send, int32_t* recv, size_t count) {
 // SPEC.md §5: crashes, then leaves (all leavers stop first), then joins.
 int process_events(Engine* e, int32_t r) {
   if (e->pending.empty()) return GH_OK;
+  e->qforce = true;
   const GhRound p = round_params(e, r);
   std::vector<gh_event> ev;
   ev.swap(e->pending);
@@ -393,7 +397,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.base[0], e->ld, 0)) || (rc = dalloc(e, &d.base[1], e->ld, 0)) ||
         (rc = dalloc(e, &d.colq, e->ld, 0)) || (rc = dalloc(e, &d.ts, cells, 0)) ||
         (rc = dalloc(e, &d.slow, (size_t)(e->ld / tw) * e->n, 0)) || (rc = dalloc(e, &d.slow_n, 4, 0)) ||
-        (rc = dalloc(e, &d.mode, 4, 0)) || (rc = dalloc(e, &d.nstorm, 4, 0)))
+        (rc = dalloc(e, &d.mode, 4, 0)) || (rc = dalloc(e, &d.nstorm, 4, 0)) ||
+        (rc = dalloc(e, &d.nflag, 2, 0)))
       break;
     if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
         (rc = dalloc(e, &d.det_any, e->n, 0)) || (rc = dalloc(e, &d.und, e->n, 0)) ||
@@ -609,6 +614,7 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
       return set_err(e, GH_ERANGE, "ts of a listed member after the round being imported");
   }
   HIPCHK(e, hipSetDevice(e->cfg.device));
+  e->qforce = true;
   int rc;
   const GhRound p = round_params(e, round + 1);
   if (n_rows > 0) {
@@ -660,6 +666,7 @@ int gh_init_full(void* h, int32_t hb0, int32_t ts0, int32_t round) {
   if (hb0 < 0 || hb0 > GH_HB_MAX) return set_err(e, GH_ERANGE, "hb0 out of range");
   if ((int64_t)ts0 > (int64_t)round + 1) return set_err(e, GH_ERANGE, "ts0 after the start round");
   HIPCHK(e, hipSetDevice(e->cfg.device));
+  e->qforce = true;
   std::fill(e->alive.begin(), e->alive.end(), 1);
   int rc;
   if ((rc = upload_alive(e))) return rc;
@@ -705,7 +712,16 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     const GhRound p = round_params(e, r);
     launch_base(e->d, e->cur, e->dcur, p, e->stream);
     if ((rc = decide_active(e, p))) return rc;
-    if (e->cfg.detect_mode == GH_DETECT_QUIRK && (rc = quirk_flags(e, p))) return rc;
+    if (e->cfg.detect_mode == GH_DETECT_QUIRK) {
+      // single shard: skip the pre-pass when the table holds no flag (the
+      // round kernels count flagged segments as they write); shards always
+      // run it, their summaries feed the other shards' carries
+      GhRound pq = p;
+      pq.qgate = e->world == 1 && !e->qforce;
+      pq.qcur = e->cur;
+      if ((rc = quirk_flags(e, pq))) return rc;
+      e->qforce = false;
+    }
     if ((rc = build_inboxes(e, p))) return rc;
     // the two variants of k_round; the one not selected returns at once
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[3 * q], e->stream));
@@ -826,6 +842,7 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
     if (std::adjacent_find(s.begin(), s.end()) != s.end()) return set_err(e, GH_EINVAL, "member ids must be distinct");
   }
   HIPCHK(e, hipSetDevice(e->cfg.device));
+  e->qforce = true;
   int32_t cnt = 0;
   if (n > 0 && e->alive[observer]) {  // GetMsg runs only while Alive (slave/slave.go:208)
     Staging st;

@@ -404,6 +404,7 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
     *d.mode = measure * 32 > d.ntiles * (int64_t)d.n;
     *d.slow_n = 0;
     *d.nstorm = 0;
+    d.nflag[cur ^ 1] = 0;  // counted by this round's writers
     d.cntl[d.n] = d.nd[dcur];  // |D_{r-1}| of this shard next to the local counts, for one allreduce
   }
   if (c >= p.ld) return;
@@ -524,6 +525,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   uint32_t n_mrg16 = 0;  // merges x 16
   int n_det = 0, n_rel = 0;
   int n_tomb = 0, n_unk = 0;  // REMOVE: tombstoned / unknown member
+  int wflag = 0;              // wrote a flagged cell (quirk pre-pass gate)
   int32_t* __restrict__ tsb = d.ts;
 
 #pragma unroll 1
@@ -725,6 +727,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     if (al) {
       if (seg_ok) {
         stn<NT>(hnn + off, o);
+        wflag |= fo != 0;
         dpres = dp16 >> 4;
         n_mrg16 += mcnt;
         if constexpr (STORM) {
@@ -781,8 +784,9 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   if (n_rel) atomicAdd(&s_rel, (unsigned long long)n_rel);
   if (n_tomb) atomicAdd(&s_tomb, (unsigned long long)n_tomb);
   if (n_unk) atomicAdd(&s_unk, (unsigned long long)n_unk);
-  __syncthreads();
+  wflag = __syncthreads_or(wflag);
   if (tid == 0) {
+    if (wflag) atomicAdd(&d.nflag[cur ^ 1], 1);
     if (s_merged) atomicAdd(&d.stats[ST_MERGED], s_merged);
     if (s_det) atomicAdd(&d.stats[ST_DETECTIONS], s_det);
     if (s_rel) atomicAdd(&d.stats[ST_RELEASED], s_rel);
@@ -844,6 +848,7 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int64_t nseg = *d.slow_n;
+  if (nseg > 0 && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&d.nflag[cur ^ 1], 1);  // may write flags
   const bool pull = p.peer_mode == GH_PEER_PULL;
   const int32_t r = p.r;
   const uint16_t* __restrict__ hno = d.hn[cur];
@@ -1038,6 +1043,7 @@ __device__ __forceinline__ int q_summary8(uint32_t P, uint32_t F) {
 // the SEG lanes, last lane holds the whole tile)
 template <int TW>
 __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, GhRound p) {
+  if (p.qgate && d.nflag[p.qcur] == 0) return;  // no candidate in the table
   constexpr int SEG = SegWalk<TW>::SEG;
   const SegWalk<TW> w(p);
   for (int64_t base = w.first; base < w.nseg; base += w.stride) {
@@ -1063,6 +1069,7 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
 // one thread per row: exclusive prefix over the shard's tiles (in place),
 // the shard's total and its last tile holding a present cell
 __global__ __launch_bounds__(256) void k_quirk_prefix(GhDev d, GhRound p) {
+  if (p.qgate && d.nflag[p.qcur] == 0) return;  // no candidate in the table
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n) return;
   const int64_t ntiles = p.ld / d.tw;
@@ -1098,6 +1105,7 @@ __global__ __launch_bounds__(256) void k_quirk_carry(GhDev d, GhRound p) {
 // clears the flag of every candidate the reference's loop skips
 template <int TW>
 __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur, GhRound p) {
+  if (p.qgate && d.nflag[p.qcur] == 0) return;  // no candidate in the table
   constexpr int SEG = SegWalk<TW>::SEG;
   const SegWalk<TW> w(p);
   for (int64_t base = w.first; base < w.nseg; base += w.stride) {
