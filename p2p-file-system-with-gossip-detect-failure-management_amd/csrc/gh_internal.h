@@ -342,6 +342,7 @@ struct GhRound {
   int32_t exact;      // T_fail or T_cleanup >= GH_AGE_CAP: every cell by the slow rule (exact ts)
   int32_t qgate;      // quirk pre-pass: 1 = return at once when nflag[qcur] == 0 (no candidate anywhere)
   int32_t qcur;       // the buffer the pre-pass rewrites
+  int32_t force_storm;  // diagnostics (GH_FORCE_STORM): run the storm variant every round
 };
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------

@@ -47,6 +47,7 @@ struct Engine {
   bool nt = true;        // k_round non-temporal streams (gh_set_round_variant)
   int xmap = 1;          // k_round XCD-aware tile map (gh_set_round_variant)
   int tpw = 1;           // k_round tiles per workgroup (GH_ROUND_TPW)
+  int force_storm = 0;   // storm variant every round (GH_FORCE_STORM, diagnostics)
   bool timing = false;
   // the current table may hold flags no round kernel counted (import, fill,
   // events, list merges): the next quirk pre-pass runs ungated
@@ -125,6 +126,7 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.peer_mode = e->cfg.peer_mode;
   p.xmap = e->xmap;
   p.tpw = e->tpw;
+  p.force_storm = e->force_storm;
   p.exact = e->cfg.t_fail >= GH_AGE_CAP || e->cfg.t_cleanup >= GH_AGE_CAP;
   return p;
 }
@@ -337,6 +339,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_ROUND_XMAP")) e->xmap = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_ROUND_TPW")) e->tpw = std::atoi(v);
+  if (const char* v = std::getenv("GH_FORCE_STORM")) e->force_storm = std::atoi(v) != 0;
   if (tw != 8 && tw != 16 && tw != 32 && tw != 64 && tw != 128 && tw != 256) {
     delete e;
     return GH_EINVAL;

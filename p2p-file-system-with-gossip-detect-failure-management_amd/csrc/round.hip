@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void k_ring_tiles(GhDev d, int cur, int dcur, 
     const int i = valid ? (int)(sid - t * p.n) : 0;
     const int64_t l0 = t * TW + w.lc * 8;
     int cnt = 0;
-    if (valid) {
+    if (valid && d.alive[i] && d.active[i]) {  // only sending rows' counts are read
       const uint32_t pf = gh_pf8(d, cur, i, l0);
       const uint32_t rm = removed8(d, dcur, l0, i);
       cnt = __builtin_popcount(pf & ~(pf >> 8) & ~rm & 0xFFu);  // present, not flagged, not REMOVE'd
@@ -304,14 +304,25 @@ __global__ __launch_bounds__(256) void k_inbox_count(GhDev d, GhRound p) {
   }
 }
 
-// Exclusive scan of inbox_cnt -> inbox_beg; one 1024-thread workgroup.
+// Exclusive scan of inbox_cnt -> inbox_beg; one 1024-thread workgroup. Each
+// thread owns a run of a multiple of 4 counters, read and written as int4
+// (the arrays are 16-B aligned), so its loads are independent of each other.
 __global__ __launch_bounds__(1024) void k_inbox_scan(GhDev d, GhRound p) {
   __shared__ int s_sum[1024];
   const int tid = threadIdx.x;
-  const int per = (p.n + 1023) / 1024;
+  const int per = ((p.n + 1023) / 1024 + 3) & ~3;
   const int b = min(p.n, tid * per), e = min(p.n, b + per);
+  const bool vec = e - b == per;
   int acc = 0;
-  for (int x = b; x < e; ++x) acc += d.inbox_cnt[x];
+  if (vec) {
+#pragma unroll 4
+    for (int x = b; x < e; x += 4) {
+      const int4 v = *reinterpret_cast<const int4*>(d.inbox_cnt + x);
+      acc += v.x + v.y + v.z + v.w;
+    }
+  } else {
+    for (int x = b; x < e; ++x) acc += d.inbox_cnt[x];
+  }
   s_sum[tid] = acc;
   __syncthreads();
   for (int off = 1; off < 1024; off <<= 1) {
@@ -321,10 +332,25 @@ __global__ __launch_bounds__(1024) void k_inbox_scan(GhDev d, GhRound p) {
     __syncthreads();
   }
   int run = tid ? s_sum[tid - 1] : 0;
-  for (int x = b; x < e; ++x) {
-    d.inbox_beg[x] = run;
-    d.inbox_fill[x] = 0;
-    run += d.inbox_cnt[x];
+  if (vec) {
+#pragma unroll 4
+    for (int x = b; x < e; x += 4) {
+      const int4 v = *reinterpret_cast<const int4*>(d.inbox_cnt + x);
+      int4 o;
+      o.x = run;
+      o.y = o.x + v.x;
+      o.z = o.y + v.y;
+      o.w = o.z + v.z;
+      run = o.w + v.w;
+      *reinterpret_cast<int4*>(d.inbox_beg + x) = o;
+      *reinterpret_cast<int4*>(d.inbox_fill + x) = int4{0, 0, 0, 0};
+    }
+  } else {
+    for (int x = b; x < e; ++x) {
+      d.inbox_beg[x] = run;
+      d.inbox_fill[x] = 0;
+      run += d.inbox_cnt[x];
+    }
   }
 }
 
@@ -401,7 +427,7 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
     // guard rows); flags are set one round ahead, so a detection wave is
     // seen the round before it happens
     const int64_t measure = (int64_t)*d.nstorm + *d.slow_n;
-    *d.mode = measure * 32 > d.ntiles * (int64_t)d.n;
+    *d.mode = p.force_storm || measure * 32 > d.ntiles * (int64_t)d.n;
     *d.slow_n = 0;
     *d.nstorm = 0;
     d.nflag[cur ^ 1] = 0;  // counted by this round's writers
@@ -502,18 +528,40 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 
   if (tid == 0) s_merged = s_det = s_rel = s_storm = s_tomb = s_unk = 0;
   const bool pull = p.peer_mode == GH_PEER_PULL;
-  for (int t = tid; t < RB * KB; t += 256) {
-    const int row = t / KB, q = t - row * KB;
-    const int i = rb * RB + row;
-    int meta = 0, sv = 0;
-    if (i < p.n) {
-      const int al = d.alive[i];
-      const int cnt = al ? gh_in_cnt(d, pull, p.k, i) : 0;
-      meta = al | (d.active[i] << 1) | (cnt << 2);
-      if (q < cnt) sv = d.inbox[gh_in_beg(d, pull, p.k, i) + q];
+  if constexpr (STORM) {
+    // row metadata once per row, then only the inbox slots in use (storms
+    // and guard rows have few senders)
+    for (int row = tid; row < RB; row += 256) {
+      const int i = rb * RB + row;
+      int meta = 0;
+      if (i < p.n) {
+        const int al = d.alive[i];
+        const int cnt = al ? gh_in_cnt(d, pull, p.k, i) : 0;
+        meta = al | (d.active[i] << 1) | (cnt << 2);
+      }
+      s_meta[row] = meta;
     }
-    if (q == 0) s_meta[row] = meta;
-    s_inb[t] = sv;
+    __syncthreads();
+    for (int t = tid; t < RB * KB; t += 256) {
+      const int row = t / KB, q = t - row * KB;
+      const int i = rb * RB + row;
+      if (q < (s_meta[row] >> 2)) s_inb[t] = d.inbox[gh_in_beg(d, pull, p.k, i) + q];
+    }
+  } else {
+    // one pass, no barrier in between: healthy rounds use every slot
+    for (int t = tid; t < RB * KB; t += 256) {
+      const int row = t / KB, q = t - row * KB;
+      const int i = rb * RB + row;
+      int meta = 0, sv = 0;
+      if (i < p.n) {
+        const int al = d.alive[i];
+        const int cnt = al ? gh_in_cnt(d, pull, p.k, i) : 0;
+        meta = al | (d.active[i] << 1) | (cnt << 2);
+        if (q < cnt) sv = d.inbox[gh_in_beg(d, pull, p.k, i) + q];
+      }
+      if (q == 0) s_meta[row] = meta;
+      s_inb[t] = sv;
+    }
   }
   __syncthreads();
 
@@ -525,7 +573,6 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   uint32_t n_mrg16 = 0;  // merges x 16
   int n_det = 0, n_rel = 0;
   int n_tomb = 0, n_unk = 0;  // REMOVE: tombstoned / unknown member
-  int wflag = 0;              // wrote a flagged cell (quirk pre-pass gate)
   int32_t* __restrict__ tsb = d.ts;
 
 #pragma unroll 1
@@ -607,7 +654,16 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         if constexpr (RPW == 1) s = uni(s);
       }
       ps[q] = s;
-      pv[q] = ldn<false>(hno + tb + (int64_t)s * TW);
+      if constexpr (STORM) {
+        // storms hold few senders (guard rows none): load only the used
+        // slots, the rest are absent (-1, a no-op under the max)
+        if (q < cntv)
+          pv[q] = ldn<false>(hno + tb + (int64_t)s * TW);
+        else
+          pv[q] = v4u{~0u, ~0u, ~0u, ~0u};
+      } else {
+        pv[q] = ldn<false>(hno + tb + (int64_t)s * TW);
+      }
     }
     bad |= (w[0] & 0xFFFFu) == GH_N_WIDE;  // own segment wide
 #pragma unroll
@@ -727,7 +783,6 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     if (al) {
       if (seg_ok) {
         stn<NT>(hnn + off, o);
-        wflag |= fo != 0;
         dpres = dp16 >> 4;
         n_mrg16 += mcnt;
         if constexpr (STORM) {
@@ -784,9 +839,11 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   if (n_rel) atomicAdd(&s_rel, (unsigned long long)n_rel);
   if (n_tomb) atomicAdd(&s_tomb, (unsigned long long)n_tomb);
   if (n_unk) atomicAdd(&s_unk, (unsigned long long)n_unk);
-  wflag = __syncthreads_or(wflag);
+  __syncthreads();
   if (tid == 0) {
-    if (wflag) atomicAdd(&d.nflag[cur ^ 1], 1);
+    // s_storm counts every written segment with a flagged cell (lean: only
+    // those): the quirk pre-pass gate
+    if (s_storm) atomicAdd(&d.nflag[cur ^ 1], 1);
     if (s_merged) atomicAdd(&d.stats[ST_MERGED], s_merged);
     if (s_det) atomicAdd(&d.stats[ST_DETECTIONS], s_det);
     if (s_rel) atomicAdd(&d.stats[ST_RELEASED], s_rel);
