@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=2048, help="observer rows in the CPU sample")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--files", type=int, default=1 << 20,
+                    help="placement leg (SURVEY.md §8d C5 files, after the timed rounds; 0 = skip)")
     return ap.parse_args()
 
 
@@ -126,6 +128,59 @@ def cpu_baseline(n, fanout, seed, rows, seconds, threads, t_fail):
     }
 
 
+def placement_leg(gs, eng, n, files, t_fail):
+    """SURVEY.md §8d placement figure, on the benched cluster after its timed
+    rounds (outside them): put `files` files through gh_put (Init_replica /
+    Handle_put_request, master/master.go:129-175), crash 1% of the members,
+    run the rounds until they are detected and REMOVE'd, then one repair pass
+    gh_repair (Update_metadata, master/master.go:74-127) from the master's
+    view. Host-buffer calls: the times include the PCIe copies of the file
+    ids, replicas and plan."""
+    import ctypes as C
+    import numpy as np
+    f = np.arange(files, dtype=np.int32)
+    eng.sync()
+    t0 = time.perf_counter()
+    rep, ver, st = eng.put(f)
+    t_put = time.perf_counter() - t0
+    rng = np.random.default_rng(0x5EED0005)
+    crashed = rng.choice(np.arange(1, n), size=max(1, n // 100), replace=False)
+    eng.apply_events([(gs.GH_EV_CRASH, int(c)) for c in crashed])
+    # rounds until the detections stop (the last round's REMOVE is applied
+    # in the round that reports none)
+    rounds, det = 0, 0
+    while rounds < 4 * t_fail + 8:
+        d = eng.step(1)["detections"]
+        rounds += 1
+        if d == 0 and det:
+            break
+        det += d
+    cap = files
+    plan = (gs.PlanEntry * cap)()
+    nout = C.c_int64()
+    eng.sync()
+    t0 = time.perf_counter()
+    rc = eng.lib.gh_repair(eng.h, 0, plan, cap, C.byref(nout))
+    t_rep = time.perf_counter() - t0
+    if rc not in (gs.GH_OK, gs.GH_EPLACEMENT_STARVED):
+        raise RuntimeError(f"gh_repair: {rc}")
+    hit = np.isin(rep, crashed).any(axis=1)
+    return {
+        "files": files,
+        "put_files_per_s": files / t_put,
+        "put_ms": t_put * 1e3,
+        "crashed_members": int(len(crashed)),
+        "detections": int(det),
+        "rounds_to_detection_and_remove": rounds,
+        "files_with_crashed_replica": int(hit.sum()),
+        "repair_plan_entries": int(min(nout.value, cap)),
+        "repair_ms": t_rep * 1e3,
+        "repair_files_per_s": files / t_rep,
+        "replaced_files_per_s": int(min(nout.value, cap)) / t_rep,
+        "note": "host-buffer C-ABI calls (PCIe copies included); files checked per second = files / repair time",
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,6 +191,7 @@ def main():
 
     n, k = args.n, args.fanout
     cfg = gs.default_config(n, fanout=k, seed=args.seed, device=local, t_fail=args.t_fail, t_cleanup=args.t_fail,
+                            max_files=args.files if world == 1 else 0,
                             peer_mode=gs.GH_PEER_RING if args.peer_mode == "ring" else gs.GH_PEER_PULL,
                             detect_mode=gs.GH_DETECT_QUIRK if args.detect == "quirk" else gs.GH_DETECT_CANONICAL)
     if world > 1:
@@ -171,6 +227,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms, launches = eng.read_timing()
+    eng.set_timing(False)
+    placement = None
+    if world == 1 and args.files > 0:
+        placement = placement_leg(gs, eng, n, args.files, args.t_fail)
     eng.close()
 
     if rank != 0:
@@ -224,6 +284,7 @@ def main():
             "traffic_frac": traffic["traffic_bytes"] / avg_s / 1e9 / HBM_PEAK_GBS if traffic else None,
         },
         "cpu_baseline": None,
+        "placement": placement,
     }
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(n, k, args.seed, args.cpu_rows, args.cpu_seconds, args.cpu_threads,
