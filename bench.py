@@ -92,12 +92,10 @@ def pmc_traffic(n, k, world):
     return best
 
 
-def cpu_baseline(n, fanout, seed, rows, seconds, threads, t_fail):
-    """Time the C oracle (same semantics) on `rows` observer rows of an
-    N-column table; peers are drawn among the sampled rows."""
+def cpu_rate(n, fanout, seed, rows, seconds, threads, t_fail):
+    """Whole-cluster rounds/s of the C oracle on `rows` observer rows of an
+    N-column table (peers drawn among the sampled rows), scaled by rows/N."""
     from oracle import oracle as om
-    om.build()
-    threads = threads or min(16, os.cpu_count() or 1)
     cfg = om.default_config(n, fanout=fanout, seed=seed, t_fail=t_fail, t_cleanup=t_fail)
     o = om.Oracle(cfg, rows=rows, threads=threads)
     o.init_full(2, 0, 0)
@@ -110,8 +108,20 @@ def cpu_baseline(n, fanout, seed, rows, seconds, threads, t_fail):
         if el >= seconds or done >= 50:
             break
     o.close()
-    per_round_sample = el / done
-    rounds_per_s = (rows / n) / per_round_sample
+    return (rows / n) / (el / done), done, el
+
+
+def cpu_baseline(n, fanout, seed, rows, seconds, threads, t_fail):
+    """Time the C oracle (same semantics) on `rows` observer rows of an
+    N-column table; peers are drawn among the sampled rows. Also one core on
+    the same sample (the parallel run plus a 1-core run)."""
+    from oracle import oracle as om
+    om.build()
+    threads = threads or min(16, os.cpu_count() or 1)
+    rows_per_s, done, el = cpu_rate(n, fanout, seed, rows, seconds, threads, t_fail)
+    rows1 = rows
+    one, done1, el1 = cpu_rate(n, fanout, seed, rows1, seconds / 2, 1, t_fail)
+    rounds_per_s = rows_per_s
     cpu = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -125,6 +135,8 @@ def cpu_baseline(n, fanout, seed, rows, seconds, threads, t_fail):
         "sample": f"oracle/tablesim.c (OpenMP, {threads} threads) on {rows} of {n} observer rows x {n} columns, "
                   f"k={fanout} peers drawn among the sampled rows, {done} rounds in {el:.1f} s, scaled by "
                   f"rows/N to whole-cluster rounds/s; host CPU: {cpu}",
+        "value_1core": one,
+        "sample_1core": f"the same on 1 thread, {rows1} observer rows, {done1} rounds in {el1:.1f} s",
     }
 
 

@@ -143,7 +143,7 @@ struct GhDev {
   int32_t *nflag;   // [2]: segments written into buffer b holding flagged cells (quirk pre-pass gate)
   int32_t *ts;
   uint8_t *alive, *active, *det_any, *und;
-  int32_t *cntl, *cntg;  // [n + 8]: per-row present counts (local / allreduced), [n] = |D|
+  int32_t *cntl, *cntg;  // [n + 8]: per-row present counts (local / allreduced), [n] = |D|, [n + 1] = nflag[cur]
   int32_t *post;         // [n]: post-REMOVE present counts of undecided rows (allreduced)
   int32_t *det_cnt[2], *det_min[2];
   uint32_t *dbits;
@@ -340,8 +340,7 @@ struct GhRound {
   int32_t xmap;       // k_round block->tile map: 0 tile-major, 1 XCD-aware
   int32_t tpw;        // k_round tiles per workgroup (1, 2, 4, 8)
   int32_t exact;      // T_fail or T_cleanup >= GH_AGE_CAP: every cell by the slow rule (exact ts)
-  int32_t qgate;      // quirk pre-pass: 1 = return at once when nflag[qcur] == 0 (no candidate anywhere)
-  int32_t qcur;       // the buffer the pre-pass rewrites
+  int32_t qgate;      // quirk pre-pass: 1 = return at once when cntg[n + 1] (flagged segments, all shards) is 0
   int32_t force_storm;  // diagnostics (GH_FORCE_STORM): run the storm variant every round
 };
 

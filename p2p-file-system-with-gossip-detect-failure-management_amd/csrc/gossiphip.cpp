@@ -455,7 +455,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
 int decide_active(Engine* e, const GhRound& p) {
   GhDev& d = e->d;
   int rc;
-  if ((rc = allreduce_i32(e, d.cntl, d.cntg, (size_t)e->n + 1))) return rc;
+  if ((rc = allreduce_i32(e, d.cntl, d.cntg, (size_t)e->n + 2))) return rc;
   launch_active_pre(d, e->cur, e->dcur, p, e->stream);
   HIPCHK(e, hipGetLastError());
   if (e->world > 1 && (rc = allreduce_i32(e, d.post, d.post, (size_t)e->n))) return rc;
@@ -716,12 +716,11 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     launch_base(e->d, e->cur, e->dcur, p, e->stream);
     if ((rc = decide_active(e, p))) return rc;
     if (e->cfg.detect_mode == GH_DETECT_QUIRK) {
-      // single shard: skip the pre-pass when the table holds no flag (the
-      // round kernels count flagged segments as they write); shards always
-      // run it, their summaries feed the other shards' carries
+      // skip the pre-pass when no shard's table holds a flag (the round
+      // kernels count flagged segments as they write; the counts are summed
+      // by decide_active's allreduce, so every shard takes the same branch)
       GhRound pq = p;
-      pq.qgate = e->world == 1 && !e->qforce;
-      pq.qcur = e->cur;
+      pq.qgate = !e->qforce;
       if ((rc = quirk_flags(e, pq))) return rc;
       e->qforce = false;
     }

@@ -432,6 +432,7 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
     *d.nstorm = 0;
     d.nflag[cur ^ 1] = 0;  // counted by this round's writers
     d.cntl[d.n] = d.nd[dcur];  // |D_{r-1}| of this shard next to the local counts, for one allreduce
+    d.cntl[d.n + 1] = d.nflag[cur];  // flagged segments of this shard's table (quirk gate, summed)
   }
   if (c >= p.ld) return;
   int32_t b = d.base[cur][c];
@@ -1100,7 +1101,7 @@ __device__ __forceinline__ int q_summary8(uint32_t P, uint32_t F) {
 // the SEG lanes, last lane holds the whole tile)
 template <int TW>
 __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, GhRound p) {
-  if (p.qgate && d.nflag[p.qcur] == 0) return;  // no candidate in the table
+  if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no candidate in any shard's table
   constexpr int SEG = SegWalk<TW>::SEG;
   const SegWalk<TW> w(p);
   for (int64_t base = w.first; base < w.nseg; base += w.stride) {
@@ -1126,7 +1127,7 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
 // one thread per row: exclusive prefix over the shard's tiles (in place),
 // the shard's total and its last tile holding a present cell
 __global__ __launch_bounds__(256) void k_quirk_prefix(GhDev d, GhRound p) {
-  if (p.qgate && d.nflag[p.qcur] == 0) return;  // no candidate in the table
+  if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no candidate in any shard's table
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n) return;
   const int64_t ntiles = p.ld / d.tw;
@@ -1162,7 +1163,7 @@ __global__ __launch_bounds__(256) void k_quirk_carry(GhDev d, GhRound p) {
 // clears the flag of every candidate the reference's loop skips
 template <int TW>
 __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur, GhRound p) {
-  if (p.qgate && d.nflag[p.qcur] == 0) return;  // no candidate in the table
+  if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no candidate in any shard's table
   constexpr int SEG = SegWalk<TW>::SEG;
   const SegWalk<TW> w(p);
   for (int64_t base = w.first; base < w.nseg; base += w.stride) {
