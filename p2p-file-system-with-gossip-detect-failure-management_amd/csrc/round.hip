@@ -646,7 +646,12 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     v4u pv[KB];
     int ps[KB];
     const bool act = (meta >> 1) & 1;  // else the row is under the <4 guard (step 2)
-    bool bad = (!STORM && !act) || cntv > KB;
+    // guard rows in the lean variant: the 8-slot instantiation (ring
+    // inboxes, pull k > 4) takes them, so a collapsed cluster runs lean; the
+    // 4-slot one lists them (the stamp select cost 4% of the healthy pull
+    // round, measured A/B on one box)
+    constexpr bool LEAN_GUARD = KB > 4;
+    bool bad = (!STORM && !LEAN_GUARD && !act) || cntv > KB;
 #pragma unroll
     for (int q = 0; q < KB; ++q) {
       int s = i;
@@ -725,6 +730,8 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         acc |= (pk_add_u16(x, 0x00010001u) & 0x80008000u) | ((((x & 0x001F001Fu) + 0x00020002u) & ~hx) & 0x00200020u);
         mm = pk_sra15(pk_subs_i16(x | 0x001F001Fu, m));     // merged: a sender's heartbeat is larger
         y0 = pk_adds_u16(x, 0x00010001u);                   // not merged: age + 1 (absent stays)
+        // a guard row (step 2, :504-509) stamps its present cells: age 1
+        if (LEAN_GUARD && !act) y0 = (((x & 0x7FE07FE0u) | 0x00010001u) & ~hx) | (x & hx);
         pre = ~hx;
       } else {
         // cell classes: (x | 31) + 1 is 0 for a tombstone or absent cell, has
@@ -754,7 +761,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         const uint32_t yact = pk_adds_u16(xr | (fl & 0xFFE0FFE0u), 0x00010001u) | rel;
         y0 = (((xr & 0x7FE07FE0u) | 0x00010001u) & nowm) | (yact & ~nowm);
         pre = ~ta0;
-        stb |= ((fl0 | ta) & ~ab) | ~actm;                     // what the lean variant lists
+        stb |= ((fl0 | ta) & ~ab) | (LEAN_GUARD ? 0u : ~actm);  // what the lean variant lists
         detb |= pair_bits(fl, j);
         relb |= pair_bits(rel & ~ab, j);
       }
