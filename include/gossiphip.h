@@ -183,6 +183,30 @@ int gh_get_files(void* h, const int32_t* files, int64_t n, int32_t* replicas,
 int gh_delete_files(void* h, const int32_t* files, int64_t n,
                     int32_t* old_replicas);
 
+/* ---- master re-election (SPEC §9; slave/slave.go:930-1051) ------------- */
+/* The master check at the end of updateMemberList (slave/slave.go:451-457)
+ * and revote_master's target (:930-948), for every row of the current table:
+ * list_len[i] = len(MemberList_i); has_master[i] = 1 if member mview[i] (row
+ * i's own idea of the master, self.master) is in row i's list; first[i] =
+ * MemberList_i[0], the lowest present member id (SPEC D1), -1 for an empty
+ * list. mview: [N] member ids. Outputs: [N] each; any output may be NULL.
+ * The vote tally (Receive_vote :968-984, RPC TCPServer.Vote
+ * server/server.go:231) is per-candidate control flow and stays on the host
+ * (gossipsim.Cluster). */
+int gh_vote_scan(void* h, const int32_t* mview, int32_t* first, int32_t* list_len,
+                 uint8_t* has_master);
+/* rebuild_file_meta (slave/slave.go:986-1043) run by the newly elected
+ * master M: the file table is rebuilt from the members' local stores as the
+ * reference reads them (M's own, and MemberList_M[0]'s for every other member,
+ * :994), Node_list = the first 4 entries in ascending-version order, Version
+ * = the first entry's, Timestamp = the current tick; files in no store read
+ * are dropped. M becomes the engine's master row (placement candidates,
+ * gh_put/gh_repair). *f0 = MemberList_M[0] (the member that receives
+ * Assign_new_master, :1000 / server/server.go:236), may be NULL;
+ * *n_files = files left in the table, may be NULL. GH_EINVAL if M's list is
+ * empty. */
+int gh_rebuild_meta(void* h, int32_t new_master, int32_t* f0, int64_t* n_files);
+
 /* ---- multi-GPU: one cluster column-sharded over G ranks ----------------
  * Rank g holds all N observer rows for member columns [g*ncs, g*ncs+ncol)
  * (ncs = roundup(ceil(N/G), 32)) of hb (x2) and ts: 12*N*ncs bytes of HBM.

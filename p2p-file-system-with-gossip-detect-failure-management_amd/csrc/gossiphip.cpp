@@ -976,6 +976,62 @@ int gh_delete_files(void* h, const int32_t* files, int64_t n, int32_t* old_repli
   return get_or_delete(e, files, n, old_replicas, nullptr, 1);
 }
 
+// SPEC §9: the per-row half of the election on the device; the tally is the
+// host's (gossipsim.Cluster), as Receive_vote is per-candidate control flow.
+int gh_vote_scan(void* h, const int32_t* mview, int32_t* first, int32_t* list_len, uint8_t* has_master) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || !mview) return GH_EINVAL;
+  const int32_t n = e->n;
+  for (int32_t i = 0; i < n; ++i)
+    if (mview[i] < 0 || mview[i] >= n) return set_err(e, GH_EINVAL, "mview: member id out of range");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  Staging st;
+  int rc;
+  if ((rc = st.alloc(e, sizeof(int32_t) * 4 * (size_t)n))) return rc;
+  int32_t* mv = st.as<int32_t>();
+  int32_t* out = mv + n;       // [2n]: MAX-reduced first / has_master
+  int32_t* len = out + 2 * n;  // [n]: SUM-reduced list lengths
+  HIPCHK(e, hipMemcpyAsync(mv, mview, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
+  launch_vote_scan(e->d, e->cur, mv, out, e->stream);
+  HIPCHK(e, hipGetLastError());
+  COMMCHK(e, e->comm->allreduce(out, out, 2 * (size_t)n, GH_DT_I32, GH_OP_MAX, e->stream));
+  if ((rc = allreduce_i32(e, e->d.cntl, len, (size_t)n))) return rc;
+  std::vector<int32_t> host(3 * (size_t)n);
+  HIPCHK(e, hipMemcpyAsync(host.data(), out, sizeof(int32_t) * 3 * n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  for (int32_t i = 0; i < n; ++i) {
+    if (first) first[i] = host[i] > 0 ? n - host[i] : -1;
+    if (has_master) has_master[i] = (uint8_t)host[n + i];
+    if (list_len) list_len[i] = host[2 * (size_t)n + i];
+  }
+  return GH_OK;
+}
+
+int gh_rebuild_meta(void* h, int32_t new_master, int32_t* f0, int64_t* n_files) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  if (new_master < 0 || new_master >= e->n) return set_err(e, GH_EINVAL, "new_master");
+  if (e->d.fcap <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
+  // the first 5 members of M's list (ID order); 5 covers "first 4 other than M"
+  std::vector<int32_t> ids(e->n);
+  int64_t nl = 0;
+  int rc = gh_lsm(h, new_master, ids.data(), nullptr, nullptr, e->n, &nl);
+  if (rc != GH_OK) return rc;
+  if (nl == 0) return set_err(e, GH_EINVAL, "new master's list is empty");
+  int32_t L[5] = {-1, -1, -1, -1, -1};
+  const int32_t k = (int32_t)std::min<int64_t>(nl, 5);
+  for (int32_t q = 0; q < k; ++q) L[q] = ids[q];
+  launch_rebuild(e->d, e->cfg.replicas, new_master, L, k, e->round, e->stream);
+  HIPCHK(e, hipGetLastError());
+  std::vector<int32_t> ver(e->d.fcap);
+  HIPCHK(e, hipMemcpyAsync(ver.data(), e->d.ver, sizeof(int32_t) * e->d.fcap, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  e->cfg.master = new_master;
+  if (f0) *f0 = L[0];
+  if (n_files) *n_files = std::count_if(ver.begin(), ver.end(), [](int32_t v) { return v >= 0; });
+  return GH_OK;
+}
+
 int gh_set_round_variant(void* h, int32_t nontemporal, int32_t xcd_map) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;

@@ -234,6 +234,27 @@ class Engine:
         self._chk(self.lib.gh_delete_files(self.h, _p(f), len(f), _p(rep)))
         return rep
 
+    # ---- master re-election (SPEC §9) -------------------------------------
+    def vote_scan(self, mview):
+        """Per row: MemberList[0] (-1 if empty), len(MemberList), and whether
+        the row's master mview[i] is in its list (slave/slave.go:451-457,
+        930-948)."""
+        mv = np.ascontiguousarray(mview, dtype=np.int32)
+        first = np.empty(self.n, np.int32)
+        ln = np.empty(self.n, np.int32)
+        has = np.empty(self.n, np.uint8)
+        self._chk(self.lib.gh_vote_scan(self.h, _p(mv), _p(first), _p(ln), _p(has)))
+        return first, ln, has
+
+    def rebuild_meta(self, new_master):
+        """rebuild_file_meta (slave/slave.go:986-1043) at `new_master`, which
+        becomes the master row. Returns (f0 = the member that gets
+        Assign_new_master, files left)."""
+        f0 = C.c_int32()
+        nf = C.c_int64()
+        self._chk(self.lib.gh_rebuild_meta(self.h, int(new_master), C.byref(f0), C.byref(nf)))
+        return f0.value, nf.value
+
     # ---- tuning / timing -------------------------------------------------
     def set_round_variant(self, nontemporal=True, xcd_map=False):
         self._chk(self.lib.gh_set_round_variant(self.h, int(nontemporal), int(xcd_map)))
@@ -320,10 +341,23 @@ class Cluster:
     a failure in round r triggers Update_metadata with its own list as
     `available` at round r + repair_delay (slave/slave.go:1122-1133)."""
 
-    def __init__(self, n, repair_delay=8, addresses=None, **cfg_kw):
+    def __init__(self, n, repair_delay=8, addresses=None, elect=False, **cfg_kw):
         self.engine = Engine(default_config(n, **cfg_kw))
         self.n = n
         self.repair_delay = repair_delay
+        # master re-election (SPEC §9, slave/slave.go:930-1051), when `elect`:
+        # each member's self.master, VoteStatus, the pending rebuilds and the
+        # members whose process is gone (crash; log.Fatal)
+        self.elect = elect
+        self.master = int(self.engine.cfg.master)
+        self.mview = np.full(n, self.master, np.int32)
+        self.vote_on = np.zeros(n, bool)
+        self.vote_num = np.zeros(n, np.int64)
+        self.voters: list[set] = [set() for _ in range(n)]
+        self.rebuilds: dict[int, list[int]] = {}
+        self.dead: set[int] = set()
+        self.elections: list[tuple[int, int]] = []  # (round, new master)
+        self.fatal: list[tuple[int, int, str]] = []  # (round, member, why)
         # member id <-> address (the reference's identity, slave/slave.go:145-159)
         self.addresses = list(addresses) if addresses is not None else [f"10.0.{i >> 8}.{i & 255}" for i in range(n)]
         self.ids = {a: i for i, a in enumerate(self.addresses)}
@@ -339,6 +373,7 @@ class Cluster:
 
     def crash(self, member):
         self.engine.apply_events([(GH_EV_CRASH, member)])
+        self.dead.add(int(member))
 
     def lsm(self, member):
         ids, hb, ts = self.engine.lsm(member)
@@ -441,7 +476,71 @@ class Cluster:
             r = self.engine.round
             if st["detections"]:
                 self.scheduled.setdefault(r + self.repair_delay, []).extend(self.engine.read_detectors().tolist())
+            if self.elect:
+                self._election_step(r)
             for obs in self.scheduled.pop(r, []):
+                if self.elect:
+                    if obs in self.dead:
+                        continue
+                    if self.mview[obs] in self.dead:  # Fail_recover dials a dead master (:1125-1127)
+                        self._fatal(r, obs, "Fail_recover: master unreachable")
+                        continue
+                    if self.mview[obs] != self.master:
+                        continue  # a stale but running master: its own (empty) metadata, not modelled
                 if self.engine.cfg.max_files > 0:
                     self.plans.append((r, obs, tuple(self.engine.repair(obs))))
         return total
+
+    # ---- master re-election (SPEC §9) -----------------------------------
+    def _touch(self, x):  # `if self.VoteStatus.Vote == false {...}` (slave/slave.go:931-935, 969-973)
+        if not self.vote_on[x]:
+            self.vote_on[x] = True
+            self.vote_num[x] = 0
+            self.voters[x] = set()
+
+    def _fatal(self, r, member, why):
+        """log.Fatal ends the member's process: a crash."""
+        self.fatal.append((r, int(member), why))
+        self.crash(member)
+
+    def _election_step(self, r):
+        """After round r: every running row whose master left its list calls
+        revote_master (slave/slave.go:451-457, 930-948); the votes are
+        Receive_vote'd in ID order (:968-984); an elected member rebuilds the
+        metadata two rounds later (:987, `time.Sleep(HEARTBEAT_PERIOD * 2)`)."""
+        for m in self.rebuilds.pop(r, []):
+            if m in self.dead:
+                continue
+            ids, _, _ = self.engine.lsm(m)
+            f0 = int(ids[0]) if len(ids) else m
+            if f0 != m and f0 in self.dead:  # rpc.Dial to MemberList[0] fails (:996-999)
+                self._fatal(r, m, "rebuild_file_meta: MemberList[0] unreachable")
+                continue
+            if self.engine.cfg.max_files > 0:
+                f0, _ = self.engine.rebuild_meta(m)
+            self.master = m
+            self.mview[f0] = m  # Assign_New_Master (:1045-1048)
+            self.vote_on[f0] = False
+            self.vote_on[m] = False  # :1039-1040
+            self.voters[m] = set()
+            self.scheduled.setdefault(r + self.repair_delay, []).append(m)  # go Fail_recover (:1042)
+        first, ln, has = self.engine.vote_scan(self.mview)
+        alive = self.engine.alive()
+        run = (alive != 0) & (ln >= self.engine.cfg.min_members) & (has == 0)
+        for i in np.flatnonzero(run).tolist():
+            t = int(first[i])
+            self._touch(i)
+            if t == i:  # self vote: counted, no majority check (:936-939)
+                self.vote_num[i] += 1
+                continue
+            if t in self.dead:  # rpc.Dial to MemberList[0] fails (:941-944)
+                self._fatal(r, i, "revote_master: MemberList[0] unreachable")
+                continue
+            self._touch(t)
+            if i not in self.voters[t]:
+                self.voters[t].add(i)
+                self.vote_num[t] += 1
+            if self.mview[t] != t and self.vote_num[t] > ln[t] // 2:
+                self.mview[t] = t
+                self.elections.append((r, t))
+                self.rebuilds.setdefault(r + 2, []).append(t)

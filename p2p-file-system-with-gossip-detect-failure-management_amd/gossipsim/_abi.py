@@ -83,6 +83,8 @@ SYMBOLS = [
     ("gh_repair", C.c_int, [_vp, _i32, _P(PlanEntry), _i64, _P(_i64)]),
     ("gh_get_files", C.c_int, [_vp, _vp, _i64, _vp, _vp]),
     ("gh_delete_files", C.c_int, [_vp, _vp, _i64, _vp]),
+    ("gh_vote_scan", C.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    ("gh_rebuild_meta", C.c_int, [_vp, _i32, _P(_i32), _P(_i64)]),
     ("gh_set_round_variant", C.c_int, [_vp, _i32, _i32]),
     ("gh_set_timing", C.c_int, [_vp, _i32]),
     ("gh_read_timing", C.c_int, [_vp, _P(C.c_double), _P(_i64)]),

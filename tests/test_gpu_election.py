@@ -1,0 +1,150 @@
+"""Master re-election on the GPU (SPEC §9): gh_vote_scan and
+gh_rebuild_meta against oracle/election.py on the oracle's tables, single and
+sharded, and gossipsim.Cluster's election against the oracle Tally round by
+round (slave/slave.go:451-457, 930-1051)."""
+import numpy as np
+import pytest
+
+import scenarios as sc
+from oracle import election as el
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gs():
+    import gossipsim
+    return gossipsim
+
+
+def _scan_check(eng, hb, rng, n):
+    for mv in (np.zeros(n, np.int32), rng.integers(0, n, n).astype(np.int32)):
+        got = eng.vote_scan(mv)
+        exp = el.vote_scan(hb, mv)
+        for g, e, name in zip(got, exp, ("first", "list_len", "has_master")):
+            np.testing.assert_array_equal(g, e, err_msg=name)
+
+
+@pytest.mark.parametrize("peer_mode", [0, 1])
+def test_vote_scan_churn(gs, oracle_mod, peer_mode):
+    """Seeded churn at N=300 (crashes, leaves, joins; tombstones and empty
+    rows), the scan checked every 3 rounds against the oracle's table."""
+    n, rounds = 300, 30
+    cfg = dict(peer_mode=peer_mode, t_fail=3, t_cleanup=3, seed=0x5EED0F31)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg))
+    sched = sc.random_churn(n, rounds, seed=31)
+    rng = np.random.default_rng(7)
+    _scan_check(eng, orc.export_state()[0], rng, n)  # empty table: first = -1
+    for r in range(1, rounds + 1):
+        ev = sched.get(r, [])
+        if ev:
+            eng.apply_events(ev)
+            orc.apply_events(ev)
+        assert eng.step(1) == orc.step(1)
+        if r % 3 == 0:
+            _scan_check(eng, orc.export_state()[0], rng, n)
+    eng.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_vote_scan_sharded(gs, world):
+    """G shards (in-process transport) agree with the single engine: the
+    first member may sit on any shard, the master's column on one."""
+    n = 500
+    cfg = gs.default_config(n, t_fail=4, t_cleanup=4, seed=0x5EED0F32)
+    one = gs.Engine(gs.Config.from_buffer_copy(cfg))
+    grp = gs.ShardGroup(cfg, world)
+    init = sc.full_state(n)
+    one.import_state(*init, 0)
+    grp.import_state(*init, 0)
+    crash = [(gs.GH_EV_CRASH, c) for c in range(0, 300, 7)]
+    one.apply_events(crash)
+    grp.apply_events(crash)
+    rng = np.random.default_rng(3)
+    for _ in range(8):
+        assert one.step(1) == grp.step(1)
+        mv = rng.integers(0, n, n).astype(np.int32)
+        for a, b in zip(one.vote_scan(mv), grp.vote_scan(mv)):
+            np.testing.assert_array_equal(a, b)
+    grp.close()
+    one.close()
+
+
+def _meta(eng, F):
+    return eng.get_files(np.arange(F, dtype=np.int32))
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_rebuild_meta(gs, world):
+    """rebuild_file_meta at several new masters after placement, crashes and
+    repairs: the file table equals the oracle's literal rebuild."""
+    n, F = 64, 3000
+    cfg = gs.default_config(n, max_files=F, seed=0x5EED0F33, t_fail=8, t_cleanup=8)
+    eng = gs.Engine(cfg) if world == 1 else gs.ShardGroup(cfg, world)
+    eng.import_state(*sc.full_state(n), 0)
+    eng.step(2)
+    eng.put(np.arange(0, F, 2, dtype=np.int32))
+    eng.apply_events([(gs.GH_EV_CRASH, c) for c in (3, 9, 17, 40)])
+    eng.step(1)
+    eng.put(np.arange(1, F, 4, dtype=np.int32))
+    eng.step(9)
+    eng.repair(5)
+    eng.step(1)
+    for m in (0, 2, 33):  # 0: its own MemberList[0]; 2, 33: f0 = another member
+        rep, ver = _meta(eng, F)
+        ids = [int(x) for x in eng.lsm(m)[0]]
+        assert len(ids) == 60  # the 4 crashed members detected and removed
+        er, ev, _ = el.rebuild(rep, ver, np.zeros(F, np.int32), m, ids, now=eng.round)
+        f0, nf = eng.rebuild_meta(m)
+        assert f0 == ids[0] and nf == int((ev >= 0).sum())
+        r2, v2 = _meta(eng, F)
+        np.testing.assert_array_equal(v2, ev)
+        np.testing.assert_array_equal(r2, er)
+        # the new master's list is the placement candidate list from now on
+        rp, _, st = eng.put(np.array([F - 1], np.int32))
+        assert st[0] == gs.GH_OK and all(x in ids for x in rp[0] if x >= 0)
+    eng.close()
+
+
+def test_cluster_master_crash_election(gs):
+    """Cluster(elect=True), 32 members, master 0 crashes: the votes go to
+    member 1 (everyone's MemberList[0]) and elect it the round its majority
+    arrives; it rebuilds two rounds later (its own MemberList[0], so every
+    listed member reports its store); the detectors' Fail_recover 8 rounds
+    after detection dials the dead master and log.Fatal's. Checked round by
+    round against the oracle Tally on the exported table."""
+    n, F = 32, 400
+    cl = gs.Cluster(n, elect=True, max_files=F, seed=0x5EED0F34, t_fail=8, t_cleanup=8)
+    eng = cl.engine
+    eng.import_state(*sc.full_state(n), 0)
+    cl.tick(2)
+    cl.put(range(F))
+    cl.crash(0)
+    tally = el.Tally(n, master=0)
+    pending, det_round, detectors = {}, None, None
+    prev = _meta(eng, F)
+    for _ in range(20):
+        cl.tick(1)
+        r = eng.round
+        hb, _, alive = eng.export_state()
+        if det_round is None and len(eng.read_detectors()):
+            det_round, detectors = r, set(eng.read_detectors().tolist())
+        for m in pending.pop(r, []):
+            lst = [int(c) for c in np.flatnonzero(hb[m] >= 0)]
+            tally.finish_rebuild(m, lst[0])
+            er, ev, _ = el.rebuild(prev[0], prev[1], np.zeros(F, np.int32), m, lst, now=r)
+            rep, ver = _meta(eng, F)
+            np.testing.assert_array_equal(ver, ev)
+            np.testing.assert_array_equal(rep, er)
+        for m in tally.round(alive, *el.vote_scan(hb, tally.mview), dead=cl.dead):
+            pending[r + 2] = pending.get(r + 2, []) + [m]
+        np.testing.assert_array_equal(cl.mview, tally.mview, err_msg=f"r={r}")
+        prev = _meta(eng, F)
+    assert [m for _, m in cl.elections] == [1] and cl.master == 1
+    assert not pending
+    # Fail_recover at det_round + 8: every detector but the new master dies
+    assert det_round is not None
+    fatal = {m for r, m, why in cl.fatal if why.startswith("Fail_recover") and r == det_round + cl.repair_delay}
+    assert fatal == detectors - {1}
+    eng.close()
