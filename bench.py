@@ -193,6 +193,49 @@ def placement_leg(gs, eng, n, files, t_fail):
     }
 
 
+def election_leg(gs, eng, n, t_fail):
+    """SURVEY.md §8f f3 figure, after the placement leg (outside the timed
+    rounds): crash the master (member 0), run the rounds until it is detected
+    and REMOVE'd, then the per-round election scan gh_vote_scan over all N
+    rows (updateMemberList's master check + revote_master's MemberList[0],
+    slave/slave.go:451-457, 930-948), and gh_rebuild_meta
+    (rebuild_file_meta, :986-1043) over the file table at the member the
+    votes elect. Host-buffer calls, PCIe copies included."""
+    import numpy as np
+    eng.apply_events([(gs.GH_EV_CRASH, 0)])
+    rounds, det = 0, 0
+    while rounds < 4 * t_fail + 8:
+        d = eng.step(1)["detections"]
+        rounds += 1
+        if d == 0 and det:
+            break
+        det += d
+    mview = np.zeros(n, np.int32)
+    eng.vote_scan(mview)  # first call allocates; time the second
+    eng.sync()
+    t0 = time.perf_counter()
+    first, ln, has = eng.vote_scan(mview)
+    t_scan = time.perf_counter() - t0
+    alive = eng.alive()
+    voters = (alive != 0) & (ln >= eng.cfg.min_members) & (has == 0)
+    votes = np.bincount(first[voters & (first >= 0)], minlength=n)
+    # remote votes, deduplicated, against the candidate's own list (Receive_vote :974-978)
+    self_v = np.bincount(first[voters & (first == np.arange(n))], minlength=n)
+    elected = np.flatnonzero(votes - self_v > ln // 2)
+    out = {"rounds_to_detection_and_remove": rounds, "voters": int(voters.sum()),
+           "vote_scan_ms": t_scan * 1e3, "rows_scanned_per_s": n / t_scan,
+           "elected": int(elected[0]) if len(elected) else None}
+    if len(elected) and eng.cfg.max_files > 0:
+        eng.sync()
+        t0 = time.perf_counter()
+        f0, kept = eng.rebuild_meta(int(elected[0]))
+        t_rb = time.perf_counter() - t0
+        out.update({"rebuild_ms": t_rb * 1e3, "rebuild_files_per_s": eng.cfg.max_files / t_rb,
+                    "files_kept": int(kept), "assign_new_master_to": int(f0)})
+    out["note"] = "host-buffer C-ABI calls (PCIe copies included)"
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -243,6 +286,7 @@ def main():
     placement = None
     if world == 1 and args.files > 0:
         placement = placement_leg(gs, eng, n, args.files, args.t_fail)
+        placement["election"] = election_leg(gs, eng, n, args.t_fail)
     eng.close()
 
     if rank != 0:
