@@ -289,6 +289,23 @@ class ShardModel:
         anyd = _allreduce(self.det_any.astype(np.int64), dist.ReduceOp.MAX)
         return [i for i in range(self.n) if anyd[i]]
 
+    def vote_scan(self, mview):
+        """gh_vote_scan's exchange (csrc/elect.hip k_vote_scan + gossiphip.cpp):
+        per row, n - (first present local member) and (mview[i] present
+        locally) reduced with MAX, the local present counts with SUM."""
+        pres = self.hb >= 0
+        n = self.n
+        loc_first = np.where(pres.any(axis=1), n - (self.col0 + pres.argmax(axis=1)), 0) if self.ncol else np.zeros(n)
+        lc = np.asarray(mview) - self.col0
+        ok = (lc >= 0) & (lc < self.ncol)
+        has = np.zeros(n, np.int64)
+        rows = np.flatnonzero(ok)
+        has[rows] = pres[rows, lc[rows]]
+        red = _allreduce(np.concatenate([loc_first, has]).astype(np.int64), dist.ReduceOp.MAX)
+        ln = _allreduce(pres.sum(axis=1).astype(np.int64))
+        first = np.where(red[:n] > 0, n - red[:n], -1)
+        return first, ln, red[n:]
+
     def master_list(self, master=0):
         """Placement candidates (k_candidates) from the gathered master row."""
         bits = _gather_rows_bool(self.hb[[master]] >= 0, self.ncs, self.n)[0]
@@ -331,6 +348,10 @@ def worker(rank, world, port, n, rounds, cfg, churn_seed, files_at):
             assert m.read_detectors() == list(orc.read_detectors())
             if r in files_at:
                 assert m.master_list() == [c for c in range(n) if hb[0, c] >= 0]
+            from oracle import election as el
+            mv = np.random.default_rng(r).integers(0, n, n)
+            for a, b in zip(m.vote_scan(mv), el.vote_scan(hb, mv)):
+                assert np.array_equal(a, b), f"rank {rank} round {r}: vote scan differs"
         sys.stdout.flush()
     finally:
         dist.destroy_process_group()
