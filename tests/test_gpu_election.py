@@ -148,3 +148,36 @@ def test_cluster_master_crash_election(gs):
     fatal = {m for r, m, why in cl.fatal if why.startswith("Fail_recover") and r == det_round + cl.repair_delay}
     assert fatal == detectors - {1}
     eng.close()
+
+
+def test_cluster_rebuild_fatal_and_self_votes(gs):
+    """A hand-built table (member ids 0..7, master 0 crashed and tombstoned
+    everywhere; member 1 tombstoned in rows 3..7):
+      row 1 = {1..7}: votes for itself (counted, no check);
+      row 2 = {1..7}: votes for 1;  rows 3..7 = {2..7}: vote for 2.
+    Round 1: Vote_num[1] = 2, not > 7 // 2; Vote_num[2] reaches 4 > 3 at
+    row 6, so 2 is elected (row 7's vote still counts: 5). Member 1 then crashes; at round 3 the rebuild
+    dials MemberList_2[0] = 1, which is gone: 2 log.Fatal's (:996-999) and
+    the master stays 0."""
+    n = 8
+    hb = np.full((n, n), -1, np.int32)
+    hb[:, 0] = -2
+    hb[1, 1:] = 5
+    hb[2, 1:] = 5
+    hb[3:, 2:] = 5
+    hb[3:, 1] = -2
+    hb[0, :] = 5
+    ts = np.zeros((n, n), np.int32)
+    alive = np.ones(n, np.uint8)
+    alive[0] = 0
+    cl = gs.Cluster(n, elect=True, t_fail=8, t_cleanup=30, fanout=2)
+    cl.engine.import_state(hb, ts, alive, 0)
+    cl.dead.add(0)
+    cl.tick(1)
+    assert cl.elections == [(1, 2)] and cl.mview[2] == 2
+    assert cl.vote_num[1] == 2 and cl.voters[1] == {2} and cl.vote_num[2] == 5
+    cl.crash(1)
+    cl.tick(2)
+    assert (3, 2, "rebuild_file_meta: MemberList[0] unreachable") in cl.fatal
+    assert cl.master == 0
+    cl.engine.close()
