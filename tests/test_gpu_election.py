@@ -25,12 +25,14 @@ def _scan_check(eng, hb, rng, n):
             np.testing.assert_array_equal(g, e, err_msg=name)
 
 
+@pytest.mark.parametrize("detect_mode", [0, 1])
 @pytest.mark.parametrize("peer_mode", [0, 1])
-def test_vote_scan_churn(gs, oracle_mod, peer_mode):
+def test_vote_scan_churn(gs, oracle_mod, peer_mode, detect_mode):
     """Seeded churn at N=300 (crashes, leaves, joins; tombstones and empty
-    rows), the scan checked every 3 rounds against the oracle's table."""
+    rows), canonical and quirk detection, the scan checked every 3 rounds
+    against the oracle's table."""
     n, rounds = 300, 30
-    cfg = dict(peer_mode=peer_mode, t_fail=3, t_cleanup=3, seed=0x5EED0F31)
+    cfg = dict(peer_mode=peer_mode, detect_mode=detect_mode, t_fail=3, t_cleanup=3, seed=0x5EED0F31)
     eng = gs.Engine(gs.default_config(n, **cfg))
     orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg))
     sched = sc.random_churn(n, rounds, seed=31)
@@ -107,15 +109,19 @@ def test_rebuild_meta(gs, world):
     eng.close()
 
 
-def test_cluster_master_crash_election(gs):
+@pytest.mark.parametrize("peer_mode", [0, 1])
+def test_cluster_master_crash_election(gs, peer_mode):
     """Cluster(elect=True), 32 members, master 0 crashes: the votes go to
     member 1 (everyone's MemberList[0]) and elect it the round its majority
     arrives; it rebuilds two rounds later (its own MemberList[0], so every
     listed member reports its store); the detectors' Fail_recover 8 rounds
     after detection dials the dead master and log.Fatal's. Checked round by
-    round against the oracle Tally on the exported table."""
+    round against the oracle Tally on the exported table. Pull and the
+    reference's ring (there only the ring neighbours of 0 detect it; the
+    rest get the REMOVE and vote a round later)."""
     n, F = 32, 400
-    cl = gs.Cluster(n, elect=True, max_files=F, seed=0x5EED0F34, t_fail=8, t_cleanup=8)
+    tf = 8 if peer_mode == 0 else 16  # ring dissemination needs the longer timeout to stay healthy
+    cl = gs.Cluster(n, elect=True, max_files=F, seed=0x5EED0F34, t_fail=tf, t_cleanup=tf, peer_mode=peer_mode)
     eng = cl.engine
     eng.import_state(*sc.full_state(n), 0)
     cl.tick(2)
@@ -124,7 +130,7 @@ def test_cluster_master_crash_election(gs):
     tally = el.Tally(n, master=0)
     pending, det_round, detectors = {}, None, None
     prev = _meta(eng, F)
-    for _ in range(20):
+    for _ in range(30):
         cl.tick(1)
         r = eng.round
         hb, _, alive = eng.export_state()
