@@ -48,7 +48,7 @@ __global__ __launch_bounds__(256) void k_vote_scan(GhDev d, int cur, const int32
 // the file's version and the sorted order is list order. M's metadata map
 // starts empty, so a file in neither store is gone.
 __global__ __launch_bounds__(256) void k_rebuild(GhDev d, int32_t R, int32_t M, int4 L03, int32_t L4, int32_t nl,
-                                                 int32_t now) {
+                                                 int32_t m_listed, int32_t now) {
   const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (f >= d.fcap || d.ver[f] < 0) return;
   int32_t* rp = d.rep + f * R;
@@ -65,8 +65,9 @@ __global__ __launch_bounds__(256) void k_rebuild(GhDev d, int32_t R, int32_t M, 
     // every m != M of the list holds it; among L's first 5 at most one is M
     for (int q = 0; q < nl && k < cap; ++q)
       if (L[q] != M || in_m) rp[k++] = L[q];
-  } else if (in_m) {
-    rp[k++] = M;  // only M's own store has it (M may sit anywhere in L)
+  } else if (in_m && m_listed) {
+    rp[k++] = M;  // only M's own store has it (M may sit anywhere in L; a
+                  // list without M never reads M's store)
   }
   for (int q = k; q < R; ++q) rp[q] = -1;
   if (k == 0) {
@@ -82,8 +83,9 @@ void launch_vote_scan(const GhDev& d, int cur, const int32_t* mview, int32_t* ou
   hipLaunchKernelGGL(k_vote_scan, dim3((unsigned)((d.n + 3) / 4)), dim3(256), 0, s, d, cur, mview, out);
 }
 
-void launch_rebuild(const GhDev& d, int32_t R, int32_t M, const int32_t* L, int32_t nl, int32_t now, hipStream_t s) {
+void launch_rebuild(const GhDev& d, int32_t R, int32_t M, const int32_t* L, int32_t nl, int32_t m_listed,
+                    int32_t now, hipStream_t s) {
   const int4 l03 = make_int4(L[0], L[1], L[2], L[3]);
   hipLaunchKernelGGL(k_rebuild, dim3((unsigned)((d.fcap + 255) / 256)), dim3(256), 0, s, d, R, M, l03, L[4], nl,
-                     now);
+                     m_listed, now);
 }

@@ -407,4 +407,5 @@ void launch_conflicts(const GhDev& d, int64_t n, int32_t now, int32_t window, hi
 // member, 0 none) and (mview[i] present locally), both MAX-reducible
 void launch_vote_scan(const GhDev& d, int cur, const int32_t* mview, int32_t* out, hipStream_t s);
 // rebuild_file_meta at new master M with its list's first nl (<= 5) members L
-void launch_rebuild(const GhDev& d, int32_t R, int32_t M, const int32_t* L, int32_t nl, int32_t now, hipStream_t s);
+void launch_rebuild(const GhDev& d, int32_t R, int32_t M, const int32_t* L, int32_t nl, int32_t m_listed,
+                    int32_t now, hipStream_t s);

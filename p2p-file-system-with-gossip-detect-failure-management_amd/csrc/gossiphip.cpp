@@ -1,5 +1,5 @@
 // libgossiphip host side: the C-ABI of include/gossiphip.h over the HIP
-// kernels in round.hip / events.hip / place.hip. One handle = one engine =
+// kernels in round.hip / events.hip / place.hip / elect.hip. One handle = one engine =
 // one gfx950 device, one HIP stream, its tables resident in HBM. A sharded
 // engine (gh_create_sharded) is rank g of G column shards of one cluster;
 // its O(N) per-round exchanges go through comm.h (RCCL, or threads of one
@@ -12,6 +12,7 @@
 //   UDP list exchange between hosts   slave/slave.go:527-542 (-> comm.h)
 //   Handle_put_request / Update_metadata / Get_* / Delete_file_info
 //                                     master/master.go:74-259
+//   revote_master / rebuild_file_meta slave/slave.go:930-1043
 // There is no CPU fallback: without a gfx950 device gh_create fails.
 #include <hip/hip_runtime.h>
 
@@ -1021,7 +1022,8 @@ int gh_rebuild_meta(void* h, int32_t new_master, int32_t* f0, int64_t* n_files) 
   int32_t L[5] = {-1, -1, -1, -1, -1};
   const int32_t k = (int32_t)std::min<int64_t>(nl, 5);
   for (int32_t q = 0; q < k; ++q) L[q] = ids[q];
-  launch_rebuild(e->d, e->cfg.replicas, new_master, L, k, e->round, e->stream);
+  const int32_t m_listed = std::find(ids.begin(), ids.begin() + nl, new_master) != ids.begin() + nl;
+  launch_rebuild(e->d, e->cfg.replicas, new_master, L, k, m_listed, e->round, e->stream);
   HIPCHK(e, hipGetLastError());
   std::vector<int32_t> ver(e->d.fcap);
   HIPCHK(e, hipMemcpyAsync(ver.data(), e->d.ver, sizeof(int32_t) * e->d.fcap, hipMemcpyDeviceToHost, e->stream));

@@ -187,3 +187,28 @@ def test_cluster_rebuild_fatal_and_self_votes(gs):
     assert (3, 2, "rebuild_file_meta: MemberList[0] unreachable") in cl.fatal
     assert cl.master == 0
     cl.engine.close()
+
+
+def test_rebuild_master_not_in_own_list(gs):
+    """A new master whose own list lacks itself (its self entry tombstoned):
+    the rebuild loop never reaches member == M (:991-992), so M's own store
+    is never read, and a file only M holds is dropped."""
+    n, F = 8, 64
+    hb = np.full((n, n), 5, np.int32)
+    hb[5, 5] = -2
+    ts = np.zeros((n, n), np.int32)
+    eng = gs.Engine(gs.default_config(n, max_files=F, seed=0x5EED0F35, t_fail=8, t_cleanup=8))
+    eng.import_state(hb, ts, np.ones(n, np.uint8), 0)
+    eng.put(np.arange(F, dtype=np.int32))
+    rep, ver = _meta(eng, F)
+    ids = [int(x) for x in eng.lsm(5)[0]]
+    assert 5 not in ids and ids[0] == 0
+    er, ev, _ = el.rebuild(rep, ver, np.zeros(F, np.int32), 5, ids, now=eng.round)
+    only_m = [f for f in range(F) if 5 in rep[f] and 0 not in rep[f]]
+    assert only_m and all(ev[f] == -1 for f in only_m)
+    f0, nf = eng.rebuild_meta(5)
+    r2, v2 = _meta(eng, F)
+    assert f0 == 0 and nf == int((ev >= 0).sum())
+    np.testing.assert_array_equal(v2, ev)
+    np.testing.assert_array_equal(r2, er)
+    eng.close()
