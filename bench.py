@@ -219,9 +219,10 @@ def election_leg(gs, eng, n, t_fail):
     alive = eng.alive()
     voters = (alive != 0) & (ln >= eng.cfg.min_members) & (has == 0)
     votes = np.bincount(first[voters & (first >= 0)], minlength=n)
-    # remote votes, deduplicated, against the candidate's own list (Receive_vote :974-978)
+    # Vote_num (self vote included) against the candidate's own list; the
+    # check runs only when a remote vote arrives (Receive_vote :974-978)
     self_v = np.bincount(first[voters & (first == np.arange(n))], minlength=n)
-    elected = np.flatnonzero(votes - self_v > ln // 2)
+    elected = np.flatnonzero((votes > ln // 2) & (votes - self_v > 0))
     out = {"rounds_to_detection_and_remove": rounds, "voters": int(voters.sum()),
            "vote_scan_ms": t_scan * 1e3, "rows_scanned_per_s": n / t_scan,
            "elected": int(elected[0]) if len(elected) else None}
