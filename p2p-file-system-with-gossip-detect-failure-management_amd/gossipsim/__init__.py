@@ -527,20 +527,63 @@ class Cluster:
         first, ln, has = self.engine.vote_scan(self.mview)
         alive = self.engine.alive()
         run = (alive != 0) & (ln >= self.engine.cfg.min_members) & (has == 0)
-        for i in np.flatnonzero(run).tolist():
-            t = int(first[i])
-            self._touch(i)
-            if t == i:  # self vote: counted, no majority check (:936-939)
-                self.vote_num[i] += 1
-                continue
-            if t in self.dead:  # rpc.Dial to MemberList[0] fails (:941-944)
-                self._fatal(r, i, "revote_master: MemberList[0] unreachable")
-                continue
-            self._touch(t)
-            if i not in self.voters[t]:
-                self.voters[t].add(i)
-                self.vote_num[t] += 1
-            if self.mview[t] != t and self.vote_num[t] > ln[t] // 2:
-                self.mview[t] = t
-                self.elections.append((r, t))
-                self.rebuilds.setdefault(r + 2, []).append(t)
+        self._tally(r, np.flatnonzero(run), first, ln)
+
+    def _tally(self, r, idx, first, ln):
+        """The votes of one round, in voter-ID order, as array operations
+        (the same result as running revote_master / Receive_vote voter by
+        voter; oracle/election.py's Tally is that loop). idx: the voting
+        rows, ascending."""
+        if len(idx) == 0:
+            return
+        tgt = first[idx].astype(np.int64)
+        remote = tgt != idx
+        # log.Fatal when the target's process is gone: already dead, or a
+        # voter that died earlier in this round's order (its own vote failed)
+        dead = np.zeros(self.n, bool)
+        if self.dead:
+            dead[list(self.dead)] = True
+        fatal = remote & dead[tgt]
+        while True:
+            fdead = np.zeros(self.n, bool)
+            fdead[idx[fatal]] = True
+            more = remote & ~fatal & fdead[tgt] & (tgt < idx)
+            if not more.any():
+                break
+            fatal |= more
+        ok = remote & ~fatal
+        # touch (slave/slave.go:931-935, 969-973): every voter, and every target of a vote that arrives
+        touched = np.unique(np.concatenate([idx, tgt[ok]]))
+        fresh = touched[~self.vote_on[touched]]
+        self.vote_on[fresh] = True
+        self.vote_num[fresh] = 0
+        for x in fresh.tolist():
+            if self.voters[x]:
+                self.voters[x] = set()
+        selfv = idx[~remote]
+        self.vote_num[selfv] += 1  # self votes: counted, no majority check (:936-939)
+        events = []
+        if ok.any():
+            selfset = set(selfv.tolist())
+            vs, ts = idx[ok], tgt[ok]
+            for t in np.unique(ts).tolist():
+                who = vs[ts == t]  # ascending
+                old = self.voters[t]
+                new = np.array([v not in old for v in who.tolist()]) if old else np.ones(len(who), bool)
+                sv = int(t in selfset)
+                # Vote_num as each remote vote is checked: the count after the
+                # touch, + the new voters so far, + t's own vote if t came first
+                start = int(self.vote_num[t]) - sv
+                cum = start + np.cumsum(new) + (sv & (who > t)).astype(np.int64)
+                self.voters[t].update(who[new].tolist())
+                self.vote_num[t] = start + int(new.sum()) + sv
+                if self.mview[t] != t:
+                    hit = np.flatnonzero(cum > ln[t] // 2)
+                    if len(hit):
+                        events.append((int(who[hit[0]]), t))
+        for _, t in sorted(events):
+            self.mview[t] = t
+            self.elections.append((r, t))
+            self.rebuilds.setdefault(r + 2, []).append(t)
+        for i in idx[fatal].tolist():
+            self._fatal(r, i, "revote_master: MemberList[0] unreachable")

@@ -82,3 +82,61 @@ def test_rebuild_kat():
     r3, v3, _ = el.rebuild(rep, ver, fts, 1, [1, 2, 3], now=40)
     assert r3.tolist() == [[1, 2, 3, -1], [-1] * 4, [1, 2, 3, -1], [-1] * 4, [-1] * 4]
     assert v3.tolist() == [3, -1, 2, -1, -1]
+
+
+class _NoEngine:
+    """Stands in for the engine in Cluster._tally (only crash events reach it)."""
+
+    def __init__(self):
+        self.events = []
+
+    def apply_events(self, ev):
+        self.events.extend(ev)
+
+
+def test_cluster_tally_matches_oracle_loop():
+    """gossipsim.Cluster._tally (array form) against the oracle's voter-by-
+    voter Tally on random vote patterns over many rounds: several
+    candidates, self votes before and after remote ones, repeat voters,
+    dead targets and chains of log.Fatal, candidates that are voters."""
+    import gossipsim as gs
+    rng = np.random.default_rng(11)
+    for trial in range(40):
+        n = int(rng.integers(6, 60))
+        cl = object.__new__(gs.Cluster)
+        cl.n, cl.engine = n, _NoEngine()
+        cl.mview = np.zeros(n, np.int32)
+        cl.vote_on = np.zeros(n, bool)
+        cl.vote_num = np.zeros(n, np.int64)
+        cl.voters = [set() for _ in range(n)]
+        cl.rebuilds, cl.elections, cl.fatal = {}, [], []
+        cl.dead = set(rng.choice(n, size=int(rng.integers(0, 3)), replace=False).tolist())
+        t = el.Tally(n, master=0)
+        for r in range(1, 6):
+            idx = np.flatnonzero(rng.random(n) < 0.7)
+            cands = rng.choice(n, size=int(rng.integers(1, 4)), replace=False)
+            first = np.where(rng.random(n) < 0.2, np.arange(n), rng.choice(cands, size=n)).astype(np.int32)
+            ln = rng.integers(4, 2 * n, size=n).astype(np.int32)
+            run = np.zeros(n, bool)
+            run[idx] = True
+            dead_before = set(cl.dead)
+            alive = run.astype(np.uint8)
+            has = np.zeros(n, np.uint8)
+            ln_run = np.where(run, np.maximum(ln, 4), 0).astype(np.int32)
+            # the oracle loop, with log.Fatal deaths taking effect in voter order
+            elected, fatal, dead = [], [], set(dead_before)
+            for i in idx.tolist():
+                e = t.round(np.eye(1, n, i, dtype=np.uint8)[0], first, ln_run, has, dead=dead)
+                elected += e
+                if t.fatal:
+                    fatal += t.fatal
+                    dead |= set(t.fatal)
+            n_el = len(cl.elections)
+            cl._tally(r, idx, first, ln_run)
+            assert [m for _, m in cl.elections[n_el:]] == elected, (trial, r)
+            assert [m for rr, m, _ in cl.fatal if rr == r] == fatal, (trial, r)
+            np.testing.assert_array_equal(cl.vote_num, t.num)
+            np.testing.assert_array_equal(cl.mview, t.mview)
+            np.testing.assert_array_equal(cl.vote_on, t.on)
+            assert cl.voters == t.voters
+            assert cl.dead == dead
