@@ -161,11 +161,12 @@ class Oracle:
         alive = np.ascontiguousarray(alive, dtype=np.uint8)
         self._chk(lib().or_import_state(self.h, _p(hb), _p(ts), _p(alive), row0, hb.shape[0], round_))
 
-    def export_state(self):
-        hb = np.empty((self.rows, self.n), np.int32)
-        ts = np.empty((self.rows, self.n), np.int32)
-        alive = np.empty(self.rows, np.uint8)
-        self._chk(lib().or_export_state(self.h, _p(hb), _p(ts), _p(alive), 0, self.rows))
+    def export_state(self, row0=0, n_rows=None):
+        n_rows = self.rows - row0 if n_rows is None else n_rows
+        hb = np.empty((n_rows, self.n), np.int32)
+        ts = np.empty((n_rows, self.n), np.int32)
+        alive = np.empty(n_rows, np.uint8)
+        self._chk(lib().or_export_state(self.h, _p(hb), _p(ts), _p(alive), row0, n_rows))
         return hb, ts, alive
 
     def init_full(self, hb0=2, ts0=0, round_=0):

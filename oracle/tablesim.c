@@ -310,7 +310,7 @@ static void apply_events(ors *s, int32_t r, gh_round_stats *st) {
 }
 
 /* Phase A for one alive row i: steps 1-5 of SPEC §2. Returns 1 if active. */
-static int phase_a(ors *s, int64_t i, int32_t r, gh_round_stats *st) {
+static int phase_a(ors *s, int64_t i, int32_t r, gh_round_stats *st, int32_t *ldc, int32_t *ldm) {
   int32_t n = s->n;
   int32_t *row = s->hb + i * n;
   int32_t *trow = s->ts + i * n;
@@ -365,12 +365,8 @@ static int phase_a(ors *s, int64_t i, int32_t r, gh_round_stats *st) {
     row[c] = GH_TOMBSTONE; /* removeMember keeps the stale ts (:280) */
     st->detections++;
     found = 1;
-#pragma omp atomic
-    s->ndet_cnt[c] += 1;
-#pragma omp critical(or_detmin)
-    {
-      if ((int32_t)i < s->ndet_min[c]) s->ndet_min[c] = (int32_t)i;
-    }
+    ldc[c] += 1; /* this thread's D_r counts; rows ascend within a thread */
+    if ((int32_t)i < ldm[c]) ldm[c] = (int32_t)i;
   }
   if (found) s->det_any[i] = 1;
   /* step 5: clean (:484-497) */
@@ -407,19 +403,30 @@ static void one_round(ors *s, gh_round_stats *acc) {
     s->ndet_cnt[c] = 0;
     s->ndet_min[c] = INT_MAX;
   }
-  /* phase A */
+  /* phase A (per-thread D_r accumulators, merged once per thread) */
 #pragma omp parallel num_threads(s->threads)
   {
     gh_round_stats ls;
     memset(&ls, 0, sizeof ls);
+    int32_t *ldc = (int32_t *)calloc(n, 4);
+    int32_t *ldm = (int32_t *)malloc((size_t)n * 4);
+    for (int32_t c = 0; c < n; ++c) ldm[c] = INT_MAX;
 #pragma omp for schedule(static)
     for (int64_t i = 0; i < rows; ++i) {
       s->active[i] = 0;
       if (!s->alive[i]) continue;
-      s->active[i] = (uint8_t)phase_a(s, i, r, &ls);
+      s->active[i] = (uint8_t)phase_a(s, i, r, &ls, ldc, ldm);
     }
 #pragma omp critical(or_stats)
-    stats_add(&st, &ls);
+    {
+      stats_add(&st, &ls);
+      for (int32_t c = 0; c < n; ++c) {
+        s->ndet_cnt[c] += ldc[c];
+        if (ldm[c] < s->ndet_min[c]) s->ndet_min[c] = ldm[c];
+      }
+    }
+    free(ldc);
+    free(ldm);
   }
   /* snapshot of every active alive row after steps 1-5 (what it sends) */
 #pragma omp parallel for num_threads(s->threads) schedule(static)
