@@ -32,16 +32,16 @@
 extern "C" {
 #endif
 
-#define GH_ABI_VERSION 1
+#define GH_ABI_VERSION 2
 
 /* ---- error codes ---------------------------------------------------- */
 #define GH_OK 0
 #define GH_EINVAL (-1)               /* bad argument / shape                    */
 #define GH_ENODEV (-2)               /* no usable HIP device                    */
-#define GH_ENOMEM (-3)               /* device allocation failed                */
+#define GH_ENOMEM (-3)               /* device allocation failed / wide arena full */
 #define GH_EHIP (-4)                 /* HIP runtime error                       */
 #define GH_EPLACEMENT_STARVED (-5)   /* master/master.go:130-135 hang / panic   */
-#define GH_ERANGE (-6)               /* value out of encodable range            */
+#define GH_ERANGE (-6)               /* heartbeat would pass INT32_MAX / < range */
 
 /* ---- cell encoding (SPEC.md §1) -------------------------------------- */
 #define GH_ABSENT (-1)     /* not in MemberList                              */
@@ -74,7 +74,10 @@ typedef struct gh_config {
                             256; 0 = default 64), see DESIGN.md             */
   uint64_t seed;         /* Philox key for peers and placement draws         */
   int64_t max_files;     /* file-metadata capacity (0 = no files)            */
-  int32_t reserved[8];
+  int64_t wide_segments; /* slots of each wide-segment arena (HBM layout,
+                            DESIGN.md); 0 = auto (all segments when small,
+                            else 1/32 of them, grown between calls)        */
+  int32_t reserved[6];
 } gh_config;
 
 typedef struct gh_event {
@@ -110,17 +113,22 @@ typedef struct gh_plan_entry {
 void gh_config_default(gh_config* cfg);
 
 /* Replaces InitSlave/InitMaster (slave/slave.go:95, master/master.go:38) for
- * N members at once. Allocates hb (x2) and ts tables in HBM: 12*N*N bytes. */
+ * N members at once. HBM: the 16-bit narrow table (x2), 4*N*N bytes, plus the
+ * wide-segment arenas (gh_config.wide_segments) and a frozen store for
+ * stopped rows that grows with them (gh_memory_info). */
 int gh_create(const gh_config* cfg, void** handle);
 void gh_destroy(void* h);
 const char* gh_last_error(void* h);
 int gh_abi_version(void);
 
 /* Whole-state transfer (host <-> HBM). Rows [row0, row0+n_rows) of the N x N
- * tables. `round` is the tick of the last completed round; heartbeats above
- * 2^23-1 and listed members with ts > round+1 are rejected (GH_ERANGE: the
- * device keeps a 23-bit heartbeat and the cell's age); pending
- * REMOVEs are cleared on import. */
+ * tables. `round` is the tick of the last completed round. hb: any int32
+ * >= -2 (GH_ABSENT, GH_TOMBSTONE, heartbeats up to INT32_MAX; below -2 is
+ * GH_ERANGE); ts: any int32. Pending REMOVEs are cleared on import. Export:
+ * the ts of an absent cell is 0 (the reference keeps no entry for it), and
+ * with T_cleanup < 30 a tombstone older than 30 rounds exports ts =
+ * round + 1 - 30 (its age is only ever compared with COOLDOWN,
+ * slave/slave.go:490; SPEC.md §1). */
 int gh_import_state(void* h, const int32_t* hb, const int32_t* ts,
                     const uint8_t* alive, int64_t row0, int64_t n_rows,
                     int32_t round);
@@ -138,7 +146,11 @@ int gh_apply_events(void* h, const gh_event* ev, int64_t n);
 /* Run `rounds` synchronous gossip rounds (HeartBeat, slave/slave.go:499,
  * driven by the 1 s loop of main.go:27-33, with MergeMemberList :414,
  * detectfailure :460, cleanFailList :484). Blocks until done; stats may be
- * NULL. */
+ * NULL. Heartbeats are Go ints in the reference (master/master.go:18) and
+ * int32 here: a round in which a running member's own heartbeat is
+ * INT32_MAX is refused with GH_ERANGE (the rounds before it completed;
+ * stats->rounds says how many). GH_ENOMEM: the wide arena overflowed inside
+ * a round and the state is lost (re-import or destroy). */
 int gh_step(void* h, int32_t rounds, gh_round_stats* stats);
 
 /* Members detected in the last round as an N-bit bitmap (REMOVE broadcast
@@ -209,7 +221,7 @@ int gh_rebuild_meta(void* h, int32_t new_master, int32_t* f0, int64_t* n_files);
 
 /* ---- multi-GPU: one cluster column-sharded over G ranks ----------------
  * Rank g holds all N observer rows for member columns [g*ncs, g*ncs+ncol)
- * (ncs = roundup(ceil(N/G), 32)) of hb (x2) and ts: 12*N*ncs bytes of HBM.
+ * (ncs = roundup(ceil(N/G), 32)): 4*N*ncs bytes of narrow table plus arenas.
  * Merge, detection, cleanup and REMOVE delivery of a member happen on its
  * column's rank; per round the ranks exchange only O(N) vectors (present
  * counts, pull inboxes or ring positions/targets) by RCCL over xGMI. This
@@ -232,13 +244,17 @@ int gh_create_sharded(const gh_config* cfg, int32_t rank, int32_t world, int32_t
 int gh_shard_info(void* h, int32_t* rank, int32_t* world, int64_t* col0, int64_t* ncols);
 
 /* Table encoding of this engine's shard (diagnostic; DESIGN.md "Data layout"):
- * (tile, row) segments of the current table held in the wide 32-bit encoding
- * (stopped rows included); segments the last round ran through the per-cell
+ * (tile, row) segments of the current table held wide (arena or frozen
+ * store, stopped rows included); segments the last round ran through the per-cell
  * rule (k_round_slow); the round kernel variant of the last round (0 lean,
  * 1 storm) and its storm measure. Any output may be NULL. No reference
  * counterpart. */
 int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, int32_t* storm_mode,
                      int64_t* storm_segments);
+/* HBM held by the tables (narrow x2 + wide arenas + frozen store), wide-arena
+ * slots in use / per buffer, and stopped rows in the frozen store. Any
+ * output may be NULL. Diagnostic; no reference counterpart. */
+int gh_memory_info(void* h, int64_t* device_bytes, int64_t* wide_used, int64_t* wide_cap, int64_t* frozen_rows);
 
 /* Tuning knobs of the round kernel (k_round): non-temporal stores of the new
  * table and the XCD-aware block->tile map. Results do not depend on them;

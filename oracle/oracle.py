@@ -18,7 +18,9 @@ HERE = pathlib.Path(__file__).resolve().parent
 LIB_PATH = HERE / "_build" / "liboracle.so"
 
 GH_OK = 0
+GH_EINVAL = -1
 GH_EPLACEMENT_STARVED = -5
+GH_ERANGE = -6
 GH_PEER_PULL, GH_PEER_RING = 0, 1
 GH_DETECT_CANONICAL, GH_DETECT_QUIRK = 0, 1
 GH_EV_JOIN, GH_EV_LEAVE, GH_EV_CRASH = 1, 2, 3
@@ -30,7 +32,8 @@ class Config(C.Structure):
         ("detect_mode", C.c_int32), ("t_fail", C.c_int32), ("t_cleanup", C.c_int32),
         ("min_members", C.c_int32), ("replicas", C.c_int32), ("introducer", C.c_int32),
         ("master", C.c_int32), ("device", C.c_int32), ("tile_width", C.c_int32),
-        ("seed", C.c_uint64), ("max_files", C.c_int64), ("reserved", C.c_int32 * 8),
+        ("seed", C.c_uint64), ("max_files", C.c_int64), ("wide_segments", C.c_int64),
+        ("reserved", C.c_int32 * 6),
     ]
 
 
@@ -186,6 +189,13 @@ class Oracle:
         st = Stats()
         self._chk(lib().or_step(self.h, rounds, C.byref(st)))
         return st.as_dict()
+
+    def step_rc(self, rounds=1):
+        """(return code, stats of the rounds run): GH_ERANGE stops at the
+        round that would pass INT32_MAX."""
+        st = Stats()
+        rc = lib().or_step(self.h, rounds, C.byref(st))
+        return rc, st.as_dict()
 
     def read_failed(self):
         words = (self.n + 31) // 32

@@ -152,7 +152,7 @@ int or_import_state(void *h, const int32_t *hb, const int32_t *ts, const uint8_t
   ors *s = (ors *)h;
   if (row0 < 0 || n_rows < 0 || row0 + n_rows > s->rows) return fail(s, GH_EINVAL, "row range");
   for (int64_t x = 0; x < n_rows * s->n; ++x) {
-    if (hb[x] < GH_TOMBSTONE || hb[x] >= (1 << 30)) return fail(s, GH_ERANGE, "hb out of range");
+    if (hb[x] < GH_TOMBSTONE) return fail(s, GH_ERANGE, "hb below -2"); /* Go int: any value >= 0 */
   }
   memcpy(s->hb + row0 * s->n, hb, n_rows * s->n * 4);
   memcpy(s->ts + row0 * s->n, ts, n_rows * s->n * 4);
@@ -166,19 +166,34 @@ int or_import_state(void *h, const int32_t *hb, const int32_t *ts, const uint8_t
   return GH_OK;
 }
 
+/* Exported ts (SPEC.md §1): 0 for an absent member (the reference keeps no
+ * entry for it); with COOLDOWN < 30 rounds, a tombstone older than 30 rounds
+ * as exactly 30 rounds old -- its UpdateTime is only ever compared with
+ * now - COOLDOWN (cleanFailList, slave/slave.go:490), so every older value
+ * decides the same. */
+static int32_t export_ts(const ors *s, int32_t hb, int32_t ts) {
+  if (hb == GH_ABSENT) return 0;
+  int32_t now = s->round + 1;
+  if (hb == GH_TOMBSTONE && s->cfg.t_cleanup < 30 && (int64_t)now - ts > 30) return now - 30;
+  return ts;
+}
+
 int or_export_state(void *h, int32_t *hb, int32_t *ts, uint8_t *alive, int64_t row0,
                     int64_t n_rows) {
   ors *s = (ors *)h;
   if (row0 < 0 || n_rows < 0 || row0 + n_rows > s->rows) return fail(s, GH_EINVAL, "row range");
   if (hb) memcpy(hb, s->hb + row0 * s->n, n_rows * s->n * 4);
-  if (ts) memcpy(ts, s->ts + row0 * s->n, n_rows * s->n * 4);
+  if (ts) {
+    const int32_t *H = s->hb + row0 * s->n, *T = s->ts + row0 * s->n;
+    for (int64_t x = 0; x < n_rows * s->n; ++x) ts[x] = export_ts(s, H[x], T[x]);
+  }
   if (alive) memcpy(alive, s->alive + row0, n_rows);
   return GH_OK;
 }
 
 int or_init_full(void *h, int32_t hb0, int32_t ts0, int32_t round) {
   ors *s = (ors *)h;
-  if (hb0 < 0 || hb0 >= (1 << 30)) return fail(s, GH_ERANGE, "hb0");
+  if (hb0 < 0) return fail(s, GH_ERANGE, "hb0");
   int64_t cells = s->rows * s->n;
   for (int64_t x = 0; x < cells; ++x) {
     s->hb[x] = hb0;
@@ -391,13 +406,21 @@ static void stats_add(gh_round_stats *a, const gh_round_stats *b) {
   a->tombstoned += b->tombstoned;
 }
 
-static void one_round(ors *s, gh_round_stats *acc) {
+/* One round; GH_ERANGE (nothing done) when a running member's own heartbeat
+ * is INT32_MAX: Go's int would go on counting (slave/slave.go:446), our
+ * int32 cannot (SPEC.md §2). */
+static int one_round(ors *s, gh_round_stats *acc) {
   int32_t r = s->round + 1;
   int32_t n = s->n;
   int64_t rows = s->rows;
   gh_round_stats st;
   memset(&st, 0, sizeof st);
   apply_events(s, r, &st);
+  for (int64_t i = 0; i < rows && i < n; ++i)
+    if (s->alive[i] && HB(s, i, i) == INT32_MAX) {
+      stats_add(acc, &st); /* the round's events happened; the round did not */
+      return fail(s, GH_ERANGE, "a heartbeat would pass INT32_MAX");
+    }
   memset(s->det_any, 0, rows);
   for (int32_t c = 0; c < n; ++c) {
     s->ndet_cnt[c] = 0;
@@ -534,15 +557,18 @@ static void one_round(ors *s, gh_round_stats *acc) {
   acc->rounds++;
   acc->last_round = r;
   stats_add(acc, &st);
+  return GH_OK;
 }
 
 int or_step(void *h, int32_t rounds, gh_round_stats *stats) {
   ors *s = (ors *)h;
   gh_round_stats acc;
   memset(&acc, 0, sizeof acc);
-  for (int32_t x = 0; x < rounds; ++x) one_round(s, &acc);
+  acc.last_round = s->round;
+  int rc = GH_OK;
+  for (int32_t x = 0; x < rounds && rc == GH_OK; ++x) rc = one_round(s, &acc);
   if (stats) *stats = acc;
-  return GH_OK;
+  return rc;
 }
 
 int or_read_failed(void *h, uint32_t *bitmap, int64_t n_words) {
@@ -589,6 +615,16 @@ int or_lsm(void *h, int32_t obs, int32_t *ids, int32_t *hb, int32_t *ts, int64_t
 int or_merge_list(void *h, int32_t obs, const int32_t *ids, const int32_t *hb, int64_t n, int64_t *merged) {
   ors *s = (ors *)h;
   if (obs < 0 || obs >= s->rows) return fail(s, GH_EINVAL, "observer");
+  uint8_t *seen = (uint8_t *)calloc(s->n, 1);
+  for (int64_t x = 0; x < n; ++x) {
+    int bad = ids[x] < 0 || ids[x] >= s->n ? GH_EINVAL : hb[x] < 0 ? GH_ERANGE : seen[ids[x]] ? GH_EINVAL : 0;
+    if (bad) {
+      free(seen);
+      return fail(s, bad, bad == GH_ERANGE ? "heartbeat below 0" : "member ids out of range or repeated");
+    }
+    seen[ids[x]] = 1;
+  }
+  free(seen);
   int64_t m = 0;
   if (s->alive[obs]) {
     for (int64_t x = 0; x < n; ++x) {

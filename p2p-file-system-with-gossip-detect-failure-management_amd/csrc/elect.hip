@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void k_vote_scan(GhDev d, int cur, const int32
   int32_t first = 0;
   for (int64_t c0 = 0; c0 < d.ncol; c0 += 64) {
     const int64_t c = c0 + lane;
-    const bool pres = c < d.ncol && gh_get(d, cur, i, c) >= 0;
+    const bool pres = c < d.ncol && gh_get(d, cur, i, c, 0).x >= 0;
     const unsigned long long m = __ballot(pres);
     if (m) {
       first = d.n - (int32_t)(d.col0 + c0 + __ffsll((long long)m) - 1);
@@ -33,7 +33,7 @@ __global__ __launch_bounds__(256) void k_vote_scan(GhDev d, int cur, const int32
   if (lane == 0) {
     const int64_t mc = (int64_t)mview[i] - d.col0;
     out[i] = first;
-    out[d.n + i] = (mc >= 0 && mc < d.ncol && gh_get(d, cur, i, mc) >= 0) ? 1 : 0;
+    out[d.n + i] = (mc >= 0 && mc < d.ncol && gh_get(d, cur, i, mc, 0).x >= 0) ? 1 : 0;
   }
 }
 

@@ -4,7 +4,9 @@
 //   k_fill         synthetic full-membership start (BASELINE configs 2-4)
 //   k_pack/unpack  host (hb, ts) rows <-> encoded tiled local columns
 //                  (import/export/lsm; gh_internal.h "cell encoding")
-//   k_freeze       exact ts of rows that stop (crash / leave) into ts[]
+//   k_freeze       exact cells of rows that stop (crash / leave) into the
+//                  frozen store
+//   k_hb_check     the int32 heartbeat bound (slave/slave.go:446, Go int)
 //   k_rowbits      presence bitmap of some rows over the local columns (the
 //                  rows' lists, gathered across shards by the host)
 //   k_leave        LEAVE delivery: slave/slave.go:310-336 -> :232-235
@@ -18,27 +20,27 @@ namespace {
 
 constexpr unsigned kMaxGrid = 65536;
 
-// One wave per row: each lane reads 4 consecutive members (gh_load4), the
-// wave 256 members per step.
+// One wave per row: each lane reads 8 consecutive members (gh_pf8), the wave
+// 512 members per step.
 __global__ __launch_bounds__(256) void k_count(GhDev d, int cur, GhRound p) {
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= p.n) return;
   int cnt = 0;
-  for (int64_t c = lane * 4; c < p.ld; c += 256) {
-    const v4i v = gh_load4(d, cur, i, c);
-    cnt += (v.x >= 0) + (v.y >= 0) + (v.z >= 0) + (v.w >= 0);
-  }
+  for (int64_t c = lane * 8; c < p.ld; c += 512) cnt += __builtin_popcount(gh_pf8(d, cur, i, c) & 0xFFu);
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
   if (lane == 0) d.cntl[i] = cnt;
 }
 
-// Encoded cell (member cg of row i) for external (hb, ts) in the round r
-// about to run.
-__device__ __forceinline__ int32_t encode(int32_t x, int32_t t, int64_t cg, int64_t i, const GhRound& p) {
-  if (x == GH_ABSENT) return GH_ABSENT;
-  const int a = min(max(p.r - t, 0), GH_AGE_CAP);
-  return x >= 0 ? gh_present(x, a, x > 1 && cg != i && t < p.r - p.t_fail) : gh_tomb(a);
+// Cell of an external (hb, ts) for member cg of row i, in a buffer for round r.
+__device__ __forceinline__ GhCell external(int32_t x, int32_t t, int64_t cg, int64_t i, const GhRound& p) {
+  if (x == GH_ABSENT) return gh_absent();
+  if (x < 0) return GhCell{GH_TOMBSTONE, t, false};
+  return GhCell{x, t, gh_flag_for(x, t, cg, i, p.r, p.t_fail)};
+}
+
+__device__ __forceinline__ bool same(const GhCell& a, const GhCell& b) {
+  return a.x == b.x && (a.x == GH_ABSENT || a.ts == b.ts) && (a.x < 0 || a.f == b.f);
 }
 
 // A set of (tile, row) segments: rows (a list, or [row0, row0 + nrows)) x
@@ -57,63 +59,60 @@ struct SegSet {
   }
 };
 
-// Read-modify-write of whole segments: G = min(TW, 64) lanes per segment,
-// CPL = TW / G cells per lane. op(i, c, off, v) returns the new wide value
-// of cell (i, local c) at table offset off. A segment that changed is
-// stored narrow when every cell has a narrow code, else wide. Nothing else
-// in the launch reads the segments it writes.
+// Read-modify-write of whole segments of buffer buf (for round p.r), in
+// k_round's lane shape: a lane owns one 8-cell chunk, SEG = TW/8 lanes a
+// segment. op(i, c, v) returns the new cell (i, local c). A segment that
+// changed (every segment when `force`: rows that start running again must
+// lose their GH_N_FROZEN marks) is stored narrow when every cell has a
+// narrow code, else wide (its old arena slot when it was wide, a fresh one
+// otherwise). Nothing else in the launch reads the segments it writes.
 template <int TW, class Op>
-__global__ __launch_bounds__(256) void k_seg(GhDev d, int buf, SegSet set, const int32_t* gate, Op op) {
+__global__ __launch_bounds__(256) void k_seg(GhDev d, int buf, SegSet set, const int32_t* gate, GhRound p, bool force,
+                                             Op op) {
   if (gate && *gate == 0) return;
-  constexpr int G = TW < 64 ? TW : 64;
-  constexpr int CPL = TW / G;
-  constexpr int SPW = 64 / G;
+  constexpr int SEG = TW / 8;
+  constexpr int RPW = 64 / SEG;
   const int lane = threadIdx.x & 63;
-  const int sub = lane / G, lg = lane % G;
+  const int sub = lane / SEG, lc = lane % SEG;
+  const unsigned long long gmask = (SEG == 64 ? ~0ull : ((1ull << SEG) - 1)) << (sub * SEG);
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int64_t total = set.count();
-  const unsigned long long gmask = (G == 64 ? ~0ull : ((1ull << G) - 1)) << (sub * G);
-  uint16_t* hn = d.hn[buf];
-  int32_t* hw = d.hw[buf];
-  const int32_t* base = d.base[buf];
-  for (int64_t s0 = wave * SPW; s0 < total; s0 += nw * SPW) {
+  for (int64_t s0 = wave * RPW; s0 < total; s0 += nw * RPW) {
     const int64_t sid = s0 + sub;
     const bool valid = sid < total;
     int64_t i = 0, t = 0;
     if (valid) set.at(sid, i, t);
-    int32_t v[CPL];
-    bool changed = false, fit = true;
+    const int64_t c = t * TW + lc * 8;
+    bool changed = force, fit = true;
+    GhCell v[8];
+    uint4 x = {0u, 0u, 0u, 0u}, nx = {0u, 0u, 0u, 0u};
+    if (valid) {
+      x = *reinterpret_cast<const uint4*>(d.hn[buf] + gh_cell(d, i, c));
+      gh_dec8(d, buf, i, c, p.r, x, v);
 #pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-      const int64_t c = t * TW + lg + k * G;
-      const int64_t off = t * d.tstride + i * TW + lg + k * G;
-      int32_t x = GH_ABSENT;
-      if (valid) {
-        const uint32_t nx = hn[off];
-        x = nx == GH_N_WIDE ? hw[off] : gh_dec16(nx, base[c]);
-        const int32_t y = op(i, c, off, x);
-        changed |= y != x;
-        x = y;
-        gh_enc16(x, base[c], fit);
+      for (int j = 0; j < 8; ++j) {
+        const GhCell y = op(i, c + j, v[j]);
+        changed |= !same(y, v[j]);
+        v[j] = y;
       }
-      v[k] = x;
+      nx = gh_enc8(d, buf, c, p.r, v, fit);
     }
     const bool any = (__ballot(changed) & gmask) != 0;
-    const bool narrow = (__ballot(!fit) & gmask) == 0;
+    const bool narrow = (__ballot(valid && !fit) & gmask) == 0;
     if (!valid || !any) continue;
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-      const int64_t c = t * TW + lg + k * G;
-      const int64_t off = t * d.tstride + i * TW + lg + k * G;
-      if (narrow) {
-        bool f = true;
-        hn[off] = (uint16_t)gh_enc16(v[k], base[c], f);
+    int64_t slot = 0;
+    if (!narrow) {
+      // a wide segment keeps its slot (every chunk holds it); else a new one
+      if ((x.x & 0xFFFFu) == GH_N_WIDE) {
+        slot = gh_wide_slot(x.x, x.y);
       } else {
-        hw[off] = v[k];
-        hn[off] = (uint16_t)GH_N_WIDE;
+        int64_t s = lc == 0 ? gh_wide_alloc(d, buf) : 0;
+        slot = __shfl(s, sub * SEG);
       }
     }
+    if (slot < 0) continue;  // arena full: the state is lost (d.err)
+    gh_put8(d, buf, i, c, narrow, nx, slot, v);
   }
 }
 
@@ -121,13 +120,9 @@ struct OpFill {
   GhDev d;
   int32_t hb0, ts0;
   GhRound p;
-  __device__ int32_t operator()(int64_t i, int64_t c, int64_t off, int32_t) const {
-    if (c >= d.ncol) {
-      d.ts[off] = 0;
-      return GH_ABSENT;
-    }
-    d.ts[off] = ts0;
-    return encode(hb0, ts0, d.col0 + c, i, p);
+  __device__ GhCell operator()(int64_t i, int64_t c, const GhCell&) const {
+    if (c >= d.ncol) return gh_absent();
+    return external(hb0, ts0, d.col0 + c, i, p);
   }
 };
 
@@ -136,21 +131,16 @@ struct OpPack {
   const int32_t *hb_rows, *ts_rows;
   int64_t row0;
   GhRound p;
-  __device__ int32_t operator()(int64_t i, int64_t c, int64_t off, int32_t x) const {
-    if (c >= d.ncol) return x;
+  __device__ GhCell operator()(int64_t i, int64_t c, const GhCell& v) const {
+    if (c >= d.ncol) return v;
     const int64_t src = (i - row0) * d.n + d.col0 + c;
-    d.ts[off] = ts_rows[src];
-    return encode(hb_rows[src], ts_rows[src], d.col0 + c, i, p);
+    return external(hb_rows[src], ts_rows[src], d.col0 + c, i, p);
   }
 };
 
 // Fresh joiner processes start with an empty MemberList (SPEC D7).
 struct OpReset {
-  GhDev d;
-  __device__ int32_t operator()(int64_t, int64_t, int64_t off, int32_t) const {
-    d.ts[off] = 0;
-    return GH_ABSENT;
-  }
+  __device__ GhCell operator()(int64_t, int64_t, const GhCell&) const { return gh_absent(); }
 };
 
 // LEAVE from each leaver c to every alive member j of c's list (j != c):
@@ -159,15 +149,15 @@ struct OpReset {
 struct OpLeave {
   GhDev d;
   int32_t nl;
-  __device__ int32_t operator()(int64_t j, int64_t c, int64_t, int32_t x) const {
+  __device__ GhCell operator()(int64_t j, int64_t c, const GhCell& v) const {
     const int q = d.colq[c];
-    if (q < 0 || !d.alive[j] || d.col0 + c == j || !gh_gbit(d, d.rbits, nl, q, j)) return x;
-    if (x >= 0) {
+    if (q < 0 || !d.alive[j] || d.col0 + c == j || !gh_gbit(d, d.rbits, nl, q, j)) return v;
+    if (v.x >= 0) {
       atomicAdd(&d.stats[ST_TOMBSTONED], 1ull);
-      return gh_tomb(gh_age(x));  // keeps its ts (slave/slave.go:280)
+      return GhCell{GH_TOMBSTONE, v.ts, false};  // keeps its ts (slave/slave.go:280)
     }
-    if (x == GH_ABSENT) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], 1ull);
-    return x;
+    if (v.x == GH_ABSENT) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], 1ull);
+    return v;
   }
 };
 
@@ -175,10 +165,11 @@ struct OpLeave {
 // whose column is local (colq[c] >= 0). nd[4] counts this shard's adds.
 struct OpJoinAdd {
   GhDev d;
-  __device__ int32_t operator()(int64_t, int64_t c, int64_t, int32_t x) const {
-    if (d.colq[c] < 0 || x >= 0) return x;
+  GhRound p;
+  __device__ GhCell operator()(int64_t, int64_t c, const GhCell& v) const {
+    if (d.colq[c] < 0 || v.x >= 0) return v;
     atomicAdd(&d.nd[4], 1);
-    return gh_present(0, 0);  // hb 0, ts = now (age 0 in round r)
+    return GhCell{0, p.r, false};  // hb 0, ts = now
   }
 };
 
@@ -189,32 +180,30 @@ struct OpJoinBcast {
   GhDev d;
   int cur;
   int32_t I;
-  __device__ int32_t operator()(int64_t j, int64_t c, int64_t, int32_t x) const {
-    if (c >= d.ncol || j == I || !d.alive[j] || !gh_gbit(d, d.rbits, 1, 0, j)) return x;
-    const int32_t mv = gh_get(d, cur, I, c);
-    if (mv < 0) return x;
-    const int32_t m = gh_hbv(mv);
-    const int32_t e = gh_ext(x);
-    if (e >= GH_ABSENT && m > e) {
+  GhRound p;
+  __device__ GhCell operator()(int64_t j, int64_t c, const GhCell& v) const {
+    if (c >= d.ncol || j == I || !d.alive[j] || !gh_gbit(d, d.rbits, 1, 0, j)) return v;
+    const GhCell m = gh_get(d, cur, I, c, p.r);
+    if (m.x < 0) return v;
+    if (v.x >= GH_ABSENT && m.x > v.x) {
       atomicAdd(&d.stats[ST_MERGED], 1ull);
-      return gh_present(m, 0);  // ts = now: not stale next round
+      return GhCell{m.x, p.r, gh_flag_for(m.x, p.r, d.col0 + c, j, p.r, p.t_fail)};  // ts = now
     }
-    return x;
+    return v;
   }
 };
 
 // MergeMemberList of an external list into row obs at tick p.r - 1 (the last
-// completed round): the cell's age in the coming round p.r is 1. colq[c] =
-// the listed heartbeat of local member c (< -2: not listed).
+// completed round). colq[c] = the listed heartbeat of local member c (< -2:
+// not listed).
 struct OpMergeList {
   GhDev d;
   GhRound p;
-  __device__ int32_t operator()(int64_t obs, int64_t c, int64_t off, int32_t x) const {
+  __device__ GhCell operator()(int64_t obs, int64_t c, const GhCell& v) const {
     const int32_t m = d.colq[c];
-    const int32_t e = gh_ext(x);
-    if (m < -2 || !(e >= GH_ABSENT && m > e)) return x;  // :424-426, :435-438; tombstones blocked (:432-434)
+    if (m < -2 || !(v.x >= GH_ABSENT && m > v.x)) return v;  // :424-426, :435-438; tombstones blocked (:432-434)
     atomicAdd(&d.nd[5], 1);
-    return gh_present(m, 1, gh_flag_for<false>(d, m, 1, d.col0 + c, obs, off, p.r, p.t_fail));
+    return GhCell{m, p.r - 1, gh_flag_for(m, p.r - 1, d.col0 + c, obs, p.r, p.t_fail)};
   }
 };
 
@@ -226,51 +215,53 @@ __global__ void k_scatter(GhDev d, const int32_t* ids, const int32_t* vals, int3
   if (lc >= 0 && lc < d.ncol) d.colq[lc] = vals ? vals[q] : q;
 }
 
-// what = 0: external hb; what = 1: exact ts = r - age where the age has it
-// (alive rows, unsaturated), else the kept ts[].
+// One chunk per thread: what = 0: external hb; what = 1: exported ts
+// (gh_export_ts).
 __global__ __launch_bounds__(256) void k_unpack(GhDev d, int cur, int32_t* dst, int64_t row0, int64_t nrows,
                                                 int what, GhRound p) {
-  const int64_t per_tile = nrows * d.tw, total = nrows * d.ld;
+  const int64_t cpt = d.tw >> 3;  // chunks per segment
+  const int64_t per_tile = nrows * cpt, total = per_tile * d.ntiles;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = idx / per_tile, rem = idx - t * per_tile;
-    const int64_t i = row0 + (rem >> d.lgtw);
-    const int64_t c = (t << d.lgtw) + (rem & (d.tw - 1));
+    const int64_t i = row0 + rem / cpt;
+    const int64_t c = t * d.tw + (rem % cpt) * 8;
     if (c >= d.ncs) continue;
-    const int32_t v = gh_get(d, cur, i, c);
-    int32_t x;
-    if (what == 0)
-      x = gh_ext(v);
-    else if (v != GH_ABSENT && d.alive[i] && gh_age(v) < GH_AGE_CAP)
-      x = p.r - gh_age(v);
-    else
-      x = d.ts[gh_cell(d, i, c)];
-    dst[(i - row0) * d.ncs + c] = x;
+    GhCell v[8];
+    gh_get8(d, cur, i, c, p.r, v);
+    int32_t* o = dst + (i - row0) * d.ncs + c;
+    const int lim = (int)min<int64_t>(8, d.ncs - c);
+    for (int j = 0; j < lim; ++j) o[j] = what == 0 ? v[j].x : gh_export_ts(v[j], p.r, d.tsat != 0);
   }
 }
 
-// A stopped row is frozen while the round counter moves on, so its ages stop
-// meaning anything: keep the exact ts, and store the row wide in BOTH
-// buffers (the round skips it). Flags after values: k_freeze_mark.
+// A stopped row is frozen while the round counter moves on: its exact cells
+// go to the frozen store (slot frow[i], set by the host), then both buffers
+// mark the row GH_N_FROZEN (k_freeze_mark; the round never touches it).
 __global__ __launch_bounds__(256) void k_freeze(GhDev d, int cur, const int32_t* rows, int32_t nr, GhRound p) {
-  const int64_t total = (int64_t)nr * d.ld;
+  const int64_t cpr = d.ld >> 3;  // chunks per row
+  const int64_t total = (int64_t)nr * cpr;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = rows[idx / d.ld], c = idx % d.ld;
-    const int64_t off = gh_cell(d, i, c);
-    const int32_t v = gh_get(d, cur, i, c);
-    if (c < d.ncol && v != GH_ABSENT && gh_age(v) < GH_AGE_CAP) d.ts[off] = p.r - gh_age(v);
-    d.hw[0][off] = v;
-    d.hw[1][off] = v;
+    const int64_t i = rows[idx / cpr], c = (idx % cpr) * 8;
+    GhCell v[8];
+    gh_get8(d, cur, i, c, p.r, v);
+    const int64_t w = (int64_t)d.frow[i] * d.ld + c;
+    *reinterpret_cast<int4*>(d.fzh + w) = int4{v[0].x, v[1].x, v[2].x, v[3].x};
+    *reinterpret_cast<int4*>(d.fzh + w + 4) = int4{v[4].x, v[5].x, v[6].x, v[7].x};
+    *reinterpret_cast<int4*>(d.fzt + w) = int4{v[0].ts, v[1].ts, v[2].ts, v[3].ts};
+    *reinterpret_cast<int4*>(d.fzt + w + 4) = int4{v[4].ts, v[5].ts, v[6].ts, v[7].ts};
   }
 }
 __global__ __launch_bounds__(256) void k_freeze_mark(GhDev d, const int32_t* rows, int32_t nr) {
-  const int64_t total = (int64_t)nr * d.ld;
+  const int64_t cpr = d.ld >> 3;
+  const int64_t total = (int64_t)nr * cpr;
+  const uint32_t m = GH_N_FROZEN | (GH_N_FROZEN << 16);
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t off = gh_cell(d, rows[idx / d.ld], idx % d.ld);
-    d.hn[0][off] = (uint16_t)GH_N_WIDE;
-    d.hn[1][off] = (uint16_t)GH_N_WIDE;
+    const int64_t off = gh_cell(d, rows[idx / cpr], (idx % cpr) * 8);
+    *reinterpret_cast<uint4*>(d.hn[0] + off) = uint4{m, m, m, m};
+    *reinterpret_cast<uint4*>(d.hn[1] + off) = uint4{m, m, m, m};
   }
 }
 
@@ -284,28 +275,42 @@ __global__ __launch_bounds__(256) void k_rowbits(GhDev d, int cur, const int32_t
     const int64_t w = idx - (int64_t)q * d.ncsw;
     const int row = rows[q];
     uint32_t bits = 0;
-    for (int b = 0; b < 32; b += 4) {
+    for (int b = 0; b < 32; b += 8) {
       const int64_t c = w * 32 + b;
       if (c >= d.ncol) break;
-      const v4i v = gh_load4(d, cur, row, c);
-      for (int j = 0; j < 4; ++j)
-        if (c + j < d.ncol && v[j] >= 0) bits |= 1u << (b + j);
+      bits |= (gh_pf8(d, cur, row, c) & 0xFFu) << b;  // padding cells are absent
     }
     out[idx] = bits;
   }
 }
 
-// wide segments of buffer buf (first narrow cell = GH_N_WIDE) -> *out
+// segments of buffer buf: wide -> out[0], frozen -> out[1]
 __global__ __launch_bounds__(256) void k_count_wide(GhDev d, int buf, unsigned long long* out) {
   const int64_t total = d.ntiles * d.n;
-  unsigned long long cnt = 0;
+  unsigned long long cw = 0, cf = 0;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = idx / d.n, i = idx - t * d.n;
-    cnt += d.hn[buf][t * d.tstride + i * d.tw] == GH_N_WIDE;
+    const uint32_t h = d.hn[buf][t * d.tstride + i * d.tw];
+    cw += h == GH_N_WIDE;
+    cf += h == GH_N_FROZEN;
   }
-  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(out, cnt);
+  for (int o = 32; o > 0; o >>= 1) {
+    cw += __shfl_xor(cw, o);
+    cf += __shfl_xor(cf, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (cw) atomicAdd(out, cw);
+    if (cf) atomicAdd(out + 1, cf);
+  }
+}
+
+// an alive row whose own heartbeat is INT32_MAX (its column is local)
+__global__ __launch_bounds__(256) void k_hb_check(GhDev d, int cur, int32_t* flag, GhRound p) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d.ncol) return;
+  const int64_t i = d.col0 + c;
+  if (i < d.n && d.alive[i] && gh_get(d, cur, i, c, p.r).x == INT32_MAX) *flag = 1;
 }
 
 // base[buf][c] = v for every local column
@@ -321,19 +326,23 @@ unsigned grid_for(int64_t work) {
 }  // namespace
 
 template <class Op>
-static void seg_launch(const GhDev& d, int buf, SegSet set, const int32_t* gate, Op op, hipStream_t s) {
+static void seg_launch(const GhDev& d, int buf, SegSet set, const int32_t* gate, const GhRound& p, Op op,
+                       hipStream_t s, bool force = false) {
   const int64_t segs = set.nrows * set.ntl;
   if (segs == 0) return;
-  const int64_t spw = d.tw < 64 ? 64 / d.tw : 1;
+  const int64_t spw = 64 / (d.tw / 8);  // segments per wave
   const unsigned grid = grid_for((segs + spw - 1) / spw * 64);
+#define GH_SEG_CASE(TW) \
+  hipLaunchKernelGGL((k_seg<TW, Op>), dim3(grid), dim3(256), 0, s, d, buf, set, gate, p, force, op)
   switch (d.tw) {
-    case 8: hipLaunchKernelGGL((k_seg<8, Op>), dim3(grid), dim3(256), 0, s, d, buf, set, gate, op); break;
-    case 16: hipLaunchKernelGGL((k_seg<16, Op>), dim3(grid), dim3(256), 0, s, d, buf, set, gate, op); break;
-    case 32: hipLaunchKernelGGL((k_seg<32, Op>), dim3(grid), dim3(256), 0, s, d, buf, set, gate, op); break;
-    case 128: hipLaunchKernelGGL((k_seg<128, Op>), dim3(grid), dim3(256), 0, s, d, buf, set, gate, op); break;
-    case 256: hipLaunchKernelGGL((k_seg<256, Op>), dim3(grid), dim3(256), 0, s, d, buf, set, gate, op); break;
-    default: hipLaunchKernelGGL((k_seg<64, Op>), dim3(grid), dim3(256), 0, s, d, buf, set, gate, op); break;
+    case 8: GH_SEG_CASE(8); break;
+    case 16: GH_SEG_CASE(16); break;
+    case 32: GH_SEG_CASE(32); break;
+    case 128: GH_SEG_CASE(128); break;
+    case 256: GH_SEG_CASE(256); break;
+    default: GH_SEG_CASE(64); break;
   }
+#undef GH_SEG_CASE
 }
 
 static SegSet rows_set(const GhDev& d, const int32_t* rows, int64_t row0, int64_t nrows) {
@@ -352,28 +361,29 @@ void launch_count(const GhDev& d, int cur, const GhRound& p, hipStream_t s) {
 
 void launch_fill(const GhDev& d, int cur, int32_t hb0, int32_t ts0, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_setbase, dim3((unsigned)((d.ld + 255) / 256)), dim3(256), 0, s, d, cur, hb0 - GH_BASE_LAG);
-  seg_launch(d, cur, rows_set(d, nullptr, 0, p.n), nullptr, OpFill{d, hb0, ts0, p}, s);
+  seg_launch(d, cur, rows_set(d, nullptr, 0, p.n), nullptr, p, OpFill{d, hb0, ts0, p}, s, true);
 }
 
 void launch_pack(const GhDev& d, int cur, const int32_t* hb_rows, const int32_t* ts_rows, int64_t row0,
                  int64_t nrows, const GhRound& p, hipStream_t s) {
-  seg_launch(d, cur, rows_set(d, nullptr, row0, nrows), nullptr, OpPack{d, hb_rows, ts_rows, row0, p}, s);
+  seg_launch(d, cur, rows_set(d, nullptr, row0, nrows), nullptr, p, OpPack{d, hb_rows, ts_rows, row0, p}, s, true);
 }
 
 void launch_unpack(const GhDev& d, int cur, int32_t* dst_rows, int64_t row0, int64_t nrows, int what,
                    const GhRound& p, hipStream_t s) {
   if (nrows == 0) return;
-  hipLaunchKernelGGL(k_unpack, dim3(grid_for(nrows * d.ld)), dim3(256), 0, s, d, cur, dst_rows, row0, nrows, what, p);
+  hipLaunchKernelGGL(k_unpack, dim3(grid_for(nrows * d.ld / 8)), dim3(256), 0, s, d, cur, dst_rows, row0, nrows, what,
+                     p);
 }
 
 void launch_freeze(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p, hipStream_t s) {
   if (nr == 0) return;
-  hipLaunchKernelGGL(k_freeze, dim3(grid_for((int64_t)nr * d.ld)), dim3(256), 0, s, d, cur, rows, nr, p);
-  hipLaunchKernelGGL(k_freeze_mark, dim3(grid_for((int64_t)nr * d.ld)), dim3(256), 0, s, d, rows, nr);
+  hipLaunchKernelGGL(k_freeze, dim3(grid_for((int64_t)nr * d.ld / 8)), dim3(256), 0, s, d, cur, rows, nr, p);
+  hipLaunchKernelGGL(k_freeze_mark, dim3(grid_for((int64_t)nr * d.ld / 8)), dim3(256), 0, s, d, rows, nr);
 }
 
 void launch_count_wide(const GhDev& d, int buf, unsigned long long* out, hipStream_t s) {
-  (void)hipMemsetAsync(out, 0, sizeof(unsigned long long), s);
+  (void)hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), s);
   hipLaunchKernelGGL(k_count_wide, dim3(grid_for(d.ntiles * d.n)), dim3(256), 0, s, d, buf, out);
 }
 
@@ -384,33 +394,35 @@ void launch_rowbits(const GhDev& d, int cur, const int32_t* rows, int32_t nr, hi
 
 void launch_leave(const GhDev& d, int cur, const int32_t* leavers, const int32_t* tiles, int32_t ntl, int32_t nl,
                   const GhRound& p, hipStream_t s) {
-  (void)p;
   if (ntl == 0) return;
   scatter(d, leavers, nullptr, nl, 0xFF, s);
-  seg_launch(d, cur, SegSet{nullptr, 0, d.n, tiles, ntl}, nullptr, OpLeave{d, nl}, s);
+  seg_launch(d, cur, SegSet{nullptr, 0, d.n, tiles, ntl}, nullptr, p, OpLeave{d, nl}, s);
 }
 
 void launch_join_add(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, int32_t introducer,
                      const GhRound& p, hipStream_t s) {
-  (void)p;
   (void)hipMemsetAsync(d.nd + 4, 0, sizeof(int32_t), s);
   scatter(d, joiners, nullptr, nj, 0xFF, s);
-  seg_launch(d, cur, rows_set(d, nullptr, introducer, 1), nullptr, OpJoinAdd{d}, s);
+  seg_launch(d, cur, rows_set(d, nullptr, introducer, 1), nullptr, p, OpJoinAdd{d, p}, s);
 }
 
 void launch_join_bcast(const GhDev& d, int cur, int32_t introducer, const GhRound& p, hipStream_t s) {
-  seg_launch(d, cur, rows_set(d, nullptr, 0, p.n), d.nd + 4, OpJoinBcast{d, cur, introducer}, s);
+  seg_launch(d, cur, rows_set(d, nullptr, 0, p.n), d.nd + 4, p, OpJoinBcast{d, cur, introducer, p}, s);
 }
 
 void launch_join_reset(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p,
                        hipStream_t s) {
-  (void)p;
-  seg_launch(d, cur, rows_set(d, rows, 0, nr), nullptr, OpReset{d}, s);
+  seg_launch(d, cur, rows_set(d, rows, 0, nr), nullptr, p, OpReset{}, s, true);
 }
 
 void launch_merge_list(const GhDev& d, int cur, int32_t obs, const int32_t* ids, const int32_t* hb, int64_t n,
                        const GhRound& p, hipStream_t s) {
   if (n == 0) return;
   scatter(d, ids, hb, (int32_t)n, 0x80, s);
-  seg_launch(d, cur, rows_set(d, nullptr, obs, 1), nullptr, OpMergeList{d, p}, s);
+  seg_launch(d, cur, rows_set(d, nullptr, obs, 1), nullptr, p, OpMergeList{d, p}, s);
+}
+
+void launch_hb_check(const GhDev& d, int cur, int32_t* flag, const GhRound& p, hipStream_t s) {
+  if (d.ncol > 0)
+    hipLaunchKernelGGL(k_hb_check, dim3((unsigned)((d.ncol + 255) / 256)), dim3(256), 0, s, d, cur, flag, p);
 }

@@ -15,42 +15,51 @@
 //   rows contiguous. One tile of the narrow table is N*TW*2 bytes (8 MiB at
 //   N=65,536, TW=64): the round kernel sweeps tile by tile, so its own-row
 //   streams are sequential and every peer gather of a tile stays inside
-//   that slice.
-//   Each cell has one 32-bit meaning (the "wide" encoding):
-//                    present    0 <= v:  heartbeat in bits 0..22, age in
-//                                        23..29, flag in bit 30
-//                    tombstone  v < -1:  INT_MIN | age << 23
-//                    absent     v == -1
-//                  age = (last completed round + 1) - ts, the cell's age in the
-//                  round about to run, saturating at GH_AGE_CAP. flag = the
-//                  row's process detects the member in that round (SPEC §2
-//                  step 4: hb > 1, member != observer, ts < r - T_fail),
-//                  decided when the cell is written, so neither the row nor
-//                  the peers reading it as a snapshot re-derive it. Every
-//                  decision of a round on ts is a flag test or an age
-//                  comparison: a round reads and writes one table, not two.
-//   hn[2]  uint16  double-buffered NARROW table, where the round streams: a
-//                  heartbeat is stored as an offset from a per-column base
-//                  (base[buf][c]):
-//                    present    H<<15 | off<<5 | age   off 0..1022, H = flag
-//                    tombstone  0xFFE0 | age           age 0..30
+//   that slice. A (tile, row) SEGMENT is TW cells; a CHUNK is 8 consecutive
+//   cells (one 16-B lane load).
+//   A cell's meaning is (x, ts, flag): x >= 0 present with heartbeat x (full
+//   int32 range, Go's HeartbeatCount, master/master.go:18), -1 absent, -2
+//   tombstone; ts its exact UpdateTime tick (present / tombstone); flag (on
+//   present cells) = the row's process detects the member in the round the
+//   buffer is for (SPEC §2 step 4: x > 1, member != observer,
+//   ts < r - T_fail), decided when the cell is written, so neither the row
+//   nor the peers reading it as a snapshot re-derive it.
+//   hn[2]  uint16  double-buffered NARROW table, where the round streams;
+//                  buffer b is "for" round r (its ages count to r):
+//                    present    H<<15 | off<<5 | age   off = x - base 0..1022,
+//                                                      age = r - ts 0..31 exact
+//                    tombstone  0xFFE0 | age           age 0..30 (tsat: 30 =
+//                                                      "30 or more")
 //                    absent     0xFFFF
 //                  Visible (present, unflagged) cells are the non-negative
 //                  int16 values and compare like their heartbeats, so a
 //                  snapshot merge is a packed 16-bit max.
-//   hw[2]  int32   the wide encoding, for (tile, row) segments that a narrow
-//                  cell cannot hold (heartbeat outside [base, base+1022],
-//                  saturated tombstone) and for stopped rows (kept wide and
-//                  identical in both buffers: the round never touches them).
-//                  Every narrow cell of such a segment holds GH_N_WIDE, a code
-//                  no narrow cell has, so any reader finds the segment's
-//                  encoding from the cell it reads.
+//                  A segment that a narrow code cannot hold (x outside
+//                  [base, base + 1022], age past the field, a future ts) is
+//                  WIDE: cell 0 of each of its chunks holds GH_N_WIDE and
+//                  cells 1, 2 the segment's slot in the buffer's wide arena;
+//                  the segment of a stopped (crashed / left) row holds
+//                  GH_N_FROZEN in every cell: its exact cells are in the
+//                  frozen store, identical for both buffers (the round never
+//                  touches a stopped row).
 //   base[2] int32  per local column: base of buf's narrow cells. The round
 //                  sets base[next][c] = (member c's own heartbeat) - GH_BASE_LAG
 //                  (k_base), so every view of c within GH_BASE_LAG rounds of
 //                  its own counter is narrow.
+//   wide arena (per buffer b): slot s holds a segment's TW cells: wh[b] x,
+//            wt[b] exact ts, wf[b] flags (one byte per chunk, bit j = cell j).
+//            wn[b] = slots in use; the round resets the arena of the buffer
+//            it writes (nothing of a running row survives a round in it).
+//   frozen store: fzh / fzt [slot][ld] exact x / ts of stopped rows, slot =
+//            frow[i] (-1 for running rows); host-managed (events stop and
+//            restart rows between rounds).
+//   tsat = T_cleanup < 30: a tombstone's age is only ever compared with
+//            T_cleanup (cleanFailList, slave/slave.go:490), so every age
+//            past 30 decides the same; narrow tombstones saturate at 30 and
+//            the exported ts of an older tombstone is round + 1 - 30 (SPEC
+//            §1; the oracle exports the same).
 //   Local columns are padded to ld (multiple of 8*TW and 256); padding cells
-//   stay -1.
+//   stay absent.
 //   per row (global): alive, active, und (u8), cntl / cntg (local / global
 //            present count, [N] = |D|; the rounds keep cntl current by
 //            per-segment deltas), post, det_any, inboxes: pull mode
@@ -64,15 +73,15 @@
 
 #include "../../include/gossiphip.h"
 
-#define GH_HB_BITS 23
-#define GH_HB_MAX ((1 << GH_HB_BITS) - 1)  // largest heartbeat a cell holds (saturates)
-#define GH_AGE_CAP 31                      // age saturates here; exact ts is then in ts[]
 #define GH_N_ABSENT 0xFFFFu                // narrow absent
 #define GH_N_TOMB 0xFFE0u                  // narrow tombstone | age
-#define GH_N_WIDE 0x7FFFu                  // narrow cell of a wide segment
+#define GH_N_WIDE 0x7FFFu                  // chunk marker of a wide segment (cells 1, 2: arena slot)
+#define GH_N_FROZEN 0x7FFEu                // every cell of a stopped row (frozen store)
 #define GH_N_OFFMAX 1022                   // largest narrow heartbeat offset
+#define GH_N_AGEMAX 31                     // largest narrow age of a present cell
+#define GH_N_TAGEMAX 30                    // largest narrow age of a tombstone (saturates when tsat)
+#define GH_TSAT_T 30                       // tsat = T_cleanup < GH_TSAT_T
 #define GH_BASE_LAG 1000                   // base = own heartbeat - GH_BASE_LAG
-#define GH_FLAG (1 << 30)                  // detected next round (present cells)
 #define GH_PAD 256               // column padding granule (ld % 256 == 0)
 #ifndef GH_WG_CELLS
 #define GH_WG_CELLS 16384        // round kernel: cells per workgroup tile (rows = GH_WG_CELLS / TW)
@@ -133,15 +142,22 @@ struct GhDev {
   int32_t rank, world;
   int64_t ntiles;   // ld / tw
   uint16_t *hn[2];  // narrow double buffer
-  int32_t *hw[2];   // wide double buffer
   int32_t *base[2]; // [ld] narrow base per buffer
+  // wide arena per buffer: [wcap][tw] x / exact ts, [wcap][tw/8] flag bytes
+  int32_t *wh[2], *wt[2];
+  uint8_t *wf[2];
+  int32_t *wn;      // [2] slots in use per buffer
+  int64_t wcap;     // slots per buffer
+  int32_t *err;     // device-side error (GH_ENOMEM: arena full; GH_ERANGE), 0 = none
+  // frozen store of stopped rows: [fzcap][ld] exact x / ts; frow[i] = slot or -1
+  int32_t *frow, *fzh, *fzt;
+  int32_t tsat;     // T_cleanup < GH_TSAT_T: tombstone ages saturate at 30
   int32_t *colq;    // [ld] scratch: per local column event index / merged value
   int64_t *slow;    // [ntiles * n] round: segments for k_round_slow, tile << 32 | row
   int32_t *slow_n;  // their count
   int32_t *mode;    // k_round variant of the round: 0 lean, 1 storm (k_base)
   int32_t *nstorm;  // storm variant: segments holding flagged or tombstoned cells
   int32_t *nflag;   // [2]: segments written into buffer b holding flagged cells (quirk pre-pass gate)
-  int32_t *ts;
   uint8_t *alive, *active, *det_any, *und;
   int32_t *cntl, *cntg;  // [n + 8]: per-row present counts (local / allreduced), [n] = |D|, [n + 1] = nflag[cur]
   int32_t *post;         // [n]: post-REMOVE present counts of undecided rows (allreduced)
@@ -171,82 +187,141 @@ struct GhDev {
   int64_t io_cap;
 };
 
-// ---- cell encoding --------------------------------------------------------
-__host__ __device__ __forceinline__ int gh_age(int32_t v) { return (v >> GH_HB_BITS) & 0x7F; }
-__host__ __device__ __forceinline__ int32_t gh_hbv(int32_t v) { return v & GH_HB_MAX; }
-__host__ __device__ __forceinline__ int32_t gh_present(int32_t hb, int age, bool flag = false) {
-  return hb | (age << GH_HB_BITS) | (flag ? GH_FLAG : 0);
-}
-__host__ __device__ __forceinline__ int32_t gh_tomb(int age) {
-  return (int32_t)(0x80000000u | ((uint32_t)age << GH_HB_BITS));
-}
-// age one round later (saturating)
-__host__ __device__ __forceinline__ int gh_inc(int a) { return a < GH_AGE_CAP ? a + 1 : GH_AGE_CAP; }
-// external value (>= 0 heartbeat, -1 absent, -2 tombstone)
-__host__ __device__ __forceinline__ int32_t gh_ext(int32_t v) {
-  return v >= 0 ? gh_hbv(v) : (v == GH_ABSENT ? GH_ABSENT : GH_TOMBSTONE);
+// ---- cells -----------------------------------------------------------
+// One cell: x (>= 0 heartbeat, GH_ABSENT, GH_TOMBSTONE), exact ts (present
+// and tombstone; 0 for absent), flag (present cells).
+struct GhCell {
+  int32_t x, ts;
+  bool f;
+};
+__host__ __device__ __forceinline__ GhCell gh_absent() { return GhCell{GH_ABSENT, 0, false}; }
+
+// The flag a present cell (x, ts) of member cg in row i gets when written for
+// round r: a step-4 candidate (slave/slave.go:468-470).
+__host__ __device__ __forceinline__ bool gh_flag_for(int32_t x, int32_t ts, int64_t cg, int64_t i, int32_t r,
+                                                     int32_t t_fail) {
+  return x > 1 && cg != i && (int64_t)ts < (int64_t)r - t_fail;
 }
 
 // Linear index of cell (observer i, LOCAL member column c) in the tiled layout.
 __host__ __device__ __forceinline__ int64_t gh_cell(const GhDev& d, int64_t i, int64_t c) {
   return (c >> d.lgtw) * d.tstride + (i << d.lgtw) + (c & (d.tw - 1));
 }
-
-// ---- narrow <-> wide --------------------------------------------------
-__host__ __device__ __forceinline__ int32_t gh_dec16(uint32_t x, int32_t base) {
-  if (x == GH_N_ABSENT) return GH_ABSENT;
-  const int a = x & 31, f = (x >> 5) & 1023;
-  if (f == 1023) return gh_tomb(a);
-  return gh_present(base + f, a, (x >> 15) != 0);
+// Arena index of cell (slot s, local column c) (the segment's column offset).
+__host__ __device__ __forceinline__ int64_t gh_wcell(const GhDev& d, int64_t s, int64_t c) {
+  return (s << d.lgtw) + (c & (d.tw - 1));
 }
-// narrow code of wide value v; fit &= it has one
-__host__ __device__ __forceinline__ uint32_t gh_enc16(int32_t v, int32_t base, bool& fit) {
-  if (v == GH_ABSENT) return GH_N_ABSENT;
-  const int a = gh_age(v);
-  if (v < 0) {
-    fit &= a < 31;
-    return GH_N_TOMB | (a & 31);
+
+// ---- narrow codes ---------------------------------------------------------
+// Decodes a narrow (non-marker) code of a column with base b in a buffer for
+// round r.
+__host__ __device__ __forceinline__ GhCell gh_dec16(uint32_t h, int32_t b, int32_t r) {
+  if (h == GH_N_ABSENT) return gh_absent();
+  const int a = h & 31, off = (h >> 5) & 1023;
+  if (off == 1023) return GhCell{GH_TOMBSTONE, r - a, false};
+  return GhCell{b + off, r - a, (h >> 15) != 0};
+}
+// Narrow code of cell v in a buffer for round r with column base b; fit &= it
+// has one. tsat: tombstone ages past 30 saturate (SPEC §1).
+__host__ __device__ __forceinline__ uint32_t gh_enc16(const GhCell& v, int32_t b, int32_t r, bool tsat, bool& fit) {
+  if (v.x == GH_ABSENT) return GH_N_ABSENT;
+  int64_t a = (int64_t)r - v.ts;
+  if (v.x < 0) {
+    if (tsat && a > GH_N_TAGEMAX) a = GH_N_TAGEMAX;
+    fit &= a >= 0 && a <= GH_N_TAGEMAX;
+    return GH_N_TOMB | (uint32_t)(a & 31);
   }
-  const int64_t off = (int64_t)gh_hbv(v) - base;
-  fit &= off >= 0 && off <= GH_N_OFFMAX && a <= 31;
-  return ((v & GH_FLAG) ? 0x8000u : 0u) | ((uint32_t)(off & 1023) << 5) | (uint32_t)(a & 31);
+  const int64_t off = (int64_t)v.x - b;
+  fit &= off >= 0 && off <= GH_N_OFFMAX && a >= 0 && a <= GH_N_AGEMAX;
+  return (v.f ? 0x8000u : 0u) | ((uint32_t)(off & 1023) << 5) | (uint32_t)(a & 31);
+}
+// The 16-B chunk of a wide segment (slot s): marker, slot, markers.
+__host__ __device__ __forceinline__ uint4 gh_wide_chunk(int64_t s) {
+  const uint32_t lo = (uint32_t)s & 0xFFFFu, hi = ((uint32_t)s >> 16) & 0xFFFFu;
+  const uint32_t m = GH_N_WIDE | (GH_N_WIDE << 16);
+  return uint4{GH_N_WIDE | (lo << 16), hi | (GH_N_WIDE << 16), m, m};
+}
+__host__ __device__ __forceinline__ int64_t gh_wide_slot(uint32_t w0, uint32_t w1) {
+  return (int64_t)((w0 >> 16) | ((w1 & 0xFFFFu) << 16));
 }
 
-// Cell (i, local c) of buffer buf, wide encoding.
-__device__ __forceinline__ int32_t gh_get(const GhDev& d, int buf, int64_t i, int64_t c) {
-  const int64_t off = gh_cell(d, i, c);
-  const uint32_t x = d.hn[buf][off];
-  return x == GH_N_WIDE ? d.hw[buf][off] : gh_dec16(x, d.base[buf][c]);
+// The 8 cells (i, c..c+7), c % 8 == 0, of buffer buf (for round r); the
+// chunk's narrow codes are x (already loaded).
+// A marker whose slot is out of range (never written by a correct engine)
+// decodes as absent rather than reading outside the arena / store.
+__device__ __forceinline__ void gh_dec8(const GhDev& d, int buf, int64_t i, int64_t c, int32_t r, const uint4& x,
+                                        GhCell out[8]) {
+  const uint32_t h0 = x.x & 0xFFFFu;
+  if ((h0 == GH_N_WIDE && gh_wide_slot(x.x, x.y) >= d.wcap) || (h0 == GH_N_FROZEN && d.frow[i] < 0)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = gh_absent();
+  } else if (h0 == GH_N_WIDE) {
+    const int64_t w = gh_wcell(d, gh_wide_slot(x.x, x.y), c);
+    const int4 a = *reinterpret_cast<const int4*>(d.wh[buf] + w);
+    const int4 b = *reinterpret_cast<const int4*>(d.wh[buf] + w + 4);
+    const int4 ta = *reinterpret_cast<const int4*>(d.wt[buf] + w);
+    const int4 tb = *reinterpret_cast<const int4*>(d.wt[buf] + w + 4);
+    const uint32_t fl = d.wf[buf][w >> 3];
+    const int32_t xs[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const int32_t tss[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = GhCell{xs[j], xs[j] == GH_ABSENT ? 0 : tss[j], ((fl >> j) & 1u) != 0};
+  } else if (h0 == GH_N_FROZEN) {
+    const int64_t w = (int64_t)d.frow[i] * d.ld + c;
+    const int4 a = *reinterpret_cast<const int4*>(d.fzh + w);
+    const int4 b = *reinterpret_cast<const int4*>(d.fzh + w + 4);
+    const int4 ta = *reinterpret_cast<const int4*>(d.fzt + w);
+    const int4 tb = *reinterpret_cast<const int4*>(d.fzt + w + 4);
+    const int32_t xs[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    const int32_t tss[8] = {ta.x, ta.y, ta.z, ta.w, tb.x, tb.y, tb.z, tb.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = GhCell{xs[j], xs[j] == GH_ABSENT ? 0 : tss[j], false};
+  } else {
+    const int32_t* bp = d.base[buf] + c;
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) out[j] = gh_dec16((w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, bp[j], r);
+  }
+}
+__device__ __forceinline__ void gh_get8(const GhDev& d, int buf, int64_t i, int64_t c, int32_t r, GhCell out[8]) {
+  const uint4 x = *reinterpret_cast<const uint4*>(d.hn[buf] + gh_cell(d, i, c));
+  gh_dec8(d, buf, i, c, r, x, out);
 }
 
-typedef int v4i __attribute__((ext_vector_type(4)));
-// Cells (i, c..c+3) of buffer buf (c % 4 == 0), wide encoding.
-__device__ __forceinline__ v4i gh_load4(const GhDev& d, int buf, int64_t i, int64_t c) {
-  const int64_t off = gh_cell(d, i, c);
-  const uint2 x = *reinterpret_cast<const uint2*>(d.hn[buf] + off);
-  if ((x.x & 0xFFFFu) == GH_N_WIDE) return *reinterpret_cast<const v4i*>(d.hw[buf] + off);
-  const v4i b = *reinterpret_cast<const v4i*>(d.base[buf] + c);
-  v4i v;
-  v.x = gh_dec16(x.x & 0xFFFFu, b.x);
-  v.y = gh_dec16(x.x >> 16, b.y);
-  v.z = gh_dec16(x.y & 0xFFFFu, b.z);
-  v.w = gh_dec16(x.y >> 16, b.w);
-  return v;
+// Cell (i, local c) of buffer buf (for round r).
+__device__ __forceinline__ GhCell gh_get(const GhDev& d, int buf, int64_t i, int64_t c, int32_t r) {
+  const int64_t c8 = c & ~(int64_t)7;
+  const uint16_t* np = d.hn[buf] + gh_cell(d, i, c8);
+  const uint2 hd = *reinterpret_cast<const uint2*>(np);
+  const uint32_t h0 = hd.x & 0xFFFFu;
+  if (h0 == GH_N_WIDE) {
+    if (gh_wide_slot(hd.x, hd.y) >= d.wcap) return gh_absent();
+    const int64_t w = gh_wcell(d, gh_wide_slot(hd.x, hd.y), c);
+    const int32_t x = d.wh[buf][w];
+    return GhCell{x, x == GH_ABSENT ? 0 : d.wt[buf][w], ((d.wf[buf][w >> 3] >> (c & 7)) & 1u) != 0};
+  }
+  if (h0 == GH_N_FROZEN) {
+    if (d.frow[i] < 0) return gh_absent();
+    const int64_t w = (int64_t)d.frow[i] * d.ld + c;
+    const int32_t x = d.fzh[w];
+    return GhCell{x, x == GH_ABSENT ? 0 : d.fzt[w], false};
+  }
+  return gh_dec16(np[c & 7], d.base[buf][c], r);
 }
+
 // Presence and flag bits of cells (i, c..c+7) of buffer buf (c % 8 == 0):
 // bit j = present, bit 8 + j = present and flagged. Narrow codes answer
-// directly (no base).
+// directly (no base, no round).
 __device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, int64_t c) {
-  const int64_t off = gh_cell(d, i, c);
-  const uint4 x = *reinterpret_cast<const uint4*>(d.hn[buf] + off);
+  const uint4 x = *reinterpret_cast<const uint4*>(d.hn[buf] + gh_cell(d, i, c));
+  const uint32_t h0 = x.x & 0xFFFFu;
   uint32_t out = 0;
-  if ((x.x & 0xFFFFu) == GH_N_WIDE) {
-    const v4i a = *reinterpret_cast<const v4i*>(d.hw[buf] + off);
-    const v4i b = *reinterpret_cast<const v4i*>(d.hw[buf] + off + 4);
-    const int32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  if (h0 == GH_N_WIDE || h0 == GH_N_FROZEN) {
+    GhCell v[8];
+    gh_dec8(d, buf, i, c, 0, x, v);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-      if (v[j] >= 0) out |= (1u << j) | ((v[j] & GH_FLAG) ? 1u << (8 + j) : 0u);
+      if (v[j].x >= 0) out |= (1u << j) | (v[j].f ? 1u << (8 + j) : 0u);
   } else {
     const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
@@ -258,20 +333,16 @@ __device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, i
   return out;
 }
 // Clears the flag of present cells (i, c + j) for the bits j of m (c % 8 == 0).
+// A stopped row has no flags.
 __device__ __forceinline__ void gh_clearflags8(const GhDev& d, int buf, int64_t i, int64_t c, uint32_t m) {
-  const int64_t off = gh_cell(d, i, c);
-  uint4* np = reinterpret_cast<uint4*>(d.hn[buf] + off);
+  uint4* np = reinterpret_cast<uint4*>(d.hn[buf] + gh_cell(d, i, c));
   uint4 x = *np;
-  if ((x.x & 0xFFFFu) == GH_N_WIDE) {
-    v4i* wp = reinterpret_cast<v4i*>(d.hw[buf] + off);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      v4i v = wp[h];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if ((m >> (4 * h + j)) & 1u) v[j] &= ~GH_FLAG;
-      wp[h] = v;
-    }
+  const uint32_t h0 = x.x & 0xFFFFu;
+  if (h0 == GH_N_FROZEN) return;
+  if (h0 == GH_N_WIDE) {
+    if (gh_wide_slot(x.x, x.y) >= d.wcap) return;
+    uint8_t* fp = d.wf[buf] + (gh_wcell(d, gh_wide_slot(x.x, x.y), c) >> 3);
+    *fp = (uint8_t)(*fp & ~m);
     return;
   }
   uint32_t w[4] = {x.x, x.y, x.z, x.w};
@@ -281,34 +352,52 @@ __device__ __forceinline__ void gh_clearflags8(const GhDev& d, int buf, int64_t 
   *np = uint4{w[0], w[1], w[2], w[3]};
 }
 
-// ts < r - T for a present or tombstoned cell (stored v at table offset off)
-// in round r: the age decides, except for a saturated age when T itself
-// reaches the cap (then the exact ts is in d.ts).
-// EXACT = false is the form for T < GH_AGE_CAP (every realistic timeout):
-// pure register arithmetic, no conditional load in the streaming loops.
-template <bool EXACT = true>
-__device__ __forceinline__ bool gh_stale(const GhDev& d, int32_t v, int64_t off, int32_t r, int32_t T) {
-  const int a = gh_age(v);
-  if constexpr (!EXACT) {
-    return a > T;
-  } else {
-    if (a < GH_AGE_CAP || T < GH_AGE_CAP) return a > T;
-    return d.ts[off] < r - T;
+// Writes 8 cells of one chunk (i, c..c+7) of buffer buf: narrow codes nx
+// when the whole segment is narrow (narrow = the segment-wide decision),
+// else the cells into arena slot `slot` and the chunk's marker.
+__device__ __forceinline__ void gh_put8(const GhDev& d, int buf, int64_t i, int64_t c, bool narrow, const uint4& nx,
+                                        int64_t slot, const GhCell v[8]) {
+  uint4* np = reinterpret_cast<uint4*>(d.hn[buf] + gh_cell(d, i, c));
+  if (narrow) {
+    *np = nx;
+    return;
   }
+  const int64_t w = gh_wcell(d, slot, c);
+  *reinterpret_cast<int4*>(d.wh[buf] + w) = int4{v[0].x, v[1].x, v[2].x, v[3].x};
+  *reinterpret_cast<int4*>(d.wh[buf] + w + 4) = int4{v[4].x, v[5].x, v[6].x, v[7].x};
+  *reinterpret_cast<int4*>(d.wt[buf] + w) = int4{v[0].ts, v[1].ts, v[2].ts, v[3].ts};
+  *reinterpret_cast<int4*>(d.wt[buf] + w + 4) = int4{v[4].ts, v[5].ts, v[6].ts, v[7].ts};
+  uint32_t fl = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fl |= (v[j].x >= 0 && v[j].f) ? 1u << j : 0u;
+  d.wf[buf][w >> 3] = (uint8_t)fl;
+  *np = gh_wide_chunk(slot);
+}
+// Narrow codes of 8 cells for buffer buf (for round r); fit &= all have one.
+__device__ __forceinline__ uint4 gh_enc8(const GhDev& d, int buf, int64_t c, int32_t r, const GhCell v[8], bool& fit) {
+  const int32_t* bp = d.base[buf] + c;
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j >> 1] |= gh_enc16(v[j], bp[j], r, d.tsat != 0, fit) << (16 * (j & 1));
+  return uint4{w[0], w[1], w[2], w[3]};
+}
+// A fresh arena slot of buffer buf (one lane per segment calls it); on
+// overflow the engine's state is lost: err = GH_ENOMEM and -1.
+__device__ __forceinline__ int64_t gh_wide_alloc(const GhDev& d, int buf) {
+  const int64_t s = atomicAdd(&d.wn[buf], 1);
+  if (s >= d.wcap) {
+    atomicExch(d.err, GH_ENOMEM);
+    return -1;
+  }
+  return s;
 }
 
-// The flag of a present cell written for round rn (member cg of row i, exact
-// ts: age < cap ? rn - age : ts[off]).
-template <bool EXACT>
-__device__ __forceinline__ bool gh_flag_for(const GhDev& d, int32_t hb, int age, int64_t cg, int64_t i, int64_t off,
-                                           int32_t rn, int32_t t_fail) {
-  if (hb <= 1 || cg == i) return false;
-  if constexpr (!EXACT) {
-    return age > t_fail;
-  } else {
-    if (age < GH_AGE_CAP || t_fail < GH_AGE_CAP) return age > t_fail;
-    return d.ts[off] < rn - t_fail;
-  }
+// The exported ts of a cell (SPEC §1): 0 for absent; a tombstone older than
+// 30 rounds (tsat) as 30 rounds old (r = the round the buffer is for).
+__host__ __device__ __forceinline__ int32_t gh_export_ts(const GhCell& v, int32_t r, bool tsat) {
+  if (v.x == GH_ABSENT) return 0;
+  if (v.x == GH_TOMBSTONE && tsat && (int64_t)r - v.ts > GH_N_TAGEMAX) return r - GH_N_TAGEMAX;
+  return v.ts;
 }
 
 // Bit of GLOBAL member j in row q of a gathered bitmap [world][nr][ncsw].
@@ -339,9 +428,9 @@ struct GhRound {
   int32_t peer_mode;
   int32_t xmap;       // k_round block->tile map: 0 tile-major, 1 XCD-aware
   int32_t tpw;        // k_round tiles per workgroup (1, 2, 4, 8)
-  int32_t exact;      // T_fail or T_cleanup >= GH_AGE_CAP: every cell by the slow rule (exact ts)
   int32_t qgate;      // quirk pre-pass: 1 = return at once when cntg[n + 1] (flagged segments, all shards) is 0
   int32_t force_storm;  // diagnostics (GH_FORCE_STORM): run the storm variant every round
+  int32_t force_slow;   // diagnostics (GH_FORCE_SLOW): every segment by the per-cell rule
 };
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------
@@ -375,14 +464,18 @@ void launch_fill(const GhDev& d, int cur, int32_t hb0, int32_t ts0, const GhRoun
 void launch_pack(const GhDev& d, int cur, const int32_t* hb_rows, const int32_t* ts_rows, int64_t row0,
                  int64_t nrows, const GhRound& p, hipStream_t s);
 // tiled local columns -> [nrows][ncs] (local column order) of the external hb
-// (what = 0) or the exact ts (what = 1); p.r is the round about to run
+// (what = 0) or the exported ts (what = 1, gh_export_ts); p.r is the round
+// about to run
 void launch_unpack(const GhDev& d, int cur, int32_t* dst_rows, int64_t row0, int64_t nrows, int what,
                    const GhRound& p, hipStream_t s);
-// rows that stop (crash / leave): exact ts of their cells into ts[], rows
-// stored wide in both buffers
+// rows that stop (crash / leave), their frozen-store slots already in frow:
+// exact cells into the store, GH_N_FROZEN in both buffers
 void launch_freeze(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p, hipStream_t s);
-// number of wide segments of buffer buf -> *out (device)
+// segments of buffer buf: wide (arena) -> out[0], frozen -> out[1] (device)
 void launch_count_wide(const GhDev& d, int buf, unsigned long long* out, hipStream_t s);
+// 1 -> *flag if an alive row's own heartbeat is INT32_MAX (the round would
+// overflow it, slave/slave.go:446); *flag is zeroed by the caller
+void launch_hb_check(const GhDev& d, int cur, int32_t* flag, const GhRound& p, hipStream_t s);
 // presence bitmaps of rows[0..nr) over the local columns -> rbits + rank*nr*ncsw
 void launch_rowbits(const GhDev& d, int cur, const int32_t* rows, int32_t nr, hipStream_t s);
 // leavers[0..nl) (global ids); tiles[0..ntl): the distinct local tiles of

@@ -49,10 +49,19 @@ struct Engine {
   int xmap = 1;          // k_round XCD-aware tile map (gh_set_round_variant)
   int tpw = 1;           // k_round tiles per workgroup (GH_ROUND_TPW)
   int force_storm = 0;   // storm variant every round (GH_FORCE_STORM, diagnostics)
+  int force_slow = 0;    // every segment by the per-cell rule (GH_FORCE_SLOW, diagnostics)
   bool timing = false;
   // the current table may hold flags no round kernel counted (import, fill,
   // events, list merges): the next quirk pre-pass runs ungated
   bool qforce = true;
+  // upper bound of every heartbeat in the table (int32 overflow check,
+  // slave/slave.go:446): +1 per round, max of imported / merged values
+  int64_t hb_bound = 0;
+  // frozen store (stopped rows): slot per row (-1 running), free slots
+  std::vector<int32_t> frow;
+  std::vector<int32_t> fz_free;
+  int64_t fzcap = 0;
+  std::string lost;  // non-empty: the device state was lost (arena overflow)
   double timed_ms = 0.0;
   int64_t timed_launches = 0;
   std::vector<hipEvent_t> evs;
@@ -128,8 +137,162 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.xmap = e->xmap;
   p.tpw = e->tpw;
   p.force_storm = e->force_storm;
-  p.exact = e->cfg.t_fail >= GH_AGE_CAP || e->cfg.t_cleanup >= GH_AGE_CAP;
+  p.force_slow = e->force_slow;
   return p;
+}
+
+// Releases one allocation made by dalloc.
+void dfree(Engine* e, void* p) {
+  if (!p) return;
+  auto it = std::find(e->allocs.begin(), e->allocs.end(), p);
+  if (it != e->allocs.end()) e->allocs.erase(it);
+  (void)hipFree(p);
+}
+
+int upload_frow(Engine* e) {
+  HIPCHK(e, hipMemcpyAsync(e->d.frow, e->frow.data(), sizeof(int32_t) * e->n, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+// Frozen-store slots for rows that stop (growing the store), then their
+// exact cells into it and GH_N_FROZEN into both buffers. rows_dev holds the
+// same ids on the device.
+int freeze_rows(Engine* e, const std::vector<int32_t>& rows, const int32_t* rows_dev, const GhRound& p) {
+  if (rows.empty()) return GH_OK;
+  GhDev& d = e->d;
+  int64_t need = 0;
+  for (int32_t i : rows)
+    if (e->frow[i] < 0) need++;
+  if (need > (int64_t)e->fz_free.size()) {
+    const int64_t cap = std::max<int64_t>(e->fzcap + need - (int64_t)e->fz_free.size(),
+                                          std::min<int64_t>(2 * e->fzcap + 16, e->n));
+    int32_t *h = nullptr, *t = nullptr;
+    int rc;
+    if ((rc = dalloc(e, &h, (size_t)cap * e->ld, 0xFF)) || (rc = dalloc(e, &t, (size_t)cap * e->ld, 0))) return rc;
+    if (e->fzcap > 0) {
+      HIPCHK(e, hipMemcpyAsync(h, d.fzh, sizeof(int32_t) * e->fzcap * e->ld, hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(e, hipMemcpyAsync(t, d.fzt, sizeof(int32_t) * e->fzcap * e->ld, hipMemcpyDeviceToDevice, e->stream));
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    dfree(e, d.fzh);
+    dfree(e, d.fzt);
+    d.fzh = h;
+    d.fzt = t;
+    for (int64_t q = cap - 1; q >= e->fzcap; --q) e->fz_free.push_back((int32_t)q);
+    e->fzcap = cap;
+  }
+  for (int32_t i : rows)
+    if (e->frow[i] < 0) {
+      e->frow[i] = e->fz_free.back();
+      e->fz_free.pop_back();
+    }
+  int rc;
+  if ((rc = upload_frow(e))) return rc;
+  launch_freeze(d, e->cur, rows_dev, (int32_t)rows.size(), p, e->stream);
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+// Rows that run again (join of a stopped member, import, init_full) after
+// their segments were rewritten: their frozen-store slots are free.
+int release_rows(Engine* e, const std::vector<int32_t>& rows) {
+  bool any = false;
+  for (int32_t i : rows)
+    if (e->frow[i] >= 0) {
+      e->fz_free.push_back(e->frow[i]);
+      e->frow[i] = -1;
+      any = true;
+    }
+  return any ? upload_frow(e) : GH_OK;
+}
+
+// Device error flag: GH_ENOMEM (wide arena overflow in a round) loses the
+// state; the caller decides what else may be recovered.
+int read_err(Engine* e, int32_t* err) {
+  HIPCHK(e, hipMemcpyAsync(err, e->d.err, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+// The device state is gone after an arena overflow inside a round.
+int check_lost(Engine* e) {
+  if (!e->lost.empty()) return set_err(e, GH_ENOMEM, e->lost);
+  return GH_OK;
+}
+int lose(Engine* e, const char* where) {
+  e->lost = std::string(where) + ": the wide-segment arena overflowed (" + std::to_string(e->d.wcap) +
+            " slots per buffer); the engine state is lost. Raise gh_config.wide_segments.";
+  return set_err(e, GH_ENOMEM, e->lost);
+}
+
+// Slots of the wide arena per buffer (DESIGN.md "Data layout"): the
+// configured count, else every segment when that is small, else 1/32 of
+// them (grown between calls when half full).
+int64_t arena_slots(const gh_config* cfg, int64_t segs, int tw) {
+  if (cfg->wide_segments > 0) return std::min<int64_t>(cfg->wide_segments, segs);
+  const int64_t slot_bytes = (int64_t)tw * 8 + tw / 8;
+  if (2 * segs * slot_bytes <= (int64_t)2 << 30) return segs;
+  return std::max<int64_t>(std::min<int64_t>(segs, 1 << 20), segs / 32);
+}
+
+// Grows both wide arenas to `cap` slots, keeping the current buffer's slots
+// (same indices, so its chunks' slot numbers stay valid).
+int grow_arena(Engine* e, int64_t cap) {
+  GhDev& d = e->d;
+  int32_t used = 0;
+  HIPCHK(e, hipMemcpyAsync(&used, d.wn + e->cur, sizeof used, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  used = (int32_t)std::min<int64_t>(used, d.wcap);
+  const int64_t tw = d.tw;
+  for (int b = 0; b < 2; ++b) {
+    int32_t *h = nullptr, *t = nullptr;
+    uint8_t* f = nullptr;
+    int rc;
+    if ((rc = dalloc(e, &h, (size_t)cap * tw, 0xFF)) || (rc = dalloc(e, &t, (size_t)cap * tw, 0)) ||
+        (rc = dalloc(e, &f, (size_t)cap * tw / 8, 0)))
+      return rc;
+    if (b == e->cur && used > 0) {
+      HIPCHK(e, hipMemcpyAsync(h, d.wh[b], sizeof(int32_t) * used * tw, hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(e, hipMemcpyAsync(t, d.wt[b], sizeof(int32_t) * used * tw, hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(e, hipMemcpyAsync(f, d.wf[b], (size_t)used * tw / 8, hipMemcpyDeviceToDevice, e->stream));
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    dfree(e, d.wh[b]);
+    dfree(e, d.wt[b]);
+    dfree(e, d.wf[b]);
+    d.wh[b] = h;
+    d.wt[b] = t;
+    d.wf[b] = f;
+  }
+  d.wcap = cap;
+  // allocations past the old capacity were refused (never written)
+  HIPCHK(e, hipMemcpyAsync(d.wn + e->cur, &used, sizeof used, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+// Before and between rounds: grow the arena when the current buffer uses
+// more than half of it (all shards take the same decision). *busy = more
+// than a quarter is in use (gh_step then checks after every round).
+int maybe_grow(Engine* e, bool* busy = nullptr) {
+  GhDev& d = e->d;
+  const int64_t segs = d.ntiles * (int64_t)e->n;
+  if (busy) *busy = false;
+  if (d.wcap >= segs) return GH_OK;
+  int32_t used = 0;
+  HIPCHK(e, hipMemcpyAsync(&used, d.wn + e->cur, sizeof used, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (busy) *busy = 4 * (int64_t)used > d.wcap;
+  int32_t* flag = d.wn + 2;
+  int32_t want = 2 * (int64_t)used > d.wcap ? 1 : 0;
+  HIPCHK(e, hipMemcpyAsync(flag, &want, sizeof want, hipMemcpyHostToDevice, e->stream));
+  COMMCHK(e, e->comm->allreduce(flag, flag, 1, GH_DT_I32, GH_OP_MAX, e->stream));
+  HIPCHK(e, hipMemcpyAsync(&want, flag, sizeof want, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (!want) return GH_OK;
+  return grow_arena(e, std::min<int64_t>(segs, 2 * d.wcap));
 }
 
 int reset_pending_removes(Engine* e) {
@@ -203,8 +366,7 @@ int process_events(Engine* e, int32_t r) {
   int rc;
   if (!stopped.empty()) {
     if ((rc = upload(e, e->ev_buf, stopped))) return rc;
-    launch_freeze(e->d, e->cur, e->ev_buf, (int32_t)stopped.size(), p, e->stream);
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if ((rc = freeze_rows(e, stopped, e->ev_buf, p))) return rc;
   }
   if ((rc = upload_alive(e))) return rc;
   if (!leavers.empty()) {
@@ -237,6 +399,7 @@ int process_events(Engine* e, int32_t r) {
     if ((rc = upload(e, e->ev_buf, fresh))) return rc;
     launch_join_reset(e->d, e->cur, e->ev_buf, (int32_t)fresh.size(), p, e->stream);
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if ((rc = release_rows(e, fresh))) return rc;
   }
   if ((rc = upload_alive(e))) return rc;
   const int32_t I = e->cfg.introducer;
@@ -314,7 +477,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
       (cfg->peer_mode != GH_PEER_PULL && cfg->peer_mode != GH_PEER_RING) ||
       (cfg->detect_mode != GH_DETECT_CANONICAL && cfg->detect_mode != GH_DETECT_QUIRK) ||
       cfg->introducer < 0 || cfg->introducer >= cfg->n_members || cfg->master < 0 ||
-      cfg->master >= cfg->n_members || cfg->t_fail < 0 || cfg->t_cleanup < 0)
+      cfg->master >= cfg->n_members || cfg->t_fail < 0 || cfg->t_cleanup < 0 || cfg->wide_segments < 0)
     return GH_EINVAL;
   if (world < 1 || rank < 0 || rank >= world) return GH_EINVAL;
   if (world > 1 && !comm_id) return GH_EINVAL;
@@ -335,12 +498,14 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   e->rank = rank;
   e->world = world;
   e->alive.assign(e->n, 0);
+  e->frow.assign(e->n, -1);
   int tw = cfg->tile_width ? cfg->tile_width : GH_TW_DEFAULT;
   if (const char* v = std::getenv("GH_TILE_W")) tw = std::atoi(v);
   if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_ROUND_XMAP")) e->xmap = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_ROUND_TPW")) e->tpw = std::atoi(v);
   if (const char* v = std::getenv("GH_FORCE_STORM")) e->force_storm = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_FORCE_SLOW")) e->force_slow = std::atoi(v) != 0;
   if (tw != 8 && tw != 16 && tw != 32 && tw != 64 && tw != 128 && tw != 256) {
     delete e;
     return GH_EINVAL;
@@ -389,6 +554,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   d.ncsw = (int32_t)(ncs / 32);
   d.rank = rank;
   d.world = world;
+  d.tsat = cfg->t_cleanup < GH_TSAT_T;
+  d.wcap = arena_slots(cfg, d.ntiles * (int64_t)e->n, tw);
   e->cfg.tile_width = tw;
   const int64_t cells = (int64_t)e->n * e->ld;
   const int64_t nch = e->ld / tw;  // tiles: per-(tile, row) ring / quirk summaries
@@ -397,9 +564,9 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   int rc = GH_OK;
   do {
     if ((rc = dalloc(e, &d.hn[0], cells, 0xFF)) || (rc = dalloc(e, &d.hn[1], cells, 0xFF)) ||
-        (rc = dalloc(e, &d.hw[0], cells, 0xFF)) || (rc = dalloc(e, &d.hw[1], cells, 0xFF)) ||
         (rc = dalloc(e, &d.base[0], e->ld, 0)) || (rc = dalloc(e, &d.base[1], e->ld, 0)) ||
-        (rc = dalloc(e, &d.colq, e->ld, 0)) || (rc = dalloc(e, &d.ts, cells, 0)) ||
+        (rc = dalloc(e, &d.colq, e->ld, 0)) || (rc = dalloc(e, &d.wn, 4, 0)) || (rc = dalloc(e, &d.err, 1, 0)) ||
+        (rc = dalloc(e, &d.frow, e->n, 0xFF)) ||
         (rc = dalloc(e, &d.slow, (size_t)(e->ld / tw) * e->n, 0)) || (rc = dalloc(e, &d.slow_n, 4, 0)) ||
         (rc = dalloc(e, &d.mode, 4, 0)) || (rc = dalloc(e, &d.nstorm, 4, 0)) ||
         (rc = dalloc(e, &d.nflag, 2, 0)))
@@ -428,6 +595,11 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
          (rc = dalloc(e, &d.qcarry, e->n, 0)) || (rc = dalloc(e, &d.qlast, e->n, 0))))
       break;
     if ((rc = dalloc(e, &d.rbits, (size_t)world * 2 * d.ncsw, 0))) break;
+    for (int b = 0; b < 2 && rc == GH_OK; ++b)
+      if ((rc = dalloc(e, &d.wh[b], (size_t)d.wcap * tw, 0xFF)) || (rc = dalloc(e, &d.wt[b], (size_t)d.wcap * tw, 0)) ||
+          (rc = dalloc(e, &d.wf[b], (size_t)d.wcap * tw / 8, 0)))
+        break;
+    if (rc) break;
     e->rbits_rows = 2;
     if ((rc = dalloc(e, &d.cand, e->n, 0)) || (rc = dalloc(e, &d.ncand, 4, 0))) break;
     d.fcap = cfg->max_files;
@@ -503,6 +675,59 @@ int build_inboxes(Engine* e, const GhRound& p) {
     COMMCHK(e, e->comm->allreduce(d.targets, d.targets, 3 * (size_t)e->n, GH_DT_I32, GH_OP_MAX, e->stream));
   launch_inbox(d, p, e->stream);
   HIPCHK(e, hipGetLastError());
+  return GH_OK;
+}
+
+// Runs an encoding launch (pack / fill) of buffer cur until it fits the wide
+// arena: on overflow the arena grows and the launch repeats (both are
+// idempotent rewrites of whole rows).
+template <class F>
+int encode_rows(Engine* e, const char* what, F launch) {
+  const int64_t segs = e->d.ntiles * (int64_t)e->n;
+  for (;;) {
+    launch();
+    HIPCHK(e, hipGetLastError());
+    int32_t err = 0;
+    int rc;
+    if ((rc = read_err(e, &err))) return rc;
+    if (e->world > 1) {  // every shard grows together
+      int32_t* flag = e->d.wn + 2;
+      HIPCHK(e, hipMemcpyAsync(flag, &err, sizeof err, hipMemcpyHostToDevice, e->stream));
+      COMMCHK(e, e->comm->allreduce(flag, flag, 1, GH_DT_I32, GH_OP_MAX, e->stream));
+      HIPCHK(e, hipMemcpyAsync(&err, flag, sizeof err, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+      err = err ? GH_ENOMEM : 0;
+    }
+    if (err == 0) return GH_OK;
+    if (err != GH_ENOMEM || e->d.wcap >= segs) return lose(e, what);
+    HIPCHK(e, hipMemsetAsync(e->d.err, 0, sizeof(int32_t), e->stream));
+    if ((rc = grow_arena(e, std::min<int64_t>(segs, 2 * e->d.wcap)))) return rc;
+  }
+}
+
+// Buffer cur emptied (all absent narrow, arena reset) before a whole-table
+// rewrite.
+int clear_table(Engine* e) {
+  GhDev& d = e->d;
+  HIPCHK(e, hipMemsetAsync(d.hn[e->cur], 0xFF, sizeof(uint16_t) * (size_t)e->n * e->ld, e->stream));
+  HIPCHK(e, hipMemsetAsync(d.wn + e->cur, 0, sizeof(int32_t), e->stream));
+  HIPCHK(e, hipMemsetAsync(d.err, 0, sizeof(int32_t), e->stream));
+  e->lost.clear();
+  return GH_OK;
+}
+
+// Stopped rows of [row0, row0 + n) go to the frozen store, running ones
+// leave it (after their segments were rewritten).
+int settle_rows(Engine* e, int64_t row0, int64_t n, const GhRound& p) {
+  std::vector<int32_t> stopped, running;
+  for (int64_t i = row0; i < row0 + n; ++i) (e->alive[i] ? running : stopped).push_back((int32_t)i);
+  int rc;
+  if ((rc = release_rows(e, running))) return rc;
+  for (size_t b = 0; b < stopped.size(); b += (size_t)e->n) {
+    const std::vector<int32_t> part(stopped.begin() + b, stopped.begin() + std::min(stopped.size(), b + e->n));
+    if ((rc = upload(e, e->ev_buf, part))) return rc;
+    if ((rc = freeze_rows(e, part, e->ev_buf, p))) return rc;
+  }
   return GH_OK;
 }
 
@@ -582,20 +807,41 @@ int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, in
   HIPCHK(e, hipSetDevice(e->cfg.device));
   Staging st;
   int rc;
-  if ((rc = st.alloc(e, sizeof(unsigned long long)))) return rc;
+  if ((rc = st.alloc(e, 2 * sizeof(unsigned long long)))) return rc;
   launch_count_wide(e->d, e->cur, st.as<unsigned long long>(), e->stream);
   HIPCHK(e, hipGetLastError());
-  unsigned long long w = 0;
+  unsigned long long w[2] = {0, 0};
   int32_t sl = 0, mode = 0, ns = 0;
-  HIPCHK(e, hipMemcpyAsync(&w, st.p, sizeof w, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(w, st.p, sizeof w, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipMemcpyAsync(&sl, e->d.slow_n, sizeof sl, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipMemcpyAsync(&mode, e->d.mode, sizeof mode, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipMemcpyAsync(&ns, e->d.nstorm, sizeof ns, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  if (wide_segments) *wide_segments = (int64_t)w;
+  if (wide_segments) *wide_segments = (int64_t)(w[0] + w[1]);
   if (slow_segments) *slow_segments = sl;
   if (storm_mode) *storm_mode = mode;
   if (storm_segments) *storm_segments = ns;
+  return GH_OK;
+}
+
+int gh_memory_info(void* h, int64_t* device_bytes, int64_t* wide_used, int64_t* wide_cap, int64_t* frozen_rows) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  const GhDev& d = e->d;
+  int32_t used = 0;
+  HIPCHK(e, hipMemcpyAsync(&used, d.wn + e->cur, sizeof used, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (device_bytes) {
+    // the tables (narrow x2, wide arenas x2, frozen store); per-row and
+    // per-column vectors and the file table are counted by hipMemGetInfo
+    // callers, not here
+    const int64_t cells = (int64_t)e->n * e->ld;
+    *device_bytes = 2 * cells * 2 + 2 * d.wcap * ((int64_t)d.tw * 8 + d.tw / 8) + e->fzcap * e->ld * 8;
+  }
+  if (wide_used) *wide_used = std::min<int64_t>(used, d.wcap);
+  if (wide_cap) *wide_cap = d.wcap;
+  if (frozen_rows) *frozen_rows = (int64_t)std::count_if(e->frow.begin(), e->frow.end(), [](int32_t x) { return x >= 0; });
   return GH_OK;
 }
 
@@ -612,14 +858,16 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
   if (!e) return GH_EINVAL;
   if (row0 < 0 || n_rows < 0 || row0 + n_rows > e->n || (n_rows > 0 && (!hb || !ts || !alive)))
     return set_err(e, GH_EINVAL, "row range / null buffer");
+  int64_t hmax = 0;
   for (int64_t x = 0; x < n_rows * e->n; ++x) {
-    if (hb[x] < GH_TOMBSTONE || hb[x] > GH_HB_MAX) return set_err(e, GH_ERANGE, "hb value out of range");
-    if (hb[x] != GH_ABSENT && (int64_t)ts[x] > (int64_t)round + 1)
-      return set_err(e, GH_ERANGE, "ts of a listed member after the round being imported");
+    if (hb[x] < GH_TOMBSTONE) return set_err(e, GH_ERANGE, "hb value below -2");
+    hmax = std::max<int64_t>(hmax, hb[x]);
   }
   HIPCHK(e, hipSetDevice(e->cfg.device));
-  e->qforce = true;
+  const bool full = row0 == 0 && n_rows == e->n;
   int rc;
+  if (!full && (rc = check_lost(e))) return rc;
+  e->qforce = true;
   const GhRound p = round_params(e, round + 1);
   if (n_rows > 0) {
     // host rows -> device staging -> encoded tiled local columns
@@ -628,22 +876,17 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
     if ((rc = sh.alloc(e, bytes)) || (rc = st.alloc(e, bytes))) return rc;
     HIPCHK(e, hipMemcpyAsync(sh.p, hb, bytes, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(st.p, ts, bytes, hipMemcpyHostToDevice, e->stream));
-    launch_pack(e->d, e->cur, sh.as<int32_t>(), st.as<int32_t>(), row0, n_rows, p, e->stream);
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (full && (rc = clear_table(e))) return rc;
+    rc = encode_rows(e, "gh_import_state", [&] {
+      launch_pack(e->d, e->cur, sh.as<int32_t>(), st.as<int32_t>(), row0, n_rows, p, e->stream);
+    });
+    if (rc) return rc;
     std::copy(alive, alive + n_rows, e->alive.begin() + row0);
-    // stopped rows are kept wide in both buffers (the round skips them)
-    std::vector<int32_t> stopped;
-    for (int64_t x = 0; x < n_rows; ++x)
-      if (!alive[x]) stopped.push_back((int32_t)(row0 + x));
-    for (size_t b = 0; b < stopped.size(); b += (size_t)e->n) {
-      const std::vector<int32_t> part(stopped.begin() + b, stopped.begin() + std::min(stopped.size(), b + e->n));
-      if ((rc = upload(e, e->ev_buf, part))) return rc;
-      launch_freeze(e->d, e->cur, e->ev_buf, (int32_t)part.size(), p, e->stream);
-      HIPCHK(e, hipStreamSynchronize(e->stream));
-    }
+    if ((rc = settle_rows(e, row0, n_rows, p))) return rc;
   }
   if ((rc = upload_alive(e))) return rc;
   e->round = round;
+  e->hb_bound = full ? hmax : std::max(e->hb_bound, hmax);
   e->pending.clear();
   if ((rc = reset_pending_removes(e))) return rc;
   launch_count(e->d, e->cur, p, e->stream);
@@ -658,6 +901,7 @@ int gh_export_state(void* h, int32_t* hb, int32_t* ts, uint8_t* alive, int64_t r
   if (row0 < 0 || n_rows < 0 || row0 + n_rows > e->n) return set_err(e, GH_EINVAL, "row range");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   int rc;
+  if ((rc = check_lost(e))) return rc;
   if (n_rows > 0 && hb && (rc = export_table(e, hb, 0, row0, n_rows))) return rc;
   if (n_rows > 0 && ts && (rc = export_table(e, ts, 1, row0, n_rows))) return rc;
   if (alive) std::copy(e->alive.begin() + row0, e->alive.begin() + row0 + n_rows, alive);
@@ -667,8 +911,7 @@ int gh_export_state(void* h, int32_t* hb, int32_t* ts, uint8_t* alive, int64_t r
 int gh_init_full(void* h, int32_t hb0, int32_t ts0, int32_t round) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
-  if (hb0 < 0 || hb0 > GH_HB_MAX) return set_err(e, GH_ERANGE, "hb0 out of range");
-  if ((int64_t)ts0 > (int64_t)round + 1) return set_err(e, GH_ERANGE, "ts0 after the start round");
+  if (hb0 < 0) return set_err(e, GH_ERANGE, "hb0 below 0");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   e->qforce = true;
   std::fill(e->alive.begin(), e->alive.end(), 1);
@@ -677,7 +920,11 @@ int gh_init_full(void* h, int32_t hb0, int32_t ts0, int32_t round) {
   e->round = round;
   e->pending.clear();
   const GhRound p = round_params(e, round + 1);
-  launch_fill(e->d, e->cur, hb0, ts0, p, e->stream);
+  if ((rc = clear_table(e))) return rc;
+  rc = encode_rows(e, "gh_init_full", [&] { launch_fill(e->d, e->cur, hb0, ts0, p, e->stream); });
+  if (rc) return rc;
+  if ((rc = settle_rows(e, 0, e->n, p))) return rc;
+  e->hb_bound = hb0;
   if ((rc = reset_pending_removes(e))) return rc;
   launch_count(e->d, e->cur, p, e->stream);
   HIPCHK(e, hipGetLastError());
@@ -700,6 +947,9 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   Engine* e = static_cast<Engine*>(h);
   if (!e || rounds < 0) return GH_EINVAL;
   HIPCHK(e, hipSetDevice(e->cfg.device));
+  int rc0;
+  bool busy = false;
+  if ((rc0 = check_lost(e)) || (rc0 = maybe_grow(e, &busy))) return rc0;
   HIPCHK(e, hipMemsetAsync(e->d.stats, 0, sizeof(unsigned long long) * ST_COUNT, e->stream));
   if (e->timing && (int64_t)e->evs.size() < 3 * (int64_t)rounds) {
     while ((int64_t)e->evs.size() < 3 * (int64_t)rounds) {
@@ -709,11 +959,29 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     }
   }
   const int32_t first = e->round + 1;
+  int32_t done = 0;
+  int status = GH_OK;
   for (int32_t q = 0; q < rounds; ++q) {
     const int32_t r = e->round + 1;
     int rc;
     if ((rc = process_events(e, r))) return rc;
     const GhRound p = round_params(e, r);
+    if (e->hb_bound >= INT32_MAX) {
+      // a heartbeat may sit at INT32_MAX: the round would overflow Go's
+      // HeartbeatCount (slave/slave.go:446) in our int32; refused (SPEC §2)
+      int32_t* flag = e->d.wn + 2;
+      int32_t hit = 0;
+      HIPCHK(e, hipMemsetAsync(flag, 0, sizeof(int32_t), e->stream));
+      launch_hb_check(e->d, e->cur, flag, p, e->stream);
+      HIPCHK(e, hipGetLastError());
+      COMMCHK(e, e->comm->allreduce(flag, flag, 1, GH_DT_I32, GH_OP_MAX, e->stream));
+      HIPCHK(e, hipMemcpyAsync(&hit, flag, sizeof hit, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+      if (hit) {
+        status = set_err(e, GH_ERANGE, "a running member's heartbeat is INT32_MAX: the round would overflow it");
+        break;
+      }
+    }
     launch_base(e->d, e->cur, e->dcur, p, e->stream);
     if ((rc = decide_active(e, p))) return rc;
     if (e->cfg.detect_mode == GH_DETECT_QUIRK) {
@@ -738,13 +1006,30 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     e->cur ^= 1;
     e->dcur ^= 1;
     e->round = r;
+    e->hb_bound = std::min<int64_t>(INT32_MAX, e->hb_bound + 1);
+    done++;
+    if (busy && q + 1 < rounds) {
+      // a quarter of the arena in use: check and grow after every round, so
+      // only a jump from under 1/4 to over 1/1 in one round can overflow it
+      int32_t err = 0;
+      if ((rc = read_err(e, &err))) return rc;
+      if (err == GH_ENOMEM) return lose(e, "gh_step");
+      if ((rc = maybe_grow(e, &busy))) return rc;
+    }
   }
   unsigned long long st[ST_COUNT];
   COMMCHK(e, e->comm->allreduce(e->d.stats, e->d.stats, ST_COUNT, GH_DT_U64, GH_OP_SUM, e->stream));
   HIPCHK(e, hipMemcpyAsync(st, e->d.stats, sizeof st, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
+  {
+    int32_t err = 0;
+    int rc;
+    if ((rc = read_err(e, &err))) return rc;
+    if (err == GH_ENOMEM) return lose(e, "gh_step");
+    if (err) return set_err(e, err, "device error in a round");
+  }
   if (e->timing) {
-    for (int32_t q = 0; q < rounds; ++q) {
+    for (int32_t q = 0; q < done; ++q) {
       float ms = 0.f;
       float ms2 = 0.f;  // the variant that ran
       HIPCHK(e, hipEventElapsedTime(&ms, e->evs[3 * q], e->evs[3 * q + 1]));
@@ -756,8 +1041,8 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   }
   if (stats) {
     std::memset(stats, 0, sizeof(*stats));
-    stats->rounds = rounds;
-    stats->last_round = rounds ? e->round : first - 1;
+    stats->rounds = done;
+    stats->last_round = done ? e->round : first - 1;
     stats->detections = (int64_t)st[ST_DETECTIONS];
     stats->failed_members = (int64_t)st[ST_FAILED];
     stats->remove_unknown = (int64_t)st[ST_REMOVE_UNKNOWN];
@@ -767,7 +1052,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     stats->released = (int64_t)st[ST_RELEASED];
     stats->tombstoned = (int64_t)st[ST_TOMBSTONED];
   }
-  return GH_OK;
+  return status;
 }
 
 int gh_read_failed(void* h, uint32_t* bitmap, int64_t n_words) {
@@ -839,12 +1124,14 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
     std::vector<int32_t> s(ids, ids + n);
     for (int64_t x = 0; x < n; ++x) {
       if (ids[x] < 0 || ids[x] >= e->n) return set_err(e, GH_EINVAL, "member id out of range");
-      if (hb[x] < 0 || hb[x] > GH_HB_MAX) return set_err(e, GH_ERANGE, "heartbeat out of range");
+      if (hb[x] < 0) return set_err(e, GH_ERANGE, "heartbeat below 0");
     }
     std::sort(s.begin(), s.end());
     if (std::adjacent_find(s.begin(), s.end()) != s.end()) return set_err(e, GH_EINVAL, "member ids must be distinct");
   }
   HIPCHK(e, hipSetDevice(e->cfg.device));
+  int rc0;
+  if ((rc0 = check_lost(e)) || (rc0 = maybe_grow(e))) return rc0;
   e->qforce = true;
   int32_t cnt = 0;
   if (n > 0 && e->alive[observer]) {  // GetMsg runs only while Alive (slave/slave.go:208)
@@ -861,6 +1148,10 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
     launch_count(e->d, e->cur, p, e->stream);  // presence changed: refresh the row counts
     HIPCHK(e, hipMemcpyAsync(&cnt, e->d.nd + 5, sizeof cnt, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    int32_t err = 0;
+    if ((rc = read_err(e, &err))) return rc;
+    if (err) return lose(e, "gh_merge_list");
+    for (int64_t x = 0; x < n; ++x) e->hb_bound = std::max<int64_t>(e->hb_bound, hb[x]);
   }
   if (merged) *merged = cnt;
   return GH_OK;
@@ -1056,6 +1347,19 @@ int gh_read_timing(void* h, double* total_ms, int64_t* launches) {
   if (!e) return GH_EINVAL;
   if (total_ms) *total_ms = e->timed_ms;
   if (launches) *launches = e->timed_launches;
+  return GH_OK;
+}
+
+// Debug hook (not part of the ABI header): raw narrow codes of row `row`,
+// local columns [c0, c0 + n) of the current buffer, and their bases.
+int gh_debug_raw(void* h, int32_t row, int64_t c0, int64_t n, uint16_t* codes, int32_t* bases) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || row < 0 || row >= e->n || c0 < 0 || c0 + n > e->ld) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  for (int64_t c = c0; c < c0 + n; ++c) {
+    HIPCHK(e, hipMemcpy(codes + (c - c0), e->d.hn[e->cur] + gh_cell(e->d, row, c), 2, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(bases + (c - c0), e->d.base[e->cur] + c, 4, hipMemcpyDeviceToHost));
+  }
   return GH_OK;
 }
 

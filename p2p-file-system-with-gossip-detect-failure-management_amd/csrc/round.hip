@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void k_active_pre(GhDev d, int cur, int dcur, 
       const int nd = d.nd[dcur];
       for (int q = 0; q < nd; ++q) {
         const int col = d.dlist[(int64_t)dcur * p.ld + q];
-        rem += (gh_get(d, cur, i, col) >= 0) && removes_at(dc[col], dm[col], i);
+        rem += (gh_get(d, cur, i, col, p.r).x >= 0) && removes_at(dc[col], dm[col], i);
       }
       post = d.cntl[i] - rem;
     }
@@ -92,13 +92,12 @@ __global__ __launch_bounds__(256) void k_active_exact(GhDev d, int cur, int dcur
   const int32_t* dc = d.det_cnt[dcur];
   const int32_t* dm = d.det_min[dcur];
   int cnt = 0;
-  for (int64_t c = lane * 4; c < p.ld; c += 256) {
-    const v4i v = gh_load4(d, cur, i, c);
-    const uint32_t b4 = (d.dbits[c >> 5] >> (c & 31)) & 0xFu;
-    const int x[4] = {v.x, v.y, v.z, v.w};
+  for (int64_t c = lane * 8; c < p.ld; c += 512) {
+    const uint32_t pf = gh_pf8(d, cur, i, c);
+    const uint32_t b8 = (d.dbits[c >> 5] >> (c & 31)) & 0xFFu;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      cnt += x[j] >= 0 && !(((b4 >> j) & 1u) && removes_at(dc[c + j], dm[c + j], i));
+    for (int j = 0; j < 8; ++j)
+      cnt += ((pf >> j) & 1u) && !(((b8 >> j) & 1u) && removes_at(dc[c + j], dm[c + j], i));
   }
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
   if (lane == 0) d.post[i] = cnt;
@@ -138,10 +137,10 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
       const uint32_t w = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
       const int s = (int)w + ((int64_t)w >= i);
       if (!d.alive[s] || !d.active[s]) continue;
-      const int32_t v = gh_get(d, cur, s, t);
+      const GhCell v = gh_get(d, cur, s, t, p.r);
       // i must be in s's snapshot list: present, not detected by s this
       // round and not REMOVE'd at s in step 1.
-      if (v < 0 || (v & GH_FLAG)) continue;
+      if (v.x < 0 || v.f) continue;
       if (ib && removes_at(dci, dmi, s)) continue;
       d.inbox[beg + nv++] = s;
     }
@@ -208,8 +207,8 @@ __global__ __launch_bounds__(256) void k_ring_tiles(GhDev d, int cur, int dcur, 
 __device__ __forceinline__ int64_t ring_find(const GhDev& d, int cur, int dcur, int s, int64_t t, int want) {
   for (int j = 0; j < d.tw; ++j) {
     const int64_t c = t * d.tw + j;
-    const int32_t v = gh_get(d, cur, s, c);
-    if (v < 0 || (v & GH_FLAG)) continue;
+    const GhCell v = gh_get(d, cur, s, c, 0);
+    if (v.x < 0 || v.f) continue;
     if (dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], s)) continue;
     if (want-- == 0) return c;
   }
@@ -233,14 +232,14 @@ __global__ __launch_bounds__(256) void k_ring_count(GhDev d, int cur, int dcur, 
   int64_t total = 0, pos = -1;
   for (int64_t t = 0; t < ntiles; ++t) {
     if (t == own_t) {
-      const int32_t v = gh_get(d, cur, sdr, ls);
-      const bool in = v >= 0 && !(v & GH_FLAG) &&
+      const GhCell v = gh_get(d, cur, sdr, ls, 0);
+      const bool in = v.x >= 0 && !v.f &&
                       !(dbit(d.dbits, ls) && removes_at(d.det_cnt[dcur][ls], d.det_min[dcur][ls], sdr));
       if (in) {
         pos = total;
         for (int64_t c = t * d.tw; c < ls; ++c) {
-          const int32_t x = gh_get(d, cur, sdr, c);
-          pos += x >= 0 && !(x & GH_FLAG) &&
+          const GhCell x = gh_get(d, cur, sdr, c, 0);
+          pos += x.x >= 0 && !x.f &&
                  !(dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], sdr));
         }
       }
@@ -430,6 +429,7 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
     *d.mode = p.force_storm || measure * 32 > d.ntiles * (int64_t)d.n;
     *d.slow_n = 0;
     *d.nstorm = 0;
+    d.wn[cur ^ 1] = 0;  // the round rewrites every running row of the next buffer
     d.nflag[cur ^ 1] = 0;  // counted by this round's writers
     d.cntl[d.n] = d.nd[dcur];  // |D_{r-1}| of this shard next to the local counts, for one allreduce
     d.cntl[d.n + 1] = d.nflag[cur];  // flagged segments of this shard's table (quirk gate, summed)
@@ -438,8 +438,8 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
   int32_t b = d.base[cur][c];
   const int64_t cg = d.col0 + c;
   if (c < d.ncol && cg < p.n) {
-    const int32_t v = gh_get(d, cur, cg, c);
-    if (v >= 0) b = gh_hbv(v) - GH_BASE_LAG;
+    const GhCell v = gh_get(d, cur, cg, c, p.r);
+    if (v.x >= 0) b = v.x - GH_BASE_LAG;
   }
   d.base[cur ^ 1][c] = b;
 }
@@ -570,11 +570,9 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   uint16_t* __restrict__ hnn = d.hn[cur ^ 1];
   const int32_t* __restrict__ bo = d.base[cur];
   const int32_t* __restrict__ bn = d.base[cur ^ 1];
-  const int32_t r = p.r;
   uint32_t n_mrg16 = 0;  // merges x 16
   int n_det = 0, n_rel = 0;
   int n_tomb = 0, n_unk = 0;  // REMOVE: tombstoned / unknown member
-  int32_t* __restrict__ tsb = d.ts;
 
 #pragma unroll 1
   for (int tt = 0; tt < TPW; ++tt) {
@@ -618,7 +616,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   __syncthreads();
   // lean: no REMOVE in the lane; storm: REMOVE applied in the packed path
   // unless a column has a single detector (that row keeps the member)
-  bool lane_ok = !p.exact;
+  bool lane_ok = !p.force_slow;
   if constexpr (STORM) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) lane_ok &= s_rm1[lc * 4 + j] == 0;
@@ -697,7 +695,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       for (int j = 0; j < 4; ++j)
         if (j == (jd >> 1)) {
           const uint32_t hv = (w[j] >> sh) & 0xFFFFu;
-          if (hv >= 0x8000u || (int64_t)bo[l0 + jd] + (hv >> 5) >= GH_HB_MAX ||
+          if (hv >= 0x8000u || (int64_t)bo[l0 + jd] + (hv >> 5) >= INT32_MAX ||
               (STORM && ((s_rm[lc * 4 + j] >> sh) & 1u)))
             bad = true;
           else
@@ -750,7 +748,9 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         const uint32_t ag = x & 0x001F001Fu;
         const uint32_t st = pk_sra15(pk_subs_i16(tcp, ag)) & actm;  // age > T_cleanup (step 5, active rows)
         const uint32_t rel = (ta | fl) & st;                   // absent after step 5 (released, or absent)
-        const uint32_t keep = (ta | fl) & ~st & ~(ab & ~actm); // tombstone next round
+        // tombstone next round (absent cells never are: they merge, even
+        // when T_cleanup reaches the age field and st says "fresh")
+        const uint32_t keep = ((ta & ~ab) | fl) & ~st;
         const uint32_t nowm = ~ta & ~actm;                     // guard rows: present cells stamped now
         acc |= (ag + 0x00020002u) & ~ab & ~nowm & 0x00200020u; // age >= 30 (saturation) or wide marker
         const uint32_t key = ((xr & ~(nowm & 0x80008000u)) | 0x001F001Fu) | rel;  // heartbeat key (absent: -1)
@@ -797,14 +797,13 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
           n_tomb += (int)(tomb16 >> 4);
           n_unk += (int)(unk16 >> 4);
         }
-        if (STORM && (detb | relb)) {  // storms: detections (per column) and released cells' ts
+        if (STORM && (detb | relb)) {  // storms: detections per column, releases
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             if ((detb >> j) & 1u) {
               atomicAdd(&s_dcnt[lc * CPL + j], 1);
               atomicMin(&s_dmin[lc * CPL + j], i);
             }
-            if ((relb >> j) & 1u) tsb[off + j] = r - (int)((w[j >> 1] >> (16 * (j & 1))) & 31u);
           }
           n_det += __builtin_popcount(detb);
           n_rel += __builtin_popcount(relb);
@@ -879,30 +878,14 @@ __global__ __launch_bounds__(256, (STORM && TW >= 32) ? 4 : 1) void k_round(GhDe
   }
 }
 
-// 8 wide values of the row segment cells [off, off + 8) whose narrow codes are
-// x: decoded against base[l0 ..], or read from hw for a wide segment.
-__device__ __forceinline__ void wide8(const int32_t* hw, const int32_t* base, int64_t off, int64_t l0, const v4u& x,
-                                      int32_t out[8]) {
-  if ((x[0] & 0xFFFFu) == GH_N_WIDE) {
-    const v4i a = *reinterpret_cast<const v4i*>(hw + off);
-    const v4i b = *reinterpret_cast<const v4i*>(hw + off + 4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      out[j] = a[j];
-      out[4 + j] = b[j];
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) out[j] = gh_dec16((x[j >> 1] >> (16 * (j & 1))) & 0xFFFFu, base[l0 + j]);
-  }
-}
-
 // The round, slow part: the segments k_round listed, the reference's rule
-// cell by cell on wide values (slave/slave.go:276-286, 414-497; SPEC §2
+// cell by cell on exact cells (slave/slave.go:276-286, 414-497; SPEC §2
 // steps 1-6), with k_round's lane shape (8 consecutive members per lane, SEG
 // lanes per segment, 16-B loads). Reads buffer cur and writes only the
-// listed segments of cur ^ 1. In failure storms most segments come here.
-template <int TW, bool EXACT>
+// listed segments of cur ^ 1, narrow where every cell of a segment has a
+// narrow code, else into a fresh slot of the next buffer's wide arena. In
+// failure storms most segments come here.
+template <int TW>
 __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, GhRound p) {
   constexpr int CPL = 8;
   constexpr int SEG = TW / CPL;
@@ -916,13 +899,7 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
   if (nseg > 0 && blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&d.nflag[cur ^ 1], 1);  // may write flags
   const bool pull = p.peer_mode == GH_PEER_PULL;
   const int32_t r = p.r;
-  const uint16_t* __restrict__ hno = d.hn[cur];
-  uint16_t* __restrict__ hnn = d.hn[cur ^ 1];
-  const int32_t* __restrict__ hwo = d.hw[cur];
-  int32_t* __restrict__ hwn = d.hw[cur ^ 1];
-  const int32_t* __restrict__ bo = d.base[cur];
-  const int32_t* __restrict__ bn = d.base[cur ^ 1];
-  int32_t* __restrict__ tsb = d.ts;
+  const int nxt = cur ^ 1;
   int n_unknown = 0, n_tomb = 0, n_det = 0, n_rel = 0, n_merged = 0;
   for (int64_t s0 = wave * RPW; s0 < nseg; s0 += nw * RPW) {
     const int64_t sid = s0 + sub;
@@ -931,32 +908,29 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
     const int64_t tile = e >> 32;
     const int i = (int)(e & 0xFFFFFFFF);
     const int64_t l0 = tile * TW + lc * CPL;
-    const int c0 = (int)(d.col0 + l0);
-    const int64_t tb = tile * d.tstride + lc * CPL;
-    const int64_t off = tb + (int64_t)i * TW;
+    const int64_t c0 = d.col0 + l0;
     const bool ac = d.active[i];
     const int cnt = gh_in_cnt(d, pull, p.k, i);
     const int64_t beg = gh_in_beg(d, pull, p.k, i);
     const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
     bool fit = true, any_det = false;
     int dpres = 0;  // present after - present before
-    int32_t o32[8];
-    v4u o = {0u, 0u, 0u, 0u};
+    GhCell o[8];
+    uint4 nx = {0u, 0u, 0u, 0u};
     if (valid) {
-      int32_t A[8], X[8];
-      wide8(hwo, bo, off, l0, ldn<false>(hno + off), A);
-      int m[8];
+      GhCell A[8], X[8];
+      gh_get8(d, cur, i, l0, r, A);
+      int64_t m[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) m[j] = -1;
       for (int q = 0; q < cnt; ++q) {
         const int s = d.inbox[beg + q];
-        const int64_t so = tb + (int64_t)s * TW;
-        wide8(hwo, bo, so, l0, ldn<false>(hno + so), X);
+        gh_get8(d, cur, s, l0, r, X);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          // sender snapshot: present and not detected by s (sign and flag
-          // clear), +1 on s's diagonal, not REMOVE'd at s
-          int val = (X[j] & (int)(0x80000000u | GH_FLAG)) ? -1 : gh_hbv(X[j]) + ((c0 + j) == s);
+          // sender snapshot: present and not detected by s, +1 on s's
+          // diagonal (its heartbeat of this round), not REMOVE'd at s
+          int64_t val = (X[j].x < 0 || X[j].f) ? -1 : (int64_t)X[j].x + ((c0 + j) == s);
           if (((my8 >> j) & 1u) && removes_at(d.det_cnt[dcur][l0 + j], d.det_min[dcur][l0 + j], s)) val = -1;
           m[j] = max(m[j], val);
         }
@@ -964,11 +938,9 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int64_t c = c0 + j;
-        const int64_t oj = off + j;
-        const int32_t wv = A[j];
-        int x = gh_ext(wv);
-        const int a = gh_age(wv);  // meaningful unless absent
-        bool now = false;          // ts := r in this round
+        const GhCell v = A[j];
+        int64_t x = v.x;
+        bool now = false;  // ts := r in this round
         // step 1: REMOVE delivery (slave/slave.go:236-240, 276-286)
         if (((my8 >> j) & 1u) && removes_at(d.det_cnt[dcur][l0 + j], d.det_min[dcur][l0 + j], i)) {
           if (x >= 0) {
@@ -982,21 +954,21 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
           if (x >= 0) now = true;  // step 2 guard (:505-507)
         } else {
           if (c == i) {
-            if (x >= 0) {  // step 3 own heartbeat (:443-448)
-              x = min(x + 1, GH_HB_MAX);
+            if (x >= 0) {  // step 3 own heartbeat (:443-448); INT32_MAX is refused before the round
+              if (x == INT32_MAX) atomicExch(d.err, GH_ERANGE);
+              else x += 1;
               now = true;
             }
-          } else if (x >= 0 && (wv & GH_FLAG)) {  // step 4 detect (:468-473), decided at the last write
+          } else if (x >= 0 && v.f) {  // step 4 detect (:468-473), decided at the last write
             x = GH_TOMBSTONE;
             n_det++;
             any_det = true;
             atomicAdd(&d.det_cnt[dcur ^ 1][l0 + j], 1);
             atomicMin(&d.det_min[dcur ^ 1][l0 + j], i);
           }
-          if (x == GH_TOMBSTONE && gh_stale<EXACT>(d, wv, oj, r, p.t_cleanup)) {  // step 5 clean (:490-492)
+          if (x == GH_TOMBSTONE && (int64_t)v.ts < (int64_t)r - p.t_cleanup) {  // step 5 clean (:490-492)
             x = GH_ABSENT;
             n_rel++;
-            if (a < GH_AGE_CAP) tsb[oj] = r - a;  // an absent cell keeps its ts in ts[]
           }
         }
         if (x >= GH_ABSENT && m[j] > x) {  // step 6 merge (:424-426, :435-437)
@@ -1004,31 +976,25 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
           now = true;
           n_merged++;
         }
-        int32_t out = GH_ABSENT;
+        GhCell out = gh_absent();
         if (x != GH_ABSENT) {
-          int an = 1;  // age in round r+1 of a cell stamped now
-          if (!now) {
-            an = gh_inc(a);
-            if (a == GH_AGE_CAP - 1) tsb[oj] = r + 1 - GH_AGE_CAP;  // saturates: keep the exact ts
-          }
-          out = x >= 0 ? gh_present(x, an, gh_flag_for<EXACT>(d, x, an, c, i, oj, r + 1, p.t_fail)) : gh_tomb(an);
+          const int32_t t2 = now ? r : v.ts;
+          out = GhCell{(int32_t)x, t2, x >= 0 && gh_flag_for((int32_t)x, t2, c, i, r + 1, p.t_fail)};
         }
-        o32[j] = out;
-        dpres += (out >= 0) - (wv >= 0);
-        o[j >> 1] |= gh_enc16(out, bn[l0 + j], fit) << (16 * (j & 1));
+        o[j] = out;
+        dpres += (out.x >= 0) - (v.x >= 0);
       }
+      nx = gh_enc8(d, nxt, l0, r + 1, o, fit);
     }
     // a segment is narrow iff every lane of it has narrow codes
     const bool narrow = (__ballot(valid && !fit) & gmask) == 0;
     if (valid) {
-      if (narrow) {
-        stn<false>(hnn + off, o);
-      } else {
-        *reinterpret_cast<v4i*>(hwn + off) = v4i{o32[0], o32[1], o32[2], o32[3]};
-        *reinterpret_cast<v4i*>(hwn + off + 4) = v4i{o32[4], o32[5], o32[6], o32[7]};
-        const uint32_t wm = GH_N_WIDE | (GH_N_WIDE << 16);
-        stn<false>(hnn + off, v4u{wm, wm, wm, wm});
+      int64_t slot = 0;
+      if (!narrow) {
+        const int64_t sl = lc == 0 ? gh_wide_alloc(d, nxt) : 0;
+        slot = __shfl(sl, sub * SEG);
       }
+      if (slot >= 0) gh_put8(d, nxt, i, l0, narrow, nx, slot, o);
     }
 #pragma unroll
     for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) {
@@ -1307,11 +1273,7 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
 
 template <int TW>
 static void round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
-  // timeouts at or above the age cap need the exact ts of saturated cells
-  if (p.exact)
-    hipLaunchKernelGGL((k_round_slow<TW, true>), dim3(2048), dim3(256), 0, s, d, cur, dcur, p);
-  else
-    hipLaunchKernelGGL((k_round_slow<TW, false>), dim3(2048), dim3(256), 0, s, d, cur, dcur, p);
+  hipLaunchKernelGGL((k_round_slow<TW>), dim3(2048), dim3(256), 0, s, d, cur, dcur, p);
 }
 
 

@@ -104,6 +104,13 @@ class Engine:
         self._chk(self.lib.gh_encoding_info(self.h, C.byref(w), C.byref(sl), C.byref(mode), C.byref(ns)))
         return (w.value, sl.value, mode.value, ns.value) if full else (w.value, sl.value)
 
+    def memory_info(self):
+        """dict(device_bytes, wide_used, wide_cap, frozen_rows) of this
+        engine's tables (gh_memory_info)."""
+        v = [C.c_int64() for _ in range(4)]
+        self._chk(self.lib.gh_memory_info(self.h, *[C.byref(x) for x in v]))
+        return dict(zip(("device_bytes", "wide_used", "wide_cap", "frozen_rows"), (x.value for x in v)))
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.gh_destroy(self.h)
@@ -159,6 +166,15 @@ class Engine:
         st = _abi.RoundStats()
         self._chk(self.lib.gh_step(self.h, rounds, C.byref(st)))
         return st.as_dict()
+
+    def step_rc(self, rounds=1):
+        """(return code, stats of the rounds run) without raising on
+        GH_ERANGE: a round that would push a heartbeat past INT32_MAX is
+        refused and stats["rounds"] tells how many ran."""
+        st = _abi.RoundStats()
+        rc = self.lib.gh_step(self.h, rounds, C.byref(st))
+        self._chk(rc, ok=(GH_OK, _abi.GH_ERANGE))
+        return rc, st.as_dict()
 
     def read_failed(self):
         words = (self.n + 31) // 32

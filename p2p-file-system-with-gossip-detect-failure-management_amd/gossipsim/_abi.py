@@ -37,7 +37,8 @@ class Config(C.Structure):
         ("detect_mode", C.c_int32), ("t_fail", C.c_int32), ("t_cleanup", C.c_int32),
         ("min_members", C.c_int32), ("replicas", C.c_int32), ("introducer", C.c_int32),
         ("master", C.c_int32), ("device", C.c_int32), ("tile_width", C.c_int32),
-        ("seed", C.c_uint64), ("max_files", C.c_int64), ("reserved", C.c_int32 * 8),
+        ("seed", C.c_uint64), ("max_files", C.c_int64), ("wide_segments", C.c_int64),
+        ("reserved", C.c_int32 * 6),
     ]
 
 
@@ -93,6 +94,7 @@ SYMBOLS = [
     ("gh_create_sharded", C.c_int, [_P(Config), _i32, _i32, _i32, _vp, _P(_vp)]),
     ("gh_shard_info", C.c_int, [_vp, _P(_i32), _P(_i32), _P(_i64), _P(_i64)]),
     ("gh_encoding_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i32), _P(_i64)]),
+    ("gh_memory_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i64), _P(_i64)]),
 ]
 
 _lib = None

@@ -341,7 +341,8 @@ def worker(rank, world, port, n, rounds, cfg, churn_seed, files_at):
             assert s_cpu == s_mod, f"rank {rank} round {r}: oracle {s_cpu} != model {s_mod}"
             hb, ts, alive = orc.export_state()
             assert np.array_equal(hb[:, sl], m.hb), f"rank {rank} round {r}: hb slice differs"
-            assert np.array_equal(ts[:, sl], m.ts), f"rank {rank} round {r}: ts slice differs"
+            mts = sc.export_view(m.hb, m.ts, r, cfg["t_cleanup"])[1]
+            assert np.array_equal(ts[:, sl], mts), f"rank {rank} round {r}: ts slice differs"
             assert np.array_equal(alive.astype(bool), m.alive)
             bm = orc.read_failed()
             assert m.read_failed() == [c for c in range(n) if bm[c >> 5] >> (c & 31) & 1]

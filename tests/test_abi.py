@@ -37,8 +37,8 @@ def test_every_declared_symbol_is_exported(abi):
 
 
 def test_struct_layouts(abi):
-    # sizes implied by the header (int32 x 12 + u64 + i64 + int32 x 8)
-    assert C.sizeof(abi.Config) == 12 * 4 + 8 + 8 + 8 * 4
+    # sizes implied by the header (int32 x 12 + u64 + i64 x 2 + int32 x 6)
+    assert C.sizeof(abi.Config) == 12 * 4 + 8 + 8 + 8 + 6 * 4
     assert C.sizeof(abi.Event) == 8
     assert C.sizeof(abi.RoundStats) == 10 * 8
     assert C.sizeof(abi.PlanEntry) == 13 * 4
@@ -46,7 +46,7 @@ def test_struct_layouts(abi):
 
 def test_abi_version_and_defaults(abi):
     lib = abi.load()
-    assert lib.gh_abi_version() == 1
+    assert lib.gh_abi_version() == 2
     cfg = abi.Config()
     lib.gh_config_default(C.byref(cfg))
     # reference constants: PERIOD/COOLDOWN 5 s at 1 s rounds, 4 replicas, literal 4

@@ -37,8 +37,7 @@ def run_pair(om, n, rounds, sched, peer_mode, fanout=3, quirk=False, seed=0x5EED
             h2, t2, a2 = ls.dense()
             np.testing.assert_array_equal(a1, a2, err_msg=f"alive r={r}")
             np.testing.assert_array_equal(h1, h2, err_msg=f"hb r={r}")
-            np.testing.assert_array_equal(*[sc.masked(h1, t1)[1], sc.masked(h2, t2)[1]],
-                                          err_msg=f"ts r={r}")
+            np.testing.assert_array_equal(t1, sc.export_view(h2, t2, r, t_cleanup)[1], err_msg=f"ts r={r}")
             bm = orc.read_failed()
             failed = [c for c in range(n) if bm[c >> 5] >> (c & 31) & 1]
             assert failed == ls.last_failed
