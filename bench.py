@@ -24,17 +24,27 @@ healthy steady state with T_fail = T_cleanup = 16 rounds (--t-fail). Parity
 tests cover both regimes.
 
 The JSON line also carries
-  roofline: the round kernel (k_round) — algorithmic bytes per launch
-            2*N*ncols*(k+2): own segment in, k peer segments in, own segment
-            out, 2-byte narrow cells (DESIGN.md "Kernels"; SURVEY.md §8d's
-            4*N^2*(k+4) counted int32 hb and ts streams, which the narrow
-            age-encoded cells no longer move, reported as
-            survey_bytes_per_launch) / its mean duration from HIP events on
-            the engine's stream; peak 8.0 TB/s (MI355X_MICROARCH.md);
-            traffic = HBM-side bytes per launch from the rocprofv3 PMC passes of
-            tools/pmc.sh for this configuration (profiles/, null if none).
+  roofline: the round kernel (k_round) — achieved = its COMPULSORY bytes per
+            launch, 4*N*ncols (every 2-byte narrow cell read once and written
+            once; DESIGN.md "Kernels"), / its mean duration from HIP events on
+            the engine's stream; peak 8.0 TB/s (MI355X_MICROARCH.md), so
+            frac <= 1 is the share of the HBM peak the round moves. The k
+            sender gathers (2*N*ncols*k more bytes, mostly served by L2 and the
+            Infinity Cache) are reported as gather_bytes_per_launch, SURVEY.md
+            §8d's int32 model 4*N^2*(k+4) as survey_bytes_per_launch;
+            traffic = fabric-side bytes per launch from the rocprofv3 PMC
+            passes of tools/pmc.sh for this configuration and warm-up
+            (profiles/, FETCH_SIZE x2 + WRITE_SIZE, the guide's gfx950
+            correction; they include Infinity-Cache hits), null if none.
   cpu_baseline: the CPU restatement (oracle/tablesim.c, "port") timed on this
-            host on a bounded sample (rank 0, N=1 only).
+            host's cores (nproc threads and 1 thread) on the full benched
+            configuration, plus N=4,096 and N=10 rates and the literal list
+            replay (oracle/listsim.py) at N <= 256 (rank 0, N=1 only).
+  secondary: the same engine at the reference's own PERIOD = COOLDOWN = 5
+            rounds (slave/slave.go:24-25; the cluster collapses under the <4
+            guard in round 7), the reference's ring push, and BASELINE config
+            2 (N=4,096, k=3, 1% crash at r=8, 64 rounds: the launch-gap
+            regime).
 """
 from __future__ import annotations
 
@@ -68,17 +78,18 @@ def parse():
     ap.add_argument("--t-fail", type=int, default=16,
                     help="T_fail = T_cleanup in rounds (reference: 5; see module doc)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rows", type=int, default=2048, help="observer rows in the CPU sample")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="timed CPU rounds per rate (at least 1 round)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = nproc (OMP_NUM_THREADS, else the CPU count)")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the reference-constant / ring / C2 legs")
     ap.add_argument("--files", type=int, default=1 << 20,
                     help="placement leg (SURVEY.md §8d C5 files, after the timed rounds; 0 = skip)")
     return ap.parse_args()
 
 
-def pmc_traffic(n, k, world):
-    """HBM-side bytes per k_round launch from the committed PMC summary of
-    the same configuration (tools/pmc.sh -> profiles/*k_round_pmc*.json)."""
+def pmc_traffic(n, k, world, warmup):
+    """Fabric-side bytes per k_round launch from the committed PMC summary of
+    the same configuration and steady state (tools/pmc.sh ->
+    profiles/*k_round_pmc*.json, warm-up >= 5 rounds)."""
     best = None
     for f in sorted((REPO / "profiles").glob("*k_round_pmc*.json")):
         try:
@@ -87,57 +98,157 @@ def pmc_traffic(n, k, world):
             continue
         c = d.get("config", {})
         if (c.get("n") == n and c.get("k") == k and c.get("world", 1) == world and c.get("cell_bytes", 4) == 2
-                and "traffic_bytes" in d):
-            best = {"traffic_bytes": d["traffic_bytes"], "source": f"profiles/{f.name}"}
+                and c.get("warmup", 0) >= min(5, warmup) and "traffic_bytes" in d):
+            best = {"traffic_bytes": d["traffic_bytes"], "source": f"profiles/{f.name}",
+                    "l2_hit_rate": d.get("l2_hit_rate")}
     return best
 
 
-def cpu_rate(n, fanout, seed, rows, seconds, threads, t_fail):
-    """Whole-cluster rounds/s of the C oracle on `rows` observer rows of an
-    N-column table (peers drawn among the sampled rows), scaled by rows/N."""
-    from oracle import oracle as om
-    cfg = om.default_config(n, fanout=fanout, seed=seed, t_fail=t_fail, t_cleanup=t_fail)
-    o = om.Oracle(cfg, rows=rows, threads=threads)
+def progress(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def host_info():
+    import subprocess
+    model = "unknown"
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True).stdout.splitlines():
+            if line.startswith("Model name"):
+                model = line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
+    except (OSError, ValueError):
+        nproc = os.cpu_count() or 1
+    return {"nproc": nproc, "cpu_count": os.cpu_count(), "lscpu_model": model}
+
+
+def oracle_rate(om, n, fanout, seed, t_fail, threads, seconds, peer_mode=0):
+    """Whole-cluster rounds/s of the C oracle on the full N x N tables (full
+    membership start, one untimed round, then >= 1 timed round and at least
+    `seconds` of them)."""
+    cfg = om.default_config(n, fanout=fanout, seed=seed, t_fail=t_fail, t_cleanup=t_fail, peer_mode=peer_mode)
+    o = om.Oracle(cfg, threads=threads)
     o.init_full(2, 0, 0)
-    o.step(1)  # first touch
+    o.step(1)
     done, t0 = 0, time.perf_counter()
     while True:
         o.step(1)
         done += 1
         el = time.perf_counter() - t0
-        if el >= seconds or done >= 50:
+        if el >= seconds:
             break
     o.close()
-    return (rows / n) / (el / done), done, el
+    return done / el, done, el
 
 
-def cpu_baseline(n, fanout, seed, rows, seconds, threads, t_fail):
-    """Time the C oracle (same semantics) on `rows` observer rows of an
-    N-column table; peers are drawn among the sampled rows. Also one core on
-    the same sample (the parallel run plus a 1-core run)."""
+def cpu_baseline(n, fanout, seed, seconds, threads, t_fail):
+    """BASELINE.md "CPU baseline plan": the oracle (the same semantics as the
+    GPU path) on this host: the benched configuration in full with nproc
+    threads and with 1, N=4,096 (k=3) both ways, BASELINE config 1 (N=10,
+    ring push, bootstrap + crash), and the literal list replay at N <= 256."""
+    import numpy as np
     from oracle import oracle as om
+    from oracle.listsim import ListSim
     om.build()
-    threads = threads or min(16, os.cpu_count() or 1)
-    rows_per_s, done, el = cpu_rate(n, fanout, seed, rows, seconds, threads, t_fail)
-    rows1 = rows
-    one, done1, el1 = cpu_rate(n, fanout, seed, rows1, seconds / 2, 1, t_fail)
-    rounds_per_s = rows_per_s
-    cpu = "unknown"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                cpu = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
+    host = host_info()
+    threads = threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or host["nproc"]
+    b_round = 4.0 * n * n * (fanout + 4)  # SURVEY.md §8d int32 bytes per round
+    progress(f"cpu baseline: tablesim N={n}, {threads} threads")
+    full, done, el = oracle_rate(om, n, fanout, seed, t_fail, threads, seconds)
+    progress("cpu baseline: 1 thread")
+    one, done1, el1 = oracle_rate(om, n, fanout, seed, t_fail, 1, 0.0)
+    progress("cpu baseline: N=4096, N=10, listsim")
+    c2, _, _ = oracle_rate(om, 4096, 3, 0x5EED0002, 5, threads, 1.0)
+    c2_1, _, _ = oracle_rate(om, 4096, 3, 0x5EED0002, 5, 1, 1.0)
+    # BASELINE config 1: 10 members join one per round, ring push, member 7
+    # crashes at r=30, 60 rounds (tablesim and the literal list replay)
+    cfg1 = om.default_config(10, peer_mode=om.GH_PEER_RING, seed=0x5EED0001)
+    o1 = om.Oracle(cfg1)
+    t0 = time.perf_counter()
+    for r in range(1, 61):
+        ev = ([(om.GH_EV_JOIN, r - 1)] if r <= 10 else []) + ([(om.GH_EV_CRASH, 7)] if r == 30 else [])
+        if ev:
+            o1.apply_events(ev)
+        o1.step(1)
+    c1 = 60 / (time.perf_counter() - t0)
+    o1.close()
+    ls = {}
+    for m in (64, 128, 256):
+        hb = np.full((m, m), 2, np.int32)
+        sim = ListSim.from_dense(hb, np.zeros((m, m), np.int32), np.ones(m, np.uint8), 0, seed=seed,
+                                 peer_mode="pull", fanout=fanout)
+        t0 = time.perf_counter()
+        sim.step(1)
+        ls[str(m)] = time.perf_counter() - t0
     return {
-        "value": rounds_per_s, "unit": "rounds/s", "cores": threads, "kind": "port",
-        "sample": f"oracle/tablesim.c (OpenMP, {threads} threads) on {rows} of {n} observer rows x {n} columns, "
-                  f"k={fanout} peers drawn among the sampled rows, {done} rounds in {el:.1f} s, scaled by "
-                  f"rows/N to whole-cluster rounds/s; host CPU: {cpu}",
+        "value": full, "unit": "rounds/s", "cores": threads, "kind": "port",
+        "sample": f"oracle/tablesim.c (C, OpenMP, {threads} threads = nproc) on the full benched configuration: "
+                  f"N={n} x {n} int32 hb/ts tables, k={fanout} Philox pull, full membership start, "
+                  f"T_fail={t_fail}; {done} timed rounds in {el:.1f} s after one untimed round",
+        "host": host,
+        "host_gbs": b_round * full / 1e9,
+        "host_gbs_note": "SURVEY.md §8d bytes per round 4*N^2*(k+4) x rounds/s",
         "value_1core": one,
-        "sample_1core": f"the same on 1 thread, {rows1} observer rows, {done1} rounds in {el1:.1f} s",
+        "sample_1core": f"the same on 1 thread: {done1} round(s) in {el1:.1f} s",
+        "c2_n4096_k3_rounds_per_s": c2, "c2_n4096_k3_rounds_per_s_1core": c2_1,
+        "c1_n10_ring_rounds_per_s": c1,
+        "listsim_s_per_round": ls,
+        "listsim_note": "oracle/listsim.py, the literal Go-list replay (pure Python, O(N^3) per round), "
+                        "full membership, one round at each N",
     }
+
+
+def secondary_legs(gs):
+    """The engine at the reference's constants and on BASELINE config 2 (one
+    engine at a time; outside the main timed region)."""
+    out = {}
+
+    def timed(cfg, warmup, steps, sched=None):
+        eng = gs.Engine(cfg)
+        eng.init_full(2, 0, 0)
+        if warmup:
+            eng.step(warmup)
+        eng.set_timing(True)
+        eng.sync()
+        t0 = time.perf_counter()
+        st = {}
+        if sched:
+            for r in range(1, steps + 1):
+                if r in sched:
+                    eng.apply_events(sched[r])
+                s1 = eng.step(1)
+                for k, v in s1.items():
+                    st[k] = st.get(k, 0) + v
+        else:
+            st = eng.step(steps)
+        eng.sync()
+        el = time.perf_counter() - t0
+        ms, launches = eng.read_timing()
+        mode = eng.encoding_info(full=True)[2]
+        eng.close()
+        return {"rounds_per_s": steps / el, "k_round_ms": ms / max(launches, 1), "last_variant": "storm" if mode else
+                "lean", "detections": st["detections"], "active_rows": st["active_rows"]}
+
+    n = 65536
+    progress("secondary legs")
+    out["reference_timeouts"] = dict(
+        workload=f"N={n}, k=4 pull, T_fail=T_cleanup=5 (slave/slave.go:24-25), full start, 12 warm-up rounds "
+                 "(the round-6 detection storm and the round-7 collapse under the <4 guard), 20 timed rounds",
+        **timed(gs.default_config(n, fanout=4, seed=0x5EED0003, t_fail=5, t_cleanup=5), 12, 20))
+    out["ring_reference"] = dict(
+        workload=f"N={n}, the reference's ring push (3 targets, slave/slave.go:515-524), T_fail=T_cleanup=5, "
+                 "full start, 12 warm-up rounds, 20 timed rounds",
+        **timed(gs.default_config(n, seed=0x5EED0003, t_fail=5, t_cleanup=5, peer_mode=gs.GH_PEER_RING), 12, 20))
+    import numpy as np
+    crash = np.random.default_rng(0x5EED0002).choice(np.arange(1, 4096), size=41, replace=False)
+    out["c2_n4096"] = dict(
+        workload="BASELINE config 2: N=4096, k=3 pull, T_fail=T_cleanup=5, full start, 1% crash (41 members) "
+                 "at r=8, 64 rounds timed one gh_step call per round",
+        **timed(gs.default_config(4096, fanout=3, seed=0x5EED0002), 0, 64,
+                sched={8: [(gs.GH_EV_CRASH, int(c)) for c in crash]}))
+    return out
 
 
 def placement_leg(gs, eng, n, files, t_fail):
@@ -286,20 +397,23 @@ def main():
     eng.set_timing(False)
     placement = None
     if world == 1 and args.files > 0:
+        progress("placement and election legs")
         placement = placement_leg(gs, eng, n, args.files, args.t_fail)
         placement["election"] = election_leg(gs, eng, n, args.t_fail)
+    mem = eng.memory_info()
     eng.close()
+    secondary = secondary_legs(gs) if world == 1 and not args.no_secondary else None
 
     if rank != 0:
         return
     value = args.steps / elapsed
-    # algorithmic bytes of one k_round launch (this rank's columns)
-    b_round = 2.0 * n * ncols * (k + 2)        # narrow cells: own in + out, k peers in
-    b_survey = 4.0 * n * ncols * (k + 4)       # SURVEY.md §8d (int32 hb + a ts stream)
-    b_compulsory = 4.0 * n * ncols             # each narrow cell read and written once
-    traffic = pmc_traffic(n, k, world)
+    # bytes of one k_round launch (this rank's columns)
+    b_compulsory = 4.0 * n * ncols             # each 2-byte narrow cell read once and written once
+    b_gather = 2.0 * n * ncols * k             # the k sender segments per cell (L2 / Infinity Cache / HBM)
+    b_survey = 4.0 * n * ncols * (k + 4)       # SURVEY.md §8d (int32 hb + ts streams)
+    traffic = pmc_traffic(n, k, world, args.warmup)
     avg_s = (kern_ms / 1e3) / max(launches, 1)
-    achieved = b_round / avg_s / 1e9
+    achieved = b_compulsory / avg_s / 1e9
     line = {
         "metric": "gossip rounds/sec at N=65,536 members (achieved HBM GB/s, % of peak)",
         "value": value,
@@ -330,22 +444,26 @@ def main():
             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic["traffic_bytes"] if traffic else None,
             "traffic_source": traffic["source"] if traffic else None,
-            "bytes_per_launch": b_round, "survey_bytes_per_launch": b_survey,
+            "bytes_per_launch": b_compulsory, "bytes_model": "compulsory: 4*N*ncols (2-byte cells read + written once)",
             "avg_launch_ms": avg_s * 1e3, "launches": launches,
-            "compulsory_bytes_per_launch": b_compulsory,
-            "compulsory_achieved": b_compulsory / avg_s / 1e9,
+            "gather_bytes_per_launch": b_gather, "gather_achieved": b_gather / avg_s / 1e9,
+            "survey_bytes_per_launch": b_survey,
             "frac_of_measured_copy_peak": achieved / HBM_MEASURED_GBS,
-            # the measured HBM-side bytes over the same duration: above 1 the
-            # algorithmic frac counts sender re-reads the on-die caches serve
+            # fabric-side bytes (FETCH_SIZE x2 + WRITE_SIZE; Infinity-Cache
+            # hits included) over the same duration; traffic / compulsory =
+            # the sender gathers that missed L2
             "traffic_achieved": traffic["traffic_bytes"] / avg_s / 1e9 if traffic else None,
-            "traffic_frac": traffic["traffic_bytes"] / avg_s / 1e9 / HBM_PEAK_GBS if traffic else None,
+            "traffic_over_compulsory": traffic["traffic_bytes"] / b_compulsory if traffic else None,
+            "l2_hit_rate": traffic["l2_hit_rate"] if traffic else None,
         },
         "cpu_baseline": None,
+        "memory": {"table_bytes": mem["device_bytes"], "wide_slots_per_buffer": mem["wide_cap"],
+                   "wide_slots_used": mem["wide_used"]},
+        "secondary": secondary,
         "placement": placement,
     }
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(n, k, args.seed, args.cpu_rows, args.cpu_seconds, args.cpu_threads,
-                                            args.t_fail)
+        line["cpu_baseline"] = cpu_baseline(n, k, args.seed, args.cpu_seconds, args.cpu_threads, args.t_fail)
     print(json.dumps(line), flush=True)
 
 
