@@ -747,6 +747,8 @@ int or_repair(void *h, int32_t observer, gh_plan_entry *plan, int64_t cap, int64
   uint8_t *map = choosable_map(s, cand, M);
   int64_t np = 0;
   int rc = GH_OK;
+  gh_plan_entry last;
+  memset(&last, 0, sizeof last);
   for (int64_t f = 0; f < s->fcap; ++f) {
     if (s->ver[f] < 0) continue;
     int32_t *rp = s->rep + f * R;
@@ -762,8 +764,8 @@ int or_repair(void *h, int32_t observer, gh_plan_entry *plan, int64_t cap, int64
     int len = wl;
     int st = or_init_replica(s, (int32_t)f, rp, &len, cand, M, map); /* :107 */
     if (st != GH_OK) rc = GH_EPLACEMENT_STARVED;
-    if (np < cap) {
-      gh_plan_entry *e = plan + np;
+    {
+      gh_plan_entry *e = np < cap ? plan + np : &last;
       memset(e, 0, sizeof *e);
       e->file = (int32_t)f;
       e->node1 = wl > 0 ? working[0] : -1; /* :120 */
@@ -773,11 +775,18 @@ int or_repair(void *h, int32_t observer, gh_plan_entry *plan, int64_t cap, int64
       for (int q = wl; q < len; ++q) e->new_nodes[nn++] = rp[q]; /* :110-115 */
       for (int q = nn; q < 8; ++q) e->new_nodes[q] = -1;
       e->n_new = nn;
+      if (e != &last) last = *e;
     }
     np++;
   }
   free(cand);
   free(map);
+  /* quirk mode: the plan map is re-made per file (master/master.go:118), so
+   * only the last repaired file's entry is returned */
+  if (s->cfg.detect_mode == GH_DETECT_QUIRK && np > 1) {
+    if (cap > 0) plan[0] = last;
+    np = 1;
+  }
   *n_plan = np;
   return rc;
 }

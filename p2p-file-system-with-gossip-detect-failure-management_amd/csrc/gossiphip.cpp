@@ -1227,10 +1227,18 @@ int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap, int64
   }
   std::sort(all.begin(), all.end(), [](const gh_plan_entry& a, const gh_plan_entry& b) { return a.file < b.file; });
   rc = GH_OK;
-  for (int64_t x = 0; x < np; ++x) {
-    if (x < cap) plan[x] = all[x];
+  for (int64_t x = 0; x < np; ++x)
     if (all[x].status != GH_OK) rc = GH_EPLACEMENT_STARVED;
+  // quirk mode: Update_metadata re-makes its plan map for every repaired
+  // file (master/master.go:118), so it returns the last one only (SPEC D5;
+  // files in ID order stand for Go's map order); the metadata of every file
+  // was repaired all the same
+  if (e->cfg.detect_mode == GH_DETECT_QUIRK && np > 1) {
+    all.erase(all.begin(), all.end() - 1);
+    np = 1;
   }
+  for (int64_t x = 0; x < np; ++x)
+    if (x < cap) plan[x] = all[x];
   *n_plan = np;
   if (rc != GH_OK) set_err(e, rc, "placement starved for some file");
   return rc;

@@ -348,7 +348,7 @@ class ShardGroup:
 
 
 PutResult = namedtuple("PutResult", "file put_or_not replicas version status acks quorum_met")
-GetResult = namedtuple("GetResult", "file replicas version acks quorum_met")
+GetResult = namedtuple("GetResult", "file replicas version acks quorum_met source")
 
 
 class Cluster:
@@ -366,6 +366,7 @@ class Cluster:
         # members whose process is gone (crash; log.Fatal)
         self.elect = elect
         self.master = int(self.engine.cfg.master)
+        self._configured_master = self.master  # INTRODUCER_ADDR: what a fresh process believes
         self.mview = np.full(n, self.master, np.int32)
         self.vote_on = np.zeros(n, bool)
         self.vote_num = np.zeros(n, np.int64)
@@ -382,7 +383,18 @@ class Cluster:
 
     # REPL vocabulary (slave/slave.go:546-613)
     def join(self, member):
+        """A (re)started process joins (Join, slave/slave.go:288-308): it is
+        a fresh Slave (new_slave, :99-112), so a member whose process was
+        gone runs again with self.master = the configured master and its
+        VoteStatus off."""
+        member = int(member)
         self.engine.apply_events([(GH_EV_JOIN, member)])
+        if member in self.dead:
+            self.dead.discard(member)
+            self.mview[member] = self._configured_master
+            self.vote_on[member] = False
+            self.vote_num[member] = 0
+            self.voters[member] = set()
 
     def leave(self, member):
         self.engine.apply_events([(GH_EV_LEAVE, member)])
@@ -443,7 +455,7 @@ class Cluster:
         placed = {}
         if go:
             rep, ver, st = self.engine.put(go)
-            alive = self.engine.alive()
+            alive = self._running()
             for x, f in enumerate(go):
                 r = [int(a) for a in rep[x] if a >= 0]
                 placed[f] = (r, int(ver[x]), int(st[x]), sum(int(alive[a]) for a in r))
@@ -461,13 +473,28 @@ class Cluster:
         version (-1: "No File Found"), and whether a read quorum of replicas
         is alive to answer."""
         rep, ver = self.engine.get_files(files)
-        alive = self.engine.alive()
+        alive = self._running()
         out = []
         for x, f in enumerate(files):
             r = [int(a) for a in rep[x] if a >= 0]
             acks = sum(int(alive[a]) for a in r)
-            out.append(GetResult(int(f), r, int(ver[x]), acks, int(ver[x]) >= 0 and acks >= self.quorum(len(r))))
+            # Get's copy source (slave/slave.go:857-878): the first response
+            # whose local version is <= the master's, or the only one. Under
+            # the store model (SPEC §9) every live replica holds the file at
+            # the master's version, so responses arrive in replica order and
+            # the first live replica is the source.
+            src = next((a for a in r if alive[a]), -1)
+            out.append(GetResult(int(f), r, int(ver[x]), acks, int(ver[x]) >= 0 and acks >= self.quorum(len(r)), src))
         return out
+
+    def _running(self):
+        """The engine's alive vector with the members whose process already
+        ended in a log.Fatal this round masked out (their crash event is
+        applied by the next round)."""
+        alive = self.engine.alive().copy()
+        if self.dead:
+            alive[list(self.dead)] = 0
+        return alive
 
     def ls(self, files):
         """ls (slave/slave.go:892-917): replica list and version per file."""

@@ -113,16 +113,18 @@ def test_cluster_tally_matches_oracle_loop():
         cl.dead = set(rng.choice(n, size=int(rng.integers(0, 3)), replace=False).tolist())
         t = el.Tally(n, master=0)
         for r in range(1, 6):
-            idx = np.flatnonzero(rng.random(n) < 0.7)
+            # voters: running members only (Cluster never lets a gone
+            # process vote); every target keeps its own list length, voter
+            # or not, so majorities reached by remote votes alone are covered
+            dead_before = set(cl.dead)
+            gone = np.zeros(n, bool)
+            gone[list(dead_before)] = True
+            idx = np.flatnonzero((rng.random(n) < 0.7) & ~gone)
             cands = rng.choice(n, size=int(rng.integers(1, 4)), replace=False)
             first = np.where(rng.random(n) < 0.2, np.arange(n), rng.choice(cands, size=n)).astype(np.int32)
-            ln = rng.integers(4, 2 * n, size=n).astype(np.int32)
-            run = np.zeros(n, bool)
-            run[idx] = True
-            dead_before = set(cl.dead)
-            alive = run.astype(np.uint8)
+            ln_run = rng.integers(0, 2 * n, size=n).astype(np.int32)
+            idx = idx[ln_run[idx] >= 4]  # HeartBeat's gate (slave/slave.go:504-511)
             has = np.zeros(n, np.uint8)
-            ln_run = np.where(run, np.maximum(ln, 4), 0).astype(np.int32)
             # the oracle loop, with log.Fatal deaths taking effect in voter order
             elected, fatal, dead = [], [], set(dead_before)
             for i in idx.tolist():

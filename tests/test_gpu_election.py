@@ -212,3 +212,29 @@ def test_rebuild_master_not_in_own_list(gs):
     np.testing.assert_array_equal(v2, ev)
     np.testing.assert_array_equal(r2, er)
     eng.close()
+
+
+def test_crash_join_then_master_crash(gs):
+    """A member that crashed and joins again is a fresh process
+    (new_slave, slave/slave.go:99-112): out of the gone set, master = the
+    configured one, VoteStatus off; when the master then crashes it votes
+    like everyone else and is not taken for a dead process."""
+    n = 32
+    cl = gs.Cluster(n, elect=True, max_files=64, seed=0x5EED0F36, t_fail=8, t_cleanup=8)
+    cl.engine.import_state(*sc.full_state(n), 0)
+    cl.tick(2)
+    cl.put(range(64))
+    cl.crash(5)
+    cl.vote_on[5], cl.vote_num[5] = True, 3  # stale state the dead process held
+    cl.tick(20)
+    assert 5 in cl.dead
+    cl.join(5)
+    assert 5 not in cl.dead and cl.mview[5] == 0 and not cl.vote_on[5] and cl.vote_num[5] == 0
+    cl.tick(12)
+    cl.crash(0)
+    cl.tick(30)
+    assert [m for _, m in cl.elections] == [1] and cl.master == 1
+    # its vote reaches member 1 (no log.Fatal on the vote path for it)
+    assert all(not (m == 5 and why.startswith("revote")) for _, m, why in cl.fatal)
+    g = cl.get([0, 1])
+    assert all(x.source == next((a for a in x.replicas if a not in cl.dead), -1) for x in g)

@@ -361,3 +361,29 @@ def test_c5_churn_rereplication_1m_files(gs, oracle_mod):
     eng.import_state(hb, ts, alive, 0)
     orc.import_state(hb, ts, alive, 0)
     assert c5_run(eng, orc, n, F) > 0
+
+
+def test_quirk_repair_plan_last_file_only(gs, oracle_mod):
+    """Quirk mode: Update_metadata re-makes its plan map per repaired file
+    (master/master.go:118) and returns the last one only, while every file's
+    metadata is repaired (SPEC D5)."""
+    n, F = 64, 300
+    cfg = dict(max_files=F, seed=0x5EED0007, detect_mode=1, t_fail=4, t_cleanup=4)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg))
+    init = sc.full_state(n)
+    eng.import_state(*init, 0)
+    orc.import_state(*init, 0)
+    f = np.arange(F, dtype=np.int32)
+    for x, y in zip(eng.put(f), orc.put(f)):
+        np.testing.assert_array_equal(x, y)
+    ev = [(sc.CRASH, c) for c in sc.crash_ids(n, 0.1, 0x5EED0007)]
+    eng.apply_events(ev)
+    orc.apply_events(ev)
+    for r in range(1, 10):
+        assert eng.step(1) == orc.step(1), r
+    p1, p2 = eng.repair(0), orc.repair(0)
+    assert p1 == p2 and len(p1) == 1
+    for x, y in zip(eng.get_files(f), orc.get_files(f)):
+        np.testing.assert_array_equal(x, y)
+    eng.close()
