@@ -53,6 +53,26 @@
 //   frozen store: fzh / fzt [slot][ld] exact x / ts of stopped rows, slot =
 //            frow[i] (-1 for running rows); host-managed (events stop and
 //            restart rows between rounds).
+//   pl[2]  uint32  SENDER SNAPSHOT PLANE beside each narrow buffer, 4 bits per
+//                  cell in the narrow table's tiled order: word gh_cell(i, c)
+//                  >> 3 holds cells c..c+7 of row i, cell c+2j in bits 4j..
+//                  4j+3 and cell c+2j+1 in bits 16+4j.. (one field per 16-bit
+//                  half, so packed 16-bit min/shift work on it). The code is
+//                  what row i contributes as a sender in the round buffer b is
+//                  for (visible cells, +1 on the diagonal), as u = GH_P_REF +
+//                  1 - offset in base[b]'s frame:
+//                    0      unknown (offset above GH_P_REF, wide segment)
+//                    1..13  visible, offset = GH_P_REF + 1 - code exactly
+//                    14     visible, offset below GH_P_REF - 12
+//                    15     not in the snapshot (absent, tombstone, flagged)
+//                  so the min over senders is the freshest entry, and any
+//                  unknown sender shows as a 0. Written by every round kernel
+//                  for the segments it writes (pull mode, 3 <= k <= 4); read by
+//                  k_round's lean variant, whose sender gathers become one 128-B
+//                  line per 256 members at TW = 256. A wave falls back to the
+//                  16-bit gathers when a min is 0 or 14. pvalid[b] = 0 once
+//                  anything but a round wrote buffer b (events, imports, list
+//                  merges, the quirk pre-pass).
 //   tsat = T_cleanup < 30: a tombstone's age is only ever compared with
 //            T_cleanup (cleanFailList, slave/slave.go:490), so every age
 //            past 30 decides the same; narrow tombstones saturate at 30 and
@@ -82,13 +102,21 @@
 #define GH_N_TAGEMAX 30                    // largest narrow age of a tombstone (saturates when tsat)
 #define GH_TSAT_T 30                       // tsat = T_cleanup < GH_TSAT_T
 #define GH_BASE_LAG 1000                   // base = own heartbeat - GH_BASE_LAG
+#define GH_P_REF (GH_BASE_LAG + 2)         // plane: an active member's own snapshot offset
+#define GH_P_UNK 0u                        // plane: unknown (read the narrow table)
+#define GH_P_OLD 14u                       // plane: visible, offset below GH_P_REF - 12
+#define GH_P_NONE 15u                      // plane: not in the snapshot
 #define GH_PAD 256               // column padding granule (ld % 256 == 0)
 #ifndef GH_WG_CELLS
 #define GH_WG_CELLS 16384        // round kernel: cells per workgroup tile (rows = GH_WG_CELLS / TW)
 #endif
+#ifndef GH_WG_ROWS_WIDE
+#define GH_WG_ROWS_WIDE 256      // round kernel: rows per workgroup at TW >= 128
+#endif
 #define GH_MAXK 8                // max pull fanout
 #define GH_DLIST_MAX 1024        // local |D| above which undecided rows are recounted in full
 #define GH_TW_DEFAULT 64         // default tile width (members per tile)
+#define GH_TW_PLANE 256          // default tile width with the sender plane (pull, k <= 4)
 #define GH_TAG_PEER 0x50454552u
 #define GH_TAG_PLACE 0x504C4143u
 #define GH_MAX_DRAWS (1u << 20)
@@ -142,6 +170,10 @@ struct GhDev {
   int32_t rank, world;
   int64_t ntiles;   // ld / tw
   uint16_t *hn[2];  // narrow double buffer
+  uint32_t *pl[2];  // sender snapshot plane per buffer (null: plane off)
+  int32_t *pvalid;  // [2]: plane of buffer b written by the round that wrote b
+  int32_t *pfb;     // waves of the last round that gathered 16-bit codes with a valid plane
+  uint32_t *pnone;  // [64] all GH_P_NONE: the plane word of an unused inbox slot
   int32_t *base[2]; // [ld] narrow base per buffer
   // wide arena per buffer: [wcap][tw] x / exact ts, [wcap][tw/8] flag bytes
   int32_t *wh[2], *wt[2];
@@ -431,6 +463,7 @@ struct GhRound {
   int32_t qgate;      // quirk pre-pass: 1 = return at once when cntg[n + 1] (flagged segments, all shards) is 0
   int32_t force_storm;  // diagnostics (GH_FORCE_STORM): run the storm variant every round
   int32_t force_slow;   // diagnostics (GH_FORCE_SLOW): every segment by the per-cell rule
+  int32_t plane;        // the round writes the next buffer's sender plane (and may read cur's)
 };
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------

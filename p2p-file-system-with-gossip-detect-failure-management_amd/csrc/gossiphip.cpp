@@ -54,6 +54,10 @@ struct Engine {
   // the current table may hold flags no round kernel counted (import, fill,
   // events, list merges): the next quirk pre-pass runs ungated
   bool qforce = true;
+  // the current table was written by something other than a round: its
+  // sender plane is stale (pvalid[cur] = 0 before the next round)
+  bool pforce = true;
+  int plane = 0;         // sender snapshot plane (pull mode, 3 <= k <= 4; GH_PLANE=0 turns it off)
   // upper bound of every heartbeat in the table (int32 overflow check,
   // slave/slave.go:446): +1 per round, max of imported / merged values
   int64_t hb_bound = 0;
@@ -138,6 +142,7 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.tpw = e->tpw;
   p.force_storm = e->force_storm;
   p.force_slow = e->force_slow;
+  p.plane = e->plane;
   return p;
 }
 
@@ -229,12 +234,12 @@ int lose(Engine* e, const char* where) {
 
 // Slots of the wide arena per buffer (DESIGN.md "Data layout"): the
 // configured count, else every segment when that is small, else 1/32 of
-// them (grown between calls when half full).
+// them, at least 2^26 cells' worth (grown between calls when half full).
 int64_t arena_slots(const gh_config* cfg, int64_t segs, int tw) {
   if (cfg->wide_segments > 0) return std::min<int64_t>(cfg->wide_segments, segs);
   const int64_t slot_bytes = (int64_t)tw * 8 + tw / 8;
   if (2 * segs * slot_bytes <= (int64_t)2 << 30) return segs;
-  return std::max<int64_t>(std::min<int64_t>(segs, 1 << 20), segs / 32);
+  return std::max<int64_t>(std::min<int64_t>(segs, ((int64_t)1 << 26) / tw), segs / 32);
 }
 
 // Grows both wide arenas to `cap` slots, keeping the current buffer's slots
@@ -347,6 +352,7 @@ int allreduce_i32(Engine* e, int32_t* send, int32_t* recv, size_t count) {
 int process_events(Engine* e, int32_t r) {
   if (e->pending.empty()) return GH_OK;
   e->qforce = true;
+  e->pforce = true;
   const GhRound p = round_params(e, r);
   std::vector<gh_event> ev;
   ev.swap(e->pending);
@@ -499,7 +505,11 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   e->world = world;
   e->alive.assign(e->n, 0);
   e->frow.assign(e->n, -1);
-  int tw = cfg->tile_width ? cfg->tile_width : GH_TW_DEFAULT;
+  // slower dissemination (k < 3) leaves views outside the plane's window
+  e->plane = cfg->peer_mode == GH_PEER_PULL && cfg->fanout >= 3 && cfg->fanout <= 4;
+  if (const char* v = std::getenv("GH_PLANE")) e->plane = e->plane && std::atoi(v) != 0;
+  // plane mode gathers one 128-B plane line per 256 members
+  int tw = cfg->tile_width ? cfg->tile_width : e->plane ? GH_TW_PLANE : GH_TW_DEFAULT;
   if (const char* v = std::getenv("GH_TILE_W")) tw = std::atoi(v);
   if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_ROUND_XMAP")) e->xmap = std::atoi(v) != 0;
@@ -569,7 +579,10 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.frow, e->n, 0xFF)) ||
         (rc = dalloc(e, &d.slow, (size_t)(e->ld / tw) * e->n, 0)) || (rc = dalloc(e, &d.slow_n, 4, 0)) ||
         (rc = dalloc(e, &d.mode, 4, 0)) || (rc = dalloc(e, &d.nstorm, 4, 0)) ||
-        (rc = dalloc(e, &d.nflag, 2, 0)))
+        (rc = dalloc(e, &d.nflag, 2, 0)) || (rc = dalloc(e, &d.pvalid, 2, 0)) ||
+        (rc = dalloc(e, &d.pfb, 1, 0)) || (rc = dalloc(e, &d.pnone, 64, 0xFF)))
+      break;
+    if (e->plane && ((rc = dalloc(e, &d.pl[0], cells / 8, 0xFF)) || (rc = dalloc(e, &d.pl[1], cells / 8, 0xFF))))
       break;
     if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
         (rc = dalloc(e, &d.det_any, e->n, 0)) || (rc = dalloc(e, &d.und, e->n, 0)) ||
@@ -824,6 +837,20 @@ int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, in
   return GH_OK;
 }
 
+int gh_plane_info(void* h, int32_t* enabled, int32_t* valid, int64_t* fallback_waves) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  int32_t v[2] = {0, 0};
+  HIPCHK(e, hipMemcpyAsync(&v[0], e->d.pvalid + e->cur, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(&v[1], e->d.pfb, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (enabled) *enabled = e->plane;
+  if (valid) *valid = e->pforce ? 0 : v[0];
+  if (fallback_waves) *fallback_waves = v[1];
+  return GH_OK;
+}
+
 int gh_memory_info(void* h, int64_t* device_bytes, int64_t* wide_used, int64_t* wide_cap, int64_t* frozen_rows) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
@@ -837,7 +864,8 @@ int gh_memory_info(void* h, int64_t* device_bytes, int64_t* wide_used, int64_t* 
     // per-column vectors and the file table are counted by hipMemGetInfo
     // callers, not here
     const int64_t cells = (int64_t)e->n * e->ld;
-    *device_bytes = 2 * cells * 2 + 2 * d.wcap * ((int64_t)d.tw * 8 + d.tw / 8) + e->fzcap * e->ld * 8;
+    *device_bytes = 2 * cells * 2 + (e->plane ? cells : 0) + 2 * d.wcap * ((int64_t)d.tw * 8 + d.tw / 8) +
+                    e->fzcap * e->ld * 8;
   }
   if (wide_used) *wide_used = std::min<int64_t>(used, d.wcap);
   if (wide_cap) *wide_cap = d.wcap;
@@ -868,6 +896,7 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
   int rc;
   if (!full && (rc = check_lost(e))) return rc;
   e->qforce = true;
+  e->pforce = true;
   const GhRound p = round_params(e, round + 1);
   if (n_rows > 0) {
     // host rows -> device staging -> encoded tiled local columns
@@ -914,6 +943,7 @@ int gh_init_full(void* h, int32_t hb0, int32_t ts0, int32_t round) {
   if (hb0 < 0) return set_err(e, GH_ERANGE, "hb0 below 0");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   e->qforce = true;
+  e->pforce = true;
   std::fill(e->alive.begin(), e->alive.end(), 1);
   int rc;
   if ((rc = upload_alive(e))) return rc;
@@ -965,6 +995,10 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     const int32_t r = e->round + 1;
     int rc;
     if ((rc = process_events(e, r))) return rc;
+    if (e->pforce) {
+      HIPCHK(e, hipMemsetAsync(e->d.pvalid + e->cur, 0, sizeof(int32_t), e->stream));
+      e->pforce = false;
+    }
     const GhRound p = round_params(e, r);
     if (e->hb_bound >= INT32_MAX) {
       // a heartbeat may sit at INT32_MAX: the round would overflow Go's
@@ -1133,6 +1167,7 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
   int rc0;
   if ((rc0 = check_lost(e)) || (rc0 = maybe_grow(e))) return rc0;
   e->qforce = true;
+  e->pforce = true;
   int32_t cnt = 0;
   if (n > 0 && e->alive[observer]) {  // GetMsg runs only while Alive (slave/slave.go:208)
     Staging st;

@@ -386,7 +386,14 @@ __device__ __forceinline__ uint32_t pk_adds_u16(uint32_t a, uint32_t b) {  // sa
 }
 __device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) { return as_u(as_us(a) + as_us(b)); }
 __device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) { return as_u(as_us(a) - as_us(b)); }
-__device__ __forceinline__ uint32_t pk_sra15(uint32_t a) { return as_u(as_s(a) >> (short)15); }  // 0xFFFF per negative half
+// 0xFFFF per negative half. Opaque to the compiler: as a plain shift its
+// result feeds selects that get rewritten into per-half compares and
+// v_cndmask (7 instructions where and/or take 2).
+__device__ __forceinline__ uint32_t pk_sra15(uint32_t a) {
+  uint32_t r;
+  asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(r) : "v"(a));  // both halves by 15
+  return r;
+}
 __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
   return as_u(__builtin_elementwise_min(as_us(a), as_us(b)));
 }
@@ -398,6 +405,37 @@ __device__ __forceinline__ uint32_t pk_zero_mask(uint32_t a) {
 __device__ __forceinline__ uint32_t pair_bits(uint32_t m, int j) {
   return ((m & 1u) | ((m >> 15) & 2u)) << (2 * j);
 }
+
+// ---- sender snapshot plane (gh_internal.h: pl) ---------------------------
+__device__ __forceinline__ uint32_t pk_lshr16(uint32_t a, int k) { return as_u(as_us(a) >> (unsigned short)k); }
+__device__ __forceinline__ uint32_t pk_shl16(uint32_t a, int k) { return as_u(as_us(a) << (unsigned short)k); }
+// The plane word of 8 written narrow codes o (an all-narrow chunk); jd = the
+// row's own member in the chunk (0..7) or -1: its snapshot entry carries
+// hb + 1 (the heartbeat the row sends with next round).
+__device__ __forceinline__ uint32_t plane_word(const v4u& o, int jd) {
+  uint32_t wd = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t y = o[j];
+    // u = REF + 1 - offset, clamped to [0, 14]; not visible (bit 15): 15
+    const uint32_t u = pk_sub_u16((uint32_t)(GH_P_REF + 1) * 0x10001u, pk_lshr16(y, 5));
+    uint32_t code = pk_min_u16(pk_max_i16(u, 0u), GH_P_OLD * 0x10001u);
+    code |= pk_sra15(y) & (GH_P_NONE * 0x10001u);
+    wd |= code << (4 * j);
+  }
+  if (jd >= 0) {
+    // offset + 1 on the diagonal: an exact code moves one down (1 = at the
+    // reference becomes unknown); unknown, old and not-visible stay
+    const int pos = 4 * (jd >> 1) + 16 * (jd & 1);
+    const uint32_t c = (wd >> pos) & 0xFu;
+    const uint32_t c2 = (c >= 2u && c <= 13u) ? c - 1u : (c == 1u ? 0u : c);
+    wd = (wd & ~(0xFu << pos)) | (c2 << pos);
+  }
+  return wd;
+}
+// nonzero iff a nibble of a is zero (exact when no nibble is zero; a
+// borrow can only add bits above a zero nibble)
+__device__ __forceinline__ uint32_t nib_haszero(uint32_t a) { return (a - 0x11111111u) & ~a & 0x88888888u; }
 
 template <bool NT>
 __device__ __forceinline__ v4u ldn(const uint16_t* p) {
@@ -433,6 +471,8 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
     d.nflag[cur ^ 1] = 0;  // counted by this round's writers
     d.cntl[d.n] = d.nd[dcur];  // |D_{r-1}| of this shard next to the local counts, for one allreduce
     d.cntl[d.n + 1] = d.nflag[cur];  // flagged segments of this shard's table (quirk gate, summed)
+    d.pvalid[cur ^ 1] = p.plane;  // this round writes the next buffer's plane
+    *d.pfb = 0;
   }
   if (c >= p.ld) return;
   int32_t b = d.base[cur][c];
@@ -465,11 +505,13 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
 // narrow is written here; every other segment of an alive row goes to the
 // slow list (k_round_slow, the reference's rule cell by cell). Stopped rows
 // are not written (wide and identical in both buffers).
-// Rows per workgroup tile: GH_WG_CELLS / TW within [64, 1024] (a tall,
+// Rows per workgroup tile: GH_WG_ROWS_WIDE at TW >= 128 (256 rows), else
+// GH_WG_CELLS / TW within [64, 1024] (a tall,
 // one-tile block: at TW = 64, 256 rows; measured best per width),
 // and at least one wave step of 4 waves.
 template <int TW>
 constexpr int round_rb() {
+  if (TW >= 128) return GH_WG_ROWS_WIDE;
   constexpr int rb = GH_WG_CELLS / TW < 64 ? 64 : GH_WG_CELLS / TW > 1024 ? 1024 : GH_WG_CELLS / TW;
   return rb < 2048 / TW ? 2048 / TW : rb;
 }
@@ -501,7 +543,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   // per-row metadata of the workgroup's rows, staged once for its TPW tiles:
   // s_meta = alive | active << 1 | inbox count << 2; s_inb = first KB senders
   __shared__ int s_meta[RB];
-  __shared__ int s_inb[RB * KB];
+  __shared__ __attribute__((aligned(16))) int s_inb[RB * KB];
 
   // block -> (tile group of TPW consecutive tiles, row block); group-major so
   // that the running workgroups sweep the same tiles together
@@ -570,6 +612,13 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   uint16_t* __restrict__ hnn = d.hn[cur ^ 1];
   const int32_t* __restrict__ bo = d.base[cur];
   const int32_t* __restrict__ bn = d.base[cur ^ 1];
+  // sender plane: read by the lean 4-slot variant when valid, written by
+  // every variant in plane mode
+  constexpr bool PLANE_RD = !STORM && KB == 4;
+  const bool use_plane = PLANE_RD && p.plane && d.pvalid[cur];
+  const uint32_t* __restrict__ plo = d.pl[cur];
+  uint32_t* __restrict__ pln = d.pl[cur ^ 1];
+  int n_fb = 0;  // plane fallbacks of this wave
   uint32_t n_mrg16 = 0;  // merges x 16
   int n_det = 0, n_rel = 0;
   int n_tomb = 0, n_unk = 0;  // REMOVE: tombstoned / unknown member
@@ -580,6 +629,14 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   const int64_t l0 = (int64_t)tile * TW + lc * CPL;                   // local column of this lane's first cell
   const int c0 = (int)(d.col0 + l0);                                  // its global member id
   const int64_t tb = (int64_t)tile * ((int64_t)p.n * TW) + lc * CPL;  // tile base + lane offset
+  // uniform tile bases; rows are 32-bit byte offsets from them
+  const int64_t tcell = (int64_t)tile * ((int64_t)p.n * TW);
+  const char* hno_t = reinterpret_cast<const char*>(hno + tcell);
+  char* hnn_t = reinterpret_cast<char*>(hnn + tcell);
+  const char* plo_t = reinterpret_cast<const char*>(plo) + (plo ? tcell / 2 : 0);
+  char* pln_t = reinterpret_cast<char*>(pln) + (pln ? tcell / 2 : 0);
+  const uint32_t lb = (uint32_t)lc * (CPL * 2);  // lane's byte offset in a row segment (narrow)
+  const uint32_t lbp = (uint32_t)lc * 4;         // ... in a plane row segment
   if (tid == 0) s_nslow = 0;
   for (int t = tid; t < TW; t += 256) {
     s_dcnt[t] = 0;
@@ -637,11 +694,12 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     const bool al = (meta & 1) && valid;
     const int cntv = meta >> 2;
     const int64_t off = tb + (int64_t)i * TW;
+    const uint32_t ob = (uint32_t)i * (TW * 2) + lb;  // own segment, bytes from the tile base
 
-    // own segment and the first KB senders' segments, issued together;
-    // slots q >= cntv hold the own row, a no-op under the max
-    v4u w = ldn<false>(hno + off);  // re-read by peers: keep it cached
-    v4u pv[KB];
+    // own segment and the senders' snapshots, issued together: plane words
+    // when the plane is valid, else the first KB senders' 16-bit segments
+    // (slots q >= cntv hold the own row, a no-op under the max)
+    v4u w = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + ob));  // re-read by peers: keep it cached
     int ps[KB];
     const bool act = (meta >> 1) & 1;  // else the row is under the <4 guard (step 2)
     // guard rows in the lean variant: the 8-slot instantiation (ring
@@ -650,40 +708,33 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     // round, measured A/B on one box)
     constexpr bool LEAN_GUARD = KB > 4;
     bool bad = (!STORM && !LEAN_GUARD && !act) || cntv > KB;
+    // the staged slots, one LDS read per 4 (unused slots hold 0)
+    int sv[KB];
+#pragma unroll
+    for (int q4 = 0; q4 < KB; q4 += 4) {
+      const int4 v = *reinterpret_cast<const int4*>(&s_inb[rs * KB + q4]);
+      sv[q4] = v.x;
+      sv[q4 + 1] = v.y;
+      sv[q4 + 2] = v.z;
+      sv[q4 + 3] = v.w;
+    }
 #pragma unroll
     for (int q = 0; q < KB; ++q) {
-      int s = i;
-      if (q < cntv) {
-        s = s_inb[rs * KB + q];
-        if constexpr (RPW == 1) s = uni(s);
-      }
+      int s = q < cntv ? sv[q] : i;
+      if constexpr (RPW == 1) s = uni(s);
       ps[q] = s;
-      if constexpr (STORM) {
-        // storms hold few senders (guard rows none): load only the used
-        // slots, the rest are absent (-1, a no-op under the max)
-        if (q < cntv)
-          pv[q] = ldn<false>(hno + tb + (int64_t)s * TW);
-        else
-          pv[q] = v4u{~0u, ~0u, ~0u, ~0u};
-      } else {
-        pv[q] = ldn<false>(hno + tb + (int64_t)s * TW);
+    }
+    uint32_t pw[KB];
+    if constexpr (PLANE_RD) {
+      if (use_plane) {
+        // unused slots read a line of "not in the snapshot" codes
+#pragma unroll
+        for (int q = 0; q < KB; ++q)
+          pw[q] = *(q < cntv ? reinterpret_cast<const uint32_t*>(plo_t + ((uint32_t)ps[q] * (TW / 2) + lbp))
+                             : d.pnone + lane);
       }
     }
     bad |= (w[0] & 0xFFFFu) == GH_N_WIDE;  // own segment wide
-#pragma unroll
-    for (int q = 0; q < KB; ++q) bad |= q < cntv && (pv[q][0] & 0xFFFFu) == GH_N_WIDE;
-    // A sender's own member in the lane: its snapshot carries hb + 1 there
-    // (the sender's heartbeat of this round).
-#pragma unroll
-    for (int q = 0; q < KB; ++q) {
-      const int js = ps[q] - c0;
-      if (q < cntv && (unsigned)js < 8u) {
-        const int sh = 16 * (js & 1);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (j == (js >> 1) && ((pv[q][j] >> sh) & 0x8000u) == 0) pv[q][j] += 0x20u << sh;
-      }
-    }
     // The row's own member in the lane (step 3, :443-448): hb + 1 with a
     // fresh stamp (age 0, so age 1 after the round's +1), never flagged.
     // An own cell that is not visible, or at the heartbeat cap, is slow.
@@ -702,6 +753,69 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
             w[j] = (w[j] & ~(0x1Fu << sh)) + (0x20u << sh);
         }
     }
+    // ms[j]: the senders' snapshot codes of pair j, packed max (negative
+    // halves: no visible entry)
+    uint32_t ms[4];
+    bool need16 = true;
+    if constexpr (PLANE_RD) {
+      if (use_plane) {
+        // per pair, the min over senders of the plane codes is the freshest
+        // entry (fields kept at their bit position: the min of masked
+        // halves); exact unless it is 0 (a sender unknown) or 14 (only
+        // entries older than the window): then the wave gathers 16-bit codes
+        uint32_t Lw = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t M = 0x000F000Fu << (4 * j);
+          uint32_t L = pw[0] & M;
+#pragma unroll
+          for (int q = 1; q < KB; ++q) L = pk_min_u16(L, pw[q] & M);
+          Lw |= L;
+          const uint32_t c5 = j == 0 ? pk_shl16(L, 5) : j == 1 ? pk_shl16(L, 1) : j == 2 ? pk_lshr16(L, 3) : pk_lshr16(L, 7);
+          // offset = REF + 1 - code; codes 14, 15: no merge (-1)
+          ms[j] = pk_sub_u16((uint32_t)((GH_P_REF + 1) << 5) * 0x10001u, c5) |
+                  pk_sra15(pk_sub_u16((uint32_t)(13 << 5) * 0x10001u, c5));
+        }
+        need16 = __ballot((nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu)) != 0) != 0;
+        n_fb += need16;
+      }
+    }
+    if (need16) {
+      v4u pv[KB];
+#pragma unroll
+      for (int q = 0; q < KB; ++q) {
+        if constexpr (STORM) {
+          // storms hold few senders (guard rows none): load only the used
+          // slots, the rest are absent (-1, a no-op under the max)
+          if (q < cntv)
+            pv[q] = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + ((uint32_t)ps[q] * (TW * 2) + lb)));
+          else
+            pv[q] = v4u{~0u, ~0u, ~0u, ~0u};
+        } else {
+          pv[q] = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + ((uint32_t)ps[q] * (TW * 2) + lb)));
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < KB; ++q) bad |= q < cntv && (pv[q][0] & 0xFFFFu) == GH_N_WIDE;
+      // A sender's own member in the lane: its snapshot carries hb + 1 there
+      // (the sender's heartbeat of this round).
+#pragma unroll
+      for (int q = 0; q < KB; ++q) {
+        const int js = ps[q] - c0;
+        if (q < cntv && (unsigned)js < 8u) {
+          const int sh = 16 * (js & 1);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (j == (js >> 1) && ((pv[q][j] >> sh) & 0x8000u) == 0) pv[q][j] += 0x20u << sh;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ms[j] = pv[0][j];
+#pragma unroll
+        for (int q = 1; q < KB; ++q) ms[j] = pk_max_i16(ms[j], pv[q][j]);
+      }
+    }
 
     v4u o;
     // acc: bit 5/21 = a special own cell (age >= 30, wide marker), bit 15/31
@@ -716,11 +830,9 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t rmj = rmv[j];  // REMOVE'd columns: not in any sender's snapshot
-      uint32_t m = pv[0][j] | rmj;
-#pragma unroll
-      for (int q = 1; q < KB; ++q) m = pk_max_i16(m, pv[q][j] | rmj);
+      const uint32_t m = ms[j] | rmj;
       const uint32_t x = w[j];
-      uint32_t mm, y0, pre;  // merged mask, value if not merged, present-before mask
+      uint32_t mm, y0, npre;  // merged mask, value if not merged, absent-before mask
       if constexpr (!STORM) {
         // own cells other than visible (age < 30) or absent go to the slow
         // list: flagged, tombstone, wide marker (x + 1 keeps bit 15), age 30/31
@@ -730,7 +842,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         y0 = pk_adds_u16(x, 0x00010001u);                   // not merged: age + 1 (absent stays)
         // a guard row (step 2, :504-509) stamps its present cells: age 1
         if (LEAN_GUARD && !act) y0 = (((x & 0x7FE07FE0u) | 0x00010001u) & ~hx) | (x & hx);
-        pre = ~hx;
+        npre = hx;
       } else {
         // cell classes: (x | 31) + 1 is 0 for a tombstone or absent cell, has
         // bit 15 for a flagged present one and not for a visible one
@@ -760,7 +872,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         // present cells age 1
         const uint32_t yact = pk_adds_u16(xr | (fl & 0xFFE0FFE0u), 0x00010001u) | rel;
         y0 = (((xr & 0x7FE07FE0u) | 0x00010001u) & nowm) | (yact & ~nowm);
-        pre = ~ta0;
+        npre = ta0;
         stb |= ((fl0 | ta) & ~ab) | (LEAN_GUARD ? 0u : ~actm);  // what the lean variant lists
         detb |= pair_bits(fl, j);
         relb |= pair_bits(rel & ~ab, j);
@@ -777,7 +889,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       fo |= flo;
       o[j] = y;
       mcnt += __builtin_popcount(mm);
-      dp16 += __builtin_popcount(~hy) - __builtin_popcount(pre);
+      dp16 += __builtin_popcount(npre) - __builtin_popcount(hy);
     }
     if (own_in) {  // the own member is never detected: no flag on a present own cell
 #pragma unroll
@@ -790,7 +902,15 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     bool any_det = false;
     if (al) {
       if (seg_ok) {
-        stn<NT>(hnn + off, o);
+        stn<NT>(reinterpret_cast<uint16_t*>(hnn_t + ob), o);
+        if (p.plane) {
+          const uint32_t pwd = plane_word(o, own_in ? jd : -1);
+          uint32_t* pp = reinterpret_cast<uint32_t*>(pln_t + ((uint32_t)i * (TW / 2) + lbp));
+          if constexpr (NT)
+            __builtin_nontemporal_store(pwd, pp);
+          else
+            *pp = pwd;
+        }
         dpres = dp16 >> 4;
         n_mrg16 += mcnt;
         if constexpr (STORM) {
@@ -813,14 +933,16 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         s_slow[atomicAdd(&s_nslow, 1)] = i;
       }
     }
+    if (__ballot(dpres != 0 || any_det) != 0) {  // rare in healthy rounds: skip the segment sums
 #pragma unroll
-    for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) {
-      dpres += __shfl_xor(dpres, o2);
-      any_det |= __shfl_xor((int)any_det, o2) != 0;
-    }
-    if (lc == 0) {
-      if (dpres) atomicAdd(&d.cntl[i], dpres);
-      if (any_det) d.det_any[i] = 1;
+      for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) {
+        dpres += __shfl_xor(dpres, o2);
+        any_det |= __shfl_xor((int)any_det, o2) != 0;
+      }
+      if (lc == 0) {
+        if (dpres) atomicAdd(&d.cntl[i], dpres);
+        if (any_det) d.det_any[i] = 1;
+      }
     }
     // storm measure: committed segments that hold (storm variant) or will
     // hold next round (flagged results) cells the lean variant cannot take
@@ -841,6 +963,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   __syncthreads();  // s_nslow / s_slow are reused by the next tile
   }  // tiles
 
+  if (PLANE_RD && n_fb && lane == 0) atomicAdd(d.pfb, n_fb);
   if (n_mrg16) atomicAdd(&s_merged, (unsigned long long)(n_mrg16 >> 4));
   if (n_det) atomicAdd(&s_det, (unsigned long long)n_det);
   if (n_rel) atomicAdd(&s_rel, (unsigned long long)n_rel);
@@ -995,6 +1118,11 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
         slot = __shfl(sl, sub * SEG);
       }
       if (slot >= 0) gh_put8(d, nxt, i, l0, narrow, nx, slot, o);
+      if (p.plane) {  // the sender plane of the segment (wide: unknown, 0)
+        const int64_t jd = (int64_t)i - c0;
+        d.pl[nxt][gh_cell(d, i, l0) >> 3] =
+            narrow ? plane_word(v4u{nx.x, nx.y, nx.z, nx.w}, (uint64_t)jd < 8u ? (int)jd : -1) : 0u;
+      }
     }
 #pragma unroll
     for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) {
@@ -1137,6 +1265,9 @@ __global__ __launch_bounds__(256) void k_quirk_carry(GhDev d, GhRound p) {
 template <int TW>
 __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur, GhRound p) {
   if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no candidate in any shard's table
+  // cleared flags make cells visible that the sender plane lists as not in
+  // the snapshot: this round gathers 16-bit codes
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.pvalid[cur] = 0;
   constexpr int SEG = SegWalk<TW>::SEG;
   const SegWalk<TW> w(p);
   for (int64_t base = w.first; base < w.nseg; base += w.stride) {

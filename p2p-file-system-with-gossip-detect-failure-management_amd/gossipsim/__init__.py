@@ -104,6 +104,14 @@ class Engine:
         self._chk(self.lib.gh_encoding_info(self.h, C.byref(w), C.byref(sl), C.byref(mode), C.byref(ns)))
         return (w.value, sl.value, mode.value, ns.value) if full else (w.value, sl.value)
 
+    def plane_info(self):
+        """(plane kept, plane valid for the next round, waves of the last
+        round that gathered 16-bit sender codes although it was valid) --
+        the sender snapshot plane of pull mode (gh_plane_info, diagnostic)."""
+        en, va, fb = C.c_int32(), C.c_int32(), C.c_int64()
+        self._chk(self.lib.gh_plane_info(self.h, C.byref(en), C.byref(va), C.byref(fb)))
+        return en.value, va.value, fb.value
+
     def memory_info(self):
         """dict(device_bytes, wide_used, wide_cap, frozen_rows) of this
         engine's tables (gh_memory_info)."""
