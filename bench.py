@@ -86,10 +86,10 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(n, k, world, warmup):
+def pmc_traffic(n, k, world, warmup, plane, tw):
     """Fabric-side bytes per k_round launch from the committed PMC summary of
-    the same configuration and steady state (tools/pmc.sh ->
-    profiles/*k_round_pmc*.json, warm-up >= 5 rounds)."""
+    the same configuration, layout (sender plane, tile width) and steady state
+    (tools/pmc.sh -> profiles/*k_round_pmc*.json, warm-up >= 5 rounds)."""
     best = None
     for f in sorted((REPO / "profiles").glob("*k_round_pmc*.json")):
         try:
@@ -98,7 +98,8 @@ def pmc_traffic(n, k, world, warmup):
             continue
         c = d.get("config", {})
         if (c.get("n") == n and c.get("k") == k and c.get("world", 1) == world and c.get("cell_bytes", 4) == 2
-                and c.get("warmup", 0) >= min(5, warmup) and "traffic_bytes" in d):
+                and c.get("warmup", 0) >= min(5, warmup) and "traffic_bytes" in d
+                and c.get("plane", 0) == plane and c.get("tile_width", 64) == tw):
             best = {"traffic_bytes": d["traffic_bytes"], "source": f"profiles/{f.name}",
                     "l2_hit_rate": d.get("l2_hit_rate")}
     return best
@@ -371,6 +372,8 @@ def main():
     else:
         eng = gs.Engine(cfg)
     _, _, _, ncols = eng.shard_info()
+    plane = eng.plane_info()[0]
+    tile_w = int(os.environ.get("GH_TILE_W", "256" if plane else "64"))
     eng.init_full(2, 0, 0)
     if args.warmup:
         eng.step(args.warmup)
@@ -395,6 +398,7 @@ def main():
         elapsed = float(t.item())
     kern_ms, launches = eng.read_timing()
     eng.set_timing(False)
+    plane_fb = eng.plane_info()[2]
     placement = None
     if world == 1 and args.files > 0:
         progress("placement and election legs")
@@ -411,7 +415,7 @@ def main():
     b_compulsory = 4.0 * n * ncols             # each 2-byte narrow cell read once and written once
     b_gather = 2.0 * n * ncols * k             # the k sender segments per cell (L2 / Infinity Cache / HBM)
     b_survey = 4.0 * n * ncols * (k + 4)       # SURVEY.md §8d (int32 hb + ts streams)
-    traffic = pmc_traffic(n, k, world, args.warmup)
+    traffic = pmc_traffic(n, k, world, args.warmup, plane, tile_w)
     avg_s = (kern_ms / 1e3) / max(launches, 1)
     achieved = b_compulsory / avg_s / 1e9
     line = {
@@ -459,6 +463,8 @@ def main():
         "cpu_baseline": None,
         "memory": {"table_bytes": mem["device_bytes"], "wide_slots_per_buffer": mem["wide_cap"],
                    "wide_slots_used": mem["wide_used"]},
+        "layout": {"tile_width": tile_w, "sender_plane": bool(plane),
+                   "plane_fallback_waves_last_round": plane_fb},
         "secondary": secondary,
         "placement": placement,
     }

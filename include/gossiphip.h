@@ -252,7 +252,7 @@ int gh_shard_info(void* h, int32_t* rank, int32_t* world, int64_t* col0, int64_t
 int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, int32_t* storm_mode,
                      int64_t* storm_segments);
 /* Sender snapshot plane (diagnostic; DESIGN.md "Sender plane"): whether the
- * engine keeps one (pull mode, 3 <= k <= 4), whether the current table's plane is
+ * engine keeps one (pull mode, 3 <= k <= 4, N >= 16,384), whether the current table's plane is
  * valid for the next round, and how many waves of the last round gathered
  * 16-bit sender codes although the plane was valid (a sender code outside
  * the plane's window). Any output may be NULL. No reference counterpart. */

@@ -67,7 +67,8 @@
 //                    15     not in the snapshot (absent, tombstone, flagged)
 //                  so the min over senders is the freshest entry, and any
 //                  unknown sender shows as a 0. Written by every round kernel
-//                  for the segments it writes (pull mode, 3 <= k <= 4); read by
+//                  for the segments it writes (pull mode, 3 <= k <= 4, N >=
+//                  GH_PLANE_MIN_N); read by
 //                  k_round's lean variant, whose sender gathers become one 128-B
 //                  line per 256 members at TW = 256. A wave falls back to the
 //                  16-bit gathers when a min is 0 or 14. pvalid[b] = 0 once
@@ -116,7 +117,8 @@
 #define GH_MAXK 8                // max pull fanout
 #define GH_DLIST_MAX 1024        // local |D| above which undecided rows are recounted in full
 #define GH_TW_DEFAULT 64         // default tile width (members per tile)
-#define GH_TW_PLANE 256          // default tile width with the sender plane (pull, k <= 4)
+#define GH_TW_PLANE 256          // default tile width with the sender plane (pull, 3 <= k <= 4)
+#define GH_PLANE_MIN_N 16384     // the sender plane from this many members on
 #define GH_TAG_PEER 0x50454552u
 #define GH_TAG_PLACE 0x504C4143u
 #define GH_MAX_DRAWS (1u << 20)
@@ -173,7 +175,6 @@ struct GhDev {
   uint32_t *pl[2];  // sender snapshot plane per buffer (null: plane off)
   int32_t *pvalid;  // [2]: plane of buffer b written by the round that wrote b
   int32_t *pfb;     // waves of the last round that gathered 16-bit codes with a valid plane
-  uint32_t *pnone;  // [64] all GH_P_NONE: the plane word of an unused inbox slot
   int32_t *base[2]; // [ld] narrow base per buffer
   // wide arena per buffer: [wcap][tw] x / exact ts, [wcap][tw/8] flag bytes
   int32_t *wh[2], *wt[2];

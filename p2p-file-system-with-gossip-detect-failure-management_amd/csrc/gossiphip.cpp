@@ -57,7 +57,7 @@ struct Engine {
   // the current table was written by something other than a round: its
   // sender plane is stale (pvalid[cur] = 0 before the next round)
   bool pforce = true;
-  int plane = 0;         // sender snapshot plane (pull mode, 3 <= k <= 4; GH_PLANE=0 turns it off)
+  int plane = 0;         // sender snapshot plane (pull mode, 3 <= k <= 4, N >= GH_PLANE_MIN_N; GH_PLANE=0/1)
   // upper bound of every heartbeat in the table (int32 overflow check,
   // slave/slave.go:446): +1 per round, max of imported / merged values
   int64_t hb_bound = 0;
@@ -505,9 +505,13 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   e->world = world;
   e->alive.assign(e->n, 0);
   e->frow.assign(e->n, -1);
-  // slower dissemination (k < 3) leaves views outside the plane's window
-  e->plane = cfg->peer_mode == GH_PEER_PULL && cfg->fanout >= 3 && cfg->fanout <= 4;
-  if (const char* v = std::getenv("GH_PLANE")) e->plane = e->plane && std::atoi(v) != 0;
+  // slower dissemination (k < 3) leaves views outside the plane's window;
+  // below GH_PLANE_MIN_N the tables sit in the on-die caches and the round is
+  // launch-bound, where 256-member tiles leave too few workgroups
+  // (GH_PLANE=1 keeps it at any N, GH_PLANE=0 drops it)
+  const bool plane_ok = cfg->peer_mode == GH_PEER_PULL && cfg->fanout >= 3 && cfg->fanout <= 4;
+  e->plane = plane_ok && cfg->n_members >= GH_PLANE_MIN_N;
+  if (const char* v = std::getenv("GH_PLANE")) e->plane = plane_ok && std::atoi(v) != 0;
   // plane mode gathers one 128-B plane line per 256 members
   int tw = cfg->tile_width ? cfg->tile_width : e->plane ? GH_TW_PLANE : GH_TW_DEFAULT;
   if (const char* v = std::getenv("GH_TILE_W")) tw = std::atoi(v);
@@ -580,7 +584,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.slow, (size_t)(e->ld / tw) * e->n, 0)) || (rc = dalloc(e, &d.slow_n, 4, 0)) ||
         (rc = dalloc(e, &d.mode, 4, 0)) || (rc = dalloc(e, &d.nstorm, 4, 0)) ||
         (rc = dalloc(e, &d.nflag, 2, 0)) || (rc = dalloc(e, &d.pvalid, 2, 0)) ||
-        (rc = dalloc(e, &d.pfb, 1, 0)) || (rc = dalloc(e, &d.pnone, 64, 0xFF)))
+        (rc = dalloc(e, &d.pfb, 1, 0)))
       break;
     if (e->plane && ((rc = dalloc(e, &d.pl[0], cells / 8, 0xFF)) || (rc = dalloc(e, &d.pl[1], cells / 8, 0xFF))))
       break;

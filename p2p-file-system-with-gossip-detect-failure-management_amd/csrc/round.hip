@@ -727,11 +727,12 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     uint32_t pw[KB];
     if constexpr (PLANE_RD) {
       if (use_plane) {
-        // unused slots read a line of "not in the snapshot" codes
+        // unused slots read the own row's codes: the own offsets, never
+        // above the own cell, so a no-op under the merge (an unknown or old
+        // code there only costs a fallback)
 #pragma unroll
         for (int q = 0; q < KB; ++q)
-          pw[q] = *(q < cntv ? reinterpret_cast<const uint32_t*>(plo_t + ((uint32_t)ps[q] * (TW / 2) + lbp))
-                             : d.pnone + lane);
+          pw[q] = *reinterpret_cast<const uint32_t*>(plo_t + ((uint32_t)ps[q] * (TW / 2) + lbp));
       }
     }
     bad |= (w[0] & 0xFFFFu) == GH_N_WIDE;  // own segment wide

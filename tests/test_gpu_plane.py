@@ -21,6 +21,13 @@ def gs():
     return gossipsim
 
 
+@pytest.fixture(autouse=True)
+def plane_on(monkeypatch):
+    """The plane is kept from N=16,384 on by default; these small clusters
+    keep it through GH_PLANE=1."""
+    monkeypatch.setenv("GH_PLANE", "1")
+
+
 def test_plane_steady_state_used(gs, oracle_mod):
     """N=2,048, k=4 pull from full membership with the bench's timeouts:
     the plane is kept, valid from the second round on except after events,
@@ -107,13 +114,14 @@ def run_states(gs, n, cfg, sched, rounds, init):
 @pytest.mark.parametrize("env", [{"GH_PLANE": "0", "GH_TILE_W": "256"}, {"GH_TILE_W": "64"}],
                          ids=["gather16_tw256", "plane_tw64"])
 def test_plane_matches_gather_path(gs, monkeypatch, env):
-    """Seeded churn with detections (T_fail 6): the default (plane, TW=256)
-    gives the same tables, counters, failed sets and detectors every round
-    as the 16-bit gathers at the same layout and as the plane at TW=64."""
+    """Seeded churn with detections (T_fail 6): the plane at TW=256 gives the
+    same tables, counters, failed sets and detectors every round as the
+    16-bit gathers at the same layout and as the plane at TW=64."""
     n = 1536
     cfg = dict(fanout=4, seed=0x5EED0200, t_fail=6, t_cleanup=8)
     sched = sc.random_churn(n, 36, 0x77, p_crash=0.01, p_leave=0.005, p_join=0.02)
     init = sc.full_state(n)
+    monkeypatch.setenv("GH_TILE_W", "256")
     base, info = run_states(gs, n, cfg, sched, 36, init)
     assert info[0] == 1
     for k, v in env.items():
@@ -126,3 +134,27 @@ def test_plane_matches_gather_path(gs, monkeypatch, env):
             np.testing.assert_array_equal(x, y, err_msg=f"round {r}")
         np.testing.assert_array_equal(a[2], b[2])
         np.testing.assert_array_equal(a[3], b[3])
+
+
+@pytest.mark.parametrize("detect_mode", [0, 1], ids=["canonical", "quirk"])
+def test_plane_churn_parity(gs, oracle_mod, detect_mode):
+    """Seeded crash/leave/join churn with detections in both detection modes
+    (quirk mode's pre-pass clears flags in place and invalidates the plane):
+    bit-exact against the oracle every round with the plane kept."""
+    from test_gpu_parity import run_parity
+    n = 700
+    sched = sc.random_churn(n, 40, 0x99 + detect_mode, p_crash=0.02, p_leave=0.01, p_join=0.04)
+    eng, _ = run_parity(gs, oracle_mod, dict(fanout=4, seed=0x5EED0300 + detect_mode, t_fail=4, t_cleanup=6,
+                                             detect_mode=detect_mode), n, 40, sched, init=sc.full_state(n))
+    assert eng.plane_info()[0] == 1
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_plane_sharded_parity(gs, oracle_mod, world):
+    """Column shards (in-process transport) each keep the plane of their own
+    columns; seeded churn is bit-exact against the oracle every round."""
+    from test_gpu_sharded import run_group
+    n = 1100
+    sched = sc.random_churn(n, 30, 0xA0 + world, p_crash=0.01, p_leave=0.01, p_join=0.03)
+    run_group(gs, oracle_mod, world, dict(fanout=3, seed=0x5EED0400 + world, t_fail=5, t_cleanup=7), n, 30, sched,
+              init=sc.full_state(n))

@@ -33,7 +33,14 @@ if "TCC_HIT_sum" in out and "TCC_MISS_sum" in out:
     out["l2_hit_rate"] = h / (h + m)
 if "read_bytes_corrected" in out and "write_bytes" in out:
     out["traffic_bytes"] = out["read_bytes_corrected"] + out["write_bytes"]
+import os  # noqa: E402
+# the layout the pass ran with (bench.py matches it): pull with 3 <= k <= 4
+# at N >= 16,384 keeps the sender plane at TW=256 unless GH_PLANE / GH_TILE_W
+# say otherwise
+plane = int(3 <= k <= 4 and (os.environ["GH_PLANE"] != "0" if "GH_PLANE" in os.environ else n >= 16384))
+tw = int(os.environ.get("GH_TILE_W", "256" if plane else "64"))
 out["config"] = {"n": n, "k": k, "world": 1, "cell_bytes": 2, "warmup": warmup, "steps": steps,
+                 "plane": plane, "tile_width": tw,
                  "command": f"python3 bench.py --steps {steps} --warmup {warmup} --no-cpu-baseline --no-secondary "
                             "--files 0"}
 out["compulsory_bytes"] = 4.0 * n * n
