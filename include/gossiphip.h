@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GH_ABI_VERSION 2
+#define GH_ABI_VERSION 3
 
 /* ---- error codes ---------------------------------------------------- */
 #define GH_OK 0
@@ -77,7 +77,9 @@ typedef struct gh_config {
   int64_t wide_segments; /* slots of each wide-segment arena (HBM layout,
                             DESIGN.md); 0 = auto (all segments when small,
                             else 1/32 of them, grown between calls)        */
-  int32_t reserved[6];
+  int32_t shard_layout;  /* sharded engines (gh_create_sharded):
+                            GH_LAYOUT_COLUMNS (0, default) or GH_LAYOUT_ROWS */
+  int32_t reserved[5];
 } gh_config;
 
 typedef struct gh_event {
@@ -233,6 +235,16 @@ int gh_rebuild_meta(void* h, int32_t new_master, int32_t* f0, int64_t* n_files);
 #define GH_COMM_RCCL 0    /* one process per GPU, RCCL over xGMI              */
 #define GH_COMM_LOCAL 1   /* ranks are threads of one process (any devices)  */
 #define GH_COMM_ID_BYTES 128
+/* Shard layouts (DESIGN.md "Multi-GPU"):
+ *   GH_LAYOUT_COLUMNS  rank g holds member columns [g*ncs, g*ncs + ncs) of
+ *                      ALL rows; every per-round exchange is O(N) (default)
+ *   GH_LAYOUT_ROWS     rank g holds observer rows [g*nrs, g*nrs + nrs) with
+ *                      ALL columns (north_star): each round the senders'
+ *                      rows that a shard's receivers pull cross shards by
+ *                      one alltoallv (ncclSend/ncclRecv group), O(N^2 k/G)
+ *                      bytes. Pull mode only (ring mode: GH_EINVAL). */
+#define GH_LAYOUT_COLUMNS 0
+#define GH_LAYOUT_ROWS 1
 
 /* RCCL unique id for gh_create_sharded (call on rank 0, send to all). */
 int gh_comm_unique_id(uint8_t* id);

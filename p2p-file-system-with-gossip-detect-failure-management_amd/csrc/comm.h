@@ -1,7 +1,8 @@
 // Collective transport of the column-sharded engine (DESIGN.md "Multi-GPU").
 //
-// Every per-round exchange of the sharded engine is O(N) and goes through
-// this interface, stream-ordered on the engine's HIP stream:
+// Every per-round exchange of the sharded engine goes through this
+// interface, stream-ordered on the engine's HIP stream (column layout: O(N)
+// allreduce / allgather; row layout adds the senders' rows by alltoallv):
 //   RCCL   one process per GPU, RCCL (loaded at run time) over xGMI;
 //   LOCAL  ranks are threads of one process (any devices, including G shards
 //          on one GPU, which RCCL does not allow): the parity-test transport
@@ -28,6 +29,12 @@ struct GhComm {
   // recv[r*bytes .. (r+1)*bytes) = rank r's send; send may alias
   // recv + rank*bytes (in place).
   virtual int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  // Personalized exchange (row layout): send holds one block per
+  // destination rank in rank order (sendbytes[r] bytes for rank r), recv
+  // receives one block per source rank in rank order (recvbytes[r] bytes
+  // from rank r). Host arrays of world entries; send and recv must not alias.
+  virtual int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t* recvbytes,
+                        hipStream_t s) = 0;
 };
 
 size_t gh_dtype_size(GhDType dt);

@@ -34,6 +34,9 @@ struct SingleComm final : GhComm {
   int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     return copy_if_needed(send, recv, bytes, s);
   }
+  int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t*, hipStream_t s) override {
+    return copy_if_needed(send, recv, sendbytes[0], s);
+  }
 };
 
 // ---- RCCL ----------------------------------------------------------------
@@ -44,6 +47,8 @@ struct RcclApi {
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                              hipStream_t) = nullptr;
   ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*all_to_allv)(const void*, const size_t[], const size_t[], void*, const size_t[], const size_t[],
+                              ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
   const char* (*error_string)(ncclResult_t) = nullptr;
   std::string load_err;
   bool ok = false;
@@ -68,7 +73,8 @@ const RcclApi& rccl_api() {
     };
     api.ok = sym(api.get_unique_id, "ncclGetUniqueId") && sym(api.comm_init_rank, "ncclCommInitRank") &&
              sym(api.comm_destroy, "ncclCommDestroy") && sym(api.all_reduce, "ncclAllReduce") &&
-             sym(api.all_gather, "ncclAllGather") && sym(api.error_string, "ncclGetErrorString");
+             sym(api.all_gather, "ncclAllGather") && sym(api.error_string, "ncclGetErrorString") &&
+             sym(api.all_to_allv, "ncclAllToAllv");
   });
   return api;
 }
@@ -97,6 +103,21 @@ struct RcclComm final : GhComm {
     if (bytes == 0) return 0;
     return check(api->all_gather(send, recv, bytes, ncclUint8, comm, s), "ncclAllGather");
   }
+  // ncclAllToAllv (rccl.h:815) over byte counts, displacements = prefix sums
+  int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t* recvbytes,
+                hipStream_t s) override {
+    std::vector<size_t> sd(world), rd(world);
+    size_t so = 0, ro = 0;
+    for (int r = 0; r < world; ++r) {
+      sd[r] = so;
+      rd[r] = ro;
+      so += sendbytes[r];
+      ro += recvbytes[r];
+    }
+    if (so + ro == 0) return 0;
+    return check(api->all_to_allv(send, sendbytes, sd.data(), recv, recvbytes, rd.data(), ncclUint8, comm, s),
+                 "ncclAllToAllv");
+  }
 };
 
 // ---- LOCAL (threads of one process) --------------------------------------
@@ -109,7 +130,8 @@ struct LocalGroup {
   bool broken = false;
   std::vector<const void*> ptr;
   std::vector<int> dev;
-  explicit LocalGroup(int w) : world(w), ptr(w, nullptr), dev(w, 0) {}
+  std::vector<const size_t*> counts;  // alltoallv: each rank's per-destination byte counts
+  explicit LocalGroup(int w) : world(w), ptr(w, nullptr), dev(w, 0), counts(w, nullptr) {}
   // All ranks meet. False after a 120 s wait (a rank failed or diverged);
   // the group then stays broken so that no rank hangs on it later.
   bool barrier() {
@@ -201,6 +223,32 @@ struct LocalComm final : GhComm {
     else
       hipLaunchKernelGGL((k_reduce<T, GH_OP_MAX>), dim3(grid), dim3(256), 0, s, static_cast<const T*>(tmp), world,
                          count, static_cast<T*>(recv));
+  }
+  // every rank publishes its send buffer and counts; each copies the blocks
+  // addressed to it straight from the peers' buffers
+  int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t* recvbytes,
+                hipStream_t s) override {
+    if (hipStreamSynchronize(s) != hipSuccess) return fail("local comm: stream sync failed");
+    g->ptr[rank] = send;
+    g->counts[rank] = sendbytes;
+    if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
+    size_t ro = 0;
+    for (int h = 0; h < world; ++h) {
+      size_t off = 0;
+      for (int r = 0; r < rank; ++r) off += g->counts[h][r];
+      const size_t bytes = g->counts[h][rank];
+      if (bytes != recvbytes[h]) {
+        g->barrier();
+        return fail("local comm: alltoallv counts disagree");
+      }
+      if (bytes && hipMemcpyPeerAsync(static_cast<char*>(recv) + ro, device, static_cast<const char*>(g->ptr[h]) + off,
+                                      g->dev[h], bytes, s) != hipSuccess)
+        return fail("local comm: peer copy failed");
+      ro += bytes;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) return fail("local comm: stream sync failed");
+    if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
+    return 0;
   }
   int allreduce(const void* send, void* recv, size_t count, GhDType dt, GhROp op, hipStream_t s) override {
     if (count == 0) return 0;

@@ -20,6 +20,10 @@ __global__ __launch_bounds__(256) void k_vote_scan(GhDev d, int cur, const int32
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= d.n) return;
+  if (!gh_owned(d, i)) {  // row layout: the row's owner answers (MAX over shards)
+    if (lane == 0) out[i] = out[d.n + i] = 0;
+    return;
+  }
   int32_t first = 0;
   for (int64_t c0 = 0; c0 < d.ncol; c0 += 64) {
     const int64_t c = c0 + lane;

@@ -27,7 +27,8 @@ __global__ __launch_bounds__(256) void k_count(GhDev d, int cur, GhRound p) {
   const int lane = threadIdx.x & 63;
   if (i >= p.n) return;
   int cnt = 0;
-  for (int64_t c = lane * 8; c < p.ld; c += 512) cnt += __builtin_popcount(gh_pf8(d, cur, i, c) & 0xFFu);
+  if (gh_owned(d, i))  // row layout: other shards count their rows, this one adds 0
+    for (int64_t c = lane * 8; c < p.ld; c += 512) cnt += __builtin_popcount(gh_pf8(d, cur, i, c) & 0xFFu);
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
   if (lane == 0) d.cntl[i] = cnt;
 }
@@ -226,7 +227,7 @@ __global__ __launch_bounds__(256) void k_unpack(GhDev d, int cur, int32_t* dst, 
     const int64_t t = idx / per_tile, rem = idx - t * per_tile;
     const int64_t i = row0 + rem / cpt;
     const int64_t c = t * d.tw + (rem % cpt) * 8;
-    if (c >= d.ncs) continue;
+    if (c >= d.ncs || !gh_owned(d, i)) continue;  // row layout: the owner writes the row
     GhCell v[8];
     gh_get8(d, cur, i, c, p.r, v);
     int32_t* o = dst + (i - row0) * d.ncs + c;
@@ -267,7 +268,9 @@ __global__ __launch_bounds__(256) void k_freeze_mark(GhDev d, const int32_t* row
 
 // bit b of word w of row q = local column 32w+b of rows[q] is present
 __global__ __launch_bounds__(256) void k_rowbits(GhDev d, int cur, const int32_t* rows, int32_t nr) {
-  uint32_t* out = d.rbits + (int64_t)d.rank * nr * d.ncsw;
+  // row layout: slice 0 holds every member; the row's owner writes it, the
+  // other shards write zeros (the host sums the slices)
+  uint32_t* out = d.rbits + (d.rowlay ? 0 : (int64_t)d.rank * nr * d.ncsw);
   const int64_t total = (int64_t)nr * d.ncsw;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(256) void k_rowbits(GhDev d, int cur, const int32_t
     const int64_t w = idx - (int64_t)q * d.ncsw;
     const int row = rows[q];
     uint32_t bits = 0;
-    for (int b = 0; b < 32; b += 8) {
+    for (int b = 0; b < 32 && gh_owned(d, row); b += 8) {
       const int64_t c = w * 32 + b;
       if (c >= d.ncol) break;
       bits |= (gh_pf8(d, cur, row, c) & 0xFFu) << b;  // padding cells are absent
@@ -286,11 +289,11 @@ __global__ __launch_bounds__(256) void k_rowbits(GhDev d, int cur, const int32_t
 
 // segments of buffer buf: wide -> out[0], frozen -> out[1]
 __global__ __launch_bounds__(256) void k_count_wide(GhDev d, int buf, unsigned long long* out) {
-  const int64_t total = d.ntiles * d.n;
+  const int64_t total = d.ntiles * d.nrows;  // owned rows: slots 0..nrows
   unsigned long long cw = 0, cf = 0;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t t = idx / d.n, i = idx - t * d.n;
+    const int64_t t = idx / d.nrows, i = idx - t * d.nrows;
     const uint32_t h = d.hn[buf][t * d.tstride + i * d.tw];
     cw += h == GH_N_WIDE;
     cf += h == GH_N_FROZEN;
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(256) void k_hb_check(GhDev d, int cur, int32_t* fla
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= d.ncol) return;
   const int64_t i = d.col0 + c;
-  if (i < d.n && d.alive[i] && gh_get(d, cur, i, c, p.r).x == INT32_MAX) *flag = 1;
+  if (i < d.n && gh_owned(d, i) && d.alive[i] && gh_get(d, cur, i, c, p.r).x == INT32_MAX) *flag = 1;
 }
 
 // base[buf][c] = v for every local column
@@ -361,12 +364,15 @@ void launch_count(const GhDev& d, int cur, const GhRound& p, hipStream_t s) {
 
 void launch_fill(const GhDev& d, int cur, int32_t hb0, int32_t ts0, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_setbase, dim3((unsigned)((d.ld + 255) / 256)), dim3(256), 0, s, d, cur, hb0 - GH_BASE_LAG);
-  seg_launch(d, cur, rows_set(d, nullptr, 0, p.n), nullptr, p, OpFill{d, hb0, ts0, p}, s, true);
+  seg_launch(d, cur, rows_set(d, nullptr, d.row0, d.nrows), nullptr, p, OpFill{d, hb0, ts0, p}, s, true);
 }
 
 void launch_pack(const GhDev& d, int cur, const int32_t* hb_rows, const int32_t* ts_rows, int64_t row0,
                  int64_t nrows, const GhRound& p, hipStream_t s) {
-  seg_launch(d, cur, rows_set(d, nullptr, row0, nrows), nullptr, p, OpPack{d, hb_rows, ts_rows, row0, p}, s, true);
+  // the owned rows of [row0, row0 + nrows)
+  const int64_t a = std::max<int64_t>(row0, d.row0), b = std::min<int64_t>(row0 + nrows, d.row0 + d.nrows);
+  if (b > a)
+    seg_launch(d, cur, rows_set(d, nullptr, a, b - a), nullptr, p, OpPack{d, hb_rows, ts_rows, row0, p}, s, true);
 }
 
 void launch_unpack(const GhDev& d, int cur, int32_t* dst_rows, int64_t row0, int64_t nrows, int what,
@@ -384,7 +390,7 @@ void launch_freeze(const GhDev& d, int cur, const int32_t* rows, int32_t nr, con
 
 void launch_count_wide(const GhDev& d, int buf, unsigned long long* out, hipStream_t s) {
   (void)hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), s);
-  hipLaunchKernelGGL(k_count_wide, dim3(grid_for(d.ntiles * d.n)), dim3(256), 0, s, d, buf, out);
+  if (d.nrows > 0) hipLaunchKernelGGL(k_count_wide, dim3(grid_for(d.ntiles * d.nrows)), dim3(256), 0, s, d, buf, out);
 }
 
 void launch_rowbits(const GhDev& d, int cur, const int32_t* rows, int32_t nr, hipStream_t s) {
@@ -396,18 +402,18 @@ void launch_leave(const GhDev& d, int cur, const int32_t* leavers, const int32_t
                   const GhRound& p, hipStream_t s) {
   if (ntl == 0) return;
   scatter(d, leavers, nullptr, nl, 0xFF, s);
-  seg_launch(d, cur, SegSet{nullptr, 0, d.n, tiles, ntl}, nullptr, p, OpLeave{d, nl}, s);
+  seg_launch(d, cur, SegSet{nullptr, d.row0, d.nrows, tiles, ntl}, nullptr, p, OpLeave{d, nl}, s);
 }
 
 void launch_join_add(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, int32_t introducer,
                      const GhRound& p, hipStream_t s) {
   (void)hipMemsetAsync(d.nd + 4, 0, sizeof(int32_t), s);
   scatter(d, joiners, nullptr, nj, 0xFF, s);
-  seg_launch(d, cur, rows_set(d, nullptr, introducer, 1), nullptr, p, OpJoinAdd{d, p}, s);
+  if (gh_owned(d, introducer)) seg_launch(d, cur, rows_set(d, nullptr, introducer, 1), nullptr, p, OpJoinAdd{d, p}, s);
 }
 
 void launch_join_bcast(const GhDev& d, int cur, int32_t introducer, const GhRound& p, hipStream_t s) {
-  seg_launch(d, cur, rows_set(d, nullptr, 0, p.n), d.nd + 4, p, OpJoinBcast{d, cur, introducer, p}, s);
+  seg_launch(d, cur, rows_set(d, nullptr, d.row0, d.nrows), d.nd + 4, p, OpJoinBcast{d, cur, introducer, p}, s);
 }
 
 void launch_join_reset(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p,
@@ -419,7 +425,7 @@ void launch_merge_list(const GhDev& d, int cur, int32_t obs, const int32_t* ids,
                        const GhRound& p, hipStream_t s) {
   if (n == 0) return;
   scatter(d, ids, hb, (int32_t)n, 0x80, s);
-  seg_launch(d, cur, rows_set(d, nullptr, obs, 1), nullptr, p, OpMergeList{d, p}, s);
+  if (gh_owned(d, obs)) seg_launch(d, cur, rows_set(d, nullptr, obs, 1), nullptr, p, OpMergeList{d, p}, s);
 }
 
 void launch_hb_check(const GhDev& d, int cur, int32_t* flag, const GhRound& p, hipStream_t s) {

@@ -7,6 +7,14 @@
 // its owner; only O(N) per-row / per-column vectors cross ranks (comm.h).
 // G = 1 is the same code with ncol = N.
 //
+// Row sharding (GH_LAYOUT_ROWS, north_star; DESIGN.md "Multi-GPU"): rank g
+// holds observer rows [row0, row0 + nrows) for ALL member columns (col0 = 0,
+// ncol = N), plus GHOST rows: the snapshots of the senders its receivers pull
+// this round, copied in from their owners by one alltoallv before the round.
+// Table row SLOTS: owned row i at slot i - row0, ghosts after them; rslot[i]
+// maps a global row to its slot (-1: not held). Column layout: row0 = 0,
+// nrows = nslots = N, rslot = null (slot = row id).
+//
 // Device layout (SPEC.md §1/§3, DESIGN.md "Data layout in HBM"):
 //   The N x ld local membership tables are stored in column TILES of TW
 //   members:
@@ -171,6 +179,11 @@ struct GhDev {
   int32_t ncsw;     // ncs / 32 (bitmap words per rank)
   int32_t rank, world;
   int64_t ntiles;   // ld / tw
+  int32_t rowlay;   // GH_LAYOUT_ROWS
+  int64_t row0, nrows;  // rows this engine owns (column layout: 0, n)
+  int64_t nslots;   // table rows per tile (owned + ghost slots; column layout: n)
+  int32_t *rslot;   // row layout: [n] table slot of a global row, -1 = not held
+  int32_t *pvf;     // row layout: [n][k] validity of each receiver's draws (summed over shards)
   uint16_t *hn[2];  // narrow double buffer
   uint32_t *pl[2];  // sender snapshot plane per buffer (null: plane off)
   int32_t *pvalid;  // [2]: plane of buffer b written by the round that wrote b
@@ -236,9 +249,19 @@ __host__ __device__ __forceinline__ bool gh_flag_for(int32_t x, int32_t ts, int6
   return x > 1 && cg != i && (int64_t)ts < (int64_t)r - t_fail;
 }
 
+// Linear index of cell (table slot s, LOCAL member column c) in the tiled layout.
+__host__ __device__ __forceinline__ int64_t gh_cell_slot(const GhDev& d, int64_t s, int64_t c) {
+  return (c >> d.lgtw) * d.tstride + (s << d.lgtw) + (c & (d.tw - 1));
+}
+// Table slot of global row i (device; the row must be held: owned or ghost).
+__device__ __forceinline__ int64_t gh_slot(const GhDev& d, int64_t i) { return d.rslot ? d.rslot[i] : i; }
+// Row i is one this engine owns (and rounds / events write).
+__host__ __device__ __forceinline__ bool gh_owned(const GhDev& d, int64_t i) {
+  return i >= d.row0 && i < d.row0 + d.nrows;
+}
 // Linear index of cell (observer i, LOCAL member column c) in the tiled layout.
-__host__ __device__ __forceinline__ int64_t gh_cell(const GhDev& d, int64_t i, int64_t c) {
-  return (c >> d.lgtw) * d.tstride + (i << d.lgtw) + (c & (d.tw - 1));
+__device__ __forceinline__ int64_t gh_cell(const GhDev& d, int64_t i, int64_t c) {
+  return gh_cell_slot(d, gh_slot(d, i), c);
 }
 // Arena index of cell (slot s, local column c) (the segment's column offset).
 __host__ __device__ __forceinline__ int64_t gh_wcell(const GhDev& d, int64_t s, int64_t c) {
@@ -472,6 +495,11 @@ struct GhRound {
 void launch_active_pre(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_active_post(const GhDev& d, const GhRound& p, hipStream_t s);
 void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
+// row layout: draw validity at the senders' owners (pvf, then SUM over
+// shards), then every receiver's inbox
+void launch_peers_rows(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
+void launch_inbox_rows(const GhDev& d, const GhRound& p, hipStream_t s);
+void launch_negate(int32_t* x, int64_t n, hipStream_t s);
 void launch_ring_count(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_ring_select(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
@@ -524,6 +552,19 @@ void launch_merge_list(const GhDev& d, int cur, int32_t obs, const int32_t* ids,
                        const GhRound& p, hipStream_t s);
 void launch_join_reset(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p,
                        hipStream_t s);
+// rows.hip (row layout): ghost rows. pack: rows[0..ns) (owned) with their
+// destination ranks dest[] -> out (ghost_row_bytes each), wcnt[dest] += the
+// wide segments; wide: their exact cells -> out records (ghost_wide_record_bytes
+// each) at wcur[dest]++; unpack: nr received rows -> slots slot0..; unwide:
+// nrec records -> fresh arena slots of buffer cur
+int64_t ghost_row_bytes(const GhDev& d);
+int64_t ghost_wide_record_bytes(const GhDev& d);
+void launch_ghost_pack(const GhDev& d, int cur, const int32_t* rows, const int32_t* dest, int64_t ns, char* out,
+                       int32_t* wcnt, hipStream_t s);
+void launch_ghost_wide(const GhDev& d, int cur, const int32_t* rows, const int32_t* dest, int64_t ns, int32_t* wcur,
+                       char* out, hipStream_t s);
+void launch_ghost_unpack(const GhDev& d, int cur, const char* in, int64_t nr, int64_t slot0, hipStream_t s);
+void launch_ghost_unwide(const GhDev& d, int cur, const char* in, int64_t nrec, hipStream_t s);
 // place.hip (rbits holds the master row [q=0] and, for repair, the observer row [q=1])
 void launch_candidates(const GhDev& d, int32_t nr, hipStream_t s);
 void launch_put(const GhDev& d, int32_t nr, int64_t n, int32_t R, int32_t now, uint64_t seed, hipStream_t s);

@@ -57,6 +57,17 @@ struct Engine {
   // the current table was written by something other than a round: its
   // sender plane is stale (pvalid[cur] = 0 before the next round)
   bool pforce = true;
+  // row layout (GH_LAYOUT_ROWS): rows per shard, host mirror of rslot, the
+  // current ghost rows, exchange buffers (grown on demand)
+  bool rowlay = false;
+  int64_t nrs = 0;
+  std::vector<int32_t> rslot_h;
+  std::vector<int32_t> ghosts;
+  int32_t* gwcnt = nullptr;  // [2 * world] wide counts / cursors per destination
+  void* gbuf[4] = {nullptr, nullptr, nullptr, nullptr};  // send, recv, wide send, wide recv
+  size_t gcap_bytes[4] = {0, 0, 0, 0};
+  int32_t* gidx = nullptr;   // [2 * cap] rows to send, their destinations
+  int64_t gidx_cap = 0;
   int plane = 0;         // sender snapshot plane (pull mode, 3 <= k <= 4, N >= GH_PLANE_MIN_N; GH_PLANE=0/1)
   // upper bound of every heartbeat in the table (int32 overflow check,
   // slave/slave.go:446): +1 per round, max of imported / merged values
@@ -283,7 +294,7 @@ int grow_arena(Engine* e, int64_t cap) {
 // than a quarter is in use (gh_step then checks after every round).
 int maybe_grow(Engine* e, bool* busy = nullptr) {
   GhDev& d = e->d;
-  const int64_t segs = d.ntiles * (int64_t)e->n;
+  const int64_t segs = d.ntiles * d.nslots;
   if (busy) *busy = false;
   if (d.wcap >= segs) return GH_OK;
   int32_t used = 0;
@@ -338,9 +349,142 @@ int gather_rows(Engine* e, const int32_t* rows_dev, int32_t nr) {
   }
   launch_rowbits(d, e->cur, rows_dev, nr, e->stream);
   HIPCHK(e, hipGetLastError());
+  if (e->rowlay) {  // slice 0: the owner's bits, zeros elsewhere -> their sum
+    COMMCHK(e, e->comm->allreduce(d.rbits, d.rbits, (size_t)nr * d.ncsw, GH_DT_I32, GH_OP_SUM, e->stream));
+    return GH_OK;
+  }
   const size_t bytes = sizeof(uint32_t) * (size_t)nr * d.ncsw;
   COMMCHK(e, e->comm->allgather(d.rbits + (size_t)e->rank * nr * d.ncsw, d.rbits, bytes, e->stream));
   return GH_OK;
+}
+
+// ---- row layout: ghost rows ------------------------------------------------
+int row_owner(const Engine* e, int64_t i) { return (int)(i / e->nrs); }
+
+// Device scratch b of at least `bytes` (grown, never shrunk).
+int gbuf_reserve(Engine* e, int b, size_t bytes) {
+  if (bytes <= e->gcap_bytes[b]) return GH_OK;
+  dfree(e, e->gbuf[b]);
+  e->gbuf[b] = nullptr;
+  e->gcap_bytes[b] = 0;
+  char* q = nullptr;
+  int rc;
+  if ((rc = dalloc(e, &q, bytes, 0))) return rc;
+  e->gbuf[b] = q;
+  e->gcap_bytes[b] = bytes;
+  return GH_OK;
+}
+
+// Every shard calls this with the same `want` (want[r]: the rows rank r
+// needs and does not own, ascending): the rows it owns go to the ranks that
+// want them, and its own wants land in ghost slots nrows, nrows + 1, ... of
+// the current buffer (in owner order, ascending within), wide segments
+// included. The previous ghosts are dropped.
+int ghost_exchange(Engine* e, const std::vector<std::vector<int32_t>>& want) {
+  GhDev& d = e->d;
+  const int G = e->world, me = e->rank;
+  for (int32_t s : e->ghosts) e->rslot_h[s] = -1;
+  e->ghosts = want[me];
+  if ((int64_t)e->ghosts.size() > d.nslots - d.nrows) return set_err(e, GH_ENOMEM, "ghost rows exceed their slots");
+  std::vector<size_t> rcnt(G, 0), scnt(G, 0);
+  for (size_t j = 0; j < e->ghosts.size(); ++j) {
+    e->rslot_h[e->ghosts[j]] = (int32_t)(d.nrows + (int64_t)j);
+    rcnt[row_owner(e, e->ghosts[j])]++;
+  }
+  std::vector<int32_t> idx;  // rows to send, then their destinations
+  std::vector<int32_t> dst;
+  for (int r = 0; r < G; ++r)
+    if (r != me)
+      for (int32_t s : want[r])
+        if (row_owner(e, s) == me) {
+          idx.push_back(s);
+          dst.push_back(r);
+          scnt[r]++;
+        }
+  const int64_t ns = (int64_t)idx.size(), nr = (int64_t)e->ghosts.size();
+  if (ns > e->gidx_cap) {
+    dfree(e, e->gidx);
+    e->gidx = nullptr;
+    e->gidx_cap = 0;
+    int rc;
+    if ((rc = dalloc(e, &e->gidx, 2 * std::max<int64_t>(ns, 1024), 0))) return rc;
+    e->gidx_cap = std::max<int64_t>(ns, 1024);
+  }
+  int32_t* drows = e->gidx;
+  int32_t* ddest = e->gidx + e->gidx_cap;
+  HIPCHK(e, hipMemcpyAsync(d.rslot, e->rslot_h.data(), sizeof(int32_t) * e->n, hipMemcpyHostToDevice, e->stream));
+  if (ns) {
+    HIPCHK(e, hipMemcpyAsync(drows, idx.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(ddest, dst.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice, e->stream));
+  }
+  const int64_t RB = ghost_row_bytes(d);
+  int rc;
+  if ((rc = gbuf_reserve(e, 0, (size_t)std::max<int64_t>(ns, 1) * RB)) ||
+      (rc = gbuf_reserve(e, 1, (size_t)std::max<int64_t>(nr, 1) * RB)))
+    return rc;
+  HIPCHK(e, hipMemsetAsync(e->gwcnt, 0, sizeof(int32_t) * G, e->stream));
+  launch_ghost_pack(d, e->cur, drows, ddest, ns, static_cast<char*>(e->gbuf[0]), e->gwcnt, e->stream);
+  HIPCHK(e, hipGetLastError());
+  std::vector<size_t> sb(G), rbv(G);
+  for (int r = 0; r < G; ++r) {
+    sb[r] = scnt[r] * RB;
+    rbv[r] = rcnt[r] * RB;
+  }
+  COMMCHK(e, e->comm->alltoallv(e->gbuf[0], sb.data(), e->gbuf[1], rbv.data(), e->stream));
+  launch_ghost_unpack(d, e->cur, static_cast<const char*>(e->gbuf[1]), nr, d.nrows, e->stream);
+  HIPCHK(e, hipGetLastError());
+  // wide segments of the sent rows: every shard's per-destination counts
+  int32_t* mat = e->gwcnt + 2 * G;
+  COMMCHK(e, e->comm->allgather(e->gwcnt, mat, sizeof(int32_t) * G, e->stream));
+  std::vector<int32_t> m((size_t)G * G);
+  HIPCHK(e, hipMemcpyAsync(m.data(), mat, sizeof(int32_t) * G * G, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  int64_t any = 0;
+  for (int32_t v : m) any += v;
+  if (any == 0) return GH_OK;
+  const int64_t REC = ghost_wide_record_bytes(d);
+  std::vector<int32_t> cur0(G);
+  int64_t ws = 0, wr = 0;
+  for (int r = 0; r < G; ++r) {
+    cur0[r] = (int32_t)ws;
+    ws += m[(size_t)me * G + r];  // my records to r
+    wr += m[(size_t)r * G + me];  // r's records to me
+    sb[r] = (size_t)m[(size_t)me * G + r] * REC;
+    rbv[r] = (size_t)m[(size_t)r * G + me] * REC;
+  }
+  if ((rc = gbuf_reserve(e, 2, (size_t)std::max<int64_t>(ws, 1) * REC)) ||
+      (rc = gbuf_reserve(e, 3, (size_t)std::max<int64_t>(wr, 1) * REC)))
+    return rc;
+  HIPCHK(e, hipMemcpyAsync(e->gwcnt + G, cur0.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, e->stream));
+  launch_ghost_wide(d, e->cur, drows, ddest, ns, e->gwcnt + G, static_cast<char*>(e->gbuf[2]), e->stream);
+  HIPCHK(e, hipGetLastError());
+  COMMCHK(e, e->comm->alltoallv(e->gbuf[2], sb.data(), e->gbuf[3], rbv.data(), e->stream));
+  launch_ghost_unwide(d, e->cur, static_cast<const char*>(e->gbuf[3]), wr, e->stream);
+  HIPCHK(e, hipGetLastError());
+  return GH_OK;
+}
+
+// The round's ghosts: the senders of each shard's receivers that other
+// shards own, from the (replicated) pull inboxes.
+int round_ghosts(Engine* e) {
+  const int G = e->world;
+  const int k = e->cfg.fanout;
+  std::vector<int32_t> inbox((size_t)e->n * (k + 1));
+  HIPCHK(e, hipMemcpyAsync(inbox.data(), e->d.inbox, sizeof(int32_t) * inbox.size(), hipMemcpyDeviceToHost,
+                           e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  std::vector<std::vector<uint8_t>> mark(G, std::vector<uint8_t>(e->n, 0));
+  for (int64_t i = 0; i < e->n; ++i) {
+    const int r = row_owner(e, i);
+    const int32_t* b = inbox.data() + i * (k + 1);
+    for (int q = 0; q < b[0]; ++q)
+      if (row_owner(e, b[1 + q]) != r) mark[r][b[1 + q]] = 1;
+  }
+  std::vector<std::vector<int32_t>> want(G);
+  for (int r = 0; r < G; ++r)
+    for (int32_t s = 0; s < e->n; ++s)
+      if (mark[r][s]) want[r].push_back(s);
+  return ghost_exchange(e, want);
 }
 
 int allreduce_i32(Engine* e, int32_t* send, int32_t* recv, size_t count) {
@@ -370,6 +514,12 @@ int process_events(Engine* e, int32_t r) {
       stopped.push_back(x.member);
     }
   int rc;
+  if (e->rowlay) {  // a shard freezes and resets only the rows it owns
+    std::vector<int32_t> own;
+    for (int32_t i : stopped)
+      if (gh_owned(e->d, i)) own.push_back(i);
+    stopped.swap(own);
+  }
   if (!stopped.empty()) {
     if ((rc = upload(e, e->ev_buf, stopped))) return rc;
     if ((rc = freeze_rows(e, stopped, e->ev_buf, p))) return rc;
@@ -401,6 +551,12 @@ int process_events(Engine* e, int32_t r) {
         e->alive[x.member] = 1;
       }
     }
+  if (e->rowlay) {
+    std::vector<int32_t> own;
+    for (int32_t i : fresh)
+      if (gh_owned(e->d, i)) own.push_back(i);
+    fresh.swap(own);
+  }
   if (!fresh.empty()) {
     if ((rc = upload(e, e->ev_buf, fresh))) return rc;
     launch_join_reset(e->d, e->cur, e->ev_buf, (int32_t)fresh.size(), p, e->stream);
@@ -416,6 +572,12 @@ int process_events(Engine* e, int32_t r) {
     if ((rc = allreduce_i32(e, e->d.nd + 4, e->d.nd + 4, 1))) return rc;
     if ((rc = upload(e, e->rows_buf, {I}))) return rc;
     if ((rc = gather_rows(e, e->rows_buf, 1))) return rc;
+    if (e->rowlay && e->world > 1) {  // every shard merges the introducer's row: a ghost of it
+      std::vector<std::vector<int32_t>> want(e->world);
+      for (int r = 0; r < e->world; ++r)
+        if (r != row_owner(e, I)) want[r].push_back(I);
+      if ((rc = ghost_exchange(e, want))) return rc;
+    }
     launch_join_bcast(e->d, e->cur, I, p, e->stream);
   }
   launch_count(e->d, e->cur, p, e->stream);
@@ -454,6 +616,21 @@ int check_files(Engine* e, const int32_t* files, int64_t n, bool distinct) {
 // decoded from the tiled local columns of every shard -> host [n_rows][n].
 int export_table(Engine* e, int32_t* out, int what, int64_t row0, int64_t n_rows) {
   const GhDev& d = e->d;
+  if (e->rowlay) {  // each row from its owner: zeros elsewhere, summed
+    const size_t cnt = (size_t)n_rows * d.ncs;
+    Staging st;
+    int rc;
+    if ((rc = st.alloc(e, sizeof(int32_t) * cnt))) return rc;
+    HIPCHK(e, hipMemsetAsync(st.p, 0, sizeof(int32_t) * cnt, e->stream));
+    launch_unpack(d, e->cur, st.as<int32_t>(), row0, n_rows, what, round_params(e, e->round + 1), e->stream);
+    HIPCHK(e, hipGetLastError());
+    COMMCHK(e, e->comm->allreduce(st.p, st.p, cnt, GH_DT_I32, GH_OP_SUM, e->stream));
+    std::vector<int32_t> host(cnt);
+    HIPCHK(e, hipMemcpyAsync(host.data(), st.p, sizeof(int32_t) * cnt, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    for (int64_t r = 0; r < n_rows; ++r) std::memcpy(out + r * e->n, host.data() + r * d.ncs, sizeof(int32_t) * e->n);
+    return GH_OK;
+  }
   const size_t chunk = (size_t)n_rows * d.ncs;  // one shard's [n_rows][ncs]
   Staging st;
   int rc;
@@ -525,6 +702,11 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
     return GH_EINVAL;
   }
   if (e->tpw != 1 && e->tpw != 2 && e->tpw != 4 && e->tpw != 8) e->tpw = 1;
+  if (cfg->shard_layout != GH_LAYOUT_COLUMNS &&
+      (cfg->shard_layout != GH_LAYOUT_ROWS || cfg->peer_mode != GH_PEER_PULL)) {
+    delete e;  // the row layout is the pull-mode path (ring targets need every sender's list order)
+    return GH_EINVAL;
+  }
   // communicator
   std::string cerr;
   GhComm* c = nullptr;
@@ -545,10 +727,20 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   c->world = world;
   e->comm.reset(c);
   // column shard: [rank*ncs, rank*ncs + ncol), padded so that 8 | (ld / tw)
-  // (the XCD-aware map gives each of the 8 XCDs the same number of tiles)
-  const int64_t ncs = ((e->n + world - 1) / world + 31) / 32 * 32;
-  const int64_t col0 = (int64_t)rank * ncs;
+  // (the XCD-aware map gives each of the 8 XCDs the same number of tiles).
+  // Row shard: all columns; rows [rank*nrs, rank*nrs + nrows) plus ghosts.
+  const bool rowlay = cfg->shard_layout == GH_LAYOUT_ROWS;
+  const int64_t ncs = rowlay ? (e->n + 31) / 32 * 32 : ((e->n + world - 1) / world + 31) / 32 * 32;
+  const int64_t col0 = rowlay ? 0 : (int64_t)rank * ncs;
   const int64_t ncol = std::max<int64_t>(0, std::min<int64_t>(ncs, e->n - col0));
+  const int64_t nrs = rowlay ? ((int64_t)e->n + world - 1) / world : e->n;
+  const int64_t row0 = rowlay ? std::min<int64_t>((int64_t)rank * nrs, e->n) : 0;
+  const int64_t nrows = rowlay ? std::min<int64_t>(nrs, e->n - row0) : e->n;
+  // ghost slots: every distinct remote sender of the owned receivers, and
+  // the introducer's row for a join broadcast
+  const int64_t gcap = rowlay && world > 1 ? std::min<int64_t>(e->n - nrows, nrows * cfg->fanout + 1) : 0;
+  e->rowlay = rowlay;
+  e->nrs = nrs;
   const int64_t pad = std::max<int64_t>(GH_PAD, 8 * (int64_t)tw);
   e->ld = (ncs + pad - 1) / pad * pad;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -560,7 +752,11 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   d.ld = e->ld;
   d.tw = tw;
   d.lgtw = __builtin_ctz((unsigned)tw);
-  d.tstride = (int64_t)e->n * tw;
+  d.rowlay = rowlay;
+  d.row0 = row0;
+  d.nrows = nrows;
+  d.nslots = nrows + gcap;
+  d.tstride = d.nslots * tw;
   d.ntiles = e->ld / tw;
   d.col0 = col0;
   d.ncol = (int32_t)ncol;
@@ -569,9 +765,9 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   d.rank = rank;
   d.world = world;
   d.tsat = cfg->t_cleanup < GH_TSAT_T;
-  d.wcap = arena_slots(cfg, d.ntiles * (int64_t)e->n, tw);
+  d.wcap = arena_slots(cfg, d.ntiles * d.nslots, tw);
   e->cfg.tile_width = tw;
-  const int64_t cells = (int64_t)e->n * e->ld;
+  const int64_t cells = d.nslots * e->ld;
   const int64_t nch = e->ld / tw;  // tiles: per-(tile, row) ring / quirk summaries
   const int64_t slots = (int64_t)world * ncs;  // global rows incl. the last shard's tail
   const int64_t inbox = std::max<int64_t>(slots * (cfg->fanout + 1), 3 * (int64_t)e->n);
@@ -612,6 +808,18 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
          (rc = dalloc(e, &d.qcarry, e->n, 0)) || (rc = dalloc(e, &d.qlast, e->n, 0))))
       break;
     if ((rc = dalloc(e, &d.rbits, (size_t)world * 2 * d.ncsw, 0))) break;
+    if (rowlay) {
+      e->rslot_h.assign(e->n, -1);
+      for (int64_t i = row0; i < row0 + nrows; ++i) e->rslot_h[i] = (int32_t)(i - row0);
+      if ((rc = dalloc(e, &d.rslot, e->n, 0xFF)) || (rc = dalloc(e, &d.pvf, (int64_t)e->n * cfg->fanout, 0)) ||
+          (rc = dalloc(e, &e->gwcnt, 2 * (int64_t)world + (int64_t)world * world, 0)))
+        break;
+      if (hipMemcpyAsync(d.rslot, e->rslot_h.data(), sizeof(int32_t) * e->n, hipMemcpyHostToDevice, e->stream) !=
+          hipSuccess) {
+        rc = GH_EHIP;
+        break;
+      }
+    }
     for (int b = 0; b < 2 && rc == GH_OK; ++b)
       if ((rc = dalloc(e, &d.wh[b], (size_t)d.wcap * tw, 0xFF)) || (rc = dalloc(e, &d.wt[b], (size_t)d.wcap * tw, 0)) ||
           (rc = dalloc(e, &d.wf[b], (size_t)d.wcap * tw / 8, 0)))
@@ -660,7 +868,7 @@ int quirk_flags(Engine* e, const GhRound& p) {
   GhDev& d = e->d;
   launch_quirk_scan(d, e->cur, e->dcur, p, e->stream);
   HIPCHK(e, hipGetLastError());
-  if (e->world > 1)
+  if (e->world > 1 && !e->rowlay)  // row layout: a row's runs never cross shards
     COMMCHK(e, e->comm->allgather(d.qall + (size_t)e->rank * e->n, d.qall, e->n, e->stream));
   launch_quirk_apply(d, e->cur, e->dcur, p, e->stream);
   HIPCHK(e, hipGetLastError());
@@ -671,6 +879,16 @@ int quirk_flags(Engine* e, const GhRound& p) {
 // receiver's column draws and validates, allgather) or ring targets.
 int build_inboxes(Engine* e, const GhRound& p) {
   GhDev& d = e->d;
+  if (e->rowlay) {
+    // validity at the senders' owners, summed; every shard builds all inboxes
+    launch_peers_rows(d, e->cur, e->dcur, p, e->stream);
+    HIPCHK(e, hipGetLastError());
+    int rc;
+    if (e->world > 1 && (rc = allreduce_i32(e, d.pvf, d.pvf, (size_t)e->n * e->cfg.fanout))) return rc;
+    launch_inbox_rows(d, p, e->stream);
+    HIPCHK(e, hipGetLastError());
+    return e->world > 1 ? round_ghosts(e) : GH_OK;
+  }
   if (e->cfg.peer_mode == GH_PEER_PULL) {
     launch_peers_pull(d, e->cur, e->dcur, p, e->stream);
     HIPCHK(e, hipGetLastError());
@@ -700,7 +918,7 @@ int build_inboxes(Engine* e, const GhRound& p) {
 // idempotent rewrites of whole rows).
 template <class F>
 int encode_rows(Engine* e, const char* what, F launch) {
-  const int64_t segs = e->d.ntiles * (int64_t)e->n;
+  const int64_t segs = e->d.ntiles * e->d.nslots;
   for (;;) {
     launch();
     HIPCHK(e, hipGetLastError());
@@ -726,7 +944,7 @@ int encode_rows(Engine* e, const char* what, F launch) {
 // rewrite.
 int clear_table(Engine* e) {
   GhDev& d = e->d;
-  HIPCHK(e, hipMemsetAsync(d.hn[e->cur], 0xFF, sizeof(uint16_t) * (size_t)e->n * e->ld, e->stream));
+  HIPCHK(e, hipMemsetAsync(d.hn[e->cur], 0xFF, sizeof(uint16_t) * (size_t)d.nslots * e->ld, e->stream));
   HIPCHK(e, hipMemsetAsync(d.wn + e->cur, 0, sizeof(int32_t), e->stream));
   HIPCHK(e, hipMemsetAsync(d.err, 0, sizeof(int32_t), e->stream));
   e->lost.clear();
@@ -737,7 +955,8 @@ int clear_table(Engine* e) {
 // leave it (after their segments were rewritten).
 int settle_rows(Engine* e, int64_t row0, int64_t n, const GhRound& p) {
   std::vector<int32_t> stopped, running;
-  for (int64_t i = row0; i < row0 + n; ++i) (e->alive[i] ? running : stopped).push_back((int32_t)i);
+  for (int64_t i = row0; i < row0 + n; ++i)
+    if (gh_owned(e->d, i)) (e->alive[i] ? running : stopped).push_back((int32_t)i);
   int rc;
   if ((rc = release_rows(e, running))) return rc;
   for (size_t b = 0; b < stopped.size(); b += (size_t)e->n) {
@@ -867,7 +1086,7 @@ int gh_memory_info(void* h, int64_t* device_bytes, int64_t* wide_used, int64_t* 
     // the tables (narrow x2, wide arenas x2, frozen store); per-row and
     // per-column vectors and the file table are counted by hipMemGetInfo
     // callers, not here
-    const int64_t cells = (int64_t)e->n * e->ld;
+    const int64_t cells = d.nslots * e->ld;
     *device_bytes = 2 * cells * 2 + (e->plane ? cells : 0) + 2 * d.wcap * ((int64_t)d.tw * 8 + d.tw / 8) +
                     e->fzcap * e->ld * 8;
   }
@@ -1021,6 +1240,9 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       }
     }
     launch_base(e->d, e->cur, e->dcur, p, e->stream);
+    if (e->rowlay && e->world > 1)  // each column's base from its owner row's shard
+      COMMCHK(e, e->comm->allreduce(e->d.base[e->cur ^ 1], e->d.base[e->cur ^ 1], e->ld, GH_DT_I32, GH_OP_MAX,
+                                    e->stream));
     if ((rc = decide_active(e, p))) return rc;
     if (e->cfg.detect_mode == GH_DETECT_QUIRK) {
       // skip the pre-pass when no shard's table holds a flag (the round
@@ -1039,6 +1261,17 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt, true);
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[3 * q + 2], e->stream));
     launch_round_slow(e->d, e->cur, e->dcur, p, e->stream);
+    if (e->rowlay && e->world > 1) {
+      // every shard detected in its own rows: D_r's counts and first
+      // detectors over all of them (MIN as the MAX of negations)
+      int32_t* dc = e->d.det_cnt[e->dcur ^ 1];
+      int32_t* dm = e->d.det_min[e->dcur ^ 1];
+      if ((rc = allreduce_i32(e, dc, dc, e->ld))) return rc;
+      launch_negate(dm, e->ld, e->stream);
+      COMMCHK(e, e->comm->allreduce(dm, dm, e->ld, GH_DT_I32, GH_OP_MAX, e->stream));
+      launch_negate(dm, e->ld, e->stream);
+      HIPCHK(e, hipGetLastError());
+    }
     launch_finish(e->d, e->dcur, p, e->stream);
     HIPCHK(e, hipGetLastError());
     e->cur ^= 1;
@@ -1104,7 +1337,11 @@ int gh_read_failed(void* h, uint32_t* bitmap, int64_t n_words) {
   int rc;
   if ((rc = st.alloc(e, sizeof(uint32_t) * (size_t)d.ncsw * e->world))) return rc;
   // shard g's pending D bits cover members [g*ncs, (g+1)*ncs): word-aligned
-  COMMCHK(e, e->comm->allgather(d.dbits, st.p, sizeof(uint32_t) * d.ncsw, e->stream));
+  // (row layout: every shard holds all of them)
+  if (e->rowlay)
+    HIPCHK(e, hipMemcpyAsync(st.p, d.dbits, sizeof(uint32_t) * d.ncsw, hipMemcpyDeviceToDevice, e->stream));
+  else
+    COMMCHK(e, e->comm->allgather(d.dbits, st.p, sizeof(uint32_t) * d.ncsw, e->stream));
   std::memset(bitmap, 0, n_words * sizeof(uint32_t));
   HIPCHK(e, hipMemcpyAsync(bitmap, st.p, words * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -1404,7 +1641,9 @@ int gh_debug_raw(void* h, int32_t row, int64_t c0, int64_t n, uint16_t* codes, i
   if (!e || row < 0 || row >= e->n || c0 < 0 || c0 + n > e->ld) return GH_EINVAL;
   HIPCHK(e, hipSetDevice(e->cfg.device));
   for (int64_t c = c0; c < c0 + n; ++c) {
-    HIPCHK(e, hipMemcpy(codes + (c - c0), e->d.hn[e->cur] + gh_cell(e->d, row, c), 2, hipMemcpyDeviceToHost));
+    const int64_t slot = e->rowlay ? e->rslot_h[row] : row;
+    if (slot < 0) return set_err(e, GH_EINVAL, "row not held by this shard");
+    HIPCHK(e, hipMemcpy(codes + (c - c0), e->d.hn[e->cur] + gh_cell_slot(e->d, slot, c), 2, hipMemcpyDeviceToHost));
     HIPCHK(e, hipMemcpy(bases + (c - c0), e->d.base[e->cur] + c, 4, hipMemcpyDeviceToHost));
   }
   return GH_OK;

@@ -64,6 +64,8 @@ __global__ __launch_bounds__(256) void k_active_pre(GhDev d, int cur, int dcur, 
       a = true;
     } else if (d.nd[dcur] > GH_DLIST_MAX) {
       u = 2;
+    } else if (!gh_owned(d, i)) {
+      u = 1;  // row layout: the owner counts it, this shard adds 0
     } else {
       u = 1;
       const int32_t* dc = d.det_cnt[dcur];
@@ -89,6 +91,10 @@ __global__ __launch_bounds__(256) void k_active_exact(GhDev d, int cur, int dcur
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= p.n || d.und[i] != 2) return;
+  if (!gh_owned(d, i)) {  // row layout: the owner counts it, this shard adds 0
+    if (lane == 0) d.post[i] = 0;
+    return;
+  }
   const int32_t* dc = d.det_cnt[dcur];
   const int32_t* dm = d.det_min[dcur];
   int cnt = 0;
@@ -148,25 +154,79 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
   d.inbox[beg - 1] = nv;
 }
 
+// Row layout: sender s's owner checks receiver i's draws against s's row
+// (the cells only it holds); pvf[i*k + q] = 1 there, 0 on every other shard,
+// so a SUM over shards is the validity of every draw.
+__global__ __launch_bounds__(256) void k_peers_rows(GhDev d, int cur, int dcur, GhRound p) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const bool ib = dbit(d.dbits, i);
+  const int dci = ib ? d.det_cnt[dcur][i] : 0;
+  const int dmi = ib ? d.det_min[dcur][i] : 0;
+  for (int q = 0; q < p.k; ++q) {
+    int v = 0;
+    if (d.alive[i] && p.n >= 2) {
+      const uint32_t u = gh_philox_word(p.seed, (uint32_t)i, (uint32_t)p.r, GH_TAG_PEER, (uint32_t)(q >> 2), q & 3);
+      const uint32_t w = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
+      const int s = (int)w + ((int64_t)w >= i);
+      if (gh_owned(d, s) && d.alive[s] && d.active[s]) {
+        const GhCell c = gh_get(d, cur, s, i, p.r);
+        v = c.x >= 0 && !c.f && !(ib && removes_at(dci, dmi, s));
+      }
+    }
+    d.pvf[i * p.k + q] = v;
+  }
+}
+
+// Row layout: every receiver's inbox from the summed validity of its draws
+// (the same layout as k_peers_pull's, on every shard).
+__global__ __launch_bounds__(256) void k_inbox_rows(GhDev d, GhRound p) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const int64_t beg = i * (p.k + 1) + 1;
+  int nv = 0;
+  for (int q = 0; q < p.k; ++q) {
+    if (!d.pvf[i * p.k + q]) continue;
+    const uint32_t u = gh_philox_word(p.seed, (uint32_t)i, (uint32_t)p.r, GH_TAG_PEER, (uint32_t)(q >> 2), q & 3);
+    const uint32_t w = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
+    d.inbox[beg + nv++] = (int)w + ((int64_t)w >= i);
+  }
+  d.inbox[beg - 1] = nv;
+}
+
+// x -> -x over n int32 (a MIN reduction as a MAX of negations)
+__global__ void k_negate(int32_t* x, int64_t n) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) x[t] = -x[t];
+}
+
 // ---- segment walks -------------------------------------------------------
 // The helper kernels below read the table the way k_round does: a lane owns
 // 8 consecutive members (16 B of narrow cells), SEG = TW/8 lanes cover one
 // row segment of a tile, and consecutive waves take consecutive (tile, row)
 // segments in storage order, so every wave instruction is one contiguous
 // 1 KiB access.
+// Segments are (tile, owned row) pairs, tile-major: segment sid is tile
+// sid / nrows, row row0 + sid % nrows.
 template <int TW>
 struct SegWalk {
   static constexpr int SEG = TW / 8;
   static constexpr int RPW = 64 / SEG;
   int lane, sub, lc;
-  int64_t nseg, first, stride;
-  __device__ SegWalk(const GhRound& p) {
+  int64_t nseg, first, stride, row0, nrows;
+  __device__ SegWalk(const GhDev& d, const GhRound& p) {
     lane = threadIdx.x & 63;
     sub = lane / SEG;
     lc = lane % SEG;
-    nseg = (p.ld / TW) * p.n;
+    row0 = d.row0;
+    nrows = d.nrows;
+    nseg = (p.ld / TW) * nrows;
     first = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * RPW;
     stride = (((int64_t)gridDim.x * blockDim.x) >> 6) * RPW;
+  }
+  __device__ void at(int64_t sid, int64_t& t, int& i) const {
+    t = sid / nrows;
+    i = (int)(row0 + (sid - t * nrows));
   }
 };
 
@@ -183,12 +243,13 @@ __device__ __forceinline__ uint32_t removed8(const GhDev& d, int dcur, int64_t l
 // sender's snapshot list (present after REMOVE, not detected by it).
 template <int TW>
 __global__ __launch_bounds__(256) void k_ring_tiles(GhDev d, int cur, int dcur, GhRound p) {
-  const SegWalk<TW> w(p);
+  const SegWalk<TW> w(d, p);
   for (int64_t base = w.first; base < w.nseg; base += w.stride) {
     const int64_t sid = base + w.sub;
     const bool valid = sid < w.nseg;
-    const int64_t t = valid ? sid / p.n : 0;
-    const int i = valid ? (int)(sid - t * p.n) : 0;
+    int64_t t = 0;
+    int i = 0;
+    if (valid) w.at(sid, t, i);
     const int64_t l0 = t * TW + w.lc * 8;
     int cnt = 0;
     if (valid && d.alive[i] && d.active[i]) {  // only sending rows' counts are read
@@ -198,7 +259,7 @@ __global__ __launch_bounds__(256) void k_ring_tiles(GhDev d, int cur, int dcur, 
     }
 #pragma unroll
     for (int o = SegWalk<TW>::SEG / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-    if (valid && w.lc == 0) d.rcnt[sid] = (uint16_t)cnt;
+    if (valid && w.lc == 0) d.rcnt[t * p.n + i] = (uint16_t)cnt;
   }
 }
 
@@ -469,7 +530,9 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
     *d.nstorm = 0;
     d.wn[cur ^ 1] = 0;  // the round rewrites every running row of the next buffer
     d.nflag[cur ^ 1] = 0;  // counted by this round's writers
-    d.cntl[d.n] = d.nd[dcur];  // |D_{r-1}| of this shard next to the local counts, for one allreduce
+    // |D_{r-1}| of this shard next to the local counts, for one allreduce
+    // (row layout: every shard holds all of D, rank 0 counts it)
+    d.cntl[d.n] = (d.rowlay && d.rank != 0) ? 0 : d.nd[dcur];
     d.cntl[d.n + 1] = d.nflag[cur];  // flagged segments of this shard's table (quirk gate, summed)
     d.pvalid[cur ^ 1] = p.plane;  // this round writes the next buffer's plane
     *d.pfb = 0;
@@ -477,9 +540,11 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
   if (c >= p.ld) return;
   int32_t b = d.base[cur][c];
   const int64_t cg = d.col0 + c;
-  if (c < d.ncol && cg < p.n) {
+  if (c < d.ncol && cg < p.n && gh_owned(d, cg)) {
     const GhCell v = gh_get(d, cur, cg, c, p.r);
     if (v.x >= 0) b = v.x - GH_BASE_LAG;
+  } else if (d.rowlay) {
+    b = INT_MIN;  // the owner of row cg decides; the host takes the max over shards
   }
   d.base[cur ^ 1][c] = b;
 }
@@ -544,11 +609,14 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   // s_meta = alive | active << 1 | inbox count << 2; s_inb = first KB senders
   __shared__ int s_meta[RB];
   __shared__ __attribute__((aligned(16))) int s_inb[RB * KB];
+  // row layout: the senders' table slots (owned or ghost rows)
+  __shared__ __attribute__((aligned(16))) int s_isl[RB * KB];
 
   // block -> (tile group of TPW consecutive tiles, row block); group-major so
   // that the running workgroups sweep the same tiles together
-  const int nrb = (p.n + RB - 1) / RB;
+  const int nrb = (int)((d.nrows + RB - 1) / RB);
   const int ngroups = (int)(p.ld / TW) / TPW;
+  const int rowend = (int)(d.row0 + d.nrows);
   int group, rb;
   if (p.xmap && ngroups % 8 == 0) {
     // XCD-aware: blocks b and b+8 share an XCD (round-robin dispatch, speed
@@ -575,9 +643,9 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     // row metadata once per row, then only the inbox slots in use (storms
     // and guard rows have few senders)
     for (int row = tid; row < RB; row += 256) {
-      const int i = rb * RB + row;
+      const int i = (int)d.row0 + rb * RB + row;
       int meta = 0;
-      if (i < p.n) {
+      if (i < rowend) {
         const int al = d.alive[i];
         const int cnt = al ? gh_in_cnt(d, pull, p.k, i) : 0;
         meta = al | (d.active[i] << 1) | (cnt << 2);
@@ -587,16 +655,20 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     __syncthreads();
     for (int t = tid; t < RB * KB; t += 256) {
       const int row = t / KB, q = t - row * KB;
-      const int i = rb * RB + row;
-      if (q < (s_meta[row] >> 2)) s_inb[t] = d.inbox[gh_in_beg(d, pull, p.k, i) + q];
+      const int i = (int)d.row0 + rb * RB + row;
+      if (q < (s_meta[row] >> 2)) {
+        const int sv = d.inbox[gh_in_beg(d, pull, p.k, i) + q];
+        s_inb[t] = sv;
+        if (d.rowlay) s_isl[t] = d.rslot[sv];
+      }
     }
   } else {
     // one pass, no barrier in between: healthy rounds use every slot
     for (int t = tid; t < RB * KB; t += 256) {
       const int row = t / KB, q = t - row * KB;
-      const int i = rb * RB + row;
+      const int i = (int)d.row0 + rb * RB + row;
       int meta = 0, sv = 0;
-      if (i < p.n) {
+      if (i < rowend) {
         const int al = d.alive[i];
         const int cnt = al ? gh_in_cnt(d, pull, p.k, i) : 0;
         meta = al | (d.active[i] << 1) | (cnt << 2);
@@ -604,6 +676,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       }
       if (q == 0) s_meta[row] = meta;
       s_inb[t] = sv;
+      if (d.rowlay) s_isl[t] = d.rslot[sv];
     }
   }
   __syncthreads();
@@ -628,9 +701,8 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   const int tile = group * TPW + tt;
   const int64_t l0 = (int64_t)tile * TW + lc * CPL;                   // local column of this lane's first cell
   const int c0 = (int)(d.col0 + l0);                                  // its global member id
-  const int64_t tb = (int64_t)tile * ((int64_t)p.n * TW) + lc * CPL;  // tile base + lane offset
-  // uniform tile bases; rows are 32-bit byte offsets from them
-  const int64_t tcell = (int64_t)tile * ((int64_t)p.n * TW);
+  // uniform tile bases; rows are 32-bit byte offsets (table slots) from them
+  const int64_t tcell = (int64_t)tile * d.tstride;
   const char* hno_t = reinterpret_cast<const char*>(hno + tcell);
   char* hnn_t = reinterpret_cast<char*>(hnn + tcell);
   const char* plo_t = reinterpret_cast<const char*>(plo) + (plo ? tcell / 2 : 0);
@@ -685,16 +757,16 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 #pragma unroll 1
   for (int it = 0; it < NIT; ++it) {
     const int rr = wave * RPW + it * RSTEP + sub;
-    const int i_raw = rb * RB + rr;
-    const bool valid = i_raw < p.n;
-    const int i = valid ? i_raw : p.n - 1;  // in-range row for the loads of idle lanes
+    const int i_raw = (int)d.row0 + rb * RB + rr;
+    const bool valid = i_raw < rowend;
+    const int i = valid ? i_raw : rowend - 1;  // in-range row for the loads of idle lanes
+    const uint32_t islot = (uint32_t)(i - d.row0);  // its table slot
     const int rs = valid ? rr : 0;
     int meta = s_meta[rs];
     if constexpr (RPW == 1) meta = uni(meta);
     const bool al = (meta & 1) && valid;
     const int cntv = meta >> 2;
-    const int64_t off = tb + (int64_t)i * TW;
-    const uint32_t ob = (uint32_t)i * (TW * 2) + lb;  // own segment, bytes from the tile base
+    const uint32_t ob = islot * (TW * 2) + lb;  // own segment, bytes from the tile base
 
     // own segment and the senders' snapshots, issued together: plane words
     // when the plane is valid, else the first KB senders' 16-bit segments
@@ -724,6 +796,20 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       if constexpr (RPW == 1) s = uni(s);
       ps[q] = s;
     }
+    // the senders' table slots (column layout: their row ids)
+    uint32_t psl[KB];
+    if (d.rowlay) {
+#pragma unroll
+      for (int q4 = 0; q4 < KB; q4 += 4) {
+        const int4 v = *reinterpret_cast<const int4*>(&s_isl[rs * KB + q4]);
+        const int v4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) psl[q4 + u] = q4 + u < cntv ? (uint32_t)v4[u] : islot;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < KB; ++q) psl[q] = (uint32_t)ps[q];
+    }
     uint32_t pw[KB];
     if constexpr (PLANE_RD) {
       if (use_plane) {
@@ -732,7 +818,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         // code there only costs a fallback)
 #pragma unroll
         for (int q = 0; q < KB; ++q)
-          pw[q] = *reinterpret_cast<const uint32_t*>(plo_t + ((uint32_t)ps[q] * (TW / 2) + lbp));
+          pw[q] = *reinterpret_cast<const uint32_t*>(plo_t + (psl[q] * (TW / 2) + lbp));
       }
     }
     bad |= (w[0] & 0xFFFFu) == GH_N_WIDE;  // own segment wide
@@ -789,11 +875,11 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
           // storms hold few senders (guard rows none): load only the used
           // slots, the rest are absent (-1, a no-op under the max)
           if (q < cntv)
-            pv[q] = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + ((uint32_t)ps[q] * (TW * 2) + lb)));
+            pv[q] = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + (psl[q] * (TW * 2) + lb)));
           else
             pv[q] = v4u{~0u, ~0u, ~0u, ~0u};
         } else {
-          pv[q] = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + ((uint32_t)ps[q] * (TW * 2) + lb)));
+          pv[q] = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + (psl[q] * (TW * 2) + lb)));
         }
       }
 #pragma unroll
@@ -906,7 +992,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         stn<NT>(reinterpret_cast<uint16_t*>(hnn_t + ob), o);
         if (p.plane) {
           const uint32_t pwd = plane_word(o, own_in ? jd : -1);
-          uint32_t* pp = reinterpret_cast<uint32_t*>(pln_t + ((uint32_t)i * (TW / 2) + lbp));
+          uint32_t* pp = reinterpret_cast<uint32_t*>(pln_t + (islot * (TW / 2) + lbp));
           if constexpr (NT)
             __builtin_nontemporal_store(pwd, pp);
           else
@@ -992,7 +1078,7 @@ __global__ __launch_bounds__(256, (STORM && TW >= 32) ? 4 : 1) void k_round(GhDe
   if (*d.mode != (int)STORM) return;
   if constexpr (STORM) {
     constexpr int RB = round_rb<TW>();
-    const int nblk = ((p.n + RB - 1) / RB) * ((int)(p.ld / TW) / TPW);
+    const int nblk = (int)((d.nrows + RB - 1) / RB) * ((int)(p.ld / TW) / TPW);
     for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
       round_block<KB, TW, TPW, NT, STORM>(d, cur, dcur, p, b);
       __syncthreads();  // LDS of this block before the next
@@ -1162,7 +1248,8 @@ __global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p) {
     d.dbits[w + 1] = (uint32_t)(m >> 32);
     if (m) {
       atomicAdd(&d.nd[dnew], __popcll(m));
-      atomicAdd(&d.stats[ST_FAILED], (unsigned long long)__popcll(m));
+      if (!d.rowlay || d.rank == 0)  // row layout: every shard holds all columns
+        atomicAdd(&d.stats[ST_FAILED], (unsigned long long)__popcll(m));
     }
   }
   if (has) {
@@ -1205,12 +1292,13 @@ template <int TW>
 __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, GhRound p) {
   if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no candidate in any shard's table
   constexpr int SEG = SegWalk<TW>::SEG;
-  const SegWalk<TW> w(p);
+  const SegWalk<TW> w(d, p);
   for (int64_t base = w.first; base < w.nseg; base += w.stride) {
     const int64_t sid = base + w.sub;
     const bool valid = sid < w.nseg;
-    const int64_t t = valid ? sid / p.n : 0;
-    const int i = valid ? (int)(sid - t * p.n) : 0;
+    int64_t t = 0;
+    int i = 0;
+    if (valid) w.at(sid, t, i);
     int f = 0;
     if (valid) {
       const uint32_t pf = gh_pf8(d, cur, i, t * TW + w.lc * 8);
@@ -1222,7 +1310,7 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
       const int other = __shfl_up(f, o, SEG);
       if (w.lc >= o) f = q_compose(other, f);
     }
-    if (valid && w.lc == SEG - 1) d.qsum[sid] = (uint8_t)f;
+    if (valid && w.lc == SEG - 1) d.qsum[t * p.n + i] = (uint8_t)f;
   }
 }
 
@@ -1230,8 +1318,8 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
 // the shard's total and its last tile holding a present cell
 __global__ __launch_bounds__(256) void k_quirk_prefix(GhDev d, GhRound p) {
   if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no candidate in any shard's table
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.n) return;
+  const int i = (int)d.row0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (!gh_owned(d, i)) return;
   const int64_t ntiles = p.ld / d.tw;
   int pre = 0, last = -1;
   for (int64_t t = 0; t < ntiles; ++t) {
@@ -1247,11 +1335,12 @@ __global__ __launch_bounds__(256) void k_quirk_prefix(GhDev d, GhRound p) {
 // one thread per row: the run state entering this shard (the shards before
 // it, in member order) and whether the row's last list entry is here
 __global__ __launch_bounds__(256) void k_quirk_carry(GhDev d, GhRound p) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.n) return;
+  const int i = (int)d.row0 + blockIdx.x * blockDim.x + threadIdx.x;
+  if (!gh_owned(d, i)) return;
   int s = 0;
   bool later = false;
-  for (int g = 0; g < d.world; ++g) {
+  // row layout: the whole row is here, nothing enters from other shards
+  for (int g = 0; g < (d.rowlay ? 0 : d.world); ++g) {
     const int f = d.qall[(int64_t)g * p.n + i];
     if (g < d.rank) s = q_apply(f, s);
     if (g > d.rank && (f & 4)) later = true;
@@ -1270,18 +1359,19 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
   // the snapshot: this round gathers 16-bit codes
   if (blockIdx.x == 0 && threadIdx.x == 0) d.pvalid[cur] = 0;
   constexpr int SEG = SegWalk<TW>::SEG;
-  const SegWalk<TW> w(p);
+  const SegWalk<TW> w(d, p);
   for (int64_t base = w.first; base < w.nseg; base += w.stride) {
     const int64_t sid = base + w.sub;
     const bool inr = sid < w.nseg;
-    const int64_t t = inr ? sid / p.n : 0;
-    const int i = inr ? (int)(sid - t * p.n) : 0;
+    int64_t t = 0;
+    int i = 0;
+    if (inr) w.at(sid, t, i);
     // the segment and the row's state are independent loads: issue them
     // together, decide validity after
     const uint32_t pf0 = gh_pf8(d, cur, i, t * TW + w.lc * 8);
     const uint32_t rm0 = removed8(d, dcur, t * TW + w.lc * 8, i);
     const int qc = d.qcarry[i];
-    const int qs = d.qsum[inr ? sid : 0];
+    const int qs = d.qsum[t * p.n + i];
     const int ql = d.qlast[i];
     const bool valid = inr && d.alive[i] && d.active[i];  // only active rows detect (and send)
     const uint32_t pf = valid ? pf0 : 0u, rm = valid ? rm0 : 0u;
@@ -1370,6 +1460,18 @@ void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
   hipLaunchKernelGGL(k_peers_pull, dim3((d.ncs + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
 }
 
+void launch_peers_rows(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_peers_rows, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
+}
+
+void launch_inbox_rows(const GhDev& d, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_inbox_rows, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
+}
+
+void launch_negate(int32_t* x, int64_t n, hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(k_negate, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, n);
+}
+
 void launch_ring_count(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
   GH_TW_DISPATCH(ring_tiles, d, cur, dcur, p, s)
   hipLaunchKernelGGL(k_ring_count, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
@@ -1389,8 +1491,9 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
 template <int KB, int TW, int TPW>
 static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm) {
   constexpr int RB = round_rb<TW>();
-  const int nrb = (p.n + RB - 1) / RB;
-  const int64_t nblk = (int64_t)nrb * (p.ld / TW / TPW);
+  const int64_t nrb = (d.nrows + RB - 1) / RB;
+  const int64_t nblk = nrb * (p.ld / TW / TPW);
+  if (nblk == 0) return;
   const dim3 grid((unsigned)(storm ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
   // the one k_base did not select returns at once
   if (nt && storm)

@@ -21,7 +21,7 @@ import ctypes as C
 import itertools
 from collections import namedtuple
 import os
-from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import FIRST_EXCEPTION, ThreadPoolExecutor, wait
 
 import numpy as np
 
@@ -330,8 +330,14 @@ class ShardGroup:
         self.engines = list(self.pool.map(make, range(world)))
 
     def run(self, name, *args, **kw):
-        """Every rank's result of Engine.<name>(*args, **kw)."""
+        """Every rank's result of Engine.<name>(*args, **kw). A rank that
+        raises is reported at once (the others may still wait in a collective
+        until the transport's barrier gives up)."""
         futs = [self.pool.submit(getattr(e, name), *args, **kw) for e in self.engines]
+        done, _ = wait(futs, return_when=FIRST_EXCEPTION)
+        for f in done:
+            if f.exception() is not None:
+                raise f.exception()
         return [f.result() for f in futs]
 
     def __getattr__(self, name):

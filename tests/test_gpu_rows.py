@@ -1,0 +1,157 @@
+"""GPU parity of the ROW-sharded engine (GH_LAYOUT_ROWS, north_star; DESIGN.md
+"Multi-GPU"): rank g owns observer rows [g*nrs, (g+1)*nrs) with every member
+column, and each round the rows its receivers pull from other shards arrive
+by one alltoallv (ncclAllToAllv under RCCL; peer copies under the in-process
+transport used here) into ghost slots. One cluster over G shards must give
+the oracle's results bit for bit: hb, ts, alive, failed set, detectors,
+per-round counters, placement. Run on a MI355X: pytest -m gpu."""
+import numpy as np
+import pytest
+
+import scenarios as sc
+from kat_util import KATS, kat_config, run_kat
+from test_gpu_sharded import run_group
+
+pytestmark = pytest.mark.gpu
+
+ROWS = 1  # GH_LAYOUT_ROWS
+
+
+@pytest.fixture(scope="module")
+def gs():
+    import gossipsim
+    return gossipsim
+
+
+def rows_cfg(**kw):
+    return dict(shard_layout=ROWS, **kw)
+
+
+def test_row_layout_shapes(gs):
+    """Shards own contiguous row ranges, every column; ring mode is refused."""
+    grp = gs.ShardGroup(gs.default_config(100, shard_layout=ROWS), 3)
+    try:
+        assert [x[2:] for x in grp.run("shard_info")] == [(0, 100)] * 3
+    finally:
+        grp.close()
+    with pytest.raises(gs.GossipError):
+        gs.ShardGroup(gs.default_config(100, shard_layout=ROWS, peer_mode=gs.GH_PEER_RING), 2)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("k", [k for k in KATS if k["peer_mode"] == 0], ids=lambda k: k["name"])
+def test_kats_rows(gs, k, world):
+    cfg = kat_config(gs, k)
+    cfg.shard_layout = ROWS
+    grp = gs.ShardGroup(cfg, world)
+    try:
+        run_kat(grp, k)
+    finally:
+        grp.close()
+
+
+@pytest.mark.parametrize("world,n,seed", [(1, 64, 1), (2, 64, 3), (3, 300, 5), (4, 257, 6), (5, 200, 7),
+                                          (8, 300, 8)])
+def test_random_churn_rows(gs, oracle_mod, world, n, seed):
+    """Crash / leave / join churn (freezes of owned rows, LEAVE bitmaps from
+    the leaver's owner, the introducer's row broadcast as a ghost)."""
+    sched = sc.random_churn(n, 30, seed, p_crash=0.03, p_leave=0.01, p_join=0.05)
+    run_group(gs, oracle_mod, world, rows_cfg(fanout=3, seed=0x77 + seed), n, 30, sched, init=sc.full_state(n))
+
+
+@pytest.mark.parametrize("world,n", [(2, 64), (3, 300), (4, 257)])
+def test_quirk_detection_rows(gs, oracle_mod, world, n):
+    """Quirk-mode runs never cross shards in the row layout (whole rows)."""
+    sched = sc.random_churn(n, 30, 40 + world, p_crash=0.08, p_leave=0.02, p_join=0.05)
+    run_group(gs, oracle_mod, world, rows_cfg(fanout=3, seed=0x3000 + n, detect_mode=1, t_fail=3, t_cleanup=5), n,
+              30, sched, init=sc.full_state(n))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_storm_short_timeouts_rows(gs, oracle_mod, world):
+    """Failure storms: D_r's counts and first detectors summed / minimised
+    over the shards that detected them, REMOVE from every shard."""
+    n = 700
+    sched = sc.random_churn(n, 24, 21, p_crash=0.04, p_leave=0.01, p_join=0.05)
+    run_group(gs, oracle_mod, world, rows_cfg(fanout=4, seed=0x31, t_fail=2, t_cleanup=6), n, 24, sched,
+              init=sc.full_state(n), every=4)
+
+
+def test_c1_bootstrap_crash_places_rows(gs, oracle_mod):
+    """BASELINE config 1 over 3 row shards: joins through the introducer,
+    10 files, a crash, repairs from the master's and the detectors' rows."""
+    n = 10
+    sched = sc.bootstrap_schedule(n)
+    sched.setdefault(30, []).append((sc.CRASH, 7))
+    files = {20: list(range(10))}
+    for r in range(31, 61):
+        files[r] = []
+    run_group(gs, oracle_mod, 3, rows_cfg(max_files=16, seed=0x5EED0001), n, 60, sched, files=files)
+
+
+def wide_state(n, seed):
+    """Views far ahead of some owners' counters (restarted members): wide
+    segments in every sender row, shipped with their exact cells."""
+    rng = np.random.default_rng(seed)
+    own = 5000 + rng.integers(0, 5, n)
+    hb = own[None, :] - rng.integers(0, 4, (n, n))
+    ahead = np.arange(n) % 37 == 5
+    own[ahead] = 7
+    hb[:, ahead] = 6000 + rng.integers(0, 5, (n, int(ahead.sum())))
+    np.fill_diagonal(hb, own)
+    return hb.astype(np.int32), np.zeros((n, n), np.int32), np.ones(n, np.uint8)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_wide_ghosts_rows(gs, oracle_mod, world):
+    run_group(gs, oracle_mod, world, rows_cfg(fanout=4, seed=0x5EED0500 + world, t_fail=40, t_cleanup=40), 600, 12,
+              {}, init=wide_state(600, world))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_plane_rows(gs, oracle_mod, monkeypatch, world):
+    """The sender plane travels with the ghost rows (plane words beside the
+    narrow codes) and stays exact under churn."""
+    monkeypatch.setenv("GH_PLANE", "1")
+    n = 1100
+    sched = sc.random_churn(n, 24, 0xB0 + world, p_crash=0.01, p_leave=0.01, p_join=0.03)
+    run_group(gs, oracle_mod, world, rows_cfg(fanout=4, seed=0x5EED0600 + world, t_fail=6, t_cleanup=8), n, 24,
+              sched, init=sc.full_state(n))
+
+
+def test_c2_n4096_rows(gs, oracle_mod):
+    """BASELINE config 2 (N=4,096, k=3, 1% crash at r=8) over 4 row shards."""
+    n = 4096
+    sched = {8: [(sc.CRASH, c) for c in sc.crash_ids(n, 0.01, 0x5EED0002)]}
+    run_group(gs, oracle_mod, 4, rows_cfg(fanout=3, seed=0x5EED0002), n, 24, sched, init=sc.full_state(n), every=8)
+
+
+def test_rows_match_columns_and_single(gs):
+    """N=8,192 with the plane, 16 rounds from full membership and a crash
+    wave: row shards, column shards and one engine agree every round."""
+    n = 8192
+    cfg = dict(fanout=4, seed=0x5EED0700, t_fail=10, t_cleanup=10)
+    sched = {5: [(sc.CRASH, c) for c in sc.crash_ids(n, 0.005, 0x5EED0701)]}
+
+    def states(make):
+        eng = make()
+        try:
+            eng.import_state(*sc.full_state(n), 0)
+            out = []
+            for r in range(1, 17):
+                if r in sched:
+                    eng.apply_events(sched[r])
+                st = eng.step(1)
+                out.append((st, eng.read_failed(), eng.export_state()[0][::97]))
+            return out
+        finally:
+            eng.close()
+
+    single = states(lambda: gs.Engine(gs.default_config(n, **cfg)))
+    rows = states(lambda: gs.ShardGroup(gs.default_config(n, shard_layout=ROWS, **cfg), 4))
+    cols = states(lambda: gs.ShardGroup(gs.default_config(n, **cfg), 4))
+    for r, (a, b, c) in enumerate(zip(single, rows, cols), 1):
+        assert a[0] == b[0] == c[0], (r, a[0], b[0], c[0])
+        np.testing.assert_array_equal(a[1], b[1])
+        np.testing.assert_array_equal(a[2], b[2])
+        np.testing.assert_array_equal(a[2], c[2])
