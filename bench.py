@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--peer-mode", choices=("pull", "ring"), default="pull",
                     help="pull: k Philox peers (BASELINE configs 2-4); ring: the reference's ring push")
     ap.add_argument("--detect", choices=("canonical", "quirk"), default="canonical")
+    ap.add_argument("--layout", choices=("columns", "rows"), default="columns",
+                    help="shard layout for --gpus > 1: member columns (O(N) exchanges, default) or observer "
+                         "rows with the senders' rows by ncclAllToAllv (north_star)")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0003)
     ap.add_argument("--t-fail", type=int, default=16,
                     help="T_fail = T_cleanup in rounds (reference: 5; see module doc)")
@@ -361,7 +364,8 @@ def main():
     cfg = gs.default_config(n, fanout=k, seed=args.seed, device=local, t_fail=args.t_fail, t_cleanup=args.t_fail,
                             max_files=args.files if world == 1 else 0,
                             peer_mode=gs.GH_PEER_RING if args.peer_mode == "ring" else gs.GH_PEER_PULL,
-                            detect_mode=gs.GH_DETECT_QUIRK if args.detect == "quirk" else gs.GH_DETECT_CANONICAL)
+                            detect_mode=gs.GH_DETECT_QUIRK if args.detect == "quirk" else gs.GH_DETECT_CANONICAL,
+                            shard_layout=gs.GH_LAYOUT_ROWS if args.layout == "rows" else gs.GH_LAYOUT_COLUMNS)
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -372,6 +376,9 @@ def main():
     else:
         eng = gs.Engine(cfg)
     _, _, _, ncols = eng.shard_info()
+    # cells this rank's round kernel covers: rows x columns (row layout: its
+    # rows, every column)
+    nrows_r = -(-n // world) if args.layout == "rows" else n
     plane = eng.plane_info()[0]
     tile_w = int(os.environ.get("GH_TILE_W", "256" if plane else "64"))
     eng.init_full(2, 0, 0)
@@ -398,6 +405,7 @@ def main():
         elapsed = float(t.item())
     kern_ms, launches = eng.read_timing()
     eng.set_timing(False)
+    exch = eng.exchange_info() if args.layout == "rows" else None
     plane_fb = eng.plane_info()[2]
     placement = None
     if world == 1 and args.files > 0:
@@ -412,9 +420,9 @@ def main():
         return
     value = args.steps / elapsed
     # bytes of one k_round launch (this rank's columns)
-    b_compulsory = 4.0 * n * ncols             # each 2-byte narrow cell read once and written once
-    b_gather = 2.0 * n * ncols * k             # the k sender segments per cell (L2 / Infinity Cache / HBM)
-    b_survey = 4.0 * n * ncols * (k + 4)       # SURVEY.md §8d (int32 hb + ts streams)
+    b_compulsory = 4.0 * nrows_r * ncols       # each 2-byte narrow cell read once and written once
+    b_gather = 2.0 * nrows_r * ncols * k       # the k sender segments per cell (L2 / Infinity Cache / HBM)
+    b_survey = 4.0 * nrows_r * ncols * (k + 4)  # SURVEY.md §8d (int32 hb + ts streams)
     traffic = pmc_traffic(n, k, world, args.warmup, plane, tile_w)
     avg_s = (kern_ms / 1e3) / max(launches, 1)
     achieved = b_compulsory / avg_s / 1e9
@@ -439,7 +447,9 @@ def main():
                         f"T_fail=T_cleanup={args.t_fail} rounds, seed {hex(args.seed)}",
             "t_fail": args.t_fail,
             "n_members": n, "fanout": k, "global_batch": n, "seq_len": n,
-            "parallelism": f"column-shard x{world} (RCCL)" if world > 1 else "single",
+            "parallelism": (f"row-shard x{world} (RCCL alltoallv)" if args.layout == "rows" else
+                            f"column-shard x{world} (RCCL)") if world > 1 else "single",
+            "rows_per_gpu": nrows_r,
             "columns_per_gpu": ncols,
             "rounds_checked": {"detections": st["detections"], "active_rows": st["active_rows"]},
         },
@@ -463,7 +473,8 @@ def main():
         "cpu_baseline": None,
         "memory": {"table_bytes": mem["device_bytes"], "wide_slots_per_buffer": mem["wide_cap"],
                    "wide_slots_used": mem["wide_used"]},
-        "layout": {"tile_width": tile_w, "sender_plane": bool(plane),
+        "exchange": exch,
+        "layout": {"tile_width": tile_w, "sender_plane": bool(plane), "shards": args.layout,
                    "plane_fallback_waves_last_round": plane_fb},
         "secondary": secondary,
         "placement": placement,

@@ -241,8 +241,8 @@ int gh_rebuild_meta(void* h, int32_t new_master, int32_t* f0, int64_t* n_files);
  *   GH_LAYOUT_ROWS     rank g holds observer rows [g*nrs, g*nrs + nrs) with
  *                      ALL columns (north_star): each round the senders'
  *                      rows that a shard's receivers pull cross shards by
- *                      one alltoallv (ncclSend/ncclRecv group), O(N^2 k/G)
- *                      bytes. Pull mode only (ring mode: GH_EINVAL). */
+ *                      one alltoallv (ncclAllToAllv), O(N^2 k/G) bytes.
+ *                      Pull mode only (ring mode: GH_EINVAL). */
 #define GH_LAYOUT_COLUMNS 0
 #define GH_LAYOUT_ROWS 1
 
@@ -269,6 +269,12 @@ int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, in
  * 16-bit sender codes although the plane was valid (a sender code outside
  * the plane's window). Any output may be NULL. No reference counterpart. */
 int gh_plane_info(void* h, int32_t* enabled, int32_t* valid, int64_t* fallback_waves);
+/* Row layout (GH_LAYOUT_ROWS): the last ghost-row exchange of this shard --
+ * the sender rows it received, and the bytes it sent and received by
+ * alltoallv (narrow codes, plane words, wide segments). Zero in the column
+ * layout, whose exchanges are O(N) collectives. Any output may be NULL. No
+ * reference counterpart (it replaces the UDP list pushes, slave/slave.go:527-542). */
+int gh_exchange_info(void* h, int64_t* ghost_rows, int64_t* bytes_out, int64_t* bytes_in);
 /* HBM held by the tables (narrow x2 + wide arenas + frozen store), wide-arena
  * slots in use / per buffer, and stopped rows in the frozen store. Any
  * output may be NULL. Diagnostic; no reference counterpart. */

@@ -68,6 +68,7 @@ struct Engine {
   size_t gcap_bytes[4] = {0, 0, 0, 0};
   int32_t* gidx = nullptr;   // [2 * cap] rows to send, their destinations
   int64_t gidx_cap = 0;
+  int64_t gx_rows = 0, gx_out = 0, gx_in = 0;  // the last exchange: ghost rows, bytes sent / received
   int plane = 0;         // sender snapshot plane (pull mode, 3 <= k <= 4, N >= GH_PLANE_MIN_N; GH_PLANE=0/1)
   // upper bound of every heartbeat in the table (int32 overflow check,
   // slave/slave.go:446): +1 per round, max of imported / merged values
@@ -431,6 +432,9 @@ int ghost_exchange(Engine* e, const std::vector<std::vector<int32_t>>& want) {
     rbv[r] = rcnt[r] * RB;
   }
   COMMCHK(e, e->comm->alltoallv(e->gbuf[0], sb.data(), e->gbuf[1], rbv.data(), e->stream));
+  e->gx_rows = nr;
+  e->gx_out = ns * RB;
+  e->gx_in = nr * RB;
   launch_ghost_unpack(d, e->cur, static_cast<const char*>(e->gbuf[1]), nr, d.nrows, e->stream);
   HIPCHK(e, hipGetLastError());
   // wide segments of the sent rows: every shard's per-destination counts
@@ -459,6 +463,8 @@ int ghost_exchange(Engine* e, const std::vector<std::vector<int32_t>>& want) {
   launch_ghost_wide(d, e->cur, drows, ddest, ns, e->gwcnt + G, static_cast<char*>(e->gbuf[2]), e->stream);
   HIPCHK(e, hipGetLastError());
   COMMCHK(e, e->comm->alltoallv(e->gbuf[2], sb.data(), e->gbuf[3], rbv.data(), e->stream));
+  e->gx_out += ws * REC;
+  e->gx_in += wr * REC;
   launch_ghost_unwide(d, e->cur, static_cast<const char*>(e->gbuf[3]), wr, e->stream);
   HIPCHK(e, hipGetLastError());
   return GH_OK;
@@ -1071,6 +1077,15 @@ int gh_plane_info(void* h, int32_t* enabled, int32_t* valid, int64_t* fallback_w
   if (enabled) *enabled = e->plane;
   if (valid) *valid = e->pforce ? 0 : v[0];
   if (fallback_waves) *fallback_waves = v[1];
+  return GH_OK;
+}
+
+int gh_exchange_info(void* h, int64_t* ghost_rows, int64_t* bytes_out, int64_t* bytes_in) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  if (ghost_rows) *ghost_rows = e->gx_rows;
+  if (bytes_out) *bytes_out = e->gx_out;
+  if (bytes_in) *bytes_in = e->gx_in;
   return GH_OK;
 }
 

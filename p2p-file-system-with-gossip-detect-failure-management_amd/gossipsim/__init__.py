@@ -27,6 +27,7 @@ import numpy as np
 
 from . import _abi, codec
 from ._abi import (GH_COMM_LOCAL, GH_COMM_RCCL, GH_DETECT_CANONICAL, GH_DETECT_QUIRK,  # noqa: F401
+                   GH_LAYOUT_COLUMNS, GH_LAYOUT_ROWS,
                    GH_EPLACEMENT_STARVED, GH_EV_CRASH, GH_EV_JOIN, GH_EV_LEAVE, GH_OK, GH_PEER_PULL,
                    GH_PEER_RING, Config, PlanEntry)
 
@@ -111,6 +112,13 @@ class Engine:
         en, va, fb = C.c_int32(), C.c_int32(), C.c_int64()
         self._chk(self.lib.gh_plane_info(self.h, C.byref(en), C.byref(va), C.byref(fb)))
         return en.value, va.value, fb.value
+
+    def exchange_info(self):
+        """dict(ghost_rows, bytes_out, bytes_in) of this shard's last ghost-row
+        exchange (row layout; gh_exchange_info)."""
+        v = [C.c_int64() for _ in range(3)]
+        self._chk(self.lib.gh_exchange_info(self.h, *[C.byref(x) for x in v]))
+        return dict(zip(("ghost_rows", "bytes_out", "bytes_in"), (x.value for x in v)))
 
     def memory_info(self):
         """dict(device_bytes, wide_used, wide_cap, frozen_rows) of this
