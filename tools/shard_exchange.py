@@ -1,0 +1,39 @@
+"""Per-round exchange of the two shard layouts at the headline size, G shards
+on one MI355X (in-process transport: the copies are device-local, so the
+times are NOT xGMI times; the byte counts are what RCCL would move).
+  python tools/shard_exchange.py [N] [G] [rounds]"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "p2p-file-system-with-gossip-detect-failure-management_amd"))
+import gossipsim as gs  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+G = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+out = {"n": n, "world": G, "k": 4, "transport": "LOCAL (one GPU)"}
+for layout in ("columns", "rows"):
+    cfg = gs.default_config(n, fanout=4, seed=0x5EED0003, t_fail=16, t_cleanup=16,
+                            shard_layout=gs.GH_LAYOUT_ROWS if layout == "rows" else gs.GH_LAYOUT_COLUMNS)
+    grp = gs.ShardGroup(cfg, G)
+    try:
+        grp.run("init_full", 2, 0, 0)
+        grp.run("step", 12)
+        grp.run("sync")
+        t0 = time.perf_counter()
+        grp.run("step", rounds)
+        grp.run("sync")
+        dt = (time.perf_counter() - t0) / rounds
+        rec = {"ms_per_round": dt * 1e3, "memory_per_shard": grp.run("memory_info")[0]}
+        if layout == "rows":
+            ex = grp.run("exchange_info")
+            rec["ghost_rows_per_shard"] = [x["ghost_rows"] for x in ex]
+            rec["bytes_in_per_shard"] = [x["bytes_in"] for x in ex]
+            rec["bytes_in_total_per_round"] = sum(x["bytes_in"] for x in ex)
+        out[layout] = rec
+        print(layout, json.dumps(rec), flush=True)
+    finally:
+        grp.close()
+print(json.dumps(out))
