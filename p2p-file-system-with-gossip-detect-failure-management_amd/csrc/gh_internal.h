@@ -188,6 +188,14 @@ struct GhDev {
   uint32_t *pl[2];  // sender snapshot plane per buffer (null: plane off)
   int32_t *pvalid;  // [2]: plane of buffer b written by the round that wrote b
   int32_t *pfb;     // waves of the last round that gathered 16-bit codes with a valid plane
+  // quiet rows (by round parity r & 1): stab[r & 1][i] = row i was inactive
+  // in round r - 1 and none of its segments changed (k_active_post sets it
+  // for the inactive rows, k_round / k_round_slow clear it). Round r skips
+  // such a row when it is still inactive with no senders, no REMOVE is
+  // pending and no base of the tile moved: its output equals its input,
+  // which the next buffer already holds (written two rounds ago, unchanged
+  // one round ago). A collapsed cluster stops rewriting its tables.
+  uint8_t *stab[2];
   int32_t *base[2]; // [ld] narrow base per buffer
   // wide arena per buffer: [wcap][tw] x / exact ts, [wcap][tw/8] flag bytes
   int32_t *wh[2], *wt[2];

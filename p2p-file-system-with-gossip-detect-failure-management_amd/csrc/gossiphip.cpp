@@ -786,7 +786,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.slow, (size_t)(e->ld / tw) * e->n, 0)) || (rc = dalloc(e, &d.slow_n, 4, 0)) ||
         (rc = dalloc(e, &d.mode, 4, 0)) || (rc = dalloc(e, &d.nstorm, 4, 0)) ||
         (rc = dalloc(e, &d.nflag, 2, 0)) || (rc = dalloc(e, &d.pvalid, 2, 0)) ||
-        (rc = dalloc(e, &d.pfb, 1, 0)))
+        (rc = dalloc(e, &d.pfb, 1, 0)) ||
+        (rc = dalloc(e, &d.stab[0], e->n, 0)) || (rc = dalloc(e, &d.stab[1], e->n, 0)))
       break;
     if (e->plane && ((rc = dalloc(e, &d.pl[0], cells / 8, 0xFF)) || (rc = dalloc(e, &d.pl[1], cells / 8, 0xFF))))
       break;
@@ -1233,8 +1234,9 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     const int32_t r = e->round + 1;
     int rc;
     if ((rc = process_events(e, r))) return rc;
-    if (e->pforce) {
+    if (e->pforce) {  // the table was written outside a round: no valid plane, no quiet rows
       HIPCHK(e, hipMemsetAsync(e->d.pvalid + e->cur, 0, sizeof(int32_t), e->stream));
+      for (int b = 0; b < 2; ++b) HIPCHK(e, hipMemsetAsync(e->d.stab[b], 0, e->n, e->stream));
       e->pforce = false;
     }
     const GhRound p = round_params(e, r);

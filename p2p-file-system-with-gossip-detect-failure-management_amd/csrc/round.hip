@@ -119,6 +119,7 @@ __global__ __launch_bounds__(256) void k_active_post(GhDev d, GhRound p) {
       a = d.post[i] >= p.min_members;
       d.active[i] = a;
     }
+    d.stab[(p.r + 1) & 1][i] = d.alive[i] && !a;  // quiet candidates for the next round
   }
   const unsigned long long m = __ballot(a);
   if (d.rank == 0 && (threadIdx.x & 63) == 0 && m)
@@ -604,6 +605,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   __shared__ int s_dmin[TW];
   // this tile's segments for the slow list, appended with one global atomic
   __shared__ int s_nslow, s_slowbase;
+  __shared__ int s_bmove;  // a column base of the tile moved this round
   __shared__ int s_slow[RB];
   // per-row metadata of the workgroup's rows, staged once for its TPW tiles:
   // s_meta = alive | active << 1 | inbox count << 2; s_inb = first KB senders
@@ -639,6 +641,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 
   if (tid == 0) s_merged = s_det = s_rel = s_storm = s_tomb = s_unk = 0;
   const bool pull = p.peer_mode == GH_PEER_PULL;
+  // quiet rows may be skipped: no REMOVE pending anywhere (|D_{r-1}| = 0)
+  const bool quiet = d.cntg[p.n] == 0 && !p.force_slow;
+  const uint8_t* __restrict__ stab_cur = d.stab[p.r & 1];
+  uint8_t* __restrict__ stab_nxt = d.stab[(p.r + 1) & 1];
   if constexpr (STORM) {
     // row metadata once per row, then only the inbox slots in use (storms
     // and guard rows have few senders)
@@ -648,7 +654,8 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       if (i < rowend) {
         const int al = d.alive[i];
         const int cnt = al ? gh_in_cnt(d, pull, p.k, i) : 0;
-        meta = al | (d.active[i] << 1) | (cnt << 2);
+        const int act = d.active[i];
+        meta = al | (act << 1) | (cnt << 2) | ((quiet && al && !act && cnt == 0 && stab_cur[i]) ? 1 << 30 : 0);
       }
       s_meta[row] = meta;
     }
@@ -656,7 +663,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     for (int t = tid; t < RB * KB; t += 256) {
       const int row = t / KB, q = t - row * KB;
       const int i = (int)d.row0 + rb * RB + row;
-      if (q < (s_meta[row] >> 2)) {
+      if (q < ((s_meta[row] >> 2) & 0xFFFF)) {
         const int sv = d.inbox[gh_in_beg(d, pull, p.k, i) + q];
         s_inb[t] = sv;
         if (d.rowlay) s_isl[t] = d.rslot[sv];
@@ -671,7 +678,8 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       if (i < rowend) {
         const int al = d.alive[i];
         const int cnt = al ? gh_in_cnt(d, pull, p.k, i) : 0;
-        meta = al | (d.active[i] << 1) | (cnt << 2);
+        const int act = d.active[i];
+        meta = al | (act << 1) | (cnt << 2) | ((quiet && al && !act && cnt == 0 && stab_cur[i]) ? 1 << 30 : 0);
         if (q < cnt) sv = d.inbox[gh_in_beg(d, pull, p.k, i) + q];
       }
       if (q == 0) s_meta[row] = meta;
@@ -709,7 +717,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   char* pln_t = reinterpret_cast<char*>(pln) + (pln ? tcell / 2 : 0);
   const uint32_t lb = (uint32_t)lc * (CPL * 2);  // lane's byte offset in a row segment (narrow)
   const uint32_t lbp = (uint32_t)lc * 4;         // ... in a plane row segment
-  if (tid == 0) s_nslow = 0;
+  if (tid == 0) {
+    s_nslow = 0;
+    s_bmove = 0;
+  }
   for (int t = tid; t < TW; t += 256) {
     s_dcnt[t] = 0;
     s_dmin[t] = INT_MAX;
@@ -735,6 +746,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       dd |= d5h << (16 * h);
       th |= tc << (16 * h);
     }
+    if (dd) s_bmove = 1;
     s_d5[pp] = dd;
     s_t5[pp] = th;
     s_rm[pp] = rmm;
@@ -743,6 +755,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   const uint32_t tfp = (uint32_t)min(p.t_fail, 31) * 0x10001u;
   const uint32_t tcp = (uint32_t)min(p.t_cleanup, 31) * 0x10001u;
   __syncthreads();
+  const bool tile_still = s_bmove == 0;
   // lean: no REMOVE in the lane; storm: REMOVE applied in the packed path
   // unless a column has a single detector (that row keeps the member)
   bool lane_ok = !p.force_slow;
@@ -764,8 +777,11 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     const int rs = valid ? rr : 0;
     int meta = s_meta[rs];
     if constexpr (RPW == 1) meta = uni(meta);
-    const bool al = (meta & 1) && valid;
-    const int cntv = meta >> 2;
+    // a quiet row in a tile whose bases stayed: nothing to read or write
+    const bool skip = ((meta >> 30) & 1) && tile_still;
+    if (__ballot(valid && !skip) == 0) continue;
+    const bool al = (meta & 1) && valid && !skip;
+    const int cntv = (meta >> 2) & 0xFFFF;
     const uint32_t ob = islot * (TW * 2) + lb;  // own segment, bytes from the tile base
 
     // own segment and the senders' snapshots, issued together: plane words
@@ -868,39 +884,48 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       }
     }
     if (need16) {
-      v4u pv[KB];
+      // four slots at a time (an 8-slot inbox keeps only four segments live);
+      // a later group runs only when a lane of the wave uses it
 #pragma unroll
-      for (int q = 0; q < KB; ++q) {
-        if constexpr (STORM) {
-          // storms hold few senders (guard rows none): load only the used
-          // slots, the rest are absent (-1, a no-op under the max)
-          if (q < cntv)
-            pv[q] = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + (psl[q] * (TW * 2) + lb)));
-          else
-            pv[q] = v4u{~0u, ~0u, ~0u, ~0u};
-        } else {
-          pv[q] = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + (psl[q] * (TW * 2) + lb)));
+      for (int g = 0; g < KB; g += 4) {
+        if (g > 0 && __ballot(g < cntv) == 0) break;
+        v4u pv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int q = g + u;
+          const uint16_t* src = reinterpret_cast<const uint16_t*>(hno_t + (psl[q] * (TW * 2) + lb));
+          if constexpr (STORM) {
+            // storms hold few senders (guard rows none): load only the used
+            // slots, the rest are absent (-1, a no-op under the max)
+            pv[u] = q < cntv ? ldn<false>(src) : v4u{~0u, ~0u, ~0u, ~0u};
+          } else if constexpr (KB > 4) {
+            // 8-slot inboxes (ring, pull k > 4) are mostly part-empty, and
+            // empty in a collapsed cluster: slots no lane of the wave uses
+            // are not loaded
+            pv[u] = __ballot(q < cntv) != 0 ? ldn<false>(src) : v4u{~0u, ~0u, ~0u, ~0u};
+          } else {
+            pv[u] = ldn<false>(src);  // unused slots hold the own row: a no-op under the max
+          }
         }
-      }
 #pragma unroll
-      for (int q = 0; q < KB; ++q) bad |= q < cntv && (pv[q][0] & 0xFFFFu) == GH_N_WIDE;
-      // A sender's own member in the lane: its snapshot carries hb + 1 there
-      // (the sender's heartbeat of this round).
+        for (int u = 0; u < 4; ++u) bad |= g + u < cntv && (pv[u][0] & 0xFFFFu) == GH_N_WIDE;
+        // A sender's own member in the lane: its snapshot carries hb + 1
+        // there (the sender's heartbeat of this round).
 #pragma unroll
-      for (int q = 0; q < KB; ++q) {
-        const int js = ps[q] - c0;
-        if (q < cntv && (unsigned)js < 8u) {
-          const int sh = 16 * (js & 1);
+        for (int u = 0; u < 4; ++u) {
+          const int js = ps[g + u] - c0;
+          if (g + u < cntv && (unsigned)js < 8u) {
+            const int sh = 16 * (js & 1);
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (j == (js >> 1) && ((pv[q][j] >> sh) & 0x8000u) == 0) pv[q][j] += 0x20u << sh;
+            for (int j = 0; j < 4; ++j)
+              if (j == (js >> 1) && ((pv[u][j] >> sh) & 0x8000u) == 0) pv[u][j] += 0x20u << sh;
+          }
         }
-      }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        ms[j] = pv[0][j];
-#pragma unroll
-        for (int q = 1; q < KB; ++q) ms[j] = pk_max_i16(ms[j], pv[q][j]);
+        for (int j = 0; j < 4; ++j) {
+          uint32_t m4 = pk_max_i16(pk_max_i16(pv[0][j], pv[1][j]), pk_max_i16(pv[2][j], pv[3][j]));
+          ms[j] = g == 0 ? m4 : pk_max_i16(ms[j], m4);
+        }
       }
     }
 
@@ -985,6 +1010,14 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     }
     const bool ok = lane_ok && !bad && acc == 0;
     const bool seg_ok = (__ballot(al && !ok) & gmask) == 0;
+    if constexpr (STORM || LEAN_GUARD) {
+      // an inactive row stays a quiet candidate only while none of its
+      // segments changes (the 4-slot lean variant lists inactive rows: the
+      // per-cell kernel clears them)
+      uint32_t chg = 0;
+      if (al && !act) chg = (o[0] ^ w[0]) | (o[1] ^ w[1]) | (o[2] ^ w[2]) | (o[3] ^ w[3]);
+      if ((__ballot(chg != 0) & gmask) != 0 && lc == 0) stab_nxt[i] = 0;
+    }
     int dpres = 0;  // present after - present before
     bool any_det = false;
     if (al) {
@@ -1219,6 +1252,7 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
     if (lc == 0 && valid) {
       if (dpres) atomicAdd(&d.cntl[i], dpres);
       if (any_det) d.det_any[i] = 1;
+      d.stab[(p.r + 1) & 1][i] = 0;  // not a quiet row (conservatively)
     }
   }
   if (n_unknown) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], (unsigned long long)n_unknown);
