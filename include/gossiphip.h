@@ -259,10 +259,11 @@ int gh_shard_info(void* h, int32_t* rank, int32_t* world, int64_t* col0, int64_t
  * (tile, row) segments of the current table held wide (arena or frozen
  * store, stopped rows included); segments the last round ran through the per-cell
  * rule (k_round_slow); the round kernel variant of the last round (0 lean,
- * 1 storm) and its storm measure. Any output may be NULL. No reference
- * counterpart. */
+ * 1 storm) and its storm measure; the row segments the last round skipped as
+ * quiet (inactive rows that stopped changing). Any output may be NULL. No
+ * reference counterpart. */
 int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, int32_t* storm_mode,
-                     int64_t* storm_segments);
+                     int64_t* storm_segments, int64_t* quiet_segments);
 /* Sender snapshot plane (diagnostic; DESIGN.md "Sender plane"): whether the
  * engine keeps one (pull mode, 3 <= k <= 4, N >= 16,384), whether the current table's plane is
  * valid for the next round, and how many waves of the last round gathered

@@ -196,6 +196,7 @@ struct GhDev {
   // which the next buffer already holds (written two rounds ago, unchanged
   // one round ago). A collapsed cluster stops rewriting its tables.
   uint8_t *stab[2];
+  int32_t *nquiet;  // row segments the last round skipped as quiet
   int32_t *base[2]; // [ld] narrow base per buffer
   // wide arena per buffer: [wcap][tw] x / exact ts, [wcap][tw/8] flag bytes
   int32_t *wh[2], *wt[2];

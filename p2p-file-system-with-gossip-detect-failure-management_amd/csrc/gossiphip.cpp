@@ -787,7 +787,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.mode, 4, 0)) || (rc = dalloc(e, &d.nstorm, 4, 0)) ||
         (rc = dalloc(e, &d.nflag, 2, 0)) || (rc = dalloc(e, &d.pvalid, 2, 0)) ||
         (rc = dalloc(e, &d.pfb, 1, 0)) ||
-        (rc = dalloc(e, &d.stab[0], e->n, 0)) || (rc = dalloc(e, &d.stab[1], e->n, 0)))
+        (rc = dalloc(e, &d.stab[0], e->n, 0)) || (rc = dalloc(e, &d.stab[1], e->n, 0)) ||
+        (rc = dalloc(e, &d.nquiet, 1, 0)))
       break;
     if (e->plane && ((rc = dalloc(e, &d.pl[0], cells / 8, 0xFF)) || (rc = dalloc(e, &d.pl[1], cells / 8, 0xFF))))
       break;
@@ -1044,7 +1045,7 @@ int gh_shard_info(void* h, int32_t* rank, int32_t* world, int64_t* col0, int64_t
 }
 
 int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, int32_t* storm_mode,
-                     int64_t* storm_segments) {
+                     int64_t* storm_segments, int64_t* quiet_segments) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
   HIPCHK(e, hipSetDevice(e->cfg.device));
@@ -1054,16 +1055,18 @@ int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, in
   launch_count_wide(e->d, e->cur, st.as<unsigned long long>(), e->stream);
   HIPCHK(e, hipGetLastError());
   unsigned long long w[2] = {0, 0};
-  int32_t sl = 0, mode = 0, ns = 0;
+  int32_t sl = 0, mode = 0, ns = 0, nq = 0;
   HIPCHK(e, hipMemcpyAsync(w, st.p, sizeof w, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipMemcpyAsync(&sl, e->d.slow_n, sizeof sl, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipMemcpyAsync(&mode, e->d.mode, sizeof mode, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipMemcpyAsync(&ns, e->d.nstorm, sizeof ns, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(&nq, e->d.nquiet, sizeof nq, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   if (wide_segments) *wide_segments = (int64_t)(w[0] + w[1]);
   if (slow_segments) *slow_segments = sl;
   if (storm_mode) *storm_mode = mode;
   if (storm_segments) *storm_segments = ns;
+  if (quiet_segments) *quiet_segments = nq;
   return GH_OK;
 }
 

@@ -529,6 +529,7 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
     *d.mode = p.force_storm || measure * 32 > d.ntiles * (int64_t)d.n;
     *d.slow_n = 0;
     *d.nstorm = 0;
+    *d.nquiet = 0;
     d.wn[cur ^ 1] = 0;  // the round rewrites every running row of the next buffer
     d.nflag[cur ^ 1] = 0;  // counted by this round's writers
     // |D_{r-1}| of this shard next to the local counts, for one allreduce
@@ -591,6 +592,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   constexpr int RSTEP = 4 * RPW;
   constexpr int RB = round_rb<TW>();  // rows per workgroup tile
   __shared__ unsigned long long s_merged, s_det, s_rel, s_storm, s_tomb, s_unk;
+  __shared__ int s_quiet;  // row segments skipped as quiet
   // this tile's per-pair constants: rebase (base_next - base_cur) << 5
   // (0x8000: jump beyond 1023, no present cell stays narrow) and the code
   // bound of "hb > 1"
@@ -639,7 +641,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   const int lc = lane % SEG;
   const unsigned long long gmask = (SEG == 64 ? ~0ull : ((1ull << SEG) - 1)) << (sub * SEG);
 
-  if (tid == 0) s_merged = s_det = s_rel = s_storm = s_tomb = s_unk = 0;
+  if (tid == 0) {
+    s_merged = s_det = s_rel = s_storm = s_tomb = s_unk = 0;
+    s_quiet = 0;
+  }
   const bool pull = p.peer_mode == GH_PEER_PULL;
   // quiet rows may be skipped: no REMOVE pending anywhere (|D_{r-1}| = 0)
   const bool quiet = d.cntg[p.n] == 0 && !p.force_slow;
@@ -779,6 +784,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     if constexpr (RPW == 1) meta = uni(meta);
     // a quiet row in a tile whose bases stayed: nothing to read or write
     const bool skip = ((meta >> 30) & 1) && tile_still;
+    if (valid && skip && lc == 0) atomicAdd(&s_quiet, 1);
     if (__ballot(valid && !skip) == 0) continue;
     const bool al = (meta & 1) && valid && !skip;
     const int cntv = (meta >> 2) & 0xFFFF;
@@ -1100,6 +1106,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     if (s_storm) atomicAdd(d.nstorm, (int)s_storm);
     if (s_tomb) atomicAdd(&d.stats[ST_TOMBSTONED], s_tomb);
     if (s_unk) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], s_unk);
+    if (s_quiet) atomicAdd(d.nquiet, s_quiet);
   }
 }
 

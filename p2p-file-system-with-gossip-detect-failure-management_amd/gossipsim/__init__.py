@@ -98,12 +98,13 @@ class Engine:
     def encoding_info(self, full=False):
         """(wide segments of the current table, segments the last round ran
         by the per-cell rule) of this engine's shard; full=True adds the last
-        round's kernel variant (0 lean, 1 storm) and its storm measure
-        (diagnostic)."""
-        w, sl, ns = C.c_int64(), C.c_int64(), C.c_int64()
+        round's kernel variant (0 lean, 1 storm), its storm measure and the
+        row segments it skipped as quiet (diagnostic)."""
+        w, sl, ns, nq = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
         mode = C.c_int32()
-        self._chk(self.lib.gh_encoding_info(self.h, C.byref(w), C.byref(sl), C.byref(mode), C.byref(ns)))
-        return (w.value, sl.value, mode.value, ns.value) if full else (w.value, sl.value)
+        self._chk(self.lib.gh_encoding_info(self.h, C.byref(w), C.byref(sl), C.byref(mode), C.byref(ns),
+                                            C.byref(nq)))
+        return (w.value, sl.value, mode.value, ns.value, nq.value) if full else (w.value, sl.value)
 
     def plane_info(self):
         """(plane kept, plane valid for the next round, waves of the last

@@ -94,7 +94,7 @@ SYMBOLS = [
     ("gh_comm_unique_id", C.c_int, [_vp]),
     ("gh_create_sharded", C.c_int, [_P(Config), _i32, _i32, _i32, _vp, _P(_vp)]),
     ("gh_shard_info", C.c_int, [_vp, _P(_i32), _P(_i32), _P(_i64), _P(_i64)]),
-    ("gh_encoding_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i32), _P(_i64)]),
+    ("gh_encoding_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i32), _P(_i64), _P(_i64)]),
     ("gh_plane_info", C.c_int, [_vp, _P(_i32), _P(_i32), _P(_i64)]),
     ("gh_exchange_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i64)]),
     ("gh_memory_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i64), _P(_i64)]),

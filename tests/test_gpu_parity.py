@@ -387,3 +387,31 @@ def test_quirk_repair_plan_last_file_only(gs, oracle_mod):
     for x, y in zip(eng.get_files(f), orc.get_files(f)):
         np.testing.assert_array_equal(x, y)
     eng.close()
+
+
+def test_quiet_rows_after_collapse(gs, oracle_mod):
+    """The reference's 5-round timeouts at N=2,048, k=4: the round-6
+    detection storm collapses the cluster; once the inactive rows'
+    tombstones saturate (age 30) their rows stop changing and the round
+    skips them (neither read nor rewritten). Bit-exact against the oracle
+    through round 64, a join at round 52 (a host write: every row is a
+    candidate again), and the skip did happen."""
+    n = 2048
+    cfg = dict(fanout=4, seed=0x5EED0800)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    hb, ts, alive = sc.full_state(n)
+    eng.import_state(hb, ts, alive, 0)
+    orc.import_state(hb, ts, alive, 0)
+    quiet = []
+    for r in range(1, 65):
+        if r == 52:
+            ev = [(sc.JOIN, 5)]
+            eng.apply_events(ev)
+            orc.apply_events(ev)
+        s1, s2 = eng.step(1), orc.step(1)
+        assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
+        quiet.append(eng.encoding_info(full=True)[4])
+        if r % 4 == 0 or r in (51, 52, 53):
+            compare(eng, orc, r)
+    assert max(quiet) > 0, quiet
