@@ -1018,10 +1018,11 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     const bool seg_ok = (__ballot(al && !ok) & gmask) == 0;
     if constexpr (STORM || LEAN_GUARD) {
       // an inactive row stays a quiet candidate only while none of its
-      // segments changes (the 4-slot lean variant lists inactive rows: the
-      // per-cell kernel clears them)
+      // segments changes (segments listed for the per-cell kernel, e.g. the
+      // 4-slot lean variant's inactive rows or saturated tombstones, are
+      // judged there)
       uint32_t chg = 0;
-      if (al && !act) chg = (o[0] ^ w[0]) | (o[1] ^ w[1]) | (o[2] ^ w[2]) | (o[3] ^ w[3]);
+      if (al && !act && seg_ok) chg = (o[0] ^ w[0]) | (o[1] ^ w[1]) | (o[2] ^ w[2]) | (o[3] ^ w[3]);
       if ((__ballot(chg != 0) & gmask) != 0 && lc == 0) stab_nxt[i] = 0;
     }
     int dpres = 0;  // present after - present before
@@ -1167,7 +1168,9 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
     int dpres = 0;  // present after - present before
     GhCell o[8];
     uint4 nx = {0u, 0u, 0u, 0u};
+    uint4 raw = {0u, 0u, 0u, 0u};  // the chunk as read (narrow codes or a wide marker)
     if (valid) {
+      raw = *reinterpret_cast<const uint4*>(d.hn[cur] + gh_cell(d, i, l0));
       GhCell A[8], X[8];
       gh_get8(d, cur, i, l0, r, A);
       int64_t m[8];
@@ -1238,6 +1241,11 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
     }
     // a segment is narrow iff every lane of it has narrow codes
     const bool narrow = (__ballot(valid && !fit) & gmask) == 0;
+    // an inactive row stays a quiet candidate while its segments are
+    // rewritten unchanged (narrow, same codes; a wide input never is)
+    const bool same = narrow && (raw.x & 0xFFFFu) != GH_N_WIDE && raw.x == nx.x && raw.y == nx.y &&
+                      raw.z == nx.z && raw.w == nx.w;
+    const bool seg_same = (__ballot(valid && !same) & gmask) == 0;
     if (valid) {
       int64_t slot = 0;
       if (!narrow) {
@@ -1259,7 +1267,7 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
     if (lc == 0 && valid) {
       if (dpres) atomicAdd(&d.cntl[i], dpres);
       if (any_det) d.det_any[i] = 1;
-      d.stab[(p.r + 1) & 1][i] = 0;  // not a quiet row (conservatively)
+      if (ac || !seg_same) d.stab[(p.r + 1) & 1][i] = 0;
     }
   }
   if (n_unknown) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], (unsigned long long)n_unknown);

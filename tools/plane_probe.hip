@@ -106,6 +106,39 @@ __global__ __launch_bounds__(256) void k_plane(const uint16_t* __restrict__ in, 
   }
 }
 
+// own table at 8 bits per cell (TW = 256: 256 B per row segment, a lane
+// owns 8 cells = 8 B), senders from the 4-bit plane: the byte budget of an
+// 8-bit steady-state tier
+template <int RB>
+__global__ __launch_bounds__(256) void k_own8(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                              const uint32_t* __restrict__ pin, uint32_t* __restrict__ pout,
+                                              const int4* __restrict__ inbox, int n) {
+  constexpr int PW = 256, L = PW / 8, RPI = 64 / L;
+  const int nrb = n / RB;
+  const int bid = blockIdx.x;
+  const int x = bid & 7, j = bid >> 3;
+  const int ptile = x + 8 * (j / nrb);
+  const int rb = j % nrb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int sub = lane / L, l = lane % L;
+  const int64_t oslice = (int64_t)ptile * n * PW + l * 8;
+  const int64_t pslice = (int64_t)ptile * n * (PW / 8) + l;
+  for (int r = wave * RPI + sub; r < RB; r += 4 * RPI) {
+    const int i = rb * RB + r;
+    uint2 v = *reinterpret_cast<const uint2*>(in + oslice + (int64_t)i * PW);
+    const int4 s = inbox[i];
+    const uint32_t a = pin[pslice + (int64_t)s.x * (PW / 8)];
+    const uint32_t b = pin[pslice + (int64_t)s.y * (PW / 8)];
+    const uint32_t c = pin[pslice + (int64_t)s.z * (PW / 8)];
+    const uint32_t e = pin[pslice + (int64_t)s.w * (PW / 8)];
+    const uint32_t m = nmin(nmin(a, b), nmin(c, e));
+    v.x += m & 0x0F0F0F0Fu;
+    v.y += (m >> 4) & 0x0F0F0F0Fu;
+    *reinterpret_cast<uint2*>(out + oslice + (int64_t)i * PW) = v;
+    __builtin_nontemporal_store(v.x ^ v.y, pout + pslice + (int64_t)i * (PW / 8));
+  }
+}
+
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 65536;
   const int reps = argc > 2 ? atoi(argv[2]) : 10;
@@ -173,5 +206,29 @@ int main(int argc, char** argv) {
   run("4-bit plane PW=256 RB=32", k_plane<256, 32, 0>, 256, 32);
   run("4-bit plane PW=256 RB=64 (again)", k_plane<256, 64, 0>, 256, 64);
   run("16-bit gathers PW=64 RB=256", k_plane<64, 256, 1>, 64, 256);
+  auto run8 = [&](const char* name, auto kern, int rb) {
+    const int grid = (n / 256) * (n / rb);
+    uint8_t* a = reinterpret_cast<uint8_t*>(t0);
+    uint8_t* b = reinterpret_cast<uint8_t*>(t1);
+    kern<<<grid, 256>>>(a, b, p0, p1, inbox, n);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < reps; ++r) {
+      if (r & 1)
+        kern<<<grid, 256>>>(b, a, p1, p0, inbox, n);
+      else
+        kern<<<grid, 256>>>(a, b, p0, p1, inbox, n);
+    }
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    CK(hipGetLastError());
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("%-34s %.3f ms/launch\n", name, ms / reps);
+    fflush(stdout);
+  };
+  run8("own 8-bit + 4-bit plane RB=256", k_own8<256>, 256);
+  run8("own 8-bit + 4-bit plane RB=128", k_own8<128>, 128);
+  run("own TW=256: 4-bit PW=256 RB=256", k_plane<256, 256, 0, 256>, 256, 256);
   return 0;
 }
