@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GH_ABI_VERSION 3
+#define GH_ABI_VERSION 4
 
 /* ---- error codes ---------------------------------------------------- */
 #define GH_OK 0
@@ -52,6 +52,18 @@ extern "C" {
 #define GH_PEER_RING 1     /* reference ring push, slave/slave.go:512-524     */
 #define GH_DETECT_CANONICAL 0
 #define GH_DETECT_QUIRK 1  /* Go range-over-mutated-slice skip, slave.go:464   */
+/* MemberList order (SPEC.md §7 D1). GH_ORDER_ID keeps every list in member-ID
+ * order: pull mode with canonical detection is order-free (the benched
+ * configurations), and it needs no per-row order state. GH_ORDER_APPEND keeps
+ * the reference's slice order: members are appended when added
+ * (slave/slave.go:255 addNewMember, :437 MergeMemberList, in received-list
+ * order, senders in ID order) and keep their relative order when others are
+ * removed (:283); ring targets (:515-524), quirk runs (:464-477),
+ * MemberList[0] (:936, :994), placement candidates (master/master.go:46,
+ * :135) and lsm follow it. Single-GPU engines only (gh_create); HBM +8*N*N
+ * bytes (double-buffered [N][N] int32 lists). */
+#define GH_ORDER_ID 0
+#define GH_ORDER_APPEND 1
 
 /* ---- events (SPEC.md §5) ---------------------------------------------- */
 #define GH_EV_JOIN 1       /* slave/slave.go:288 Join + :250 addNewMember     */
@@ -79,7 +91,8 @@ typedef struct gh_config {
                             else 1/32 of them, grown between calls)        */
   int32_t shard_layout;  /* sharded engines (gh_create_sharded):
                             GH_LAYOUT_COLUMNS (0, default) or GH_LAYOUT_ROWS */
-  int32_t reserved[5];
+  int32_t list_order;    /* GH_ORDER_ID (0, default) or GH_ORDER_APPEND      */
+  int32_t reserved[4];
 } gh_config;
 
 typedef struct gh_event {
@@ -161,7 +174,8 @@ int gh_read_failed(void* h, uint32_t* bitmap, int64_t n_words);
 /* Rows that detected a failure in the last round (they call Fail_recover,
  * slave/slave.go:479-481). Returns the count via *n_out (<= cap written). */
 int gh_read_detectors(void* h, int32_t* rows, int64_t cap, int64_t* n_out);
-/* "lsm" (slave/slave.go:558-561): observer's present members. */
+/* "lsm" (slave/slave.go:558-561): observer's present members, in list order
+ * (member-ID order under GH_ORDER_ID). */
 int gh_lsm(void* h, int32_t observer, int32_t* ids, int32_t* hb, int32_t* ts,
            int64_t cap, int64_t* n_out);
 
@@ -202,8 +216,8 @@ int gh_delete_files(void* h, const int32_t* files, int64_t n,
  * and revote_master's target (:930-948), for every row of the current table:
  * list_len[i] = len(MemberList_i); has_master[i] = 1 if member mview[i] (row
  * i's own idea of the master, self.master) is in row i's list; first[i] =
- * MemberList_i[0], the lowest present member id (SPEC D1), -1 for an empty
- * list. mview: [N] member ids. Outputs: [N] each; any output may be NULL.
+ * MemberList_i[0] (under GH_ORDER_ID the lowest present member id, SPEC D1),
+ * -1 for an empty list. mview: [N] member ids. Outputs: [N] each; any output may be NULL.
  * The vote tally (Receive_vote :968-984, RPC TCPServer.Vote
  * server/server.go:231) is per-candidate control flow and stays on the host
  * (gossipsim.Cluster). */

@@ -70,6 +70,10 @@ struct Engine {
   int64_t gidx_cap = 0;
   int64_t gx_rows = 0, gx_out = 0, gx_in = 0;  // the last exchange: ghost rows, bytes sent / received
   int plane = 0;         // sender snapshot plane (pull mode, 3 <= k <= 4, N >= GH_PLANE_MIN_N; GH_PLANE=0/1)
+  // GH_ORDER_APPEND: per-row list order kept beside the table (order.hip);
+  // lcur = the list buffer of the current state
+  bool lorder = false;
+  int lcur = 0;
   // upper bound of every heartbeat in the table (int32 overflow check,
   // slave/slave.go:446): +1 per round, max of imported / merged values
   int64_t hb_bound = 0;
@@ -588,6 +592,23 @@ int process_events(Engine* e, int32_t r) {
   }
   launch_count(e->d, e->cur, p, e->stream);
   HIPCHK(e, hipGetLastError());
+  if (e->lorder) {
+    // list order (order.hip): a fresh process starts from an empty list;
+    // the introducer appends its joiners in event order, every receiver of
+    // its broadcast appends what it lacks in the introducer's list order
+    for (int32_t j : fresh) HIPCHK(e, hipMemsetAsync(e->d.llen[e->lcur] + j, 0, sizeof(int32_t), e->stream));
+    if (!joiners.empty() && I >= 0 && I < e->n && e->alive[I]) {
+      if ((rc = upload(e, e->ev_buf, joiners))) return rc;
+      if ((rc = upload(e, e->rows_buf, {I}))) return rc;
+      launch_list_events(e->d, e->cur, e->lcur, e->rows_buf, 1, e->ev_buf, (int32_t)joiners.size(), -1, -1,
+                         e->stream);
+      launch_list_events(e->d, e->cur, e->lcur, nullptr, 0, nullptr, 0, I, I, e->stream);
+    } else {
+      launch_list_events(e->d, e->cur, e->lcur, nullptr, 0, nullptr, 0, -1, -1, e->stream);
+    }
+    HIPCHK(e, hipGetLastError());
+    e->lcur ^= 1;
+  }
   return GH_OK;
 }
 
@@ -666,9 +687,12 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
       (cfg->peer_mode != GH_PEER_PULL && cfg->peer_mode != GH_PEER_RING) ||
       (cfg->detect_mode != GH_DETECT_CANONICAL && cfg->detect_mode != GH_DETECT_QUIRK) ||
       cfg->introducer < 0 || cfg->introducer >= cfg->n_members || cfg->master < 0 ||
-      cfg->master >= cfg->n_members || cfg->t_fail < 0 || cfg->t_cleanup < 0 || cfg->wide_segments < 0)
+      cfg->master >= cfg->n_members || cfg->t_fail < 0 || cfg->t_cleanup < 0 || cfg->wide_segments < 0 ||
+      (cfg->list_order != GH_ORDER_ID && cfg->list_order != GH_ORDER_APPEND))
     return GH_EINVAL;
   if (world < 1 || rank < 0 || rank >= world) return GH_EINVAL;
+  // the list order of a row spans every member column: one engine holds it
+  if (cfg->list_order == GH_ORDER_APPEND && world > 1) return GH_EINVAL;
   if (world > 1 && !comm_id) return GH_EINVAL;
   if (transport != GH_COMM_RCCL && transport != GH_COMM_LOCAL) return GH_EINVAL;
   int ndev = 0;
@@ -747,6 +771,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   const int64_t gcap = rowlay && world > 1 ? std::min<int64_t>(e->n - nrows, nrows * cfg->fanout + 1) : 0;
   e->rowlay = rowlay;
   e->nrs = nrs;
+  e->lorder = cfg->list_order == GH_ORDER_APPEND;
   const int64_t pad = std::max<int64_t>(GH_PAD, 8 * (int64_t)tw);
   e->ld = (ncs + pad - 1) / pad * pad;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -816,6 +841,15 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
          (rc = dalloc(e, &d.qcarry, e->n, 0)) || (rc = dalloc(e, &d.qlast, e->n, 0))))
       break;
     if ((rc = dalloc(e, &d.rbits, (size_t)world * 2 * d.ncsw, 0))) break;
+    if (e->lorder) {
+      if (!list_lds_ok(d)) {
+        rc = set_err(e, GH_EINVAL, "GH_ORDER_APPEND: N too large for the per-row list kernels");
+        break;
+      }
+      if ((rc = dalloc(e, &d.lord[0], (size_t)e->n * e->ld, 0)) || (rc = dalloc(e, &d.lord[1], (size_t)e->n * e->ld, 0)) ||
+          (rc = dalloc(e, &d.llen[0], e->n, 0)) || (rc = dalloc(e, &d.llen[1], e->n, 0)))
+        break;
+    }
     if (rowlay) {
       e->rslot_h.assign(e->n, -1);
       for (int64_t i = row0; i < row0 + nrows; ++i) e->rslot_h[i] = (int32_t)(i - row0);
@@ -874,6 +908,11 @@ int decide_active(Engine* e, const GhRound& p) {
 // the reference's range-over-mutated-slice set before anything reads them.
 int quirk_flags(Engine* e, const GhRound& p) {
   GhDev& d = e->d;
+  if (e->lorder) {  // runs over the list order
+    launch_quirk_list(d, e->cur, e->dcur, p, e->lcur, e->stream);
+    HIPCHK(e, hipGetLastError());
+    return GH_OK;
+  }
   launch_quirk_scan(d, e->cur, e->dcur, p, e->stream);
   HIPCHK(e, hipGetLastError());
   if (e->world > 1 && !e->rowlay)  // row layout: a row's runs never cross shards
@@ -905,6 +944,12 @@ int build_inboxes(Engine* e, const GhRound& p) {
       COMMCHK(e, e->comm->allgather(d.inbox + (size_t)e->rank * d.ncs * row, d.inbox,
                                     sizeof(int32_t) * d.ncs * row, e->stream));
     }
+    return GH_OK;
+  }
+  if (e->lorder) {  // neighbours in list order (single GPU)
+    launch_ring_list(d, e->cur, e->dcur, p, e->lcur, e->stream);
+    launch_inbox(d, p, e->stream);
+    HIPCHK(e, hipGetLastError());
     return GH_OK;
   }
   launch_ring_count(d, e->cur, e->dcur, p, e->stream);
@@ -1107,7 +1152,7 @@ int gh_memory_info(void* h, int64_t* device_bytes, int64_t* wide_used, int64_t* 
     // callers, not here
     const int64_t cells = d.nslots * e->ld;
     *device_bytes = 2 * cells * 2 + (e->plane ? cells : 0) + 2 * d.wcap * ((int64_t)d.tw * 8 + d.tw / 8) +
-                    e->fzcap * e->ld * 8;
+                    e->fzcap * e->ld * 8 + (e->lorder ? 2 * (int64_t)e->n * e->ld * 4 : 0);
   }
   if (wide_used) *wide_used = std::min<int64_t>(used, d.wcap);
   if (wide_cap) *wide_cap = d.wcap;
@@ -1161,6 +1206,7 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
   e->pending.clear();
   if ((rc = reset_pending_removes(e))) return rc;
   launch_count(e->d, e->cur, p, e->stream);
+  if (e->lorder) launch_list_import(e->d, e->cur, e->lcur, row0, n_rows, e->stream);  // dense rows: ID order
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipStreamSynchronize(e->stream));
   return GH_OK;
@@ -1199,6 +1245,7 @@ int gh_init_full(void* h, int32_t hb0, int32_t ts0, int32_t round) {
   e->hb_bound = hb0;
   if ((rc = reset_pending_removes(e))) return rc;
   launch_count(e->d, e->cur, p, e->stream);
+  if (e->lorder) launch_list_import(e->d, e->cur, e->lcur, 0, e->n, e->stream);
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipStreamSynchronize(e->stream));
   return GH_OK;
@@ -1291,6 +1338,10 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       COMMCHK(e, e->comm->allreduce(dm, dm, e->ld, GH_DT_I32, GH_OP_MAX, e->stream));
       launch_negate(dm, e->ld, e->stream);
       HIPCHK(e, hipGetLastError());
+    }
+    if (e->lorder) {  // the lists of the next state (needs D_{r-1} and the inboxes)
+      launch_list_round(e->d, e->cur, e->dcur, p, e->lcur, e->stream);
+      e->lcur ^= 1;
     }
     launch_finish(e->d, e->dcur, p, e->stream);
     HIPCHK(e, hipGetLastError());
@@ -1397,8 +1448,22 @@ int gh_lsm(void* h, int32_t observer, int32_t* ids, int32_t* hb, int32_t* ts, in
   std::vector<int32_t> rh(e->n), rt(e->n);
   int rc = gh_export_state(h, rh.data(), rt.data(), nullptr, observer, 1);
   if (rc != GH_OK) return rc;
+  std::vector<int32_t> order;  // list order (GH_ORDER_APPEND), else member-ID order
+  if (e->lorder) {
+    int32_t len = 0;
+    HIPCHK(e, hipMemcpyAsync(&len, e->d.llen[e->lcur] + observer, sizeof len, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    order.resize(std::max<int32_t>(len, 0));
+    if (len > 0)
+      HIPCHK(e, hipMemcpyAsync(order.data(), e->d.lord[e->lcur] + (int64_t)observer * e->ld, sizeof(int32_t) * len,
+                               hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  } else {
+    for (int32_t c = 0; c < e->n; ++c)
+      if (rh[c] >= 0) order.push_back(c);
+  }
   int64_t k = 0;
-  for (int32_t c = 0; c < e->n; ++c)
+  for (int32_t c : order)
     if (rh[c] >= 0) {
       if (k < cap) {
         if (ids) ids[k] = c;
@@ -1442,6 +1507,15 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
     HIPCHK(e, hipGetLastError());
     if ((rc = allreduce_i32(e, e->d.nd + 5, e->d.nd + 5, 1))) return rc;
     launch_count(e->d, e->cur, p, e->stream);  // presence changed: refresh the row counts
+    if (e->lorder) {  // added members in datagram order (:433-437), then the row back in place
+      if ((rc = upload(e, e->rows_buf, {observer}))) return rc;
+      launch_list_events(e->d, e->cur, e->lcur, e->rows_buf, 1, st.as<int32_t>(), (int32_t)n, -1, -1, e->stream);
+      const int l2 = e->lcur ^ 1;
+      HIPCHK(e, hipMemcpyAsync(e->d.lord[e->lcur] + (int64_t)observer * e->ld, e->d.lord[l2] + (int64_t)observer * e->ld,
+                               sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(e, hipMemcpyAsync(e->d.llen[e->lcur] + observer, e->d.llen[l2] + observer, sizeof(int32_t),
+                               hipMemcpyDeviceToDevice, e->stream));
+    }
     HIPCHK(e, hipMemcpyAsync(&cnt, e->d.nd + 5, sizeof cnt, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     int32_t err = 0;
@@ -1465,7 +1539,10 @@ int gh_put(void* h, const int32_t* files, int64_t n, int32_t* replicas, int32_t*
   HIPCHK(e, hipMemcpyAsync(e->d.io_a, files, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
   if ((rc = upload(e, e->rows_buf, {e->cfg.master}))) return rc;
   if ((rc = gather_rows(e, e->rows_buf, 1))) return rc;
-  launch_candidates(e->d, 1, e->stream);
+  if (e->lorder)  // Member_list in list order
+    launch_list_cand(e->d, e->lcur, e->cfg.master, e->stream);
+  else
+    launch_candidates(e->d, 1, e->stream);
   launch_put(e->d, 1, n, R, e->round, e->cfg.seed, e->stream);
   HIPCHK(e, hipGetLastError());
   std::vector<int32_t> rep(n * R), ver(n), st(n);
@@ -1509,7 +1586,10 @@ int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap, int64
   int rc;
   if ((rc = upload(e, e->rows_buf, {e->cfg.master, observer}))) return rc;
   if ((rc = gather_rows(e, e->rows_buf, 2))) return rc;
-  launch_candidates(e->d, 2, e->stream);
+  if (e->lorder)
+    launch_list_cand(e->d, e->lcur, e->cfg.master, e->stream);
+  else
+    launch_candidates(e->d, 2, e->stream);
   launch_repair(e->d, 2, e->cfg.replicas, e->cfg.seed, e->stream);
   HIPCHK(e, hipGetLastError());
   int32_t np = 0;
@@ -1589,6 +1669,7 @@ int gh_vote_scan(void* h, const int32_t* mview, int32_t* first, int32_t* list_le
   int32_t* len = out + 2 * n;  // [n]: SUM-reduced list lengths
   HIPCHK(e, hipMemcpyAsync(mv, mview, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
   launch_vote_scan(e->d, e->cur, mv, out, e->stream);
+  if (e->lorder) launch_list_first(e->d, e->lcur, out, e->stream);  // MemberList[0] in list order
   HIPCHK(e, hipGetLastError());
   COMMCHK(e, e->comm->allreduce(out, out, 2 * (size_t)n, GH_DT_I32, GH_OP_MAX, e->stream));
   if ((rc = allreduce_i32(e, e->d.cntl, len, (size_t)n))) return rc;
@@ -1608,7 +1689,7 @@ int gh_rebuild_meta(void* h, int32_t new_master, int32_t* f0, int64_t* n_files) 
   if (!e) return GH_EINVAL;
   if (new_master < 0 || new_master >= e->n) return set_err(e, GH_EINVAL, "new_master");
   if (e->d.fcap <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
-  // the first 5 members of M's list (ID order); 5 covers "first 4 other than M"
+  // the first 5 members of M's list (list order); 5 covers "first 4 other than M"
   std::vector<int32_t> ids(e->n);
   int64_t nl = 0;
   int rc = gh_lsm(h, new_master, ids.data(), nullptr, nullptr, e->n, &nl);
