@@ -197,10 +197,13 @@ struct GhDev {
   // one round ago). A collapsed cluster stops rewriting its tables.
   uint8_t *stab[2];
   int32_t *nquiet;  // row segments the last round skipped as quiet
-  // MemberList order (GH_ORDER_APPEND, order.hip; null under GH_ORDER_ID):
-  // lord[b][i * ld + p] = member at position p of row i's list, llen[b][i]
-  // its length, for the state the host's list buffer index says
-  int32_t *lord[2], *llen[2];
+  // MemberList order (GH_ORDER_APPEND, order.hip; null under GH_ORDER_ID).
+  // Generation g (the host's lcur) of row i: the list is lord[lsel[g][i]] +
+  // i * ld (member at each position), llen[g][i] entries, the row's own
+  // member at lself[g][i] (-1 not listed). Two buffers per row: a rewrite
+  // goes to the other one while the senders read the current one.
+  int32_t *lord[2], *llen[2], *lself[2];
+  uint8_t *lsel[2];
   int32_t *base[2]; // [ld] narrow base per buffer
   // wide arena per buffer: [wcap][tw] x / exact ts, [wcap][tw/8] flag bytes
   int32_t *wh[2], *wt[2];
@@ -578,14 +581,16 @@ void launch_ghost_wide(const GhDev& d, int cur, const int32_t* rows, const int32
                        char* out, hipStream_t s);
 void launch_ghost_unpack(const GhDev& d, int cur, const char* in, int64_t nr, int64_t slot0, hipStream_t s);
 void launch_ghost_unwide(const GhDev& d, int cur, const char* in, int64_t nrec, hipStream_t s);
-// order.hip (GH_ORDER_APPEND): list buffers lin -> lin ^ 1 (events: rows or
-// all; added members in the order of src_ids, else of src_row's new list)
+// order.hip (GH_ORDER_APPEND): list generation lin -> lin ^ 1 (events: rows
+// or all; added members in the order of src_ids, else of src_row's new list);
+// ring: flags_known = the table's flagged-segment count is current (every
+// snapshot is a whole list when it and |D_{r-1}| are 0)
 bool list_lds_ok(const GhDev& d);
 void launch_list_round(const GhDev& d, int cur, int dcur, const GhRound& p, int lin, hipStream_t s);
 void launch_list_events(const GhDev& d, int cur, int lin, const int32_t* rows, int32_t nr, const int32_t* src_ids,
                         int32_t n_src, int32_t src_row, int32_t skip, hipStream_t s);
 void launch_list_import(const GhDev& d, int cur, int lb, int64_t row0, int64_t nr, hipStream_t s);
-void launch_ring_list(const GhDev& d, int cur, int dcur, const GhRound& p, int lin, hipStream_t s);
+void launch_ring_list(const GhDev& d, int cur, int dcur, const GhRound& p, int lin, int flags_known, hipStream_t s);
 void launch_quirk_list(const GhDev& d, int cur, int dcur, const GhRound& p, int lin, hipStream_t s);
 void launch_list_cand(const GhDev& d, int lin, int32_t master, hipStream_t s);
 void launch_list_first(const GhDev& d, int lin, int32_t* out, hipStream_t s);

@@ -74,6 +74,9 @@ struct Engine {
   // lcur = the list buffer of the current state
   bool lorder = false;
   int lcur = 0;
+  // nflag of the current buffer counts its flagged segments (a round wrote
+  // it; host writes do not count theirs)
+  bool flags_known = false;
   // upper bound of every heartbeat in the table (int32 overflow check,
   // slave/slave.go:446): +1 per round, max of imported / merged values
   int64_t hb_bound = 0;
@@ -506,6 +509,7 @@ int allreduce_i32(Engine* e, int32_t* send, int32_t* recv, size_t count) {
 int process_events(Engine* e, int32_t r) {
   if (e->pending.empty()) return GH_OK;
   e->qforce = true;
+  e->flags_known = false;
   e->pforce = true;
   const GhRound p = round_params(e, r);
   std::vector<gh_event> ev;
@@ -847,7 +851,9 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         break;
       }
       if ((rc = dalloc(e, &d.lord[0], (size_t)e->n * e->ld, 0)) || (rc = dalloc(e, &d.lord[1], (size_t)e->n * e->ld, 0)) ||
-          (rc = dalloc(e, &d.llen[0], e->n, 0)) || (rc = dalloc(e, &d.llen[1], e->n, 0)))
+          (rc = dalloc(e, &d.llen[0], e->n, 0)) || (rc = dalloc(e, &d.llen[1], e->n, 0)) ||
+          (rc = dalloc(e, &d.lself[0], e->n, 0xFF)) || (rc = dalloc(e, &d.lself[1], e->n, 0xFF)) ||
+          (rc = dalloc(e, &d.lsel[0], e->n, 0)) || (rc = dalloc(e, &d.lsel[1], e->n, 0)))
         break;
     }
     if (rowlay) {
@@ -947,7 +953,7 @@ int build_inboxes(Engine* e, const GhRound& p) {
     return GH_OK;
   }
   if (e->lorder) {  // neighbours in list order (single GPU)
-    launch_ring_list(d, e->cur, e->dcur, p, e->lcur, e->stream);
+    launch_ring_list(d, e->cur, e->dcur, p, e->lcur, e->flags_known, e->stream);
     launch_inbox(d, p, e->stream);
     HIPCHK(e, hipGetLastError());
     return GH_OK;
@@ -1183,6 +1189,7 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
   int rc;
   if (!full && (rc = check_lost(e))) return rc;
   e->qforce = true;
+  e->flags_known = false;
   e->pforce = true;
   const GhRound p = round_params(e, round + 1);
   if (n_rows > 0) {
@@ -1231,6 +1238,7 @@ int gh_init_full(void* h, int32_t hb0, int32_t ts0, int32_t round) {
   if (hb0 < 0) return set_err(e, GH_ERANGE, "hb0 below 0");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   e->qforce = true;
+  e->flags_known = false;
   e->pforce = true;
   std::fill(e->alive.begin(), e->alive.end(), 1);
   int rc;
@@ -1348,6 +1356,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     e->cur ^= 1;
     e->dcur ^= 1;
     e->round = r;
+    e->flags_known = true;
     e->hb_bound = std::min<int64_t>(INT32_MAX, e->hb_bound + 1);
     done++;
     if (busy && q + 1 < rounds) {
@@ -1451,11 +1460,13 @@ int gh_lsm(void* h, int32_t observer, int32_t* ids, int32_t* hb, int32_t* ts, in
   std::vector<int32_t> order;  // list order (GH_ORDER_APPEND), else member-ID order
   if (e->lorder) {
     int32_t len = 0;
+    uint8_t b = 0;
     HIPCHK(e, hipMemcpyAsync(&len, e->d.llen[e->lcur] + observer, sizeof len, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(&b, e->d.lsel[e->lcur] + observer, 1, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     order.resize(std::max<int32_t>(len, 0));
     if (len > 0)
-      HIPCHK(e, hipMemcpyAsync(order.data(), e->d.lord[e->lcur] + (int64_t)observer * e->ld, sizeof(int32_t) * len,
+      HIPCHK(e, hipMemcpyAsync(order.data(), e->d.lord[b & 1] + (int64_t)observer * e->ld, sizeof(int32_t) * len,
                                hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
   } else {
@@ -1493,6 +1504,7 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
   int rc0;
   if ((rc0 = check_lost(e)) || (rc0 = maybe_grow(e))) return rc0;
   e->qforce = true;
+  e->flags_known = false;
   e->pforce = true;
   int32_t cnt = 0;
   if (n > 0 && e->alive[observer]) {  // GetMsg runs only while Alive (slave/slave.go:208)
@@ -1510,10 +1522,11 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
     if (e->lorder) {  // added members in datagram order (:433-437), then the row back in place
       if ((rc = upload(e, e->rows_buf, {observer}))) return rc;
       launch_list_events(e->d, e->cur, e->lcur, e->rows_buf, 1, st.as<int32_t>(), (int32_t)n, -1, -1, e->stream);
-      const int l2 = e->lcur ^ 1;
-      HIPCHK(e, hipMemcpyAsync(e->d.lord[e->lcur] + (int64_t)observer * e->ld, e->d.lord[l2] + (int64_t)observer * e->ld,
-                               sizeof(int32_t) * e->n, hipMemcpyDeviceToDevice, e->stream));
-      HIPCHK(e, hipMemcpyAsync(e->d.llen[e->lcur] + observer, e->d.llen[l2] + observer, sizeof(int32_t),
+      const int g = e->lcur, g2 = g ^ 1;  // the row's new generation becomes its current one
+      HIPCHK(e, hipMemcpyAsync(e->d.lsel[g] + observer, e->d.lsel[g2] + observer, 1, hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(e, hipMemcpyAsync(e->d.llen[g] + observer, e->d.llen[g2] + observer, sizeof(int32_t),
+                               hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(e, hipMemcpyAsync(e->d.lself[g] + observer, e->d.lself[g2] + observer, sizeof(int32_t),
                                hipMemcpyDeviceToDevice, e->stream));
     }
     HIPCHK(e, hipMemcpyAsync(&cnt, e->d.nd + 5, sizeof cnt, hipMemcpyDeviceToHost, e->stream));

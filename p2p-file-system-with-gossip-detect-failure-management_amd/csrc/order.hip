@@ -63,22 +63,30 @@ __device__ __forceinline__ int block_prefix(bool pred, int& total, int* s_w) {
   return off + before;
 }
 
-// Copies row i's list from buffer lin to lin ^ 1 unchanged.
-__device__ void copy_row(const GhDev& d, int lin, int64_t i) {
-  const int L = d.llen[lin][i];
-  const int32_t* src = d.lord[lin] + i * d.ld;
-  int32_t* dst = d.lord[lin ^ 1] + i * d.ld;
-  for (int p = threadIdx.x; p < L; p += blockDim.x) dst[p] = src[p];
-  if (threadIdx.x == 0) d.llen[lin ^ 1][i] = L;
+// Row i's list in generation g: lord[lsel[g][i]] + i * ld, llen[g][i]
+// entries, own member at lself[g][i] (-1: not listed).
+__device__ __forceinline__ const int32_t* list_of(const GhDev& d, int g, int64_t i) {
+  return d.lord[d.lsel[g][i]] + i * d.ld;
+}
+
+// Generation g ^ 1 of row i = generation g (thread 0).
+__device__ __forceinline__ void keep_row(const GhDev& d, int g, int64_t i) {
+  if (threadIdx.x == 0) {
+    d.lsel[g ^ 1][i] = d.lsel[g][i];
+    d.llen[g ^ 1][i] = d.llen[g][i];
+    d.lself[g ^ 1][i] = d.lself[g][i];
+  }
 }
 
 // The members of row i present in buffer buf and not in the LDS set `stay`
-// -> LDS set `app`; returns their count (uniform).
-__device__ int mark_added(const GhDev& d, int buf, int64_t i, const uint32_t* stay, uint32_t* app, int* s_w) {
+// (stay null: not present in buffer old) -> LDS set `app`; returns their
+// count (uniform).
+__device__ int mark_added(const GhDev& d, int buf, int old, int64_t i, const uint32_t* stay, uint32_t* app, int* s_w) {
   int a = 0;
   for (int64_t c8 = (int64_t)threadIdx.x * 8; c8 < d.n; c8 += (int64_t)blockDim.x * 8) {
     const uint32_t pf = gh_pf8(d, buf, i, c8) & 0xFFu;
-    const uint32_t m = pf & ~((stay[c8 >> 5] >> (c8 & 31)) & 0xFFu);
+    const uint32_t was = stay ? (stay[c8 >> 5] >> (c8 & 31)) & 0xFFu : gh_pf8(d, old, i, c8) & 0xFFu;
+    const uint32_t m = pf & ~was;
     if (m) {
       atomicOr(&app[c8 >> 5], m << (c8 & 31));
       a += __builtin_popcount(m);
@@ -93,10 +101,11 @@ __device__ int mark_added(const GhDev& d, int buf, int64_t i, const uint32_t* st
 }
 
 // Appends, in the order of list src[0..ns), the members of `app` that
-// `visible` admits; clears their bits. pos / need are uniform.
+// `visible` admits; clears their bits; a row's own member i sets *s_self.
+// pos / need are uniform.
 template <class Visible>
 __device__ void append_from(const int32_t* src, int ns, uint32_t* app, int32_t* dst, int& pos, int& need, int* s_w,
-                            Visible visible) {
+                            int64_t i, int* s_self, Visible visible) {
   for (int b = 0; b < ns && need > 0; b += blockDim.x) {
     const int q = b + threadIdx.x;
     int c = -1;
@@ -109,6 +118,7 @@ __device__ void append_from(const int32_t* src, int ns, uint32_t* app, int32_t* 
     const int o = block_prefix(take, tot, s_w);
     if (take) {
       dst[pos + o] = c;
+      if (c == i) *s_self = pos + o;
       atomicAnd(&app[c >> 5], ~(1u << (c & 31)));
     }
     pos += tot;
@@ -117,32 +127,14 @@ __device__ void append_from(const int32_t* src, int ns, uint32_t* app, int32_t* 
   }
 }
 
-// After a round (before k_finish: D_{r-1} and the inboxes are intact). One
-// workgroup per row; dynamic LDS: two member bitmaps.
-__global__ __launch_bounds__(256) void k_list_round(GhDev d, int cur, int dcur, GhRound p, int lin) {
-  extern __shared__ uint32_t s_bits[];
-  __shared__ int s_w[4];
-  __shared__ int s_snd[kMaxSenders];
-  __shared__ int s_ns;
-  const int64_t i = blockIdx.x;
-  if (i >= d.n) return;
-  if (!d.alive[i]) {  // a stopped row is not touched by the round
-    copy_row(d, lin, i);
-    return;
-  }
-  const int nw = (d.n + 31) >> 5;
-  uint32_t* stay = s_bits;
-  uint32_t* app = s_bits + nw;
-  for (int w = threadIdx.x; w < 2 * nw; w += blockDim.x) s_bits[w] = 0;
-  __syncthreads();
-  const int nxt = cur ^ 1;
-  const bool act = d.active[i];
-  const int L = d.llen[lin][i];
-  const int32_t* src = d.lord[lin] + i * d.ld;
-  int32_t* dst = d.lord[lin ^ 1] + i * d.ld;
-  // members that stayed: not REMOVE'd (step 1), not detected (step 4: a flag
-  // of an active row), still present (a removed member the merge brings back
-  // is appended again)
+// Old list of row i (generation g) -> dst, keeping the members `keep` admits
+// in order; their bits -> LDS set `stay`; the own member's new position ->
+// *s_self. Returns the count (uniform).
+template <class Keep>
+__device__ int compact(const GhDev& d, int g, int64_t i, int32_t* dst, uint32_t* stay, int* s_w, int* s_self,
+                       Keep keep_fn) {
+  const int L = d.llen[g][i];
+  const int32_t* src = list_of(d, g, i);
   int pos = 0;
   for (int b = 0; b < L; b += blockDim.x) {
     const int q = b + threadIdx.x;
@@ -150,22 +142,87 @@ __global__ __launch_bounds__(256) void k_list_round(GhDev d, int cur, int dcur, 
     bool keep = false;
     if (q < L) {
       c = src[q];
-      const GhCell o = gh_get(d, cur, i, c, 0);
-      keep = gh_get(d, nxt, i, c, 0).x >= 0 && !removed_at(d, dcur, c, i) && !(act && o.f);
+      keep = keep_fn(c);
     }
     int tot;
     const int o = block_prefix(keep, tot, s_w);
     if (keep) {
       dst[pos + o] = c;
+      if (c == i) *s_self = pos + o;
       atomicOr(&stay[c >> 5], 1u << (c & 31));
     }
     pos += tot;
   }
   __syncthreads();
+  return pos;
+}
+
+// After a round (before k_finish: D_{r-1} and the inboxes are intact). One
+// workgroup per row; dynamic LDS: two member bitmaps. A row without removals
+// keeps its list and buffer (members added are appended in place, past the
+// end the senders read); a row with removals is rewritten into its other
+// buffer.
+__global__ __launch_bounds__(256) void k_list_round(GhDev d, int cur, int dcur, GhRound p, int g) {
+  extern __shared__ uint32_t s_bits[];
+  __shared__ int s_w[4];
+  __shared__ int s_snd[kMaxSenders];
+  __shared__ int s_ns, s_rem, s_self;
+  const int64_t i = blockIdx.x;
+  if (i >= d.n) return;
+  if (!d.alive[i]) {  // a stopped row is not touched by the round
+    keep_row(d, g, i);
+    return;
+  }
+  const int nxt = cur ^ 1;
+  const bool act = d.active[i];
+  const int L = d.llen[g][i];
   const int target = d.cntl[i];  // present after the round (kept current by the round kernels)
+  // removals in this row: a detection (step 4), or a REMOVE of D_{r-1} (step
+  // 1) of a member it lists
+  if (threadIdx.x == 0) {
+    s_rem = d.det_any[i];
+    s_self = d.lself[g][i];
+  }
+  __syncthreads();
+  const int nd = d.cntg[p.n];
+  if (!s_rem && nd > 0) {
+    if (d.nd[dcur] > GH_DLIST_MAX) {
+      s_rem = 1;  // storms: assume so
+    } else {
+      for (int q = threadIdx.x; q < d.nd[dcur]; q += blockDim.x) {
+        const int c = d.dlist[(int64_t)dcur * p.ld + q];
+        if (removed_at(d, dcur, c, i) && gh_get(d, cur, i, c, 0).x >= 0) s_rem = 1;
+      }
+    }
+  }
+  __syncthreads();
+  const bool rem = s_rem != 0;
+  if (!rem && target == L) {
+    keep_row(d, g, i);
+    return;
+  }
+  const int nw = (d.n + 31) >> 5;
+  uint32_t* stay = s_bits;
+  uint32_t* app = s_bits + nw;
+  for (int w = threadIdx.x; w < 2 * nw; w += blockDim.x) s_bits[w] = 0;
+  __syncthreads();
+  const int b0 = d.lsel[g][i];
+  const int bo = rem ? b0 ^ 1 : b0;  // output buffer: in place when nothing left the list
+  int32_t* dst = d.lord[bo] + i * d.ld;
+  int pos = L;
+  if (rem) {
+    if (threadIdx.x == 0) s_self = -1;
+    __syncthreads();
+    // members that stayed: not REMOVE'd (step 1), not detected (step 4: a
+    // flag of an active row), still present (a removed member the merge
+    // brings back is appended again)
+    pos = compact(d, g, i, dst, stay, s_w, &s_self, [&](int c) {
+      return gh_get(d, nxt, i, c, 0).x >= 0 && !removed_at(d, dcur, c, i) && !(act && gh_get(d, cur, i, c, 0).f);
+    });
+  }
   int need = target - pos;
   if (need > 0) {
-    need = mark_added(d, nxt, i, stay, app, s_w);
+    need = mark_added(d, nxt, cur, i, rem ? stay : nullptr, app, s_w);
     if (threadIdx.x == 0) {
       // the receiver's senders, ascending and distinct (SPEC §2 delivery order)
       const bool pull = p.peer_mode == GH_PEER_PULL;
@@ -194,119 +251,126 @@ __global__ __launch_bounds__(256) void k_list_round(GhDev d, int cur, int dcur, 
     __syncthreads();
     for (int q = 0; q < s_ns && need > 0; ++q) {
       const int s = s_snd[q];
-      // s's snapshot: its list after REMOVE delivery and detection
-      append_from(d.lord[lin] + (int64_t)s * d.ld, d.llen[lin][s], app, dst, pos, need, s_w,
+      // s's snapshot: its list (generation g) after REMOVE delivery and detection
+      append_from(list_of(d, g, s), d.llen[g][s], app, dst, pos, need, s_w, i, &s_self,
                   [&](int c) { return !gh_get(d, cur, s, c, 0).f && !removed_at(d, dcur, c, s); });
     }
   }
+  __syncthreads();
   if (threadIdx.x == 0) {
     if (pos != target) atomicExch(d.err, GH_EINVAL);  // the order lost track of the set
-    d.llen[lin ^ 1][i] = pos;
+    d.lsel[g ^ 1][i] = (uint8_t)bo;
+    d.llen[g ^ 1][i] = pos;
+    d.lself[g ^ 1][i] = s_self;
   }
 }
 
-// After events or an external datagram (table buffer cur, counts current).
-// rows: the rows to rebuild (null: blockIdx.x); skip: a row left alone (-1
-// none). Added members follow src_ids[0..n_src) if given, else the new list
-// (buffer lin ^ 1) of row src_row, else none may be added.
-__global__ __launch_bounds__(256) void k_list_events(GhDev d, int cur, int lin, const int32_t* rows,
+// After events or an external datagram (table buffer cur, counts current):
+// generation g -> g ^ 1, each row rewritten into its other buffer. rows: the
+// rows to rebuild (null: blockIdx.x); skip: a row left alone (-1 none).
+// Added members follow src_ids[0..n_src) if given, else the new list
+// (generation g ^ 1) of row src_row, else none may be added.
+__global__ __launch_bounds__(256) void k_list_events(GhDev d, int cur, int g, const int32_t* rows,
                                                      const int32_t* src_ids, int n_src, int src_row, int skip) {
   extern __shared__ uint32_t s_bits[];
   __shared__ int s_w[4];
+  __shared__ int s_self;
   const int64_t i = rows ? rows[blockIdx.x] : blockIdx.x;
   if (i >= d.n || i == skip) return;
   if (!d.alive[i]) {
-    copy_row(d, lin, i);
+    keep_row(d, g, i);
     return;
   }
   const int nw = (d.n + 31) >> 5;
   uint32_t* stay = s_bits;
   uint32_t* app = s_bits + nw;
   for (int w = threadIdx.x; w < 2 * nw; w += blockDim.x) s_bits[w] = 0;
+  if (threadIdx.x == 0) s_self = -1;
   __syncthreads();
-  const int L = d.llen[lin][i];
-  const int32_t* src = d.lord[lin] + i * d.ld;
-  int32_t* dst = d.lord[lin ^ 1] + i * d.ld;
-  int pos = 0;
-  for (int b = 0; b < L; b += blockDim.x) {
-    const int q = b + threadIdx.x;
-    int c = -1;
-    bool keep = false;
-    if (q < L) {
-      c = src[q];
-      keep = gh_get(d, cur, i, c, 0).x >= 0;
-    }
-    int tot;
-    const int o = block_prefix(keep, tot, s_w);
-    if (keep) {
-      dst[pos + o] = c;
-      atomicOr(&stay[c >> 5], 1u << (c & 31));
-    }
-    pos += tot;
-  }
-  __syncthreads();
+  const int bo = d.lsel[g][i] ^ 1;
+  int32_t* dst = d.lord[bo] + i * d.ld;
+  int pos = compact(d, g, i, dst, stay, s_w, &s_self, [&](int c) { return gh_get(d, cur, i, c, 0).x >= 0; });
   const int target = d.cntl[i];
   int need = target - pos;
   if (need > 0) {
-    need = mark_added(d, cur, i, stay, app, s_w);
+    need = mark_added(d, cur, cur, i, stay, app, s_w);
     auto any = [](int) { return true; };
     if (src_ids)
-      append_from(src_ids, n_src, app, dst, pos, need, s_w, any);
+      append_from(src_ids, n_src, app, dst, pos, need, s_w, i, &s_self, any);
     else if (src_row >= 0)
-      append_from(d.lord[lin ^ 1] + (int64_t)src_row * d.ld, d.llen[lin ^ 1][src_row], app, dst, pos, need, s_w, any);
+      append_from(list_of(d, g ^ 1, src_row), d.llen[g ^ 1][src_row], app, dst, pos, need, s_w, i, &s_self, any);
   }
+  __syncthreads();
   if (threadIdx.x == 0) {
     if (pos != target) atomicExch(d.err, GH_EINVAL);
-    d.llen[lin ^ 1][i] = pos;
+    d.lsel[g ^ 1][i] = (uint8_t)bo;
+    d.llen[g ^ 1][i] = pos;
+    d.lself[g ^ 1][i] = s_self;
   }
 }
 
 // Rows [row0, row0 + nr) written whole: their lists in member-ID order (the
-// order a dense import implies), in list buffer lb.
-__global__ __launch_bounds__(256) void k_list_import(GhDev d, int cur, int lb, int64_t row0) {
+// order a dense import implies), in place in generation g.
+__global__ __launch_bounds__(256) void k_list_import(GhDev d, int cur, int g, int64_t row0) {
   __shared__ int s_w[4];
+  __shared__ int s_self;
   const int64_t i = row0 + blockIdx.x;
   if (i >= d.n) return;
-  int32_t* dst = d.lord[lb] + i * d.ld;
+  if (threadIdx.x == 0) s_self = -1;
+  __syncthreads();
+  int32_t* dst = d.lord[d.lsel[g][i]] + i * d.ld;
   int pos = 0;
   for (int64_t b = 0; b < d.n; b += blockDim.x) {
     const int64_t c = b + threadIdx.x;
     const bool pres = c < d.n && gh_get(d, cur, i, c, 0).x >= 0;
     int tot;
     const int o = block_prefix(pres, tot, s_w);
-    if (pres) dst[pos + o] = (int32_t)c;
+    if (pres) {
+      dst[pos + o] = (int32_t)c;
+      if (c == i) s_self = pos + o;
+    }
     pos += tot;
   }
-  if (threadIdx.x == 0) d.llen[lb][i] = pos;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    d.llen[g][i] = pos;
+    d.lself[g][i] = s_self;
+  }
 }
 
 // Ring mode in list order (slave/slave.go:512-524): per sender row, its
 // snapshot list = its list without the members REMOVE'd at it or detected by
 // it; idx = its own position there (-1 if absent), L = the length; targets
 // list[(idx-1) mod L], list[(idx+1) mod L], list[(idx+2) mod L], Go's
-// truncated % plus L for negatives.
-__global__ __launch_bounds__(256) void k_ring_list(GhDev d, int cur, int dcur, GhRound p, int lin) {
+// truncated % plus L for negatives. whole (flag counts current, no REMOVE
+// pending, no flagged segment anywhere): every snapshot is the whole list,
+// indexed directly.
+__global__ __launch_bounds__(256) void k_ring_list(GhDev d, int cur, int dcur, GhRound p, int g, int whole) {
   __shared__ int s_w[4];
   __shared__ int s_idx;
   __shared__ int s_tg[3];
   const int64_t s = blockIdx.x;
   if (s >= p.n) return;
   if (threadIdx.x < 3) s_tg[threadIdx.x] = -1;
-  if (threadIdx.x == 0) s_idx = -1;
+  whole = whole && d.cntg[p.n] == 0 && d.cntg[p.n + 1] == 0;
+  if (threadIdx.x == 0) s_idx = whole ? d.lself[g][s] : -1;
   __syncthreads();
   if (d.alive[s] && d.active[s]) {
-    const int L = d.llen[lin][s];
-    const int32_t* sl = d.lord[lin] + s * d.ld;
+    const int L = d.llen[g][s];
+    const int32_t* sl = list_of(d, g, s);
     auto in_snap = [&](int c) { return !gh_get(d, cur, s, c, 0).f && !removed_at(d, dcur, c, s); };
-    int len = 0;
-    for (int b = 0; b < L; b += blockDim.x) {
-      const int q = b + threadIdx.x;
-      const int c = q < L ? sl[q] : -1;
-      const bool in = c >= 0 && in_snap(c);
-      int tot;
-      const int o = block_prefix(in, tot, s_w);
-      if (in && c == s) s_idx = len + o;
-      len += tot;
+    int len = L;
+    if (!whole) {
+      len = 0;
+      for (int b = 0; b < L; b += blockDim.x) {
+        const int q = b + threadIdx.x;
+        const int c = q < L ? sl[q] : -1;
+        const bool in = c >= 0 && in_snap(c);
+        int tot;
+        const int o = block_prefix(in, tot, s_w);
+        if (in && c == s) s_idx = len + o;
+        len += tot;
+      }
     }
     __syncthreads();
     if (len == 0) {
@@ -319,17 +383,21 @@ __global__ __launch_bounds__(256) void k_ring_list(GhDev d, int cur, int dcur, G
         if (v < 0) v += len;
         want[q] = v;
       }
-      int at = 0;
-      for (int b = 0; b < L; b += blockDim.x) {
-        const int q = b + threadIdx.x;
-        const int c = q < L ? sl[q] : -1;
-        const bool in = c >= 0 && in_snap(c);
-        int tot;
-        const int o = block_prefix(in, tot, s_w);
-        if (in)
-          for (int x = 0; x < 3; ++x)
-            if (want[x] == at + o) s_tg[x] = c;
-        at += tot;
+      if (whole) {
+        if (threadIdx.x < 3) s_tg[threadIdx.x] = sl[want[threadIdx.x]];
+      } else {
+        int at = 0;
+        for (int b = 0; b < L; b += blockDim.x) {
+          const int q = b + threadIdx.x;
+          const int c = q < L ? sl[q] : -1;
+          const bool in = c >= 0 && in_snap(c);
+          int tot;
+          const int o = block_prefix(in, tot, s_w);
+          if (in)
+            for (int x = 0; x < 3; ++x)
+              if (want[x] == at + o) s_tg[x] = c;
+          at += tot;
+        }
       }
     }
   }
@@ -373,7 +441,7 @@ __device__ void clear_flag(const GhDev& d, int buf, int64_t i, int64_t c) {
 // each run of consecutive candidates of the list after REMOVE delivery, the
 // candidates at even offsets are detected, plus the list's last entry;
 // the others' flags are cleared.
-__global__ __launch_bounds__(256) void k_quirk_list(GhDev d, int cur, int dcur, GhRound p, int lin) {
+__global__ __launch_bounds__(256) void k_quirk_list(GhDev d, int cur, int dcur, GhRound p, int g) {
   __shared__ int s_w[4];
   __shared__ int s_f[256];
   __shared__ int s_last;
@@ -381,8 +449,8 @@ __global__ __launch_bounds__(256) void k_quirk_list(GhDev d, int cur, int dcur, 
   if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no flag anywhere
   if (i == 0 && threadIdx.x == 0) d.pvalid[cur] = 0;  // cleared flags: the sender plane is stale
   if (i >= p.n || !(d.alive[i] && d.active[i])) return;
-  const int L = d.llen[lin][i];
-  const int32_t* sl = d.lord[lin] + i * d.ld;
+  const int L = d.llen[g][i];
+  const int32_t* sl = list_of(d, g, i);
   if (threadIdx.x == 0) s_last = -1;
   __syncthreads();
   // the last list entry after REMOVE delivery
@@ -423,18 +491,18 @@ __global__ __launch_bounds__(256) void k_quirk_list(GhDev d, int cur, int dcur, 
 }
 
 // Member_list (master/master.go:46): the master row's list in list order.
-__global__ __launch_bounds__(256) void k_list_cand(GhDev d, int lin, int32_t master) {
-  const int L = d.llen[lin][master];
-  const int32_t* sl = d.lord[lin] + (int64_t)master * d.ld;
+__global__ __launch_bounds__(256) void k_list_cand(GhDev d, int g, int32_t master) {
+  const int L = d.llen[g][master];
+  const int32_t* sl = list_of(d, g, master);
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < L; q += gridDim.x * blockDim.x) d.cand[q] = sl[q];
   if (blockIdx.x == 0 && threadIdx.x == 0) d.ncand[0] = L;
 }
 
 // MemberList_i[0] in k_vote_scan's encoding: n - member, 0 for an empty list.
-__global__ __launch_bounds__(256) void k_list_first(GhDev d, int lin, int32_t* out) {
+__global__ __launch_bounds__(256) void k_list_first(GhDev d, int g, int32_t* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.n) return;
-  out[i] = d.llen[lin][i] > 0 ? d.n - d.lord[lin][i * d.ld] : 0;
+  out[i] = d.llen[g][i] > 0 ? d.n - list_of(d, g, i)[0] : 0;
 }
 
 size_t list_lds(const GhDev& d) { return sizeof(uint32_t) * 2 * (size_t)((d.n + 31) / 32); }
@@ -460,8 +528,8 @@ void launch_list_import(const GhDev& d, int cur, int lb, int64_t row0, int64_t n
   hipLaunchKernelGGL(k_list_import, dim3((unsigned)nr), dim3(256), 0, s, d, cur, lb, row0);
 }
 
-void launch_ring_list(const GhDev& d, int cur, int dcur, const GhRound& p, int lin, hipStream_t s) {
-  hipLaunchKernelGGL(k_ring_list, dim3(p.n), dim3(256), 0, s, d, cur, dcur, p, lin);
+void launch_ring_list(const GhDev& d, int cur, int dcur, const GhRound& p, int lin, int whole, hipStream_t s) {
+  hipLaunchKernelGGL(k_ring_list, dim3(p.n), dim3(256), 0, s, d, cur, dcur, p, lin, whole);
 }
 
 void launch_quirk_list(const GhDev& d, int cur, int dcur, const GhRound& p, int lin, hipStream_t s) {
