@@ -378,9 +378,13 @@ class Cluster:
     """The reference's per-node commands over one Engine (member IDs stand in
     for the VM addresses). Repairs follow Fail_recover: every row that detects
     a failure in round r triggers Update_metadata with its own list as
-    `available` at round r + repair_delay (slave/slave.go:1122-1133)."""
+    `available` at round r + repair_delay (slave/slave.go:1122-1133). Lists
+    keep the reference's append order (GH_ORDER_APPEND) unless list_order is
+    given: lsm, ring targets, quirk runs, MemberList[0] and the placement
+    candidates read them as the reference's slices do (SPEC D1)."""
 
     def __init__(self, n, repair_delay=8, addresses=None, elect=False, **cfg_kw):
+        cfg_kw.setdefault("list_order", GH_ORDER_APPEND)
         self.engine = Engine(default_config(n, **cfg_kw))
         self.n = n
         self.repair_delay = repair_delay
