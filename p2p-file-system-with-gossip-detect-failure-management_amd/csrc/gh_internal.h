@@ -504,6 +504,8 @@ struct GhRound {
   int32_t force_storm;  // diagnostics (GH_FORCE_STORM): run the storm variant every round
   int32_t force_slow;   // diagnostics (GH_FORCE_SLOW): every segment by the per-cell rule
   int32_t plane;        // the round writes the next buffer's sender plane (and may read cur's)
+  int32_t ring_whole;   // ring mode: one engine and a current flag count, so the targets may come
+                        // from whole lists when no REMOVE / flag is pending (k_ring_fast)
 };
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------

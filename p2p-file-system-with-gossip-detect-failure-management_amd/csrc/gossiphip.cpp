@@ -162,6 +162,7 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.force_storm = e->force_storm;
   p.force_slow = e->force_slow;
   p.plane = e->plane;
+  p.ring_whole = e->world == 1 && e->flags_known && !e->rowlay;
   return p;
 }
 

@@ -240,10 +240,73 @@ __device__ __forceinline__ uint32_t removed8(const GhDev& d, int dcur, int64_t l
   return out;
 }
 
+// Ring mode when every snapshot list is a whole list (a single engine, the
+// flag count current, no REMOVE pending and no flagged segment anywhere): the
+// list is the row's present members in ID order, so the targets are found by
+// scanning outward from the sender (one wave per sender row, 512 members per
+// step) instead of counting the row.
+__device__ __forceinline__ bool ring_whole(const GhDev& d, const GhRound& p) {
+  return p.ring_whole && d.cntg[p.n] == 0 && d.cntg[p.n + 1] == 0;
+}
+
+// First present member of row s after x (dir > 0) or before x (dir < 0),
+// cyclically; the row holds at least one present member. Wave-uniform.
+__device__ int ring_next(const GhDev& d, int cur, int s, int x, int dir) {
+  const int lane = threadIdx.x & 63;
+  const int nch = (d.n + 7) >> 3;
+  for (int pass = 0; pass < 2; ++pass) {
+    // pass 0: from x onward; pass 1: the wrap-around, from the far end
+    int c0 = pass == 0 ? x + dir : (dir > 0 ? 0 : d.n - 1);
+    for (;;) {
+      if (c0 < 0 || c0 >= d.n) break;
+      const int k0 = c0 >> 3;
+      const int k = dir > 0 ? k0 + lane : k0 - lane;
+      uint32_t m = 0;
+      if (k >= 0 && k < nch) {
+        m = gh_pf8(d, cur, s, (int64_t)k * 8) & 0xFFu;
+        if (k == k0) m &= dir > 0 ? (0xFFu << (c0 & 7)) & 0xFFu : 0xFFu >> (7 - (c0 & 7));
+      }
+      const unsigned long long hit = __ballot(m != 0);
+      if (hit) {
+        const int src = __ffsll((long long)hit) - 1;  // the nearest chunk
+        const int c = k * 8 + (dir > 0 ? __builtin_ctz(m ? m : 1u) : 31 - __builtin_clz(m ? m : 1u));
+        return __shfl(c, src);
+      }
+      c0 = dir > 0 ? (k0 + 64) * 8 : (k0 - 64) * 8 + 7;
+    }
+  }
+  return -1;
+}
+
+__global__ __launch_bounds__(256) void k_ring_fast(GhDev d, int cur, GhRound p) {
+  if (!ring_whole(d, p)) return;
+  const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s >= p.n) return;
+  int tg[3] = {-1, -1, -1};
+  if (d.alive[s] && d.active[s]) {
+    if (d.cntl[s] == 0) {
+      if ((threadIdx.x & 63) == 0) atomicAdd(&d.stats[ST_RING_EMPTY], 1ull);  // slave.go:517 division by zero
+    } else if (gh_pf8(d, cur, s, s & ~7) >> (s & 7) & 1u) {
+      // list[(idx-1) mod L], list[(idx+1) mod L], list[(idx+2) mod L]
+      tg[0] = ring_next(d, cur, s, s, -1);
+      tg[1] = ring_next(d, cur, s, s, 1);
+      tg[2] = ring_next(d, cur, s, tg[1], 1);
+    } else {
+      // idx = -1: list[L-2], list[0], list[1] (Go's % truncates, then + L)
+      const int last = ring_next(d, cur, s, d.n, -1);
+      tg[0] = ring_next(d, cur, s, last, -1);
+      tg[1] = ring_next(d, cur, s, -1, 1);
+      tg[2] = ring_next(d, cur, s, tg[1], 1);
+    }
+  }
+  if ((threadIdx.x & 63) < 3) d.targets[(int64_t)s * 3 + (threadIdx.x & 63)] = tg[threadIdx.x & 63];
+}
+
 // Ring mode, part 1: per (tile, sender row) the number of members in the
 // sender's snapshot list (present after REMOVE, not detected by it).
 template <int TW>
 __global__ __launch_bounds__(256) void k_ring_tiles(GhDev d, int cur, int dcur, GhRound p) {
+  if (ring_whole(d, p)) return;
   const SegWalk<TW> w(d, p);
   for (int64_t base = w.first; base < w.nseg; base += w.stride) {
     const int64_t sid = base + w.sub;
@@ -280,6 +343,7 @@ __device__ __forceinline__ int64_t ring_find(const GhDev& d, int cur, int dcur, 
 // Ring mode, part 2 (one thread per sender row): this shard's list length
 // and, when the sender's own column is local, its position in that list.
 __global__ __launch_bounds__(256) void k_ring_count(GhDev d, int cur, int dcur, GhRound p) {
+  if (ring_whole(d, p)) return;
   const int sdr = blockIdx.x * blockDim.x + threadIdx.x;
   if (sdr >= p.n) return;
   int32_t* out = d.ring + ((int64_t)d.rank * p.n + sdr) * 2;
@@ -318,6 +382,7 @@ __global__ __launch_bounds__(256) void k_ring_count(GhDev d, int cur, int dcur, 
 // into this shard's columns; the other shards' targets arrive by
 // allreduce(max).
 __global__ __launch_bounds__(256) void k_ring_select(GhDev d, int cur, int dcur, GhRound p) {
+  if (ring_whole(d, p)) return;  // k_ring_fast wrote the targets
   const int sdr = blockIdx.x * blockDim.x + threadIdx.x;
   if (sdr >= p.n) return;
   int32_t tg[3] = {-1, -1, -1};
@@ -1522,6 +1587,7 @@ void launch_negate(int32_t* x, int64_t n, hipStream_t s) {
 }
 
 void launch_ring_count(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  if (p.ring_whole) hipLaunchKernelGGL(k_ring_fast, dim3((p.n + 3) / 4), dim3(256), 0, s, d, cur, p);
   GH_TW_DISPATCH(ring_tiles, d, cur, dcur, p, s)
   hipLaunchKernelGGL(k_ring_count, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
 }

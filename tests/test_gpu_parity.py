@@ -415,3 +415,18 @@ def test_quiet_rows_after_collapse(gs, oracle_mod):
         if r % 4 == 0 or r in (51, 52, 53):
             compare(eng, orc, r)
     assert max(quiet) > 0, quiet
+
+
+@pytest.mark.parametrize("n", [9, 1500])
+def test_ring_whole_lists(gs, oracle_mod, n):
+    """Ring mode with long timeouts: most rounds have no flag and no REMOVE,
+    so every sender's targets come from its whole list by the outward scan
+    (k_ring_fast); a crash wave, leaves and re-joins (own member absent from
+    a list, short lists, the wrap-around) switch rounds back to the counting
+    path. Bit-exact against the oracle every round."""
+    crash = sc.crash_ids(n, 0.2, 0x5EED0A00)
+    sched = {4: [(sc.CRASH, c) for c in crash],
+             30: [(sc.LEAVE, (n // 2) | 1)],
+             36: [(sc.JOIN, c) for c in crash[: max(1, len(crash) // 2)]]}
+    run_parity(gs, oracle_mod, dict(peer_mode=1, seed=0x5EED0A01 + n, t_fail=20, t_cleanup=20), n, 50, sched,
+               init=sc.full_state(n))
