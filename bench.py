@@ -89,7 +89,7 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(n, k, world, warmup, plane, tw):
+def pmc_traffic(n, k, world, warmup, plane, tw, cell_bytes):
     """Fabric-side bytes per k_round launch from the committed PMC summary of
     the same configuration, layout (sender plane, tile width) and steady state
     (tools/pmc.sh -> profiles/*k_round_pmc*.json, warm-up >= 5 rounds)."""
@@ -100,7 +100,7 @@ def pmc_traffic(n, k, world, warmup, plane, tw):
         except (OSError, ValueError):
             continue
         c = d.get("config", {})
-        if (c.get("n") == n and c.get("k") == k and c.get("world", 1) == world and c.get("cell_bytes", 4) == 2
+        if (c.get("n") == n and c.get("k") == k and c.get("world", 1) == world and c.get("cell_bytes", 4) == cell_bytes
                 and c.get("warmup", 0) >= min(5, warmup) and "traffic_bytes" in d
                 and c.get("plane", 0) == plane and c.get("tile_width", 64) == tw):
             best = {"traffic_bytes": d["traffic_bytes"], "source": f"profiles/{f.name}",
@@ -380,6 +380,8 @@ def main():
     # rows, every column)
     nrows_r = -(-n // world) if args.layout == "rows" else n
     plane = eng.plane_info()[0]
+    tier8 = eng.tier_info()[0]  # steady-state cells stream at 1 B (escapes: the 16-bit table)
+    cell_bytes = 1 if tier8 else 2
     tile_w = int(os.environ.get("GH_TILE_W", "256" if plane else "64"))
     eng.init_full(2, 0, 0)
     if args.warmup:
@@ -407,6 +409,7 @@ def main():
     eng.set_timing(False)
     exch = eng.exchange_info() if args.layout == "rows" else None
     plane_fb = eng.plane_info()[2]
+    tier_last = eng.tier_info()
     placement = None
     if world == 1 and args.files > 0:
         progress("placement and election legs")
@@ -420,10 +423,11 @@ def main():
         return
     value = args.steps / elapsed
     # bytes of one k_round launch (this rank's columns)
-    b_compulsory = 4.0 * nrows_r * ncols       # each 2-byte narrow cell read once and written once
+    b_compulsory = 2.0 * cell_bytes * nrows_r * ncols  # each cell read once and written once
     b_gather = 2.0 * nrows_r * ncols * k       # the k sender segments per cell (L2 / Infinity Cache / HBM)
     b_survey = 4.0 * nrows_r * ncols * (k + 4)  # SURVEY.md §8d (int32 hb + ts streams)
-    traffic = pmc_traffic(n, k, world, args.warmup, plane, tile_w)
+    traffic = pmc_traffic(n, k, world, args.warmup, plane, tile_w, cell_bytes)
+    tier_cur, tier_esc = tier_last[1], tier_last[2]
     avg_s = (kern_ms / 1e3) / max(launches, 1)
     achieved = b_compulsory / avg_s / 1e9
     line = {
@@ -437,7 +441,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "int16",
+        "dtype": "u8" if tier8 else "int16",
         "data": "synthetic",
         "config": {
             "workload": f"BASELINE config 3: N={n} members, "
@@ -458,7 +462,9 @@ def main():
             "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic["traffic_bytes"] if traffic else None,
             "traffic_source": traffic["source"] if traffic else None,
-            "bytes_per_launch": b_compulsory, "bytes_model": "compulsory: 4*N*ncols (2-byte cells read + written once)",
+            "bytes_per_launch": b_compulsory,
+            "bytes_model": (f"compulsory: {2 * cell_bytes}*N*ncols ({cell_bytes}-byte cells read + written once"
+                            + (": the 8-bit tier, escaped chunks in 16 bits)" if tier8 else ")")),
             "avg_launch_ms": avg_s * 1e3, "launches": launches,
             "gather_bytes_per_launch": b_gather, "gather_achieved": b_gather / avg_s / 1e9,
             "survey_bytes_per_launch": b_survey,
@@ -475,7 +481,8 @@ def main():
                    "wide_slots_used": mem["wide_used"]},
         "exchange": exch,
         "layout": {"tile_width": tile_w, "sender_plane": bool(plane), "shards": args.layout,
-                   "plane_fallback_waves_last_round": plane_fb},
+                   "plane_fallback_waves_last_round": plane_fb, "tier8": bool(tier8),
+                   "tier8_current": bool(tier_cur), "tier8_escaped_chunks_last_round": tier_esc},
         "secondary": secondary,
         "placement": placement,
     }

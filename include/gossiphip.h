@@ -284,6 +284,12 @@ int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, in
  * 16-bit sender codes although the plane was valid (a sender code outside
  * the plane's window). Any output may be NULL. No reference counterpart. */
 int gh_plane_info(void* h, int32_t* enabled, int32_t* valid, int64_t* fallback_waves);
+/* 8-bit tier (diagnostic; DESIGN.md "8-bit tier"): whether the engine keeps
+ * one (plane mode, column layout; GH_C8=0 drops it), whether the current
+ * table is held in it (8-bit chunks, escaped chunks in 16 bits), and how many
+ * chunks the last round's packed path wrote escaped. Any output may be NULL.
+ * No reference counterpart. */
+int gh_tier_info(void* h, int32_t* enabled, int32_t* current_8bit, int64_t* escaped_chunks);
 /* Row layout (GH_LAYOUT_ROWS): the last ghost-row exchange of this shard --
  * the sender rows it received, and the bytes it sent and received by
  * alltoallv (narrow codes, plane words, wide segments). Zero in the column

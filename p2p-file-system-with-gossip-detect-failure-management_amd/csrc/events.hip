@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void k_seg(GhDev d, int buf, SegSet set, const
     GhCell v[8];
     uint4 x = {0u, 0u, 0u, 0u}, nx = {0u, 0u, 0u, 0u};
     if (valid) {
-      x = *reinterpret_cast<const uint4*>(d.hn[buf] + gh_cell(d, i, c));
+      x = gh_ld16(d, buf, gh_cell(d, i, c));
       gh_dec8(d, buf, i, c, p.r, x, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -263,6 +263,10 @@ __global__ __launch_bounds__(256) void k_freeze_mark(GhDev d, const int32_t* row
     const int64_t off = gh_cell(d, rows[idx / cpr], (idx % cpr) * 8);
     *reinterpret_cast<uint4*>(d.hn[0] + off) = uint4{m, m, m, m};
     *reinterpret_cast<uint4*>(d.hn[1] + off) = uint4{m, m, m, m};
+    if (d.h8[0]) {  // a stopped row's chunks are escaped in both tiers' buffers at all times
+      *reinterpret_cast<uint2*>(d.h8[0] + off) = GH_C8_ESC2;
+      *reinterpret_cast<uint2*>(d.h8[1] + off) = GH_C8_ESC2;
+    }
   }
 }
 
@@ -294,7 +298,7 @@ __global__ __launch_bounds__(256) void k_count_wide(GhDev d, int buf, unsigned l
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = idx / d.nrows, i = idx - t * d.nrows;
-    const uint32_t h = d.hn[buf][t * d.tstride + i * d.tw];
+    const uint32_t h = gh_ld16(d, buf, t * d.tstride + i * d.tw).x & 0xFFFFu;
     cw += h == GH_N_WIDE;
     cf += h == GH_N_FROZEN;
   }

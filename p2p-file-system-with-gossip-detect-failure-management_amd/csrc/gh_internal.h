@@ -82,6 +82,24 @@
 //                  16-bit gathers when a min is 0 or 14. pvalid[b] = 0 once
 //                  anything but a round wrote buffer b (events, imports, list
 //                  merges, the quirk pre-pass).
+//   h8[2]  uint8   8-BIT TIER beside each narrow buffer (c8 engines: plane
+//                  mode, column layout), one byte per cell in the narrow
+//                  table's tiled order. While m8[b] = 1 the 8-cell chunk at
+//                  cell c8 of buffer b is h8[b][c8..c8+7] unless its byte 0 is
+//                  GH_C8_ESC, in which case it is hn[b]'s chunk (escaped); a
+//                  byte holds
+//                    l << 4 | age   visible (present, unflagged), offset =
+//                                   GH_C8_REF - l, l 0..14, age 0..15
+//                    0xFF           absent
+//                  so the steady state streams 1 B per cell, and anything
+//                  else (flags, tombstones, wide and frozen markers, lags or
+//                  ages past the window) keeps its 16-bit chunk. m8[b] = 0:
+//                  hn[b] alone holds the buffer (h8[b] is ignored, except
+//                  that stopped rows' chunks are GH_C8_ESC in both buffers at
+//                  all times). The round that writes buffer b picks its tier
+//                  (k_base: the lean variant writes 8-bit chunks); every
+//                  other reader and writer goes through gh_ld16 / gh_put8 /
+//                  gh_st16, which follow m8.
 //   tsat = T_cleanup < 30: a tombstone's age is only ever compared with
 //            T_cleanup (cleanFailList, slave/slave.go:490), so every age
 //            past 30 decides the same; narrow tombstones saturate at 30 and
@@ -115,6 +133,9 @@
 #define GH_P_UNK 0u                        // plane: unknown (read the narrow table)
 #define GH_P_OLD 14u                       // plane: visible, offset below GH_P_REF - 12
 #define GH_P_NONE 15u                      // plane: not in the snapshot
+#define GH_C8_REF (GH_BASE_LAG + 1)        // 8-bit tier: offset of lag l = 0 (an active member's own cell)
+#define GH_C8_ESC 0xF0u                    // 8-bit tier: byte 0 of an escaped chunk (its codes are in hn)
+#define GH_C8_ABSENT 0xFFu                 // 8-bit tier: absent
 #define GH_PAD 256               // column padding granule (ld % 256 == 0)
 #ifndef GH_WG_CELLS
 #define GH_WG_CELLS 16384        // round kernel: cells per workgroup tile (rows = GH_WG_CELLS / TW)
@@ -185,6 +206,8 @@ struct GhDev {
   int32_t *rslot;   // row layout: [n] table slot of a global row, -1 = not held
   int32_t *pvf;     // row layout: [n][k] validity of each receiver's draws (summed over shards)
   uint16_t *hn[2];  // narrow double buffer
+  uint8_t *h8[2];   // 8-bit tier per buffer (null: tier off)
+  int32_t *m8;      // [0..1] buffer b is in the 8-bit tier; [2] this round switches the next buffer's tier
   uint32_t *pl[2];  // sender snapshot plane per buffer (null: plane off)
   int32_t *pvalid;  // [2]: plane of buffer b written by the round that wrote b
   int32_t *pfb;     // waves of the last round that gathered 16-bit codes with a valid plane
@@ -284,6 +307,105 @@ __host__ __device__ __forceinline__ int64_t gh_wcell(const GhDev& d, int64_t s, 
   return (s << d.lgtw) + (c & (d.tw - 1));
 }
 
+// ---- packed 16-bit (two narrow cells per dword) ------------------------
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 as_s(uint32_t x) { return __builtin_bit_cast(s16x2, x); }
+__device__ __forceinline__ u16x2 as_us(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t as_u(s16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t as_u(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
+  return as_u(__builtin_elementwise_max(as_s(a), as_s(b)));
+}
+__device__ __forceinline__ uint32_t pk_subs_i16(uint32_t a, uint32_t b) {  // saturating a - b
+  return as_u(__builtin_elementwise_sub_sat(as_s(a), as_s(b)));
+}
+__device__ __forceinline__ uint32_t pk_adds_u16(uint32_t a, uint32_t b) {  // saturating a + b
+  return as_u(__builtin_elementwise_add_sat(as_us(a), as_us(b)));
+}
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) { return as_u(as_us(a) + as_us(b)); }
+__device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) { return as_u(as_us(a) - as_us(b)); }
+// 0xFFFF per negative half. Opaque to the compiler: as a plain shift its
+// result feeds selects that get rewritten into per-half compares and
+// v_cndmask (7 instructions where and/or take 2).
+__device__ __forceinline__ uint32_t pk_sra15(uint32_t a) {
+  uint32_t r;
+  asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(r) : "v"(a));  // both halves by 15
+  return r;
+}
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+  return as_u(__builtin_elementwise_min(as_us(a), as_us(b)));
+}
+// 0xFFFF in each half that is zero
+__device__ __forceinline__ uint32_t pk_zero_mask(uint32_t a) {
+  return pk_sub_u16(pk_min_u16(a, 0x00010001u), 0x00010001u);
+}
+__device__ __forceinline__ uint32_t pk_lshr16(uint32_t a, int k) { return as_u(as_us(a) >> (unsigned short)k); }
+__device__ __forceinline__ uint32_t pk_shl16(uint32_t a, int k) { return as_u(as_us(a) << (unsigned short)k); }
+
+// ---- 8-bit tier (h8) -------------------------------------------------------
+// 16-bit codes of two 8-bit codes t (bytes in bits 0-7 and 16-23):
+// offset GH_C8_REF - l, age; 0xFF -> absent.
+__device__ __forceinline__ uint32_t c8_pair(uint32_t t) {
+  const uint32_t code = ((uint32_t)(GH_C8_REF << 5) * 0x10001u - ((t & 0x00F000F0u) << 1)) | (t & 0x000F000Fu);
+  const uint32_t ab = ((t + 0x00010001u) >> 8) & 0x00010001u;  // 1 per 0xFF half
+  return code | pk_sub_u16(0u, ab);
+}
+// the 16-bit codes of an 8-bit chunk (not escaped)
+__device__ __forceinline__ v4u c8_dec(uint2 b) {
+  return v4u{c8_pair(__builtin_amdgcn_perm(0u, b.x, 0x0C010C00u)), c8_pair(__builtin_amdgcn_perm(0u, b.x, 0x0C030C02u)),
+             c8_pair(__builtin_amdgcn_perm(0u, b.y, 0x0C010C00u)), c8_pair(__builtin_amdgcn_perm(0u, b.y, 0x0C030C02u))};
+}
+// 8-bit codes of two 16-bit codes y (one per half: bytes 0 and 2); bit 15 /
+// 31 of bad set for a half with no 8-bit code (flagged, tombstone, marker,
+// lag past 14, offset above GH_C8_REF, age past 15)
+__device__ __forceinline__ uint32_t c8_enc_pair(uint32_t y, uint32_t& bad) {
+  const uint32_t ab = pk_zero_mask(pk_add_u16(y, 0x00010001u));         // absent halves
+  const uint32_t L = pk_sub_u16((uint32_t)GH_C8_REF * 0x10001u, pk_lshr16(y, 5));
+  bad |= (y | pk_adds_u16(L, 0x7FF17FF1u) | (y << 11)) & ~ab & 0x80008000u;
+  // (L masked first: an absent or escaped half's L must not shift into the
+  // other half's byte)
+  return (((L & 0x000F000Fu) << 4) | (y & 0x000F000Fu) | ab) & 0x00FF00FFu;
+}
+// the 8-bit chunk of 16-bit codes o; bad != 0 when one has no 8-bit code
+__device__ __forceinline__ uint2 c8_enc(const v4u& o, uint32_t& bad) {
+  const uint32_t p0 = c8_enc_pair(o[0], bad), p1 = c8_enc_pair(o[1], bad);
+  const uint32_t p2 = c8_enc_pair(o[2], bad), p3 = c8_enc_pair(o[3], bad);
+  return uint2{__builtin_amdgcn_perm(p1, p0, 0x06040200u), __builtin_amdgcn_perm(p3, p2, 0x06040200u)};
+}
+#define GH_C8_ESC2 uint2{0xF0F0F0F0u, 0xF0F0F0F0u}
+
+// buffer buf is in the 8-bit tier
+__device__ __forceinline__ bool gh_m8(const GhDev& d, int buf) { return d.h8[0] != nullptr && d.m8[buf] != 0; }
+// The 16-bit chunk at cell index `cell` (cell % 8 == 0) of buffer buf: its
+// 8-bit codes widened, or hn's chunk when escaped or the buffer is 16-bit.
+__device__ __forceinline__ uint4 gh_ld16(const GhDev& d, int buf, int64_t cell) {
+  if (gh_m8(d, buf)) {
+    const uint2 b = *reinterpret_cast<const uint2*>(d.h8[buf] + cell);
+    if ((b.x & 0xFFu) != GH_C8_ESC) {
+      const v4u w = c8_dec(b);
+      return uint4{w[0], w[1], w[2], w[3]};
+    }
+  }
+  return *reinterpret_cast<const uint4*>(d.hn[buf] + cell);
+}
+// Stores a 16-bit chunk (narrow codes or a marker) at cell `cell` of buffer
+// buf: in the 8-bit tier as 8-bit codes when every cell has one (c8 =
+// allowed), else escaped.
+__device__ __forceinline__ void gh_st16(const GhDev& d, int buf, int64_t cell, const uint4& x, bool c8 = true) {
+  if (gh_m8(d, buf)) {
+    uint32_t bad = 0;
+    const uint2 b = c8_enc(v4u{x.x, x.y, x.z, x.w}, bad);
+    if (c8 && bad == 0) {
+      *reinterpret_cast<uint2*>(d.h8[buf] + cell) = b;
+      return;
+    }
+    *reinterpret_cast<uint2*>(d.h8[buf] + cell) = GH_C8_ESC2;
+  }
+  *reinterpret_cast<uint4*>(d.hn[buf] + cell) = x;
+}
+
 // ---- narrow codes ---------------------------------------------------------
 // Decodes a narrow (non-marker) code of a column with base b in a buffer for
 // round r.
@@ -356,15 +478,14 @@ __device__ __forceinline__ void gh_dec8(const GhDev& d, int buf, int64_t i, int6
   }
 }
 __device__ __forceinline__ void gh_get8(const GhDev& d, int buf, int64_t i, int64_t c, int32_t r, GhCell out[8]) {
-  const uint4 x = *reinterpret_cast<const uint4*>(d.hn[buf] + gh_cell(d, i, c));
+  const uint4 x = gh_ld16(d, buf, gh_cell(d, i, c));
   gh_dec8(d, buf, i, c, r, x, out);
 }
 
 // Cell (i, local c) of buffer buf (for round r).
 __device__ __forceinline__ GhCell gh_get(const GhDev& d, int buf, int64_t i, int64_t c, int32_t r) {
   const int64_t c8 = c & ~(int64_t)7;
-  const uint16_t* np = d.hn[buf] + gh_cell(d, i, c8);
-  const uint2 hd = *reinterpret_cast<const uint2*>(np);
+  const uint4 hd = gh_ld16(d, buf, gh_cell(d, i, c8));
   const uint32_t h0 = hd.x & 0xFFFFu;
   if (h0 == GH_N_WIDE) {
     if (gh_wide_slot(hd.x, hd.y) >= d.wcap) return gh_absent();
@@ -378,14 +499,15 @@ __device__ __forceinline__ GhCell gh_get(const GhDev& d, int buf, int64_t i, int
     const int32_t x = d.fzh[w];
     return GhCell{x, x == GH_ABSENT ? 0 : d.fzt[w], false};
   }
-  return gh_dec16(np[c & 7], d.base[buf][c], r);
+  const uint32_t hw[4] = {hd.x, hd.y, hd.z, hd.w};
+  return gh_dec16((hw[(c & 7) >> 1] >> (16 * (c & 1))) & 0xFFFFu, d.base[buf][c], r);
 }
 
 // Presence and flag bits of cells (i, c..c+7) of buffer buf (c % 8 == 0):
 // bit j = present, bit 8 + j = present and flagged. Narrow codes answer
 // directly (no base, no round).
 __device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, int64_t c) {
-  const uint4 x = *reinterpret_cast<const uint4*>(d.hn[buf] + gh_cell(d, i, c));
+  const uint4 x = gh_ld16(d, buf, gh_cell(d, i, c));
   const uint32_t h0 = x.x & 0xFFFFu;
   uint32_t out = 0;
   if (h0 == GH_N_WIDE || h0 == GH_N_FROZEN) {
@@ -407,7 +529,10 @@ __device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, i
 // Clears the flag of present cells (i, c + j) for the bits j of m (c % 8 == 0).
 // A stopped row has no flags.
 __device__ __forceinline__ void gh_clearflags8(const GhDev& d, int buf, int64_t i, int64_t c, uint32_t m) {
-  uint4* np = reinterpret_cast<uint4*>(d.hn[buf] + gh_cell(d, i, c));
+  const int64_t cell = gh_cell(d, i, c);
+  // an 8-bit chunk holds no flag; an escaped one is hn's
+  if (gh_m8(d, buf) && (d.h8[buf][cell] != GH_C8_ESC)) return;
+  uint4* np = reinterpret_cast<uint4*>(d.hn[buf] + cell);
   uint4 x = *np;
   const uint32_t h0 = x.x & 0xFFFFu;
   if (h0 == GH_N_FROZEN) return;
@@ -429,11 +554,13 @@ __device__ __forceinline__ void gh_clearflags8(const GhDev& d, int buf, int64_t 
 // else the cells into arena slot `slot` and the chunk's marker.
 __device__ __forceinline__ void gh_put8(const GhDev& d, int buf, int64_t i, int64_t c, bool narrow, const uint4& nx,
                                         int64_t slot, const GhCell v[8]) {
-  uint4* np = reinterpret_cast<uint4*>(d.hn[buf] + gh_cell(d, i, c));
+  const int64_t cell = gh_cell(d, i, c);
   if (narrow) {
-    *np = nx;
+    gh_st16(d, buf, cell, nx);
     return;
   }
+  if (gh_m8(d, buf)) *reinterpret_cast<uint2*>(d.h8[buf] + cell) = GH_C8_ESC2;
+  uint4* np = reinterpret_cast<uint4*>(d.hn[buf] + cell);
   const int64_t w = gh_wcell(d, slot, c);
   *reinterpret_cast<int4*>(d.wh[buf] + w) = int4{v[0].x, v[1].x, v[2].x, v[3].x};
   *reinterpret_cast<int4*>(d.wh[buf] + w + 4) = int4{v[4].x, v[5].x, v[6].x, v[7].x};
@@ -522,9 +649,10 @@ void launch_ring_count(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
 void launch_ring_select(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
 // nt = non-temporal hints on the once-touched streams of k_round
-// storm: the storm variant (else the lean one); both are launched every
-// round and only the one k_base selected runs
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm);
+// variant: 0 the lean one on a 16-bit input, 1 the storm one, 2 the lean one
+// on an 8-bit input (tiered engines); all are launched every round and only
+// the one k_base and the input's tier select runs
+void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant);
 // the segments k_round listed, by the per-cell rule (after launch_round)
 void launch_round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);

@@ -70,6 +70,7 @@ struct Engine {
   int64_t gidx_cap = 0;
   int64_t gx_rows = 0, gx_out = 0, gx_in = 0;  // the last exchange: ghost rows, bytes sent / received
   int plane = 0;         // sender snapshot plane (pull mode, 3 <= k <= 4, N >= GH_PLANE_MIN_N; GH_PLANE=0/1)
+  int c8 = 0;            // 8-bit tier (plane mode, column layout; GH_C8=0 drops it)
   // GH_ORDER_APPEND: per-row list order kept beside the table (order.hip);
   // lcur = the list buffer of the current state
   bool lorder = false;
@@ -737,6 +738,11 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
     return GH_EINVAL;
   }
   if (e->tpw != 1 && e->tpw != 2 && e->tpw != 4 && e->tpw != 8) e->tpw = 1;
+  // the 8-bit tier streams the steady state the plane serves at 1 B per cell
+  // (its window is the plane's: lags of healthy pull dissemination); the row
+  // layout ships 16-bit ghost rows
+  e->c8 = e->plane && cfg->shard_layout == GH_LAYOUT_COLUMNS && e->tpw == 1;
+  if (const char* v = std::getenv("GH_C8")) e->c8 = e->c8 && std::atoi(v) != 0;
   if (cfg->shard_layout != GH_LAYOUT_COLUMNS &&
       (cfg->shard_layout != GH_LAYOUT_ROWS || cfg->peer_mode != GH_PEER_PULL)) {
     delete e;  // the row layout is the pull-mode path (ring targets need every sender's list order)
@@ -821,6 +827,11 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.nquiet, 1, 0)))
       break;
     if (e->plane && ((rc = dalloc(e, &d.pl[0], cells / 8, 0xFF)) || (rc = dalloc(e, &d.pl[1], cells / 8, 0xFF))))
+      break;
+    // 8-bit tier: every chunk escaped, both buffers 16-bit until a round
+    // writes one
+    if ((rc = dalloc(e, &d.m8, 4, 0))) break;
+    if (e->c8 && ((rc = dalloc(e, &d.h8[0], cells, GH_C8_ESC)) || (rc = dalloc(e, &d.h8[1], cells, GH_C8_ESC))))
       break;
     if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
         (rc = dalloc(e, &d.det_any, e->n, 0)) || (rc = dalloc(e, &d.und, e->n, 0)) ||
@@ -1005,6 +1016,7 @@ int encode_rows(Engine* e, const char* what, F launch) {
 int clear_table(Engine* e) {
   GhDev& d = e->d;
   HIPCHK(e, hipMemsetAsync(d.hn[e->cur], 0xFF, sizeof(uint16_t) * (size_t)d.nslots * e->ld, e->stream));
+  HIPCHK(e, hipMemsetAsync(d.m8 + e->cur, 0, sizeof(int32_t), e->stream));  // hn alone holds it
   HIPCHK(e, hipMemsetAsync(d.wn + e->cur, 0, sizeof(int32_t), e->stream));
   HIPCHK(e, hipMemsetAsync(d.err, 0, sizeof(int32_t), e->stream));
   e->lost.clear();
@@ -1136,6 +1148,19 @@ int gh_plane_info(void* h, int32_t* enabled, int32_t* valid, int64_t* fallback_w
   return GH_OK;
 }
 
+int gh_tier_info(void* h, int32_t* enabled, int32_t* current_8bit, int64_t* escaped_chunks) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  int32_t v[4] = {0, 0, 0, 0};
+  HIPCHK(e, hipMemcpyAsync(v, e->d.m8, sizeof v, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (enabled) *enabled = e->c8;
+  if (current_8bit) *current_8bit = e->c8 ? v[e->cur] : 0;
+  if (escaped_chunks) *escaped_chunks = e->c8 ? v[3] : 0;
+  return GH_OK;
+}
+
 int gh_exchange_info(void* h, int64_t* ghost_rows, int64_t* bytes_out, int64_t* bytes_in) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
@@ -1158,7 +1183,7 @@ int gh_memory_info(void* h, int64_t* device_bytes, int64_t* wide_used, int64_t* 
     // per-column vectors and the file table are counted by hipMemGetInfo
     // callers, not here
     const int64_t cells = d.nslots * e->ld;
-    *device_bytes = 2 * cells * 2 + (e->plane ? cells : 0) + 2 * d.wcap * ((int64_t)d.tw * 8 + d.tw / 8) +
+    *device_bytes = 2 * cells * 2 + (e->plane ? cells : 0) + (e->c8 ? 2 * cells : 0) + 2 * d.wcap * ((int64_t)d.tw * 8 + d.tw / 8) +
                     e->fzcap * e->ld * 8 + (e->lorder ? 2 * (int64_t)e->n * e->ld * 4 : 0);
   }
   if (wide_used) *wide_used = std::min<int64_t>(used, d.wcap);
@@ -1279,8 +1304,8 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   bool busy = false;
   if ((rc0 = check_lost(e)) || (rc0 = maybe_grow(e, &busy))) return rc0;
   HIPCHK(e, hipMemsetAsync(e->d.stats, 0, sizeof(unsigned long long) * ST_COUNT, e->stream));
-  if (e->timing && (int64_t)e->evs.size() < 3 * (int64_t)rounds) {
-    while ((int64_t)e->evs.size() < 3 * (int64_t)rounds) {
+  if (e->timing && (int64_t)e->evs.size() < 4 * (int64_t)rounds) {
+    while ((int64_t)e->evs.size() < 4 * (int64_t)rounds) {
       hipEvent_t ev;
       HIPCHK(e, hipEventCreate(&ev));
       e->evs.push_back(ev);
@@ -1330,12 +1355,14 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       e->qforce = false;
     }
     if ((rc = build_inboxes(e, p))) return rc;
-    // the two variants of k_round; the one not selected returns at once
-    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[3 * q], e->stream));
-    launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt, false);
-    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[3 * q + 1], e->stream));
-    launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt, true);
-    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[3 * q + 2], e->stream));
+    // the variants of k_round; the ones not selected return at once
+    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[4 * q], e->stream));
+    launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt, 0);
+    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[4 * q + 1], e->stream));
+    if (e->c8) launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt, 2);
+    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[4 * q + 2], e->stream));
+    launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt, 1);
+    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[4 * q + 3], e->stream));
     launch_round_slow(e->d, e->cur, e->dcur, p, e->stream);
     if (e->rowlay && e->world > 1) {
       // every shard detected in its own rows: D_r's counts and first
@@ -1382,11 +1409,12 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   }
   if (e->timing) {
     for (int32_t q = 0; q < done; ++q) {
-      float ms = 0.f;
-      float ms2 = 0.f;  // the variant that ran
-      HIPCHK(e, hipEventElapsedTime(&ms, e->evs[3 * q], e->evs[3 * q + 1]));
-      HIPCHK(e, hipEventElapsedTime(&ms2, e->evs[3 * q + 1], e->evs[3 * q + 2]));
-      ms = std::max(ms, ms2);
+      float ms = 0.f;  // the variant that ran
+      for (int v = 0; v < 3; ++v) {
+        float mv = 0.f;
+        HIPCHK(e, hipEventElapsedTime(&mv, e->evs[4 * q + v], e->evs[4 * q + v + 1]));
+        ms = std::max(ms, mv);
+      }
       e->timed_ms += ms;
       e->timed_launches++;
     }
@@ -1758,7 +1786,19 @@ int gh_debug_raw(void* h, int32_t row, int64_t c0, int64_t n, uint16_t* codes, i
   for (int64_t c = c0; c < c0 + n; ++c) {
     const int64_t slot = e->rowlay ? e->rslot_h[row] : row;
     if (slot < 0) return set_err(e, GH_EINVAL, "row not held by this shard");
-    HIPCHK(e, hipMemcpy(codes + (c - c0), e->d.hn[e->cur] + gh_cell_slot(e->d, slot, c), 2, hipMemcpyDeviceToHost));
+    const int64_t cell = gh_cell_slot(e->d, slot, c);
+    int32_t m8 = 0;
+    uint8_t b8[8] = {0};
+    if (e->c8) {
+      HIPCHK(e, hipMemcpy(&m8, e->d.m8 + e->cur, 4, hipMemcpyDeviceToHost));
+      HIPCHK(e, hipMemcpy(b8, e->d.h8[e->cur] + (cell & ~(int64_t)7), 8, hipMemcpyDeviceToHost));
+    }
+    if (m8 && b8[0] != GH_C8_ESC) {  // the 16-bit code of an 8-bit one
+      const uint32_t b = b8[c & 7];
+      codes[c - c0] = b == GH_C8_ABSENT ? (uint16_t)GH_N_ABSENT : (uint16_t)(((GH_C8_REF - (b >> 4)) << 5) | (b & 15));
+    } else {
+      HIPCHK(e, hipMemcpy(codes + (c - c0), e->d.hn[e->cur] + cell, 2, hipMemcpyDeviceToHost));
+    }
     HIPCHK(e, hipMemcpy(bases + (c - c0), e->d.base[e->cur] + c, 4, hipMemcpyDeviceToHost));
   }
   return GH_OK;

@@ -419,6 +419,8 @@ __device__ __forceinline__ int run_apply(int f, int s) { return (f & 1) ? ((f >>
 __device__ void clear_flag(const GhDev& d, int buf, int64_t i, int64_t c) {
   const int64_t c8 = c & ~(int64_t)7;
   const int64_t cell0 = gh_cell(d, i, c8);
+  // an 8-bit chunk holds no flag; an escaped one is hn's
+  if (gh_m8(d, buf) && d.h8[buf][cell0] != GH_C8_ESC) return;
   const uint2 hd = *reinterpret_cast<const uint2*>(d.hn[buf] + cell0);
   const uint32_t h0 = hd.x & 0xFFFFu;
   if (h0 == GH_N_FROZEN) return;

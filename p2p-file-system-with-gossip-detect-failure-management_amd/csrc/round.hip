@@ -494,48 +494,12 @@ __global__ __launch_bounds__(256) void k_inbox_fill(GhDev d, GhRound p) {
   }
 }
 
-// ---- packed 16-bit (two narrow cells per dword) ------------------------
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-typedef short s16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ s16x2 as_s(uint32_t x) { return __builtin_bit_cast(s16x2, x); }
-__device__ __forceinline__ u16x2 as_us(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
-__device__ __forceinline__ uint32_t as_u(s16x2 x) { return __builtin_bit_cast(uint32_t, x); }
-__device__ __forceinline__ uint32_t as_u(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
-__device__ __forceinline__ uint32_t pk_max_i16(uint32_t a, uint32_t b) {
-  return as_u(__builtin_elementwise_max(as_s(a), as_s(b)));
-}
-__device__ __forceinline__ uint32_t pk_subs_i16(uint32_t a, uint32_t b) {  // saturating a - b
-  return as_u(__builtin_elementwise_sub_sat(as_s(a), as_s(b)));
-}
-__device__ __forceinline__ uint32_t pk_adds_u16(uint32_t a, uint32_t b) {  // saturating a + b
-  return as_u(__builtin_elementwise_add_sat(as_us(a), as_us(b)));
-}
-__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b) { return as_u(as_us(a) + as_us(b)); }
-__device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) { return as_u(as_us(a) - as_us(b)); }
-// 0xFFFF per negative half. Opaque to the compiler: as a plain shift its
-// result feeds selects that get rewritten into per-half compares and
-// v_cndmask (7 instructions where and/or take 2).
-__device__ __forceinline__ uint32_t pk_sra15(uint32_t a) {
-  uint32_t r;
-  asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(r) : "v"(a));  // both halves by 15
-  return r;
-}
-__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
-  return as_u(__builtin_elementwise_min(as_us(a), as_us(b)));
-}
-// 0xFFFF in each half that is zero
-__device__ __forceinline__ uint32_t pk_zero_mask(uint32_t a) {
-  return pk_sub_u16(pk_min_u16(a, 0x00010001u), 0x00010001u);
-}
 // bits (2j, 2j+1) of the 8-bit lane mask from the halves of pair j's mask
 __device__ __forceinline__ uint32_t pair_bits(uint32_t m, int j) {
   return ((m & 1u) | ((m >> 15) & 2u)) << (2 * j);
 }
 
 // ---- sender snapshot plane (gh_internal.h: pl) ---------------------------
-__device__ __forceinline__ uint32_t pk_lshr16(uint32_t a, int k) { return as_u(as_us(a) >> (unsigned short)k); }
-__device__ __forceinline__ uint32_t pk_shl16(uint32_t a, int k) { return as_u(as_us(a) << (unsigned short)k); }
 // The plane word of 8 written narrow codes o (an all-narrow chunk); jd = the
 // row's own member in the chunk (0..7) or -1: its snapshot entry carries
 // hb + 1 (the heartbeat the row sends with next round).
@@ -592,6 +556,15 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
     // seen the round before it happens
     const int64_t measure = (int64_t)*d.nstorm + *d.slow_n;
     *d.mode = p.force_storm || measure * 32 > d.ntiles * (int64_t)d.n;
+    if (d.h8[0]) {
+      // the lean variant writes the next buffer in the 8-bit tier, the storm
+      // one in 16 bits; a buffer that changes tier is written whole (no
+      // quiet row keeps its old chunks)
+      const int w8 = *d.mode == 0;
+      d.m8[2] = w8 != d.m8[cur ^ 1];
+      d.m8[cur ^ 1] = w8;
+      d.m8[3] = 0;  // escaped chunks the round writes
+    }
     *d.slow_n = 0;
     *d.nstorm = 0;
     *d.nquiet = 0;
@@ -648,7 +621,7 @@ constexpr int round_rb() {
   return rb < 2048 / TW ? 2048 / TW : rb;
 }
 
-template <int KB, int TW, int TPW, bool NT, bool STORM>
+template <int KB, int TW, int TPW, bool NT, bool STORM, bool RD8>
 __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const int dcur, const GhRound& p,
                                             const int bid) {
   constexpr int CPL = 8;
@@ -673,6 +646,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   // this tile's segments for the slow list, appended with one global atomic
   __shared__ int s_nslow, s_slowbase;
   __shared__ int s_bmove;  // a column base of the tile moved this round
+  // 8-bit tier: per column of the tile the base move (base_next - base_cur,
+  // one byte each; the byte path's rebase), s_d8bad = a move outside 0..15
+  __shared__ uint32_t s_d8[TW / 4];
+  __shared__ int s_d8bad;
   __shared__ int s_slow[RB];
   // per-row metadata of the workgroup's rows, staged once for its TPW tiles:
   // s_meta = alive | active << 1 | inbox count << 2; s_inb = first KB senders
@@ -709,10 +686,12 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   if (tid == 0) {
     s_merged = s_det = s_rel = s_storm = s_tomb = s_unk = 0;
     s_quiet = 0;
+    s_bmove = 0;  // set by the first tile's setup after the staging barrier
+    s_d8bad = 0;
   }
   const bool pull = p.peer_mode == GH_PEER_PULL;
   // quiet rows may be skipped: no REMOVE pending anywhere (|D_{r-1}| = 0)
-  const bool quiet = d.cntg[p.n] == 0 && !p.force_slow;
+  const bool quiet = d.cntg[p.n] == 0 && !p.force_slow && !(d.h8[0] && d.m8[2]);
   const uint8_t* __restrict__ stab_cur = d.stab[p.r & 1];
   uint8_t* __restrict__ stab_nxt = d.stab[(p.r + 1) & 1];
   if constexpr (STORM) {
@@ -763,6 +742,17 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   uint16_t* __restrict__ hnn = d.hn[cur ^ 1];
   const int32_t* __restrict__ bo = d.base[cur];
   const int32_t* __restrict__ bn = d.base[cur ^ 1];
+  // 8-bit tier of the buffer read / written (gh_internal.h: h8): a lane's 8
+  // cells are one 8-B load / store, widened to packed 16-bit codes in
+  // registers; an escaped chunk is read from / written to hn
+  // (lean variants: one instantiation per input tier, RD8 = cur is 8-bit)
+  // (the 8-bit write path only where a tiered engine runs: pull k <= 4, one
+  // tile per workgroup)
+  constexpr bool W8 = !STORM && KB == 4 && TPW == 1;
+  const bool m8c = STORM ? gh_m8(d, cur) : RD8, m8n = W8 && gh_m8(d, cur ^ 1);
+  const uint8_t* __restrict__ h8o = d.h8[cur];
+  uint8_t* __restrict__ h8n = d.h8[cur ^ 1];
+  int n_esc = 0;  // escaped chunks written
   // sender plane: read by the lean 4-slot variant when valid, written by
   // every variant in plane mode
   constexpr bool PLANE_RD = !STORM && KB == 4;
@@ -785,12 +775,12 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   char* hnn_t = reinterpret_cast<char*>(hnn + tcell);
   const char* plo_t = reinterpret_cast<const char*>(plo) + (plo ? tcell / 2 : 0);
   char* pln_t = reinterpret_cast<char*>(pln) + (pln ? tcell / 2 : 0);
+  const char* h8o_t = reinterpret_cast<const char*>(h8o) + (h8o ? tcell : 0);
+  char* h8n_t = reinterpret_cast<char*>(h8n) + (h8n ? tcell : 0);
   const uint32_t lb = (uint32_t)lc * (CPL * 2);  // lane's byte offset in a row segment (narrow)
   const uint32_t lbp = (uint32_t)lc * 4;         // ... in a plane row segment
-  if (tid == 0) {
-    s_nslow = 0;
-    s_bmove = 0;
-  }
+  const uint32_t lb8 = (uint32_t)lc * CPL;       // ... in an 8-bit row segment
+  if (tid == 0) s_nslow = 0;
   for (int t = tid; t < TW; t += 256) {
     s_dcnt[t] = 0;
     s_dmin[t] = INT_MAX;
@@ -811,6 +801,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       }
       const int64_t delta = (int64_t)bn[c] - bo[c];
       const uint32_t d5h = (delta > 1023 || delta < -1023) ? 0x8000u : ((uint32_t)(delta << 5) & 0xFFFFu);
+      if constexpr (RD8) {
+        reinterpret_cast<uint8_t*>(s_d8)[2 * pp + h] = (uint8_t)(delta & 0xFF);
+        if (delta < 0 || delta > 15) s_d8bad = 1;
+      }
       const int64_t thr = 1 - (int64_t)bn[c];
       const uint32_t tc = thr < 0 ? 0xFFFFu : thr > 1023 ? 0x7FFFu : (uint32_t)((thr << 5) | 31);
       dd |= d5h << (16 * h);
@@ -826,6 +820,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   const uint32_t tcp = (uint32_t)min(p.t_cleanup, 31) * 0x10001u;
   __syncthreads();
   const bool tile_still = s_bmove == 0;
+  // the byte path (below) needs every base move of the tile in 0..15
+  const bool byte_tile = RD8 && s_d8bad == 0;
+  const uint2 d8 = RD8 ? *reinterpret_cast<const uint2*>(&s_d8[lc * 2]) : uint2{0u, 0u};
+  const uint32_t tfb = (uint32_t)(0x7F - min(p.t_fail, 15)) * 0x01010101u;  // age + tfb: bit 7 iff age > T_fail
   // lean: no REMOVE in the lane; storm: REMOVE applied in the packed path
   // unless a column has a single detector (that row keeps the member)
   bool lane_ok = !p.force_slow;
@@ -858,7 +856,13 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     // own segment and the senders' snapshots, issued together: plane words
     // when the plane is valid, else the first KB senders' 16-bit segments
     // (slots q >= cntv hold the own row, a no-op under the max)
-    v4u w = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + ob));  // re-read by peers: keep it cached
+    const uint32_t ob8 = islot * TW + lb8;      // ... in the 8-bit tier
+    v4u w = {0u, 0u, 0u, 0u};
+    uint2 w8 = {0u, 0u};
+    if (m8c)
+      w8 = *reinterpret_cast<const uint2*>(h8o_t + ob8);
+    else
+      w = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + ob));  // re-read by peers: keep it cached
     int ps[KB];
     const bool act = (meta >> 1) & 1;  // else the row is under the <4 guard (step 2)
     // guard rows in the lean variant: the 8-slot instantiation (ring
@@ -907,6 +911,94 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         for (int q = 0; q < KB; ++q)
           pw[q] = *reinterpret_cast<const uint32_t*>(plo_t + (psl[q] * (TW / 2) + lbp));
       }
+    }
+    if constexpr (RD8 && PLANE_RD && W8) {
+      // THE BYTE PATH: 8-bit tier in and out with a valid plane, the lean
+      // rule on the one-byte cells themselves, four per dword (SWAR), no
+      // widening. Per cell: l = lag (GH_C8_REF - offset), a = age; the
+      // freshest sender's plane code u = l_s + 2 (gh_internal.h: GH_P_REF =
+      // GH_C8_REF + 1) merges iff l_s < l (u <= l + 1; an absent own cell,
+      // l = 15, takes any sender; u = 15 = no sender entry). Merged: lag
+      // u - 2, age 1; else age + 1; then the rebase l += base move. A wave
+      // whose every running lane stays in the byte codes (lag 0..14, age
+      // <= min(T_fail, 15): no flag, no diagonal, no REMOVE, no guard row,
+      // no escape) is done here; any other wave runs the 16-bit rule below.
+      if (use_plane && m8n && byte_tile) {
+        uint32_t Lw = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t M = 0x000F000Fu << (4 * j);
+          uint32_t L = pw[0] & M;
+#pragma unroll
+          for (int q = 1; q < KB; ++q) L = pk_min_u16(L, pw[q] & M);
+          Lw |= L;
+        }
+        const uint32_t lo = Lw & 0x0F0F0F0Fu, hi = (Lw >> 4) & 0x0F0F0F0Fu;
+        const uint32_t U[2] = {__builtin_amdgcn_perm(hi, lo, 0x06040200u), __builtin_amdgcn_perm(hi, lo, 0x07050301u)};
+        const uint32_t X[2] = {w8.x, w8.y};
+        const uint32_t D[2] = {d8.x, d8.y};
+        uint32_t O[2], P[2];
+        uint32_t badb = 0;
+        int mrg = 0, gain = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t x = X[h], u = U[h], dd = D[h];
+          const uint32_t L = (x >> 4) & 0x0F0F0F0Fu, Ag = x & 0x0F0F0F0Fu;
+          const uint32_t A = (L + 0x01010101u) & 0x10101010u;                     // own absent (0x10)
+          const uint32_t N = (u + 0x01010101u) & 0x10101010u;                     // no sender entry
+          const uint32_t Mg = ((L + 0x81818181u) - u) & ~(N << 3) & 0x80808080u;  // merged (0x80)
+          const uint32_t MM = (Mg >> 7) * 0xFFu;
+          const uint32_t V = u + dd;
+          const uint32_t ln = ((V - 0x02020202u) & MM) | ((L + dd) & ~MM);        // next lag
+          const uint32_t an = (0x01010101u & MM) | ((Ag + 0x01010101u) & ~MM);    // next age
+          const uint32_t AN = ((A & ~(Mg >> 3)) >> 4) * 0xFFu;                    // absent next
+          // a running cell outside the byte codes: lag above 14, a merged
+          // lag below 0 (V < 2), age above min(T_fail, 15)
+          badb |= (((ln + 0x71717171u) | (an + tfb)) & ~AN & 0x80808080u) | (Mg & ~(V + 0x7E7E7E7Eu));
+          O[h] = (((ln & 0x0F0F0F0Fu) << 4) | an) | AN;
+          // plane code of the written cell: l + 2 (14 = older), absent 15
+          uint32_t pq = ln + 0x02020202u;
+          const uint32_t OM = (((pq + 0x71717171u) & 0x80808080u) >> 7) * 0xFFu;
+          P[h] = ((pq & ~OM) | (0x0E0E0E0Eu & OM) | AN) & 0x0F0F0F0Fu;
+          mrg += __builtin_popcount(Mg);
+          gain += __builtin_popcount(Mg & (A << 3));
+        }
+        const bool own_in8 = (unsigned)(i - c0) < 8u;
+        const bool okb = lane_ok && !bad && !own_in8 && (w8.x & 0xFFu) != GH_C8_ESC && badb == 0 &&
+                         (nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu)) == 0;
+        if (__ballot(al && !okb) == 0) {
+          int dpres = 0;
+          if (al) {
+            const uint64_t v8 = ((uint64_t)O[1] << 32) | O[0];
+            uint64_t* hp = reinterpret_cast<uint64_t*>(h8n_t + ob8);
+            const uint32_t E = __builtin_amdgcn_perm(P[1], P[0], 0x06040200u);
+            const uint32_t Od = __builtin_amdgcn_perm(P[1], P[0], 0x07050301u);
+            const uint32_t pwd = __builtin_amdgcn_perm(Od | (Od >> 4), E | (E >> 4), 0x06040200u);
+            uint32_t* pp = reinterpret_cast<uint32_t*>(pln_t + (islot * (TW / 2) + lbp));
+            if constexpr (NT) {
+              __builtin_nontemporal_store(v8, hp);
+              __builtin_nontemporal_store(pwd, pp);
+            } else {
+              *hp = v8;
+              *pp = pwd;
+            }
+            n_mrg16 += 16u * (uint32_t)mrg;
+            dpres = gain;
+          }
+          if (__ballot(dpres != 0) != 0) {  // absent cells merged: the row's count moves
+#pragma unroll
+            for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) dpres += __shfl_xor(dpres, o2);
+            if (lc == 0 && dpres) atomicAdd(&d.cntl[i], dpres);
+          }
+          continue;
+        }
+      }
+    }
+    if (m8c) {  // widen the own chunk (an escaped one is hn's)
+      if ((w8.x & 0xFFu) == GH_C8_ESC)
+        w = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + ob));
+      else
+        w = c8_dec(w8);
     }
     bad |= (w[0] & 0xFFFFu) == GH_N_WIDE;  // own segment wide
     // The row's own member in the lane (step 3, :443-448): hb + 1 with a
@@ -960,42 +1052,83 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 #pragma unroll
       for (int g = 0; g < KB; g += 4) {
         if (g > 0 && __ballot(g < cntv) == 0) break;
-        v4u pv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int q = g + u;
-          const uint16_t* src = reinterpret_cast<const uint16_t*>(hno_t + (psl[q] * (TW * 2) + lb));
-          if constexpr (STORM) {
-            // storms hold few senders (guard rows none): load only the used
-            // slots, the rest are absent (-1, a no-op under the max)
-            pv[u] = q < cntv ? ldn<false>(src) : v4u{~0u, ~0u, ~0u, ~0u};
-          } else if constexpr (KB > 4) {
-            // 8-slot inboxes (ring, pull k > 4) are mostly part-empty, and
-            // empty in a collapsed cluster: slots no lane of the wave uses
-            // are not loaded
-            pv[u] = __ballot(q < cntv) != 0 ? ldn<false>(src) : v4u{~0u, ~0u, ~0u, ~0u};
-          } else {
-            pv[u] = ldn<false>(src);  // unused slots hold the own row: a no-op under the max
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) bad |= g + u < cntv && (pv[u][0] & 0xFFFFu) == GH_N_WIDE;
-        // A sender's own member in the lane: its snapshot carries hb + 1
-        // there (the sender's heartbeat of this round).
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int js = ps[g + u] - c0;
-          if (g + u < cntv && (unsigned)js < 8u) {
+        // a sender's chunk into the merge: a wide segment is slow; its own
+        // member in the lane carries hb + 1 in its snapshot (the sender's
+        // heartbeat of this round); the packed max over senders
+        auto fold = [&](v4u pv, const int q) {
+          bad |= q < cntv && (pv[0] & 0xFFFFu) == GH_N_WIDE;
+          const int js = ps[q] - c0;
+          if (q < cntv && (unsigned)js < 8u) {
             const int sh = 16 * (js & 1);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-              if (j == (js >> 1) && ((pv[u][j] >> sh) & 0x8000u) == 0) pv[u][j] += 0x20u << sh;
+              if (j == (js >> 1) && ((pv[j] >> sh) & 0x8000u) == 0) pv[j] += 0x20u << sh;
           }
-        }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          uint32_t m4 = pk_max_i16(pk_max_i16(pv[0][j], pv[1][j]), pk_max_i16(pv[2][j], pv[3][j]));
-          ms[j] = g == 0 ? m4 : pk_max_i16(ms[j], m4);
+          for (int j = 0; j < 4; ++j) ms[j] = q == 0 ? pv[j] : pk_max_i16(ms[j], pv[j]);
+        };
+        if (m8c) {
+          // 8-bit sender chunks (absent: 0xFF bytes), all four issued, then
+          // widened one at a time (an escaped one is read from hn)
+          uint2 b8[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int q = g + u;
+            const uint2* src = reinterpret_cast<const uint2*>(h8o_t + (psl[q] * TW + lb8));
+            if constexpr (STORM)
+              b8[u] = q < cntv ? *src : uint2{~0u, ~0u};
+            else if constexpr (KB > 4)
+              b8[u] = __ballot(q < cntv) != 0 ? *src : uint2{~0u, ~0u};
+            else
+              b8[u] = *src;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            v4u pv;
+            if ((b8[u].x & 0xFFu) == GH_C8_ESC)
+              pv = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + (psl[g + u] * (TW * 2) + lb)));
+            else
+              pv = c8_dec(b8[u]);
+            fold(pv, g + u);
+          }
+        } else {
+          v4u pv[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int q = g + u;
+            const uint16_t* src = reinterpret_cast<const uint16_t*>(hno_t + (psl[q] * (TW * 2) + lb));
+            if constexpr (STORM) {
+              // storms hold few senders (guard rows none): load only the used
+              // slots, the rest are absent (-1, a no-op under the max)
+              pv[u] = q < cntv ? ldn<false>(src) : v4u{~0u, ~0u, ~0u, ~0u};
+            } else if constexpr (KB > 4) {
+              // 8-slot inboxes (ring, pull k > 4) are mostly part-empty, and
+              // empty in a collapsed cluster: slots no lane of the wave uses
+              // are not loaded
+              pv[u] = __ballot(q < cntv) != 0 ? ldn<false>(src) : v4u{~0u, ~0u, ~0u, ~0u};
+            } else {
+              pv[u] = ldn<false>(src);  // unused slots hold the own row: a no-op under the max
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) bad |= g + u < cntv && (pv[u][0] & 0xFFFFu) == GH_N_WIDE;
+          // A sender's own member in the lane: its snapshot carries hb + 1
+          // there (the sender's heartbeat of this round).
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int js = ps[g + u] - c0;
+            if (g + u < cntv && (unsigned)js < 8u) {
+              const int sh = 16 * (js & 1);
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                if (j == (js >> 1) && ((pv[u][j] >> sh) & 0x8000u) == 0) pv[u][j] += 0x20u << sh;
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            uint32_t m4 = pk_max_i16(pk_max_i16(pv[0][j], pv[1][j]), pk_max_i16(pv[2][j], pv[3][j]));
+            ms[j] = g == 0 ? m4 : pk_max_i16(ms[j], m4);
+          }
         }
       }
     }
@@ -1094,7 +1227,22 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     bool any_det = false;
     if (al) {
       if (seg_ok) {
-        stn<NT>(reinterpret_cast<uint16_t*>(hnn_t + ob), o);
+        if (m8n) {
+          uint32_t bad8 = 0;
+          const uint2 e8 = c8_enc(o, bad8);
+          uint64_t* hp = reinterpret_cast<uint64_t*>(h8n_t + ob8);
+          const uint64_t v8 = bad8 ? 0xF0F0F0F0F0F0F0F0ull : ((uint64_t)e8.y << 32) | e8.x;
+          if constexpr (NT)
+            __builtin_nontemporal_store(v8, hp);
+          else
+            *hp = v8;
+          if (bad8) {  // escaped: the 16-bit chunk
+            stn<NT>(reinterpret_cast<uint16_t*>(hnn_t + ob), o);
+            n_esc++;
+          }
+        } else {
+          stn<NT>(reinterpret_cast<uint16_t*>(hnn_t + ob), o);
+        }
         if (p.plane) {
           const uint32_t pwd = plane_word(o, own_in ? jd : -1);
           uint32_t* pp = reinterpret_cast<uint32_t*>(pln_t + (islot * (TW / 2) + lbp));
@@ -1142,6 +1290,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   }
 
   __syncthreads();
+  if (tid == 0) {  // read before the barrier above; the next tile's setup writes them after two more
+    s_bmove = 0;
+    s_d8bad = 0;
+  }
   for (int t = tid; t < TW; t += 256) {
     if (s_dcnt[t]) {
       const int64_t c = (int64_t)tile * TW + t;
@@ -1156,6 +1308,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   }  // tiles
 
   if (PLANE_RD && n_fb && lane == 0) atomicAdd(d.pfb, n_fb);
+  if (n_esc) atomicAdd(&d.m8[3], n_esc);
   if (n_mrg16) atomicAdd(&s_merged, (unsigned long long)(n_mrg16 >> 4));
   if (n_det) atomicAdd(&s_det, (unsigned long long)n_det);
   if (n_rel) atomicAdd(&s_rel, (unsigned long long)n_rel);
@@ -1176,21 +1329,25 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   }
 }
 
-// Both variants are launched every round; the one k_base did not select
-// returns at once. The storm variant runs 1/8 of the workgroups, each taking
-// blocks a multiple of 8 apart (same XCD), so idle it is a small dispatch.
-template <int KB, int TW, int TPW, bool NT, bool STORM>
+// The variants are launched every round (lean on a 16-bit input, lean on an
+// 8-bit one when the engine keeps the tier, storm); the ones k_base and the
+// input's tier did not select return at once. The storm variant runs 1/8 of
+// the workgroups, each taking blocks a multiple of 8 apart (same XCD), so idle
+// it is a small dispatch.
+template <int KB, int TW, int TPW, bool NT, bool STORM, bool RD8>
 __global__ __launch_bounds__(256, (STORM && TW >= 32) ? 4 : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
   if (*d.mode != (int)STORM) return;
+  if (!STORM && gh_m8(d, cur) != RD8) return;
   if constexpr (STORM) {
     constexpr int RB = round_rb<TW>();
     const int nblk = (int)((d.nrows + RB - 1) / RB) * ((int)(p.ld / TW) / TPW);
     for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
-      round_block<KB, TW, TPW, NT, STORM>(d, cur, dcur, p, b);
+      round_block<KB, TW, TPW, NT, STORM, RD8>(d, cur, dcur, p, b);
       __syncthreads();  // LDS of this block before the next
     }
   } else {
-    round_block<KB, TW, TPW, NT, STORM>(d, cur, dcur, p, blockIdx.x);
+    // one block per workgroup (a loop here costs the lean variants 20+ VGPRs)
+    round_block<KB, TW, TPW, NT, STORM, RD8>(d, cur, dcur, p, blockIdx.x);
   }
 }
 
@@ -1235,9 +1392,9 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
     uint4 nx = {0u, 0u, 0u, 0u};
     uint4 raw = {0u, 0u, 0u, 0u};  // the chunk as read (narrow codes or a wide marker)
     if (valid) {
-      raw = *reinterpret_cast<const uint4*>(d.hn[cur] + gh_cell(d, i, l0));
+      raw = gh_ld16(d, cur, gh_cell(d, i, l0));
       GhCell A[8], X[8];
-      gh_get8(d, cur, i, l0, r, A);
+      gh_dec8(d, cur, i, l0, r, raw, A);
       int64_t m[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) m[j] = -1;
@@ -1603,22 +1760,35 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_inbox_fill, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
 }
 
+// variant: 0 lean on a 16-bit input, 1 storm, 2 lean on an 8-bit input
 template <int KB, int TW, int TPW>
-static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm) {
+static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant) {
   constexpr int RB = round_rb<TW>();
   const int64_t nrb = (d.nrows + RB - 1) / RB;
   const int64_t nblk = nrb * (p.ld / TW / TPW);
   if (nblk == 0) return;
-  const dim3 grid((unsigned)(storm ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
-  // the one k_base did not select returns at once
-  if (nt && storm)
-    hipLaunchKernelGGL((k_round<KB, TW, TPW, true, true>), grid, blk, 0, s, d, cur, dcur, p);
+  const dim3 grid((unsigned)(variant == 1 ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
+#define GH_ROUND_LAUNCH(NT, ST, R8) \
+  hipLaunchKernelGGL((k_round<KB, TW, TPW, NT, ST, R8>), grid, blk, 0, s, d, cur, dcur, p)
+  if constexpr (KB == 4 && TPW == 1) {
+    if (variant == 2) {
+      if (nt)
+        GH_ROUND_LAUNCH(true, false, true);
+      else
+        GH_ROUND_LAUNCH(false, false, true);
+      return;
+    }
+  }
+  if (variant == 2) return;  // no 8-bit tier here (host: c8 needs pull k <= 4, TPW 1)
+  if (nt && variant == 1)
+    GH_ROUND_LAUNCH(true, true, false);
   else if (nt)
-    hipLaunchKernelGGL((k_round<KB, TW, TPW, true, false>), grid, blk, 0, s, d, cur, dcur, p);
-  else if (storm)
-    hipLaunchKernelGGL((k_round<KB, TW, TPW, false, true>), grid, blk, 0, s, d, cur, dcur, p);
+    GH_ROUND_LAUNCH(true, false, false);
+  else if (variant == 1)
+    GH_ROUND_LAUNCH(false, true, false);
   else
-    hipLaunchKernelGGL((k_round<KB, TW, TPW, false, false>), grid, blk, 0, s, d, cur, dcur, p);
+    GH_ROUND_LAUNCH(false, false, false);
+#undef GH_ROUND_LAUNCH
 }
 
 template <int TW>
@@ -1629,7 +1799,7 @@ static void round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
 
 // tiles per workgroup: ld / TW is a multiple of 8 (host padding)
 template <int KB, int TW>
-static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm) {
+static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm) {
   switch (p.tpw) {
     case 1: launch_round_tpw<KB, TW, 1>(d, cur, dcur, p, s, nt, storm); break;
     case 2: launch_round_tpw<KB, TW, 2>(d, cur, dcur, p, s, nt, storm); break;
@@ -1639,7 +1809,7 @@ static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p,
 }
 
 template <int KB>
-static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm) {
+static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm) {
   switch (d.tw) {
     case 8: launch_round_tw<KB, 8>(d, cur, dcur, p, s, nt, storm); break;
     case 16: launch_round_tw<KB, 16>(d, cur, dcur, p, s, nt, storm); break;
@@ -1650,7 +1820,7 @@ static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p,
   }
 }
 
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, bool storm) {
+void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm) {
   if (p.peer_mode == GH_PEER_PULL && p.k <= 4)
     launch_round_kb<4>(d, cur, dcur, p, s, nt, storm);
   else

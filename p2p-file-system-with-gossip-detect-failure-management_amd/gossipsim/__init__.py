@@ -114,6 +114,13 @@ class Engine:
         self._chk(self.lib.gh_plane_info(self.h, C.byref(en), C.byref(va), C.byref(fb)))
         return en.value, va.value, fb.value
 
+    def tier_info(self):
+        """(8-bit tier kept, current table held in it, chunks the last round's
+        packed path wrote escaped in 16 bits) -- gh_tier_info, diagnostic."""
+        en, cu, esc = C.c_int32(), C.c_int32(), C.c_int64()
+        self._chk(self.lib.gh_tier_info(self.h, C.byref(en), C.byref(cu), C.byref(esc)))
+        return en.value, cu.value, esc.value
+
     def exchange_info(self):
         """dict(ghost_rows, bytes_out, bytes_in) of this shard's last ghost-row
         exchange (row layout; gh_exchange_info)."""

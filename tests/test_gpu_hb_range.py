@@ -178,10 +178,11 @@ def test_long_collapse_stays_narrow(gs, oracle_mod):
 
 
 def test_footprint_n65536(gs):
-    """The headline configuration's tables in HBM: <= 23 GiB (the narrow
-    table x2 is 16 GiB, the sender plane x2 4 GiB, the wide arenas 2 GiB and
-    the rest < 1 GiB; GH_PLANE=0 drops the plane), measured with
-    hipMemGetInfo around the engine's creation and first rounds."""
+    """The headline configuration's tables in HBM: <= 31 GiB (the narrow
+    table x2 is 16 GiB, the 8-bit tier x2 8 GiB, the sender plane x2 4 GiB,
+    the wide arenas 2 GiB and the rest < 1 GiB; GH_PLANE=0 drops the plane and
+    the tier, GH_C8=0 the tier), measured with hipMemGetInfo around the
+    engine's creation and first rounds."""
     import ctypes as C
     hip = C.CDLL("libamdhip64.so")
 
@@ -200,4 +201,4 @@ def test_footprint_n65536(gs):
     eng.close()
     eng0.close()
     print(f"N=65536: {used / 2**30:.2f} GiB by hipMemGetInfo, tables {info['device_bytes'] / 2**30:.2f} GiB")
-    assert used <= 23 * 2**30 and info["device_bytes"] <= used
+    assert used <= 31 * 2**30 and info["device_bytes"] <= used

@@ -1,0 +1,205 @@
+"""8-bit tier (csrc/gh_internal.h `h8`, DESIGN.md "8-bit tier"): in plane
+mode the lean round variant streams each 8-cell chunk as 8 one-byte codes
+(lag behind the member's own counter, age) and keeps the chunks no byte code
+holds -- flags, tombstones, wide and frozen markers, lags past 14, ages past
+15 -- in the 16-bit table, escaped. These tests pin that the tier is in use
+where it should be, that escapes happen and stay bit-exact against the
+oracle, that events, imports, quirk flag clears, list merges, storms and
+quiet rows cross it, and that it changes no result against the 16-bit table
+(GH_C8=0). Small clusters keep the plane (and so the tier) through
+GH_PLANE=1. Run on a MI355X: pytest -m gpu."""
+import numpy as np
+import pytest
+
+import scenarios as sc
+from test_gpu_parity import compare, run_parity
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gs():
+    import gossipsim
+    return gossipsim
+
+
+@pytest.fixture(autouse=True)
+def tier_on(monkeypatch):
+    monkeypatch.setenv("GH_PLANE", "1")
+    monkeypatch.delenv("GH_C8", raising=False)
+
+
+def test_tier_steady_state(gs, oracle_mod):
+    """N=2,048, k=4 pull from full membership with the bench's timeouts: the
+    lean rounds write the 8-bit tier from round 1 on, the healthy rounds
+    escape no chunk, crash / leave / join events write into 8-bit buffers, the
+    detection wave's storm rounds switch to 16 bits and back; bit-exact every
+    round."""
+    n = 2048
+    cfg = dict(fanout=4, seed=0x5EED0007, t_fail=16, t_cleanup=16)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    hb, ts, alive = sc.full_state(n)
+    eng.import_state(hb, ts, alive, 0)
+    orc.import_state(hb, ts, alive, 0)
+    assert eng.tier_info()[:2] == (1, 0)  # an import leaves a 16-bit table
+    sched = {14: [(sc.CRASH, 7), (sc.LEAVE, 1500)], 18: [(sc.JOIN, 1500), (sc.JOIN, 7)]}
+    esc, tiers = [], []
+    for r in range(1, 56):
+        ev = sched.get(r, [])
+        if ev:
+            eng.apply_events(ev)
+            orc.apply_events(ev)
+        s1, s2 = eng.step(1), orc.step(1)
+        assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
+        compare(eng, orc, r)
+        en, cur8, e = eng.tier_info()
+        assert en == 1
+        esc.append(e)
+        tiers.append(cur8)
+    # 8-bit from the first round on; the crash's detection and tombstones
+    # (rounds ~31-48) run the storm variant (16-bit), the healthy rounds after
+    # them return to 8 bits
+    assert tiers[:13] == [1] * 13 and 0 in tiers and tiers[-1] == 1, tiers
+    assert esc[7:13] == [0] * 6, esc
+
+
+def ranged_state(n, seed):
+    """Views lagging their owners by 0..40 rounds (past the 14-round byte
+    window), ages up to 24 (past 15), ahead-of-owner views (offsets above
+    the byte reference) and a few tombstones: every kind of escape, all
+    within the 16-bit narrow window and rare enough (tombstones in ~1% of the
+    segments) for the lean variant to run."""
+    rng = np.random.default_rng(seed)
+    own = 1000 + rng.integers(0, 5, n)
+    hb = own[None, :] - rng.integers(0, 41, (n, n))
+    ahead = np.arange(n) % 97 == 3
+    hb[:, ahead] = own[ahead][None, :] + rng.integers(1, 9, (n, int(ahead.sum())))
+    tomb = rng.random((n, n)) < 0.00004
+    hb[tomb] = -2
+    np.fill_diagonal(hb, own)
+    ts = rng.integers(16, 41, (n, n)).astype(np.int32)
+    np.fill_diagonal(ts, 40)
+    return hb.astype(np.int32), ts, np.ones(n, np.uint8)
+
+
+@pytest.mark.parametrize("k", [3, 4])
+def test_tier_escapes_exact(gs, oracle_mod, k):
+    """Lags, ages and tombstones outside the byte codes: the lean rounds
+    escape chunks (escaped > 0) and every round stays bit-exact."""
+    n = 1024
+    cfg = dict(fanout=k, seed=0x5EED0110 + k, t_fail=60, t_cleanup=60)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    hb, ts, alive = ranged_state(n, k)
+    eng.import_state(hb, ts, alive, 40)
+    orc.import_state(hb, ts, alive, 40)
+    esc = []
+    for r in range(1, 16):
+        s1, s2 = eng.step(1), orc.step(1)
+        assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
+        compare(eng, orc, r)
+        esc.append(eng.tier_info()[2])
+    assert sum(esc) > 0, esc
+
+
+def run_states(gs, n, cfg, sched, rounds, init, merges=None):
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    eng.import_state(*init, 0)
+    out = []
+    for r in range(1, rounds + 1):
+        ev = sched.get(r, [])
+        if ev:
+            eng.apply_events(ev)
+        if merges and r in merges:
+            obs, ids, hbs = merges[r]
+            eng.merge_list(obs, ids, hbs)
+        st = eng.step(1)
+        out.append((st, eng.export_state(), eng.read_failed(), eng.read_detectors(), eng.lsm(3)))
+    info = eng.tier_info()
+    eng.close()
+    return out, info
+
+
+def assert_same(base, other):
+    for r, (a, b) in enumerate(zip(base, other), 1):
+        assert a[0] == b[0], (r, a[0], b[0])
+        for x, y in zip(a[1], b[1]):
+            np.testing.assert_array_equal(x, y, err_msg=f"round {r}")
+        np.testing.assert_array_equal(a[2], b[2])
+        np.testing.assert_array_equal(a[3], b[3])
+        for x, y in zip(a[4], b[4]):
+            np.testing.assert_array_equal(x, y, err_msg=f"lsm round {r}")
+
+
+@pytest.mark.parametrize("detect_mode", [0, 1], ids=["canonical", "quirk"])
+@pytest.mark.parametrize("order", [0, 1], ids=["id_order", "append_order"])
+def test_tier_matches_16bit(gs, monkeypatch, detect_mode, order):
+    """Seeded churn with detection waves (T_fail 6: storm rounds write 16-bit
+    tables, lean rounds 8-bit ones), quirk flag clears and datagram merges
+    into 8-bit buffers: the tier gives the same tables, counters, failed
+    sets, detectors and lists every round as the 16-bit table (GH_C8=0)."""
+    n = 1536
+    cfg = dict(fanout=4, seed=0x5EED0210 + 2 * detect_mode + order, t_fail=6, t_cleanup=8,
+               detect_mode=detect_mode, list_order=order)
+    sched = sc.random_churn(n, 40, 0x78 + detect_mode, p_crash=0.01, p_leave=0.005, p_join=0.02)
+    rng = np.random.default_rng(5)
+    merges = {r: (int(rng.integers(0, n)), np.arange(0, n, 7, dtype=np.int32),
+                  rng.integers(0, 60, len(range(0, n, 7))).astype(np.int32)) for r in (9, 21, 33)}
+    init = sc.full_state(n)
+    base, info = run_states(gs, n, cfg, sched, 40, init, merges)
+    assert info[0] == 1
+    monkeypatch.setenv("GH_C8", "0")
+    other, info2 = run_states(gs, n, cfg, sched, 40, init, merges)
+    assert info2[0] == 0
+    assert_same(base, other)
+
+
+def test_tier_quiet_rows_collapse(gs, oracle_mod):
+    """The reference's 5-round timeouts at N=2,048: the detection storm runs
+    the storm variant (16-bit), the collapsed cluster's lean rounds switch
+    the tables back to the 8-bit tier while rows are quiet, a join rewrites
+    rows. Bit-exact against the oracle, with quiet rows skipped."""
+    n = 2048
+    cfg = dict(fanout=4, seed=0x5EED0810)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    hb, ts, alive = sc.full_state(n)
+    eng.import_state(hb, ts, alive, 0)
+    orc.import_state(hb, ts, alive, 0)
+    quiet, tiers = [], []
+    for r in range(1, 61):
+        if r == 48:
+            ev = [(sc.JOIN, 5)]
+            eng.apply_events(ev)
+            orc.apply_events(ev)
+        s1, s2 = eng.step(1), orc.step(1)
+        assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
+        quiet.append(eng.encoding_info(full=True)[4])
+        tiers.append(eng.tier_info()[1])
+        if r % 3 == 0 or r in (47, 48, 49):
+            compare(eng, orc, r)
+    assert max(quiet) > 0, quiet
+    assert 0 in tiers and 1 in tiers, tiers
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tier_sharded_parity(gs, oracle_mod, world):
+    """Column shards (in-process transport) each keep the tier of their own
+    columns; seeded churn is bit-exact against the oracle every round."""
+    from test_gpu_sharded import run_group
+    n = 1100
+    sched = sc.random_churn(n, 30, 0xB0 + world, p_crash=0.01, p_leave=0.01, p_join=0.03)
+    run_group(gs, oracle_mod, world, dict(fanout=4, seed=0x5EED0410 + world, t_fail=9, t_cleanup=9), n, 30, sched,
+              init=sc.full_state(n))
+
+
+def test_tier_placement(gs, oracle_mod):
+    """Placement and repair read the master / observer rows from 8-bit tables:
+    churn with files, bit-exact against the oracle."""
+    n = 640
+    sched = {5: [(sc.CRASH, 3), (sc.CRASH, 200)], 12: [(sc.JOIN, 3)], 20: [(sc.LEAVE, 9)]}
+    files = {r: np.arange(r * 40, r * 40 + 40) for r in (2, 8, 15, 24)}
+    eng, orc = run_parity(gs, oracle_mod, dict(fanout=4, seed=0x5EED0910, t_fail=7, t_cleanup=7, max_files=2048),
+                          n, 28, sched, init=sc.full_state(n), files=files)
+    assert eng.tier_info()[0] == 1

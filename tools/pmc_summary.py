@@ -39,11 +39,14 @@ import os  # noqa: E402
 # say otherwise
 plane = int(3 <= k <= 4 and (os.environ["GH_PLANE"] != "0" if "GH_PLANE" in os.environ else n >= 16384))
 tw = int(os.environ.get("GH_TILE_W", "256" if plane else "64"))
-out["config"] = {"n": n, "k": k, "world": 1, "cell_bytes": 2, "warmup": warmup, "steps": steps,
+# the 8-bit tier comes with the plane (column layout, one tile per workgroup)
+tier8 = int(plane and os.environ.get("GH_C8", "1") != "0" and os.environ.get("GH_ROUND_TPW", "1") == "1")
+cb = 1 if tier8 else 2
+out["config"] = {"n": n, "k": k, "world": 1, "cell_bytes": cb, "warmup": warmup, "steps": steps,
                  "plane": plane, "tile_width": tw,
                  "command": f"python3 bench.py --steps {steps} --warmup {warmup} --no-cpu-baseline --no-secondary "
                             "--files 0"}
-out["compulsory_bytes"] = 4.0 * n * n
+out["compulsory_bytes"] = 2.0 * cb * n * n
 out["gather_bytes"] = 2.0 * n * n * k
 if "traffic_bytes" in out:
     out["traffic_over_compulsory"] = out["traffic_bytes"] / out["compulsory_bytes"]
