@@ -650,8 +650,9 @@ void launch_ring_select(const GhDev& d, int cur, int dcur, const GhRound& p, hip
 void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
 // nt = non-temporal hints on the once-touched streams of k_round
 // variant: 0 the lean one on a 16-bit input, 1 the storm one, 2 the lean one
-// on an 8-bit input (tiered engines); all are launched every round and only
-// the one k_base and the input's tier select runs
+// on an 8-bit input by the 16-bit rule, 3 by the byte path (2 and 3: tiered
+// engines); all are launched every round and only the one k_base, the
+// input's tier and the plane select runs
 void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant);
 // the segments k_round listed, by the per-cell rule (after launch_round)
 void launch_round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);

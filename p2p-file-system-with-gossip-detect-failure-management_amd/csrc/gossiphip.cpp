@@ -741,7 +741,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   // the 8-bit tier streams the steady state the plane serves at 1 B per cell
   // (its window is the plane's: lags of healthy pull dissemination); the row
   // layout ships 16-bit ghost rows
-  e->c8 = e->plane && cfg->shard_layout == GH_LAYOUT_COLUMNS && e->tpw == 1;
+  e->c8 = e->plane && cfg->shard_layout == GH_LAYOUT_COLUMNS && e->tpw == 1 && tw >= 64;
   if (const char* v = std::getenv("GH_C8")) e->c8 = e->c8 && std::atoi(v) != 0;
   if (cfg->shard_layout != GH_LAYOUT_COLUMNS &&
       (cfg->shard_layout != GH_LAYOUT_ROWS || cfg->peer_mode != GH_PEER_PULL)) {
@@ -1304,8 +1304,8 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   bool busy = false;
   if ((rc0 = check_lost(e)) || (rc0 = maybe_grow(e, &busy))) return rc0;
   HIPCHK(e, hipMemsetAsync(e->d.stats, 0, sizeof(unsigned long long) * ST_COUNT, e->stream));
-  if (e->timing && (int64_t)e->evs.size() < 4 * (int64_t)rounds) {
-    while ((int64_t)e->evs.size() < 4 * (int64_t)rounds) {
+  if (e->timing && (int64_t)e->evs.size() < 5 * (int64_t)rounds) {
+    while ((int64_t)e->evs.size() < 5 * (int64_t)rounds) {
       hipEvent_t ev;
       HIPCHK(e, hipEventCreate(&ev));
       e->evs.push_back(ev);
@@ -1356,13 +1356,12 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     }
     if ((rc = build_inboxes(e, p))) return rc;
     // the variants of k_round; the ones not selected return at once
-    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[4 * q], e->stream));
-    launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt, 0);
-    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[4 * q + 1], e->stream));
-    if (e->c8) launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt, 2);
-    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[4 * q + 2], e->stream));
-    launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt, 1);
-    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[4 * q + 3], e->stream));
+    const int nvar = e->c8 ? 4 : 2;  // lean 16-bit input, storm, lean 8-bit input (16-bit rule, byte path)
+    for (int v = 0; v < nvar; ++v) {
+      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[5 * q + v], e->stream));
+      launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt, v);
+    }
+    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[5 * q + nvar], e->stream));
     launch_round_slow(e->d, e->cur, e->dcur, p, e->stream);
     if (e->rowlay && e->world > 1) {
       // every shard detected in its own rows: D_r's counts and first
@@ -1410,9 +1409,9 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   if (e->timing) {
     for (int32_t q = 0; q < done; ++q) {
       float ms = 0.f;  // the variant that ran
-      for (int v = 0; v < 3; ++v) {
+      for (int v = 0; v < (e->c8 ? 4 : 2); ++v) {
         float mv = 0.f;
-        HIPCHK(e, hipEventElapsedTime(&mv, e->evs[4 * q + v], e->evs[4 * q + v + 1]));
+        HIPCHK(e, hipEventElapsedTime(&mv, e->evs[5 * q + v], e->evs[5 * q + v + 1]));
         ms = std::max(ms, mv);
       }
       e->timed_ms += ms;

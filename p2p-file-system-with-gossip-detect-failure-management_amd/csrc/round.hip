@@ -621,7 +621,10 @@ constexpr int round_rb() {
   return rb < 2048 / TW ? 2048 / TW : rb;
 }
 
-template <int KB, int TW, int TPW, bool NT, bool STORM, bool RD8>
+// IN: 0 = a 16-bit input (full grid), 1 = an 8-bit input by the 16-bit rule
+// (widened), 2 = an 8-bit input by the byte path, 3 = a 16-bit input in a
+// tiered engine (rarely selected: a persistent 1/8 grid)
+template <int KB, int TW, int TPW, bool NT, bool STORM, int IN>
 __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const int dcur, const GhRound& p,
                                             const int bid) {
   constexpr int CPL = 8;
@@ -647,9 +650,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   __shared__ int s_nslow, s_slowbase;
   __shared__ int s_bmove;  // a column base of the tile moved this round
   // 8-bit tier: per column of the tile the base move (base_next - base_cur,
-  // one byte each; the byte path's rebase), s_d8bad = a move outside 0..15
+  // one byte each; the byte path's rebase), s_d8bad bit l = lane l's 8
+  // columns hold a move outside 0..15
   __shared__ uint32_t s_d8[TW / 4];
-  __shared__ int s_d8bad;
+  __shared__ uint32_t s_d8bad;
   __shared__ int s_slow[RB];
   // per-row metadata of the workgroup's rows, staged once for its TPW tiles:
   // s_meta = alive | active << 1 | inbox count << 2; s_inb = first KB senders
@@ -687,7 +691,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     s_merged = s_det = s_rel = s_storm = s_tomb = s_unk = 0;
     s_quiet = 0;
     s_bmove = 0;  // set by the first tile's setup after the staging barrier
-    s_d8bad = 0;
+    s_d8bad = 0u;
   }
   const bool pull = p.peer_mode == GH_PEER_PULL;
   // quiet rows may be skipped: no REMOVE pending anywhere (|D_{r-1}| = 0)
@@ -745,7 +749,9 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   // 8-bit tier of the buffer read / written (gh_internal.h: h8): a lane's 8
   // cells are one 8-B load / store, widened to packed 16-bit codes in
   // registers; an escaped chunk is read from / written to hn
-  // (lean variants: one instantiation per input tier, RD8 = cur is 8-bit)
+  // (lean variants: one instantiation per input tier)
+  constexpr bool RD8 = IN == 1 || IN == 2;
+  constexpr bool BYTE = IN == 2;
   // (the 8-bit write path only where a tiered engine runs: pull k <= 4, one
   // tile per workgroup)
   constexpr bool W8 = !STORM && KB == 4 && TPW == 1;
@@ -801,9 +807,9 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       }
       const int64_t delta = (int64_t)bn[c] - bo[c];
       const uint32_t d5h = (delta > 1023 || delta < -1023) ? 0x8000u : ((uint32_t)(delta << 5) & 0xFFFFu);
-      if constexpr (RD8) {
+      if constexpr (BYTE) {
         reinterpret_cast<uint8_t*>(s_d8)[2 * pp + h] = (uint8_t)(delta & 0xFF);
-        if (delta < 0 || delta > 15) s_d8bad = 1;
+        if (delta < 0 || delta > 15) atomicOr(&s_d8bad, 1u << ((2 * pp + h) >> 3));
       }
       const int64_t thr = 1 - (int64_t)bn[c];
       const uint32_t tc = thr < 0 ? 0xFFFFu : thr > 1023 ? 0x7FFFu : (uint32_t)((thr << 5) | 31);
@@ -820,9 +826,9 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   const uint32_t tcp = (uint32_t)min(p.t_cleanup, 31) * 0x10001u;
   __syncthreads();
   const bool tile_still = s_bmove == 0;
-  // the byte path (below) needs every base move of the tile in 0..15
-  const bool byte_tile = RD8 && s_d8bad == 0;
-  const uint2 d8 = RD8 ? *reinterpret_cast<const uint2*>(&s_d8[lc * 2]) : uint2{0u, 0u};
+  // the byte path (below) needs the base moves of the lane's columns in 0..15
+  const bool byte_lane = BYTE && ((s_d8bad >> lc) & 1u) == 0;
+  const uint2 d8 = BYTE ? *reinterpret_cast<const uint2*>(&s_d8[lc * 2]) : uint2{0u, 0u};
   const uint32_t tfb = (uint32_t)(0x7F - min(p.t_fail, 15)) * 0x01010101u;  // age + tfb: bit 7 iff age > T_fail
   // lean: no REMOVE in the lane; storm: REMOVE applied in the packed path
   // unless a column has a single detector (that row keeps the member)
@@ -912,87 +918,106 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
           pw[q] = *reinterpret_cast<const uint32_t*>(plo_t + (psl[q] * (TW / 2) + lbp));
       }
     }
-    if constexpr (RD8 && PLANE_RD && W8) {
-      // THE BYTE PATH: 8-bit tier in and out with a valid plane, the lean
-      // rule on the one-byte cells themselves, four per dword (SWAR), no
+    if constexpr (BYTE) {
+      // THE BYTE PATH (IN = 2: 8-bit tier in and out with a valid plane; the
+      // 16-bit rule is not compiled into this instantiation): the lean rule
+      // on the one-byte cells themselves, four per dword (SWAR), no
       // widening. Per cell: l = lag (GH_C8_REF - offset), a = age; the
       // freshest sender's plane code u = l_s + 2 (gh_internal.h: GH_P_REF =
       // GH_C8_REF + 1) merges iff l_s < l (u <= l + 1; an absent own cell,
       // l = 15, takes any sender; u = 15 = no sender entry). Merged: lag
-      // u - 2, age 1; else age + 1; then the rebase l += base move. A wave
-      // whose every running lane stays in the byte codes (lag 0..14, age
-      // <= min(T_fail, 15): no flag, no diagonal, no REMOVE, no guard row,
-      // no escape) is done here; any other wave runs the 16-bit rule below.
-      if (use_plane && m8n && byte_tile) {
-        uint32_t Lw = 0;
+      // u - 2, age 1; else age + 1; then the rebase l += base move. The
+      // row's own member (step 3): hb + 1, age 1, merged only by a larger
+      // snapshot (u <= l). A row segment whose every lane stays in the byte
+      // codes (lag 0..14, age <= min(T_fail, 15): no flag, no REMOVE, no
+      // guard row, no escape, plane codes exact) is written here; any other
+      // goes to the slow list (k_round_slow, the per-cell rule).
+      uint32_t Lw = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t M = 0x000F000Fu << (4 * j);
-          uint32_t L = pw[0] & M;
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t M = 0x000F000Fu << (4 * j);
+        uint32_t L = pw[0] & M;
 #pragma unroll
-          for (int q = 1; q < KB; ++q) L = pk_min_u16(L, pw[q] & M);
-          Lw |= L;
-        }
-        const uint32_t lo = Lw & 0x0F0F0F0Fu, hi = (Lw >> 4) & 0x0F0F0F0Fu;
-        const uint32_t U[2] = {__builtin_amdgcn_perm(hi, lo, 0x06040200u), __builtin_amdgcn_perm(hi, lo, 0x07050301u)};
-        const uint32_t X[2] = {w8.x, w8.y};
-        const uint32_t D[2] = {d8.x, d8.y};
-        uint32_t O[2], P[2];
-        uint32_t badb = 0;
-        int mrg = 0, gain = 0;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t x = X[h], u = U[h], dd = D[h];
-          const uint32_t L = (x >> 4) & 0x0F0F0F0Fu, Ag = x & 0x0F0F0F0Fu;
-          const uint32_t A = (L + 0x01010101u) & 0x10101010u;                     // own absent (0x10)
-          const uint32_t N = (u + 0x01010101u) & 0x10101010u;                     // no sender entry
-          const uint32_t Mg = ((L + 0x81818181u) - u) & ~(N << 3) & 0x80808080u;  // merged (0x80)
-          const uint32_t MM = (Mg >> 7) * 0xFFu;
-          const uint32_t V = u + dd;
-          const uint32_t ln = ((V - 0x02020202u) & MM) | ((L + dd) & ~MM);        // next lag
-          const uint32_t an = (0x01010101u & MM) | ((Ag + 0x01010101u) & ~MM);    // next age
-          const uint32_t AN = ((A & ~(Mg >> 3)) >> 4) * 0xFFu;                    // absent next
-          // a running cell outside the byte codes: lag above 14, a merged
-          // lag below 0 (V < 2), age above min(T_fail, 15)
-          badb |= (((ln + 0x71717171u) | (an + tfb)) & ~AN & 0x80808080u) | (Mg & ~(V + 0x7E7E7E7Eu));
-          O[h] = (((ln & 0x0F0F0F0Fu) << 4) | an) | AN;
-          // plane code of the written cell: l + 2 (14 = older), absent 15
-          uint32_t pq = ln + 0x02020202u;
-          const uint32_t OM = (((pq + 0x71717171u) & 0x80808080u) >> 7) * 0xFFu;
-          P[h] = ((pq & ~OM) | (0x0E0E0E0Eu & OM) | AN) & 0x0F0F0F0Fu;
-          mrg += __builtin_popcount(Mg);
-          gain += __builtin_popcount(Mg & (A << 3));
-        }
-        const bool own_in8 = (unsigned)(i - c0) < 8u;
-        const bool okb = lane_ok && !bad && !own_in8 && (w8.x & 0xFFu) != GH_C8_ESC && badb == 0 &&
-                         (nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu)) == 0;
-        if (__ballot(al && !okb) == 0) {
-          int dpres = 0;
-          if (al) {
-            const uint64_t v8 = ((uint64_t)O[1] << 32) | O[0];
-            uint64_t* hp = reinterpret_cast<uint64_t*>(h8n_t + ob8);
-            const uint32_t E = __builtin_amdgcn_perm(P[1], P[0], 0x06040200u);
-            const uint32_t Od = __builtin_amdgcn_perm(P[1], P[0], 0x07050301u);
-            const uint32_t pwd = __builtin_amdgcn_perm(Od | (Od >> 4), E | (E >> 4), 0x06040200u);
-            uint32_t* pp = reinterpret_cast<uint32_t*>(pln_t + (islot * (TW / 2) + lbp));
-            if constexpr (NT) {
-              __builtin_nontemporal_store(v8, hp);
-              __builtin_nontemporal_store(pwd, pp);
-            } else {
-              *hp = v8;
-              *pp = pwd;
-            }
-            n_mrg16 += 16u * (uint32_t)mrg;
-            dpres = gain;
-          }
-          if (__ballot(dpres != 0) != 0) {  // absent cells merged: the row's count moves
-#pragma unroll
-            for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) dpres += __shfl_xor(dpres, o2);
-            if (lc == 0 && dpres) atomicAdd(&d.cntl[i], dpres);
-          }
-          continue;
-        }
+        for (int q = 1; q < KB; ++q) L = pk_min_u16(L, pw[q] & M);
+        Lw |= L;
       }
+      const uint32_t lo = Lw & 0x0F0F0F0Fu, hi = (Lw >> 4) & 0x0F0F0F0Fu;
+      const uint32_t U[2] = {__builtin_amdgcn_perm(hi, lo, 0x06040200u), __builtin_amdgcn_perm(hi, lo, 0x07050301u)};
+      const uint32_t X[2] = {w8.x, w8.y};
+      const uint32_t D[2] = {d8.x, d8.y};
+      uint32_t O[2], P[2], B[2];
+      int mrg = 0, gain = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t x = X[h], u = U[h], dd = D[h];
+        const uint32_t L = (x >> 4) & 0x0F0F0F0Fu, Ag = x & 0x0F0F0F0Fu;
+        const uint32_t A = (L + 0x01010101u) & 0x10101010u;                     // own absent (0x10)
+        const uint32_t N = (u + 0x01010101u) & 0x10101010u;                     // no sender entry
+        const uint32_t Mg = ((L + 0x81818181u) - u) & ~(N << 3) & 0x80808080u;  // merged (0x80)
+        const uint32_t MM = (Mg >> 7) * 0xFFu;
+        const uint32_t V = u + dd;
+        const uint32_t ln = ((V - 0x02020202u) & MM) | ((L + dd) & ~MM);        // next lag
+        const uint32_t an = (0x01010101u & MM) | ((Ag + 0x01010101u) & ~MM);    // next age
+        const uint32_t AN = ((A & ~(Mg >> 3)) >> 4) * 0xFFu;                    // absent next
+        // a running cell outside the byte codes: lag above 14, a merged
+        // lag below 0 (V < 2), age above min(T_fail, 15)
+        B[h] = (((ln + 0x71717171u) | (an + tfb)) & ~AN & 0x80808080u) | (Mg & ~(V + 0x7E7E7E7Eu));
+        O[h] = (((ln & 0x0F0F0F0Fu) << 4) | an) | AN;
+        // plane code of the written cell: l + 2 (14 = older), absent 15
+        const uint32_t pq = ln + 0x02020202u;
+        const uint32_t OM = (((pq + 0x71717171u) & 0x80808080u) >> 7) * 0xFFu;
+        P[h] = ((pq & ~OM) | (0x0E0E0E0Eu & OM) | AN) & 0x0F0F0F0Fu;
+        mrg += __builtin_popcount(Mg);
+        gain += __builtin_popcount(Mg & (A << 3));
+      }
+      const int jd8 = i - c0;
+      if ((unsigned)jd8 < 8u) {
+        // the row's own member (step 3, :443-448): hb + 1 with a fresh stamp,
+        // never flagged; its snapshot entry carries hb + 1 (plane code - 1).
+        // Not visible, a guard row or at the heartbeat cap: the per-cell rule
+        const int h = jd8 >> 2, sh = 8 * (jd8 & 3);
+        const int xb = (int)((X[h] >> sh) & 0xFFu), ub = (int)((U[h] >> sh) & 0xFFu), db = (int)((D[h] >> sh) & 0xFFu);
+        const int lo8 = xb >> 4;
+        const bool mo = ub <= 13 && ub <= lo8;
+        const int ln8 = (mo ? ub - 2 : lo8 - 1) + db;
+        const bool ob8b = xb == 0xFF || !act || ln8 < 0 || ln8 > 14 ||
+                          (int64_t)bo[l0 + jd8] + (GH_C8_REF - lo8) >= INT32_MAX;
+        const uint32_t m8b = 0xFFu << sh;
+        const int c = min(ln8 + 2, 14);
+        O[h] = (O[h] & ~m8b) | ((uint32_t)(((ln8 & 15) << 4) | 1) << sh);
+        P[h] = (P[h] & ~m8b) | ((uint32_t)(c <= 13 ? c - 1 : c) << sh);
+        B[h] = (B[h] & ~m8b) | (ob8b ? 0x80u << sh : 0u);
+        mrg += (int)mo - (int)((U[h] >> sh & 0xFFu) <= (uint32_t)lo8 + 1u && ub != 15);
+      }
+      const bool okb = lane_ok && !bad && byte_lane && (w8.x & 0xFFu) != GH_C8_ESC && (B[0] | B[1]) == 0 &&
+                       (nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu)) == 0;
+      const bool seg_okb = (__ballot(al && !okb) & gmask) == 0;
+      int dpres = 0;
+      if (al && seg_okb) {
+        const uint64_t v8 = ((uint64_t)O[1] << 32) | O[0];
+        uint64_t* hp = reinterpret_cast<uint64_t*>(h8n_t + ob8);
+        const uint32_t E = __builtin_amdgcn_perm(P[1], P[0], 0x06040200u);
+        const uint32_t Od = __builtin_amdgcn_perm(P[1], P[0], 0x07050301u);
+        const uint32_t pwd = __builtin_amdgcn_perm(Od | (Od >> 4), E | (E >> 4), 0x06040200u);
+        uint32_t* pp = reinterpret_cast<uint32_t*>(pln_t + (islot * (TW / 2) + lbp));
+        if constexpr (NT) {
+          __builtin_nontemporal_store(v8, hp);
+          __builtin_nontemporal_store(pwd, pp);
+        } else {
+          *hp = v8;
+          *pp = pwd;
+        }
+        n_mrg16 += 16u * (uint32_t)mrg;
+        dpres = gain;
+      } else if (al && lc == 0) {
+        s_slow[atomicAdd(&s_nslow, 1)] = i;
+      }
+      if (__ballot(dpres != 0) != 0) {  // absent cells merged: the row's count moves
+#pragma unroll
+        for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) dpres += __shfl_xor(dpres, o2);
+        if (lc == 0 && dpres) atomicAdd(&d.cntl[i], dpres);
+      }
+      continue;
     }
     if (m8c) {  // widen the own chunk (an escaped one is hn's)
       if ((w8.x & 0xFFu) == GH_C8_ESC)
@@ -1292,7 +1317,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   __syncthreads();
   if (tid == 0) {  // read before the barrier above; the next tile's setup writes them after two more
     s_bmove = 0;
-    s_d8bad = 0;
+    s_d8bad = 0u;
   }
   for (int t = tid; t < TW; t += 256) {
     if (s_dcnt[t]) {
@@ -1329,25 +1354,32 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   }
 }
 
-// The variants are launched every round (lean on a 16-bit input, lean on an
-// 8-bit one when the engine keeps the tier, storm); the ones k_base and the
-// input's tier did not select return at once. The storm variant runs 1/8 of
-// the workgroups, each taking blocks a multiple of 8 apart (same XCD), so idle
-// it is a small dispatch.
-template <int KB, int TW, int TPW, bool NT, bool STORM, bool RD8>
+// The variants are launched every round (lean on a 16-bit input; in a
+// tiered engine also lean on an 8-bit input by the byte path and by the
+// 16-bit rule; storm); the ones k_base, the input's tier and the plane did
+// not select return at once. The byte path runs one block per workgroup; the
+// storm variant and the rarely selected lean ones of a tiered engine run 1/8
+// of the workgroups, each taking blocks a multiple of 8 apart (same XCD), so
+// idle they are a small dispatch.
+template <int KB, int TW, int TPW, bool NT, bool STORM, int IN>
 __global__ __launch_bounds__(256, (STORM && TW >= 32) ? 4 : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
   if (*d.mode != (int)STORM) return;
-  if (!STORM && gh_m8(d, cur) != RD8) return;
-  if constexpr (STORM) {
+  if constexpr (!STORM) {
+    int want = 0;
+    if (d.h8[0])
+      want = !gh_m8(d, cur) ? 3 : (KB == 4 && p.plane && d.pvalid[cur] && gh_m8(d, cur ^ 1)) ? 2 : 1;
+    if (want != IN) return;
+  }
+  if constexpr (STORM || IN == 1 || IN == 3) {
     constexpr int RB = round_rb<TW>();
     const int nblk = (int)((d.nrows + RB - 1) / RB) * ((int)(p.ld / TW) / TPW);
     for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
-      round_block<KB, TW, TPW, NT, STORM, RD8>(d, cur, dcur, p, b);
+      round_block<KB, TW, TPW, NT, STORM, IN>(d, cur, dcur, p, b);
       __syncthreads();  // LDS of this block before the next
     }
   } else {
     // one block per workgroup (a loop here costs the lean variants 20+ VGPRs)
-    round_block<KB, TW, TPW, NT, STORM, RD8>(d, cur, dcur, p, blockIdx.x);
+    round_block<KB, TW, TPW, NT, STORM, IN>(d, cur, dcur, p, blockIdx.x);
   }
 }
 
@@ -1760,34 +1792,41 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_inbox_fill, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
 }
 
-// variant: 0 lean on a 16-bit input, 1 storm, 2 lean on an 8-bit input
+// variant: 0 lean on a 16-bit input, 1 storm, 2 lean on an 8-bit input by
+// the 16-bit rule, 3 lean on an 8-bit input by the byte path
 template <int KB, int TW, int TPW>
 static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant) {
   constexpr int RB = round_rb<TW>();
   const int64_t nrb = (d.nrows + RB - 1) / RB;
   const int64_t nblk = nrb * (p.ld / TW / TPW);
   if (nblk == 0) return;
-  const dim3 grid((unsigned)(variant == 1 ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
-#define GH_ROUND_LAUNCH(NT, ST, R8) \
-  hipLaunchKernelGGL((k_round<KB, TW, TPW, NT, ST, R8>), grid, blk, 0, s, d, cur, dcur, p)
-  if constexpr (KB == 4 && TPW == 1) {
-    if (variant == 2) {
-      if (nt)
-        GH_ROUND_LAUNCH(true, false, true);
-      else
-        GH_ROUND_LAUNCH(false, false, true);
-      return;
+  const bool tiered = d.h8[0] != nullptr;
+  const bool few = variant == 1 || variant == 2 || (variant == 0 && tiered);
+  const dim3 grid((unsigned)(few ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
+#define GH_ROUND_LAUNCH(NT, ST, IN) \
+  hipLaunchKernelGGL((k_round<KB, TW, TPW, NT, ST, IN>), grid, blk, 0, s, d, cur, dcur, p)
+#define GH_ROUND_NT(ST, IN)        \
+  do {                             \
+    if (nt)                        \
+      GH_ROUND_LAUNCH(true, ST, IN);  \
+    else                           \
+      GH_ROUND_LAUNCH(false, ST, IN); \
+  } while (0)
+  if constexpr (KB == 4 && TPW == 1 && TW >= 64) {  // a tiered engine (host: c8)
+    if (tiered) {
+      switch (variant) {
+        case 0: GH_ROUND_NT(false, 3); return;
+        case 2: GH_ROUND_NT(false, 1); return;
+        case 3: GH_ROUND_NT(false, 2); return;
+        default: break;
+      }
     }
   }
-  if (variant == 2) return;  // no 8-bit tier here (host: c8 needs pull k <= 4, TPW 1)
-  if (nt && variant == 1)
-    GH_ROUND_LAUNCH(true, true, false);
-  else if (nt)
-    GH_ROUND_LAUNCH(true, false, false);
-  else if (variant == 1)
-    GH_ROUND_LAUNCH(false, true, false);
-  else
-    GH_ROUND_LAUNCH(false, false, false);
+  if (variant == 1)
+    GH_ROUND_NT(true, 0);
+  else if (variant == 0)
+    GH_ROUND_NT(false, 0);
+#undef GH_ROUND_NT
 #undef GH_ROUND_LAUNCH
 }
 

@@ -74,9 +74,12 @@ def lagging_state(n, seed):
 
 
 @pytest.mark.parametrize("k", [3, 4])
-def test_plane_fallback_exact(gs, oracle_mod, k):
+def test_plane_fallback_exact(gs, oracle_mod, k, monkeypatch):
     """Views far outside the plane's window force 16-bit gathers (fallback
-    waves > 0) while the plane is valid; every round stays bit-exact."""
+    waves > 0) while the plane is valid; every round stays bit-exact. (The
+    8-bit tier's byte path sends such rows to the per-cell kernel instead:
+    GH_C8=0 here; tests/test_gpu_tier8.py covers the tier.)"""
+    monkeypatch.setenv("GH_C8", "0")
     n = 1024
     cfg = dict(fanout=k, seed=0x5EED0100 + k, t_fail=60, t_cleanup=60)
     eng = gs.Engine(gs.default_config(n, **cfg))
