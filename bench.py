@@ -423,7 +423,12 @@ def main():
         return
     value = args.steps / elapsed
     # bytes of one k_round launch (this rank's columns)
-    b_compulsory = 2.0 * cell_bytes * nrows_r * ncols  # each cell read once and written once
+    # compulsory bytes of one launch: each table cell read once and written
+    # once, and the sender plane (4 bits per cell) written once and read
+    # once -- the least the round's data structures move through HBM
+    b_table = 2.0 * cell_bytes * nrows_r * ncols
+    b_plane = 1.0 * nrows_r * ncols if plane else 0.0
+    b_compulsory = b_table + b_plane
     b_gather = 2.0 * nrows_r * ncols * k       # the k sender segments per cell (L2 / Infinity Cache / HBM)
     b_survey = 4.0 * nrows_r * ncols * (k + 4)  # SURVEY.md §8d (int32 hb + ts streams)
     traffic = pmc_traffic(n, k, world, args.warmup, plane, tile_w, cell_bytes)
@@ -463,8 +468,10 @@ def main():
             "traffic": traffic["traffic_bytes"] if traffic else None,
             "traffic_source": traffic["source"] if traffic else None,
             "bytes_per_launch": b_compulsory,
-            "bytes_model": (f"compulsory: {2 * cell_bytes}*N*ncols ({cell_bytes}-byte cells read + written once"
-                            + (": the 8-bit tier, escaped chunks in 16 bits)" if tier8 else ")")),
+            "bytes_model": (f"compulsory: {2 * cell_bytes + (1 if plane else 0)}*N*ncols ({cell_bytes}-byte cells "
+                            "read + written once" + (" (the 8-bit tier; escaped chunks in 16 bits)" if tier8 else "")
+                            + (", 4-bit sender plane written + read once" if plane else "") + ")"),
+            "table_bytes_per_launch": b_table, "plane_bytes_per_launch": b_plane,
             "avg_launch_ms": avg_s * 1e3, "launches": launches,
             "gather_bytes_per_launch": b_gather, "gather_achieved": b_gather / avg_s / 1e9,
             "survey_bytes_per_launch": b_survey,

@@ -46,7 +46,7 @@ out["config"] = {"n": n, "k": k, "world": 1, "cell_bytes": cb, "warmup": warmup,
                  "plane": plane, "tile_width": tw,
                  "command": f"python3 bench.py --steps {steps} --warmup {warmup} --no-cpu-baseline --no-secondary "
                             "--files 0"}
-out["compulsory_bytes"] = 2.0 * cb * n * n
+out["compulsory_bytes"] = (2.0 * cb + (1.0 if plane else 0.0)) * n * n  # table in + out, plane out + in
 out["gather_bytes"] = 2.0 * n * n * k
 if "traffic_bytes" in out:
     out["traffic_over_compulsory"] = out["traffic_bytes"] / out["compulsory_bytes"]
