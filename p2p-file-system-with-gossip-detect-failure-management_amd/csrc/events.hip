@@ -267,6 +267,10 @@ __global__ __launch_bounds__(256) void k_freeze_mark(GhDev d, const int32_t* row
       *reinterpret_cast<uint2*>(d.h8[0] + off) = GH_C8_ESC2;
       *reinterpret_cast<uint2*>(d.h8[1] + off) = GH_C8_ESC2;
     }
+    if (d.pl[0]) {  // never a sender: its plane words say unknown
+      d.pl[0][off >> 3] = 0u;
+      d.pl[1][off >> 3] = 0u;
+    }
   }
 }
 

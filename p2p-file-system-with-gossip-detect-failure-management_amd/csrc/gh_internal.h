@@ -79,9 +79,10 @@
 //                  GH_PLANE_MIN_N); read by
 //                  k_round's lean variant, whose sender gathers become one 128-B
 //                  line per 256 members at TW = 256. A wave falls back to the
-//                  16-bit gathers when a min is 0 or 14. pvalid[b] = 0 once
-//                  anything but a round wrote buffer b (events, imports, list
-//                  merges, the quirk pre-pass).
+//                  16-bit gathers when a min is 0 or 14. Every writer of a
+//                  chunk keeps its plane word (gh_put8, gh_clearflags8; a
+//                  stopped row's words are 0); pvalid[b] = 0 after whole-table
+//                  rewrites (imports, fill) and the list-order quirk pass.
 //   h8[2]  uint8   8-BIT TIER beside each narrow buffer (c8 engines: plane
 //                  mode, column layout), one byte per cell in the narrow
 //                  table's tiled order. While m8[b] = 1 the 8-cell chunk at
@@ -344,6 +345,31 @@ __device__ __forceinline__ uint32_t pk_zero_mask(uint32_t a) {
 __device__ __forceinline__ uint32_t pk_lshr16(uint32_t a, int k) { return as_u(as_us(a) >> (unsigned short)k); }
 __device__ __forceinline__ uint32_t pk_shl16(uint32_t a, int k) { return as_u(as_us(a) << (unsigned short)k); }
 
+// ---- sender snapshot plane (pl) ---------------------------------------------
+// The plane word of 8 written narrow codes o (an all-narrow chunk); jd = the
+// row's own member in the chunk (0..7) or -1: its snapshot entry carries
+// hb + 1 (the heartbeat the row sends with next round).
+__device__ __forceinline__ uint32_t plane_word(const v4u& o, int jd) {
+  uint32_t wd = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t y = o[j];
+    // u = REF + 1 - offset, clamped to [0, 14]; not visible (bit 15): 15
+    const uint32_t u = pk_sub_u16((uint32_t)(GH_P_REF + 1) * 0x10001u, pk_lshr16(y, 5));
+    uint32_t code = pk_min_u16(pk_max_i16(u, 0u), GH_P_OLD * 0x10001u);
+    code |= pk_sra15(y) & (GH_P_NONE * 0x10001u);
+    wd |= code << (4 * j);
+  }
+  if (jd >= 0) {
+    // offset + 1 on the diagonal: an exact code moves one down (1 = at the
+    // reference becomes unknown); unknown, old and not-visible stay
+    const int pos = 4 * (jd >> 1) + 16 * (jd & 1);
+    const uint32_t c = (wd >> pos) & 0xFu;
+    const uint32_t c2 = (c >= 2u && c <= 13u) ? c - 1u : (c == 1u ? 0u : c);
+    wd = (wd & ~(0xFu << pos)) | (c2 << pos);
+  }
+  return wd;
+}
 // ---- 8-bit tier (h8) -------------------------------------------------------
 // 16-bit codes of two 8-bit codes t (bytes in bits 0-7 and 16-23):
 // offset GH_C8_REF - l, age; 0xFF -> absent.
@@ -547,6 +573,10 @@ __device__ __forceinline__ void gh_clearflags8(const GhDev& d, int buf, int64_t 
   for (int j = 0; j < 8; ++j)
     if ((m >> j) & 1u) w[j >> 1] &= ~(0x8000u << (16 * (j & 1)));
   *np = uint4{w[0], w[1], w[2], w[3]};
+  if (d.pl[buf]) {  // cleared flags make cells visible to the row's peers
+    const int64_t jd = i - (d.col0 + c);
+    d.pl[buf][cell >> 3] = plane_word(v4u{w[0], w[1], w[2], w[3]}, (uint64_t)jd < 8u ? (int)jd : -1);
+  }
 }
 
 // Writes 8 cells of one chunk (i, c..c+7) of buffer buf: narrow codes nx
@@ -555,6 +585,12 @@ __device__ __forceinline__ void gh_clearflags8(const GhDev& d, int buf, int64_t 
 __device__ __forceinline__ void gh_put8(const GhDev& d, int buf, int64_t i, int64_t c, bool narrow, const uint4& nx,
                                         int64_t slot, const GhCell v[8]) {
   const int64_t cell = gh_cell(d, i, c);
+  // the chunk's sender plane word follows it (a wide chunk: unknown), so a
+  // host write leaves the plane valid
+  if (d.pl[buf]) {
+    const int64_t jd = i - (d.col0 + c);
+    d.pl[buf][cell >> 3] = narrow ? plane_word(v4u{nx.x, nx.y, nx.z, nx.w}, (uint64_t)jd < 8u ? (int)jd : -1) : 0u;
+  }
   if (narrow) {
     gh_st16(d, buf, cell, nx);
     return;

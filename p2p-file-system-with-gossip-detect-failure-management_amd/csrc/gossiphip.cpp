@@ -54,9 +54,12 @@ struct Engine {
   // the current table may hold flags no round kernel counted (import, fill,
   // events, list merges): the next quirk pre-pass runs ungated
   bool qforce = true;
-  // the current table was written by something other than a round: its
-  // sender plane is stale (pvalid[cur] = 0 before the next round)
+  // the current table was rewritten whole outside a round (import, fill):
+  // its sender plane is stale (pvalid[cur] = 0 before the next round). Events
+  // and list merges keep the plane (gh_put8 writes each chunk's plane word)
   bool pforce = true;
+  // the table was written outside a round: no row is a quiet candidate
+  bool sforce = true;
   // row layout (GH_LAYOUT_ROWS): rows per shard, host mirror of rslot, the
   // current ghost rows, exchange buffers (grown on demand)
   bool rowlay = false;
@@ -512,7 +515,7 @@ int process_events(Engine* e, int32_t r) {
   if (e->pending.empty()) return GH_OK;
   e->qforce = true;
   e->flags_known = false;
-  e->pforce = true;
+  e->sforce = true;
   const GhRound p = round_params(e, r);
   std::vector<gh_event> ev;
   ev.swap(e->pending);
@@ -1318,10 +1321,14 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     const int32_t r = e->round + 1;
     int rc;
     if ((rc = process_events(e, r))) return rc;
-    if (e->pforce) {  // the table was written outside a round: no valid plane, no quiet rows
+    if (e->pforce) {  // the table was rewritten outside a round: no valid plane
       HIPCHK(e, hipMemsetAsync(e->d.pvalid + e->cur, 0, sizeof(int32_t), e->stream));
-      for (int b = 0; b < 2; ++b) HIPCHK(e, hipMemsetAsync(e->d.stab[b], 0, e->n, e->stream));
       e->pforce = false;
+      e->sforce = true;
+    }
+    if (e->sforce) {  // written outside a round: no quiet rows
+      for (int b = 0; b < 2; ++b) HIPCHK(e, hipMemsetAsync(e->d.stab[b], 0, e->n, e->stream));
+      e->sforce = false;
     }
     const GhRound p = round_params(e, r);
     if (e->hb_bound >= INT32_MAX) {
@@ -1533,7 +1540,7 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
   if ((rc0 = check_lost(e)) || (rc0 = maybe_grow(e))) return rc0;
   e->qforce = true;
   e->flags_known = false;
-  e->pforce = true;
+  e->sforce = true;
   int32_t cnt = 0;
   if (n > 0 && e->alive[observer]) {  // GetMsg runs only while Alive (slave/slave.go:208)
     Staging st;

@@ -500,30 +500,8 @@ __device__ __forceinline__ uint32_t pair_bits(uint32_t m, int j) {
 }
 
 // ---- sender snapshot plane (gh_internal.h: pl) ---------------------------
-// The plane word of 8 written narrow codes o (an all-narrow chunk); jd = the
-// row's own member in the chunk (0..7) or -1: its snapshot entry carries
-// hb + 1 (the heartbeat the row sends with next round).
-__device__ __forceinline__ uint32_t plane_word(const v4u& o, int jd) {
-  uint32_t wd = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t y = o[j];
-    // u = REF + 1 - offset, clamped to [0, 14]; not visible (bit 15): 15
-    const uint32_t u = pk_sub_u16((uint32_t)(GH_P_REF + 1) * 0x10001u, pk_lshr16(y, 5));
-    uint32_t code = pk_min_u16(pk_max_i16(u, 0u), GH_P_OLD * 0x10001u);
-    code |= pk_sra15(y) & (GH_P_NONE * 0x10001u);
-    wd |= code << (4 * j);
-  }
-  if (jd >= 0) {
-    // offset + 1 on the diagonal: an exact code moves one down (1 = at the
-    // reference becomes unknown); unknown, old and not-visible stay
-    const int pos = 4 * (jd >> 1) + 16 * (jd & 1);
-    const uint32_t c = (wd >> pos) & 0xFu;
-    const uint32_t c2 = (c >= 2u && c <= 13u) ? c - 1u : (c == 1u ? 0u : c);
-    wd = (wd & ~(0xFu << pos)) | (c2 << pos);
-  }
-  return wd;
-}
+// 0xFF in each byte of m that has bit 7 set (m: 0x80 / 0x00 bytes), no multiply
+__device__ __forceinline__ uint32_t bmask(uint32_t m) { return m | (m - (m >> 7)); }
 // nonzero iff a nibble of a is zero (exact when no nibble is zero; a
 // borrow can only add bits above a zero nibble)
 __device__ __forceinline__ uint32_t nib_haszero(uint32_t a) { return (a - 0x11111111u) & ~a & 0x88888888u; }
@@ -954,24 +932,25 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         const uint32_t A = (L + 0x01010101u) & 0x10101010u;                     // own absent (0x10)
         const uint32_t N = (u + 0x01010101u) & 0x10101010u;                     // no sender entry
         const uint32_t Mg = ((L + 0x81818181u) - u) & ~(N << 3) & 0x80808080u;  // merged (0x80)
-        const uint32_t MM = (Mg >> 7) * 0xFFu;
+        const uint32_t MM = bmask(Mg);
         const uint32_t V = u + dd;
         const uint32_t ln = ((V - 0x02020202u) & MM) | ((L + dd) & ~MM);        // next lag
         const uint32_t an = (0x01010101u & MM) | ((Ag + 0x01010101u) & ~MM);    // next age
-        const uint32_t AN = ((A & ~(Mg >> 3)) >> 4) * 0xFFu;                    // absent next
+        const uint32_t AN = bmask((A & ~(Mg >> 3)) << 3);                       // absent next
         // a running cell outside the byte codes: lag above 14, a merged
         // lag below 0 (V < 2), age above min(T_fail, 15)
         B[h] = (((ln + 0x71717171u) | (an + tfb)) & ~AN & 0x80808080u) | (Mg & ~(V + 0x7E7E7E7Eu));
         O[h] = (((ln & 0x0F0F0F0Fu) << 4) | an) | AN;
         // plane code of the written cell: l + 2 (14 = older), absent 15
         const uint32_t pq = ln + 0x02020202u;
-        const uint32_t OM = (((pq + 0x71717171u) & 0x80808080u) >> 7) * 0xFFu;
+        const uint32_t OM = bmask((pq + 0x71717171u) & 0x80808080u);
         P[h] = ((pq & ~OM) | (0x0E0E0E0Eu & OM) | AN) & 0x0F0F0F0Fu;
         mrg += __builtin_popcount(Mg);
         gain += __builtin_popcount(Mg & (A << 3));
       }
       const int jd8 = i - c0;
-      if ((unsigned)jd8 < 8u) {
+      // (a wave-uniform branch: 1 wave in 256 holds an own member)
+      if (__ballot((unsigned)jd8 < 8u) != 0 && (unsigned)jd8 < 8u) {
         // the row's own member (step 3, :443-448): hb + 1 with a fresh stamp,
         // never flagged; its snapshot entry carries hb + 1 (plane code - 1).
         // Not visible, a guard row or at the heartbeat cap: the per-cell rule
@@ -1506,12 +1485,7 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
         const int64_t sl = lc == 0 ? gh_wide_alloc(d, nxt) : 0;
         slot = __shfl(sl, sub * SEG);
       }
-      if (slot >= 0) gh_put8(d, nxt, i, l0, narrow, nx, slot, o);
-      if (p.plane) {  // the sender plane of the segment (wide: unknown, 0)
-        const int64_t jd = (int64_t)i - c0;
-        d.pl[nxt][gh_cell(d, i, l0) >> 3] =
-            narrow ? plane_word(v4u{nx.x, nx.y, nx.z, nx.w}, (uint64_t)jd < 8u ? (int)jd : -1) : 0u;
-      }
+      if (slot >= 0) gh_put8(d, nxt, i, l0, narrow, nx, slot, o);  // with its plane word (wide: unknown, 0)
     }
 #pragma unroll
     for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) {
@@ -1658,9 +1632,7 @@ __global__ __launch_bounds__(256) void k_quirk_carry(GhDev d, GhRound p) {
 template <int TW>
 __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur, GhRound p) {
   if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no candidate in any shard's table
-  // cleared flags make cells visible that the sender plane lists as not in
-  // the snapshot: this round gathers 16-bit codes
-  if (blockIdx.x == 0 && threadIdx.x == 0) d.pvalid[cur] = 0;
+  // (gh_clearflags8 rewrites the plane words of the chunks it changes)
   constexpr int SEG = SegWalk<TW>::SEG;
   const SegWalk<TW> w(d, p);
   for (int64_t base = w.first; base < w.nseg; base += w.stride) {
