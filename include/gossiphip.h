@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GH_ABI_VERSION 4
+#define GH_ABI_VERSION 5
 
 /* ---- error codes ---------------------------------------------------- */
 #define GH_OK 0
@@ -128,9 +128,11 @@ typedef struct gh_plan_entry {
 void gh_config_default(gh_config* cfg);
 
 /* Replaces InitSlave/InitMaster (slave/slave.go:95, master/master.go:38) for
- * N members at once. HBM: the 16-bit narrow table (x2), 4*N*N bytes, plus the
- * wide-segment arenas (gh_config.wide_segments) and a frozen store for
- * stopped rows that grows with them (gh_memory_info). */
+ * N members at once. HBM: the 16-bit narrow table (x2), 4*N*N bytes; in pull
+ * mode with 3 <= k <= 4 from N = 16,384 the sender plane (x2, N*N bytes) and
+ * the 8-bit tier (x2, 2*N*N bytes); plus the wide-segment arenas
+ * (gh_config.wide_segments) and a frozen store for stopped rows that grows
+ * with them (gh_memory_info). */
 int gh_create(const gh_config* cfg, void** handle);
 void gh_destroy(void* h);
 const char* gh_last_error(void* h);
@@ -286,10 +288,12 @@ int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, in
 int gh_plane_info(void* h, int32_t* enabled, int32_t* valid, int64_t* fallback_waves);
 /* 8-bit tier (diagnostic; DESIGN.md "8-bit tier"): whether the engine keeps
  * one (plane mode, column layout; GH_C8=0 drops it), whether the current
- * table is held in it (8-bit chunks, escaped chunks in 16 bits), and how many
- * chunks the last round's packed path wrote escaped. Any output may be NULL.
- * No reference counterpart. */
-int gh_tier_info(void* h, int32_t* enabled, int32_t* current_8bit, int64_t* escaped_chunks);
+ * table is held in it (8-bit chunks, escaped chunks in 16 bits), how many
+ * chunks the last round's packed 16-bit path wrote escaped, and the round
+ * kernel variant of the last round (0 lean on a 16-bit input, 1 storm, 2
+ * lean on an 8-bit input widened to 16 bits, 3 the byte path). Any output may
+ * be NULL. No reference counterpart. */
+int gh_tier_info(void* h, int32_t* enabled, int32_t* current_8bit, int64_t* escaped_chunks, int32_t* last_variant);
 /* Row layout (GH_LAYOUT_ROWS): the last ghost-row exchange of this shard --
  * the sender rows it received, and the bytes it sent and received by
  * alltoallv (narrow codes, plane words, wide segments). Zero in the column

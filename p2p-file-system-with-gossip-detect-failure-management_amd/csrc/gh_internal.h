@@ -208,7 +208,8 @@ struct GhDev {
   int32_t *pvf;     // row layout: [n][k] validity of each receiver's draws (summed over shards)
   uint16_t *hn[2];  // narrow double buffer
   uint8_t *h8[2];   // 8-bit tier per buffer (null: tier off)
-  int32_t *m8;      // [0..1] buffer b is in the 8-bit tier; [2] this round switches the next buffer's tier
+  int32_t *m8;      // [0..1] buffer b is in the 8-bit tier; [2] this round switches the next buffer's tier;
+                    // [3] escaped chunks the round wrote; [4] the round variant that ran (gh_tier_info)
   uint32_t *pl[2];  // sender snapshot plane per buffer (null: plane off)
   int32_t *pvalid;  // [2]: plane of buffer b written by the round that wrote b
   int32_t *pfb;     // waves of the last round that gathered 16-bit codes with a valid plane

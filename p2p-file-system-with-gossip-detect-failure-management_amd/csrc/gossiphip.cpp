@@ -833,7 +833,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
       break;
     // 8-bit tier: every chunk escaped, both buffers 16-bit until a round
     // writes one
-    if ((rc = dalloc(e, &d.m8, 4, 0))) break;
+    if ((rc = dalloc(e, &d.m8, 8, 0))) break;
     if (e->c8 && ((rc = dalloc(e, &d.h8[0], cells, GH_C8_ESC)) || (rc = dalloc(e, &d.h8[1], cells, GH_C8_ESC))))
       break;
     if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
@@ -1151,16 +1151,17 @@ int gh_plane_info(void* h, int32_t* enabled, int32_t* valid, int64_t* fallback_w
   return GH_OK;
 }
 
-int gh_tier_info(void* h, int32_t* enabled, int32_t* current_8bit, int64_t* escaped_chunks) {
+int gh_tier_info(void* h, int32_t* enabled, int32_t* current_8bit, int64_t* escaped_chunks, int32_t* last_variant) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
   HIPCHK(e, hipSetDevice(e->cfg.device));
-  int32_t v[4] = {0, 0, 0, 0};
+  int32_t v[5] = {0, 0, 0, 0, 0};
   HIPCHK(e, hipMemcpyAsync(v, e->d.m8, sizeof v, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   if (enabled) *enabled = e->c8;
   if (current_8bit) *current_8bit = e->c8 ? v[e->cur] : 0;
   if (escaped_chunks) *escaped_chunks = e->c8 ? v[3] : 0;
+  if (last_variant) *last_variant = v[4];
   return GH_OK;
 }
 

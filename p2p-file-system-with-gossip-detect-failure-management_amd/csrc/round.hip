@@ -1349,6 +1349,7 @@ __global__ __launch_bounds__(256, (STORM && TW >= 32) ? 4 : 1) void k_round(GhDe
       want = !gh_m8(d, cur) ? 3 : (KB == 4 && p.plane && d.pvalid[cur] && gh_m8(d, cur ^ 1)) ? 2 : 1;
     if (want != IN) return;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.m8[4] = STORM ? 1 : IN == 2 ? 3 : IN == 1 ? 2 : 0;
   if constexpr (STORM || IN == 1 || IN == 3) {
     constexpr int RB = round_rb<TW>();
     const int nblk = (int)((d.nrows + RB - 1) / RB) * ((int)(p.ld / TW) / TPW);

@@ -114,12 +114,14 @@ class Engine:
         self._chk(self.lib.gh_plane_info(self.h, C.byref(en), C.byref(va), C.byref(fb)))
         return en.value, va.value, fb.value
 
-    def tier_info(self):
+    def tier_info(self, full=False):
         """(8-bit tier kept, current table held in it, chunks the last round's
-        packed path wrote escaped in 16 bits) -- gh_tier_info, diagnostic."""
-        en, cu, esc = C.c_int32(), C.c_int32(), C.c_int64()
-        self._chk(self.lib.gh_tier_info(self.h, C.byref(en), C.byref(cu), C.byref(esc)))
-        return en.value, cu.value, esc.value
+        packed 16-bit path wrote escaped) -- gh_tier_info, diagnostic;
+        full=True adds the last round's kernel variant (0 lean on a 16-bit
+        input, 1 storm, 2 lean on an 8-bit input widened, 3 the byte path)."""
+        en, cu, esc, var = C.c_int32(), C.c_int32(), C.c_int64(), C.c_int32()
+        self._chk(self.lib.gh_tier_info(self.h, C.byref(en), C.byref(cu), C.byref(esc), C.byref(var)))
+        return (en.value, cu.value, esc.value, var.value) if full else (en.value, cu.value, esc.value)
 
     def exchange_info(self):
         """dict(ghost_rows, bytes_out, bytes_in) of this shard's last ghost-row

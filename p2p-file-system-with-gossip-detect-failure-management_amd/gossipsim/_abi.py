@@ -97,7 +97,7 @@ SYMBOLS = [
     ("gh_shard_info", C.c_int, [_vp, _P(_i32), _P(_i32), _P(_i64), _P(_i64)]),
     ("gh_encoding_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i32), _P(_i64), _P(_i64)]),
     ("gh_plane_info", C.c_int, [_vp, _P(_i32), _P(_i32), _P(_i64)]),
-    ("gh_tier_info", C.c_int, [_vp, _P(_i32), _P(_i32), _P(_i64)]),
+    ("gh_tier_info", C.c_int, [_vp, _P(_i32), _P(_i32), _P(_i64), _P(_i32)]),
     ("gh_exchange_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i64)]),
     ("gh_memory_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i64), _P(_i64)]),
 ]

@@ -203,3 +203,41 @@ def test_tier_placement(gs, oracle_mod):
     eng, orc = run_parity(gs, oracle_mod, dict(fanout=4, seed=0x5EED0910, t_fail=7, t_cleanup=7, max_files=2048),
                           n, 28, sched, init=sc.full_state(n), files=files)
     assert eng.tier_info()[0] == 1
+
+
+def test_tier_plane_kept_across_events(gs, oracle_mod):
+    """Crashes, a join and a datagram merge between rounds keep the sender
+    plane valid (every chunk writer rewrites its plane word), so the round
+    after them runs the byte path: only the rows the events touched go to the
+    per-cell kernel. Bit-exact against the oracle every round."""
+    n = 2048
+    cfg = dict(fanout=4, seed=0x5EED0A10, t_fail=16, t_cleanup=16)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    hb, ts, alive = sc.full_state(n)
+    eng.import_state(hb, ts, alive, 0)
+    orc.import_state(hb, ts, alive, 0)
+    # (a LEAVE tombstones its column in every row: the storm variant's case)
+    sched = {10: [(sc.CRASH, 33), (sc.CRASH, 900)], 12: [(sc.JOIN, 33)]}
+    slow_after = []
+    for r in range(1, 16):
+        ev = sched.get(r, [])
+        if ev:
+            eng.apply_events(ev)
+            orc.apply_events(ev)
+            assert eng.plane_info()[1] == 1, r  # still valid before the round
+        if r == 11:
+            ids = np.arange(0, n, 5, dtype=np.int32)
+            vals = np.full(len(ids), 9, np.int32)
+            assert eng.merge_list(7, ids, vals) == orc.merge_list(7, ids, vals)
+            assert eng.plane_info()[1] == 1
+        s1, s2 = eng.step(1), orc.step(1)
+        assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
+        compare(eng, orc, r)
+        if r in (10, 11, 12):
+            slow_after.append(eng.encoding_info()[1])
+            assert eng.tier_info(full=True)[3] == 3, r  # the byte path ran
+        assert eng.tier_info()[1] == 1, r
+    # the rounds after the events list a few rows' segments, not the table
+    segs = (n // 256) * n
+    assert max(slow_after) < segs // 4, (slow_after, segs)
