@@ -819,6 +819,152 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   }
 
   constexpr int NIT = RB / RSTEP;
+  if constexpr (BYTE) {
+    // THE BYTE PATH (IN = 2: 8-bit tier in and out with a valid plane, the
+    // column layout, KB = 4; the 16-bit rule is not compiled into this
+    // instantiation): the lean rule on the one-byte cells themselves, four
+    // per dword (SWAR), no widening. Per cell: l = lag (GH_C8_REF - offset),
+    // a = age; the freshest sender's plane code u = l_s + 2 (gh_internal.h:
+    // GH_P_REF = GH_C8_REF + 1) merges iff l_s < l (u <= l + 1; an absent own
+    // cell, l = 15, takes any sender; u = 15 = no sender entry). Merged: lag
+    // u - 2, age 1; else age + 1; then the rebase l += base move. The row's
+    // own member (step 3): hb + 1, age 1, merged only by a larger snapshot
+    // (u <= l). A row segment whose every lane stays in the byte codes (lag
+    // 0..14, age <= min(T_fail, 15): no flag, no REMOVE, no guard row, no
+    // escape, plane codes exact) is written here; any other goes to the slow
+    // list (k_round_slow, the per-cell rule). Two row steps per iteration:
+    // both steps' loads are issued before either is computed.
+    static_assert(KB == 4 && NIT % 2 == 0, "byte path: 4 senders, an even row-step count");
+#pragma unroll 1
+    for (int it = 0; it < NIT; it += 2) {
+      int iu[2];
+      bool alu[2], oku[2];
+      uint32_t slu[2];
+      uint2 w8u[2];
+      uint32_t pwu[2][4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int rr = wave * RPW + (it + u) * RSTEP + sub;
+        const int i_raw = (int)d.row0 + rb * RB + rr;
+        const bool valid = i_raw < rowend;
+        const int i = valid ? i_raw : rowend - 1;  // in-range row for the loads of idle lanes
+        const int rs = valid ? rr : 0;
+        const int meta = s_meta[rs];
+        const bool skip = ((meta >> 30) & 1) && tile_still;  // quiet row, bases still
+        if (valid && skip && lc == 0) atomicAdd(&s_quiet, 1);
+        const int cntv = (meta >> 2) & 0xFFFF;
+        alu[u] = (meta & 1) && valid && !skip;
+        oku[u] = ((meta >> 1) & 1) && cntv <= KB;  // active (not a guard row), at most KB senders
+        iu[u] = i;
+        const uint32_t islot = (uint32_t)(i - d.row0);
+        slu[u] = islot;
+        w8u[u] = *reinterpret_cast<const uint2*>(h8o_t + (islot * TW + lb8));
+        const int4 v = *reinterpret_cast<const int4*>(&s_inb[rs * KB]);
+        const int sv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          // unused slots read the own row's codes (a no-op under the merge)
+          const uint32_t sq = q < cntv ? (uint32_t)sv[q] : islot;
+          pwu[u][q] = *reinterpret_cast<const uint32_t*>(plo_t + (sq * (TW / 2) + lbp));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = iu[u];
+        const bool al = alu[u];
+        const uint2 w8 = w8u[u];
+        const uint32_t* pw = pwu[u];
+        uint32_t Lw = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t M = 0x000F000Fu << (4 * j);
+          uint32_t L = pw[0] & M;
+#pragma unroll
+          for (int q = 1; q < 4; ++q) L = pk_min_u16(L, pw[q] & M);
+          Lw |= L;
+        }
+        const uint32_t lo = Lw & 0x0F0F0F0Fu, hi = (Lw >> 4) & 0x0F0F0F0Fu;
+        const uint32_t U[2] = {__builtin_amdgcn_perm(hi, lo, 0x06040200u), __builtin_amdgcn_perm(hi, lo, 0x07050301u)};
+        const uint32_t X[2] = {w8.x, w8.y};
+        const uint32_t D[2] = {d8.x, d8.y};
+        uint32_t O[2], P[2], B[2];
+        int mrg = 0, gain = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t x = X[h], uu = U[h], dd = D[h];
+          const uint32_t L = (x >> 4) & 0x0F0F0F0Fu, Ag = x & 0x0F0F0F0Fu;
+          const uint32_t A = (L + 0x01010101u) & 0x10101010u;                      // own absent (0x10)
+          const uint32_t N = (uu + 0x01010101u) & 0x10101010u;                     // no sender entry
+          const uint32_t Mg = ((L + 0x81818181u) - uu) & ~(N << 3) & 0x80808080u;  // merged (0x80)
+          const uint32_t MM = bmask(Mg);
+          const uint32_t V = uu + dd;
+          const uint32_t ln = ((V - 0x02020202u) & MM) | ((L + dd) & ~MM);         // next lag
+          const uint32_t an = (0x01010101u & MM) | ((Ag + 0x01010101u) & ~MM);     // next age
+          const uint32_t AN = bmask((A & ~(Mg >> 3)) << 3);                        // absent next
+          // a running cell outside the byte codes: lag above 14, a merged
+          // lag below 0 (V < 2), age above min(T_fail, 15)
+          B[h] = (((ln + 0x71717171u) | (an + tfb)) & ~AN & 0x80808080u) | (Mg & ~(V + 0x7E7E7E7Eu));
+          O[h] = (((ln & 0x0F0F0F0Fu) << 4) | an) | AN;
+          // plane code of the written cell: l + 2 (14 = older), absent 15
+          const uint32_t pq = ln + 0x02020202u;
+          const uint32_t OM = bmask((pq + 0x71717171u) & 0x80808080u);
+          P[h] = ((pq & ~OM) | (0x0E0E0E0Eu & OM) | AN) & 0x0F0F0F0Fu;
+          mrg += __builtin_popcount(Mg);
+          gain += __builtin_popcount(Mg & (A << 3));
+        }
+        const int jd8 = i - c0;
+        // (a wave-uniform branch: 1 wave in 256 holds an own member)
+        if (__ballot((unsigned)jd8 < 8u) != 0 && (unsigned)jd8 < 8u) {
+          // the row's own member (step 3, :443-448): hb + 1 with a fresh
+          // stamp, never flagged; its snapshot entry carries hb + 1 (plane
+          // code - 1). Not visible, a guard row or at the heartbeat cap: the
+          // per-cell rule
+          const int h = jd8 >> 2, sh = 8 * (jd8 & 3);
+          const int xb = (int)((X[h] >> sh) & 0xFFu), ub = (int)((U[h] >> sh) & 0xFFu),
+                    db = (int)((D[h] >> sh) & 0xFFu);
+          const int lo8 = xb >> 4;
+          const bool mo = ub <= 13 && ub <= lo8;
+          const int ln8 = (mo ? ub - 2 : lo8 - 1) + db;
+          const bool ob8b = xb == 0xFF || !oku[u] || ln8 < 0 || ln8 > 14 ||
+                            (int64_t)bo[l0 + jd8] + (GH_C8_REF - lo8) >= INT32_MAX;
+          const uint32_t m8b = 0xFFu << sh;
+          const int c = min(ln8 + 2, 14);
+          O[h] = (O[h] & ~m8b) | ((uint32_t)(((ln8 & 15) << 4) | 1) << sh);
+          P[h] = (P[h] & ~m8b) | ((uint32_t)(c <= 13 ? c - 1 : c) << sh);
+          B[h] = (B[h] & ~m8b) | (ob8b ? 0x80u << sh : 0u);
+          mrg += (int)mo - (int)(ub <= lo8 + 1 && ub != 15);
+        }
+        const bool okb = lane_ok && oku[u] && byte_lane && (w8.x & 0xFFu) != GH_C8_ESC && (B[0] | B[1]) == 0 &&
+                         (nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu)) == 0;
+        const bool seg_okb = (__ballot(al && !okb) & gmask) == 0;
+        int dpres = 0;
+        if (al && seg_okb) {
+          const uint64_t v8 = ((uint64_t)O[1] << 32) | O[0];
+          uint64_t* hp = reinterpret_cast<uint64_t*>(h8n_t + (slu[u] * TW + lb8));
+          const uint32_t E = __builtin_amdgcn_perm(P[1], P[0], 0x06040200u);
+          const uint32_t Od = __builtin_amdgcn_perm(P[1], P[0], 0x07050301u);
+          const uint32_t pwd = __builtin_amdgcn_perm(Od | (Od >> 4), E | (E >> 4), 0x06040200u);
+          uint32_t* pp = reinterpret_cast<uint32_t*>(pln_t + (slu[u] * (TW / 2) + lbp));
+          if constexpr (NT) {
+            __builtin_nontemporal_store(v8, hp);
+            __builtin_nontemporal_store(pwd, pp);
+          } else {
+            *hp = v8;
+            *pp = pwd;
+          }
+          n_mrg16 += 16u * (uint32_t)mrg;
+          dpres = gain;
+        } else if (al && lc == 0) {
+          s_slow[atomicAdd(&s_nslow, 1)] = i;
+        }
+        if (__ballot(dpres != 0) != 0) {  // absent cells merged: the row's count moves
+#pragma unroll
+          for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) dpres += __shfl_xor(dpres, o2);
+          if (lc == 0 && dpres) atomicAdd(&d.cntl[i], dpres);
+        }
+      }
+    }
+  } else {
 #pragma unroll 1
   for (int it = 0; it < NIT; ++it) {
     const int rr = wave * RPW + it * RSTEP + sub;
@@ -895,108 +1041,6 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         for (int q = 0; q < KB; ++q)
           pw[q] = *reinterpret_cast<const uint32_t*>(plo_t + (psl[q] * (TW / 2) + lbp));
       }
-    }
-    if constexpr (BYTE) {
-      // THE BYTE PATH (IN = 2: 8-bit tier in and out with a valid plane; the
-      // 16-bit rule is not compiled into this instantiation): the lean rule
-      // on the one-byte cells themselves, four per dword (SWAR), no
-      // widening. Per cell: l = lag (GH_C8_REF - offset), a = age; the
-      // freshest sender's plane code u = l_s + 2 (gh_internal.h: GH_P_REF =
-      // GH_C8_REF + 1) merges iff l_s < l (u <= l + 1; an absent own cell,
-      // l = 15, takes any sender; u = 15 = no sender entry). Merged: lag
-      // u - 2, age 1; else age + 1; then the rebase l += base move. The
-      // row's own member (step 3): hb + 1, age 1, merged only by a larger
-      // snapshot (u <= l). A row segment whose every lane stays in the byte
-      // codes (lag 0..14, age <= min(T_fail, 15): no flag, no REMOVE, no
-      // guard row, no escape, plane codes exact) is written here; any other
-      // goes to the slow list (k_round_slow, the per-cell rule).
-      uint32_t Lw = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t M = 0x000F000Fu << (4 * j);
-        uint32_t L = pw[0] & M;
-#pragma unroll
-        for (int q = 1; q < KB; ++q) L = pk_min_u16(L, pw[q] & M);
-        Lw |= L;
-      }
-      const uint32_t lo = Lw & 0x0F0F0F0Fu, hi = (Lw >> 4) & 0x0F0F0F0Fu;
-      const uint32_t U[2] = {__builtin_amdgcn_perm(hi, lo, 0x06040200u), __builtin_amdgcn_perm(hi, lo, 0x07050301u)};
-      const uint32_t X[2] = {w8.x, w8.y};
-      const uint32_t D[2] = {d8.x, d8.y};
-      uint32_t O[2], P[2], B[2];
-      int mrg = 0, gain = 0;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const uint32_t x = X[h], u = U[h], dd = D[h];
-        const uint32_t L = (x >> 4) & 0x0F0F0F0Fu, Ag = x & 0x0F0F0F0Fu;
-        const uint32_t A = (L + 0x01010101u) & 0x10101010u;                     // own absent (0x10)
-        const uint32_t N = (u + 0x01010101u) & 0x10101010u;                     // no sender entry
-        const uint32_t Mg = ((L + 0x81818181u) - u) & ~(N << 3) & 0x80808080u;  // merged (0x80)
-        const uint32_t MM = bmask(Mg);
-        const uint32_t V = u + dd;
-        const uint32_t ln = ((V - 0x02020202u) & MM) | ((L + dd) & ~MM);        // next lag
-        const uint32_t an = (0x01010101u & MM) | ((Ag + 0x01010101u) & ~MM);    // next age
-        const uint32_t AN = bmask((A & ~(Mg >> 3)) << 3);                       // absent next
-        // a running cell outside the byte codes: lag above 14, a merged
-        // lag below 0 (V < 2), age above min(T_fail, 15)
-        B[h] = (((ln + 0x71717171u) | (an + tfb)) & ~AN & 0x80808080u) | (Mg & ~(V + 0x7E7E7E7Eu));
-        O[h] = (((ln & 0x0F0F0F0Fu) << 4) | an) | AN;
-        // plane code of the written cell: l + 2 (14 = older), absent 15
-        const uint32_t pq = ln + 0x02020202u;
-        const uint32_t OM = bmask((pq + 0x71717171u) & 0x80808080u);
-        P[h] = ((pq & ~OM) | (0x0E0E0E0Eu & OM) | AN) & 0x0F0F0F0Fu;
-        mrg += __builtin_popcount(Mg);
-        gain += __builtin_popcount(Mg & (A << 3));
-      }
-      const int jd8 = i - c0;
-      // (a wave-uniform branch: 1 wave in 256 holds an own member)
-      if (__ballot((unsigned)jd8 < 8u) != 0 && (unsigned)jd8 < 8u) {
-        // the row's own member (step 3, :443-448): hb + 1 with a fresh stamp,
-        // never flagged; its snapshot entry carries hb + 1 (plane code - 1).
-        // Not visible, a guard row or at the heartbeat cap: the per-cell rule
-        const int h = jd8 >> 2, sh = 8 * (jd8 & 3);
-        const int xb = (int)((X[h] >> sh) & 0xFFu), ub = (int)((U[h] >> sh) & 0xFFu), db = (int)((D[h] >> sh) & 0xFFu);
-        const int lo8 = xb >> 4;
-        const bool mo = ub <= 13 && ub <= lo8;
-        const int ln8 = (mo ? ub - 2 : lo8 - 1) + db;
-        const bool ob8b = xb == 0xFF || !act || ln8 < 0 || ln8 > 14 ||
-                          (int64_t)bo[l0 + jd8] + (GH_C8_REF - lo8) >= INT32_MAX;
-        const uint32_t m8b = 0xFFu << sh;
-        const int c = min(ln8 + 2, 14);
-        O[h] = (O[h] & ~m8b) | ((uint32_t)(((ln8 & 15) << 4) | 1) << sh);
-        P[h] = (P[h] & ~m8b) | ((uint32_t)(c <= 13 ? c - 1 : c) << sh);
-        B[h] = (B[h] & ~m8b) | (ob8b ? 0x80u << sh : 0u);
-        mrg += (int)mo - (int)((U[h] >> sh & 0xFFu) <= (uint32_t)lo8 + 1u && ub != 15);
-      }
-      const bool okb = lane_ok && !bad && byte_lane && (w8.x & 0xFFu) != GH_C8_ESC && (B[0] | B[1]) == 0 &&
-                       (nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu)) == 0;
-      const bool seg_okb = (__ballot(al && !okb) & gmask) == 0;
-      int dpres = 0;
-      if (al && seg_okb) {
-        const uint64_t v8 = ((uint64_t)O[1] << 32) | O[0];
-        uint64_t* hp = reinterpret_cast<uint64_t*>(h8n_t + ob8);
-        const uint32_t E = __builtin_amdgcn_perm(P[1], P[0], 0x06040200u);
-        const uint32_t Od = __builtin_amdgcn_perm(P[1], P[0], 0x07050301u);
-        const uint32_t pwd = __builtin_amdgcn_perm(Od | (Od >> 4), E | (E >> 4), 0x06040200u);
-        uint32_t* pp = reinterpret_cast<uint32_t*>(pln_t + (islot * (TW / 2) + lbp));
-        if constexpr (NT) {
-          __builtin_nontemporal_store(v8, hp);
-          __builtin_nontemporal_store(pwd, pp);
-        } else {
-          *hp = v8;
-          *pp = pwd;
-        }
-        n_mrg16 += 16u * (uint32_t)mrg;
-        dpres = gain;
-      } else if (al && lc == 0) {
-        s_slow[atomicAdd(&s_nslow, 1)] = i;
-      }
-      if (__ballot(dpres != 0) != 0) {  // absent cells merged: the row's count moves
-#pragma unroll
-        for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) dpres += __shfl_xor(dpres, o2);
-        if (lc == 0 && dpres) atomicAdd(&d.cntl[i], dpres);
-      }
-      continue;
     }
     if (m8c) {  // widen the own chunk (an escaped one is hn's)
       if ((w8.x & 0xFFu) == GH_C8_ESC)
@@ -1292,6 +1336,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     // hold next round (flagged results) cells the lean variant cannot take
     if (al && seg_ok && (__ballot(stb != 0 || fo != 0) & gmask) != 0 && lc == 0) atomicAdd(&s_storm, 1ull);
   }
+  }  // the 16-bit rule's row loop
 
   __syncthreads();
   if (tid == 0) {  // read before the barrier above; the next tile's setup writes them after two more
