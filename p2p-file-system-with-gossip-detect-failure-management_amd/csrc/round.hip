@@ -121,9 +121,15 @@ __global__ __launch_bounds__(256) void k_active_post(GhDev d, GhRound p) {
     }
     d.stab[(p.r + 1) & 1][i] = d.alive[i] && !a;  // quiet candidates for the next round
   }
+  // one atomic per workgroup (per wave they serialise on one address: 15 us
+  // at N = 65,536)
+  __shared__ int s_act;
+  if (threadIdx.x == 0) s_act = 0;
+  __syncthreads();
   const unsigned long long m = __ballot(a);
-  if (d.rank == 0 && (threadIdx.x & 63) == 0 && m)
-    atomicAdd(&d.stats[ST_ACTIVE_ROWS], (unsigned long long)__popcll(m));
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_act, __popcll(m));
+  __syncthreads();
+  if (d.rank == 0 && threadIdx.x == 0 && s_act) atomicAdd(&d.stats[ST_ACTIVE_ROWS], (unsigned long long)s_act);
 }
 
 // Receivers are this shard's member columns (their column holds the senders'
@@ -858,7 +864,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         iu[u] = i;
         const uint32_t islot = (uint32_t)(i - d.row0);
         slu[u] = islot;
-        w8u[u] = *reinterpret_cast<const uint2*>(h8o_t + (islot * TW + lb8));
+        // the own bytes are read once (no peer reads them: senders come from
+        // the plane), so they stream past the caches the plane lines live in
+        const uint64_t w8v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(h8o_t + (islot * TW + lb8)));
+        w8u[u] = uint2{(uint32_t)w8v, (uint32_t)(w8v >> 32)};
         const int4 v = *reinterpret_cast<const int4*>(&s_inb[rs * KB]);
         const int sv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
