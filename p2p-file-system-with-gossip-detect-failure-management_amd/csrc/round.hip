@@ -134,31 +134,34 @@ __global__ __launch_bounds__(256) void k_active_post(GhDev d, GhRound p) {
 
 // Receivers are this shard's member columns (their column holds the senders'
 // view of them); the inbox rows of the other shards arrive by allgather.
+// Eight lanes per receiver, lane q checks draw q (q < k), so the dependent
+// loads of the draws overlap; the valid senders are compacted in draw order.
 __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, GhRound p) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= d.ncs) return;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = (int)(gid >> 3);
+  const int q = (int)(gid & 7);
+  const bool inr = t < d.ncs;
   const int64_t i = d.col0 + t;  // global receiver (>= n in the tail of the last shard)
   const int64_t beg = i * (p.k + 1) + 1;
-  int nv = 0;
-  if (t < d.ncol && d.alive[i] && p.n >= 2) {
-    const bool ib = dbit(d.dbits, t);
-    const int dci = ib ? d.det_cnt[dcur][t] : 0;
-    const int dmi = ib ? d.det_min[dcur][t] : 0;
-    for (int q = 0; q < p.k; ++q) {
-      const uint32_t u = gh_philox_word(p.seed, (uint32_t)i, (uint32_t)p.r, GH_TAG_PEER,
-                                        (uint32_t)(q >> 2), q & 3);
-      const uint32_t w = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
-      const int s = (int)w + ((int64_t)w >= i);
-      if (!d.alive[s] || !d.active[s]) continue;
+  bool ok = false;
+  int s = 0;
+  if (inr && q < p.k && t < d.ncol && d.alive[i] && p.n >= 2) {
+    const uint32_t u = gh_philox_word(p.seed, (uint32_t)i, (uint32_t)p.r, GH_TAG_PEER, (uint32_t)(q >> 2), q & 3);
+    const uint32_t w = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
+    s = (int)w + ((int64_t)w >= i);
+    if (d.alive[s] && d.active[s]) {
       const GhCell v = gh_get(d, cur, s, t, p.r);
       // i must be in s's snapshot list: present, not detected by s this
       // round and not REMOVE'd at s in step 1.
-      if (v.x < 0 || v.f) continue;
-      if (ib && removes_at(dci, dmi, s)) continue;
-      d.inbox[beg + nv++] = s;
+      ok = v.x >= 0 && !v.f;
+      if (ok && dbit(d.dbits, t) && removes_at(d.det_cnt[dcur][t], d.det_min[dcur][t], s)) ok = false;
     }
   }
-  d.inbox[beg - 1] = nv;
+  const unsigned long long m = __ballot(ok);
+  const int lane = threadIdx.x & 63;
+  const uint32_t grp = (uint32_t)(m >> (lane & ~7)) & 0xFFu;  // this receiver's valid draws
+  if (ok) d.inbox[beg + __builtin_popcount(grp & ((1u << q) - 1u))] = s;
+  if (inr && q == 0) d.inbox[beg - 1] = __builtin_popcount(grp);
 }
 
 // Row layout: sender s's owner checks receiver i's draws against s's row
@@ -1787,7 +1790,7 @@ void launch_active_post(const GhDev& d, const GhRound& p, hipStream_t s) {
 }
 
 void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_peers_pull, dim3((d.ncs + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
+  hipLaunchKernelGGL(k_peers_pull, dim3((unsigned)(((int64_t)d.ncs * 8 + 255) / 256)), dim3(256), 0, s, d, cur, dcur, p);
 }
 
 void launch_peers_rows(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {

@@ -241,3 +241,23 @@ def test_tier_plane_kept_across_events(gs, oracle_mod):
     # the rounds after the events list a few rows' segments, not the table
     segs = (n // 256) * n
     assert max(slow_after) < segs // 4, (slow_after, segs)
+
+
+@pytest.mark.parametrize("case", ["wide_spread", "stale_outliers", "base_jump"])
+def test_tier_wide_segments(gs, oracle_mod, case):
+    """The 16-bit table's wide segments (heartbeats spread over millions,
+    views stale by more than 1,022, base jumps by external lists) under the
+    8-bit tier: their chunks are escaped, the per-cell kernel writes them into
+    8-bit buffers, the rows narrow back into bytes; bit-exact against the
+    oracle (tests/test_gpu_narrow.py's scenarios with the tier kept)."""
+    import test_gpu_narrow as tn
+    if case == "wide_spread":
+        n = 300
+        sched = sc.random_churn(n, 24, 103, p_crash=0.03, p_leave=0.01, p_join=0.04)
+        wide0, _, slow = tn.run_cov(gs, oracle_mod, dict(fanout=4, seed=0x9103, t_fail=6, t_cleanup=8), n, 24, sched,
+                                    tn.spread_state(n, 3))
+        assert wide0 > 0 and slow > 0
+    elif case == "stale_outliers":
+        tn.test_stale_outliers(gs, oracle_mod, 257, 5)
+    else:
+        tn.test_base_jump_by_merge(gs, oracle_mod)
