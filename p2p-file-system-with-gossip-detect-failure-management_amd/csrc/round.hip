@@ -1203,6 +1203,9 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     v4u rmv = {0u, 0u, 0u, 0u};
     if constexpr (STORM) rmv = *reinterpret_cast<const v4u*>(&s_rm[lc * 4]);
     int dp16 = 0;  // (present after - present before) x 16
+    // storm: a guard row without senders or REMOVE in the lane takes the
+    // folded rule (the collapsed regime)
+    const bool gfast = STORM && !act && cntv == 0 && (rmv[0] | rmv[1] | rmv[2] | rmv[3]) == 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t rmj = rmv[j];  // REMOVE'd columns: not in any sender's snapshot
@@ -1219,6 +1222,19 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         // a guard row (step 2, :504-509) stamps its present cells: age 1
         if (LEAN_GUARD && !act) y0 = (((x & 0x7FE07FE0u) | 0x00010001u) & ~hx) | (x & hx);
         npre = hx;
+      } else if (gfast) {
+        // a guard row with no senders and no REMOVE in the lane (a collapsed
+        // cluster): present cells stamped, tombstones age, absent stays;
+        // nothing merges, is detected or released (the rule below with
+        // act = 0, m = -1, rmj = 0 folded)
+        const uint32_t z = pk_add_u16(x | 0x001F001Fu, 0x00010001u);
+        const uint32_t ta0 = pk_zero_mask(z);                  // tombstone or absent
+        const uint32_t ab = pk_zero_mask(pk_add_u16(x, 0x00010001u));  // absent
+        acc |= ((x & 0x001F001Fu) + 0x00020002u) & ~ab & ta0 & 0x00200020u;  // tombstone age >= 30
+        mm = 0u;
+        y0 = (((x & 0x7FE07FE0u) | 0x00010001u) & ~ta0) | (pk_adds_u16(x, 0x00010001u) & ta0);
+        npre = ta0;
+        stb = ~0u;  // a guard row: what the lean variant lists
       } else {
         // cell classes: (x | 31) + 1 is 0 for a tombstone or absent cell, has
         // bit 15 for a flagged present one and not for a visible one
