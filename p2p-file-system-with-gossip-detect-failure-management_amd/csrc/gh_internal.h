@@ -144,6 +144,9 @@
 #ifndef GH_WG_ROWS_WIDE
 #define GH_WG_ROWS_WIDE 256      // round kernel: rows per workgroup at TW >= 128
 #endif
+#ifndef GH_STORM_WAVES
+#define GH_STORM_WAVES 5         // storm variant: waves per SIMD it is compiled for (96 VGPRs, SGPR spills only)
+#endif
 #define GH_MAXK 8                // max pull fanout
 #define GH_DLIST_MAX 1024        // local |D| above which undecided rows are recounted in full
 #define GH_TW_DEFAULT 64         // default tile width (members per tile)
