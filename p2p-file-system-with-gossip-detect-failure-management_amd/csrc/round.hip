@@ -1414,7 +1414,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 // of the workgroups, each taking blocks a multiple of 8 apart (same XCD), so
 // idle they are a small dispatch.
 template <int KB, int TW, int TPW, bool NT, bool STORM, int IN>
-__global__ __launch_bounds__(256, (STORM && TW >= 32) ? GH_STORM_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
+__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
   if (*d.mode != (int)STORM) return;
   if constexpr (!STORM) {
     int want = 0;
