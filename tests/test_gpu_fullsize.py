@@ -10,9 +10,16 @@ Two regimes:
     the <4 guard (slave/slave.go:460-497, 504-509), which runs k_round's
     storm variant at full scale.
 
+  * the bench's steady state with a 1% crash (BASELINE config 2's crash rate
+    at the config-3 size): 655 Philox-drawn members stop at r=8; they are
+    detected once their views age past T_fail (slave/slave.go:460-482), the
+    REMOVE wave follows (:338-363) and the tombstones age out (:484-497).
+
 Counters, the failed set and the detectors are compared every round; the
 whole hb and ts tables (65,536 x 65,536 each) row block by row block at the
-rounds listed."""
+rounds listed. The steady-state test also asserts, from round 8 on, that the
+round ran the byte path (gh_tier_info variant 3) with no escaped chunk: the
+path the bench times is the path checked here."""
 import os
 import time
 
@@ -51,15 +58,19 @@ def compare_blocks(eng, orc, r):
     print(f"  r={r}: full tables equal ({time.perf_counter() - t0:.1f} s)", flush=True)
 
 
-def run(gs, om, t_fail, rounds, full_at, expect):
+def run(gs, om, t_fail, rounds, full_at, expect, sched=None, per_round=None):
     cfg = dict(fanout=4, seed=0x5EED0003, t_fail=t_fail, t_cleanup=t_fail)
     eng = gs.Engine(gs.default_config(N, **cfg))
     orc = om.Oracle(om.default_config(N, **cfg), threads=THREADS)
     try:
         eng.init_full(2, 0, 0)
         orc.init_full(2, 0, 0)
-        seen = {"detections": 0, "storm": False}
+        seen = {"detections": 0, "storm": False, "variants": {}, "first_detection": None}
+        pending_full = set(full_at)
         for r in range(1, rounds + 1):
+            if sched and r in sched:
+                eng.apply_events(sched[r])
+                orc.apply_events(sched[r])
             t0 = time.perf_counter()
             s2 = orc.step(1)
             t1 = time.perf_counter()
@@ -71,17 +82,55 @@ def run(gs, om, t_fail, rounds, full_at, expect):
             np.testing.assert_array_equal(eng.read_detectors(), orc.read_detectors(), err_msg=f"detectors r={r}")
             seen["detections"] += s1["detections"]
             seen["storm"] |= eng.encoding_info(full=True)[2] == 1
-            if r in full_at:
+            var = eng.tier_info(full=True)[3]
+            seen["variants"][var] = seen["variants"].get(var, 0) + 1
+            if per_round:
+                per_round(eng, r, s1)
+            if s1["detections"] and seen["first_detection"] is None:
+                seen["first_detection"] = r
+                pending_full |= {r, r + 1}  # the detection round and the REMOVE round after it
+            if r in pending_full:
                 compare_blocks(eng, orc, r)
+        print(f"  variants (round counts by gh_tier_info variant): {seen['variants']}", flush=True)
         expect(seen)
     finally:
         eng.close()
         orc.close()
 
 
+def byte_path_from(r0):
+    """per-round check: from round r0 on, the round ran the byte path (tier
+    variant 3) and wrote no escaped chunk"""
+    def check(eng, r, st):
+        if r >= r0:
+            kept, current, escaped, variant = eng.tier_info(full=True)
+            assert (kept, current, variant) == (1, 1, 3), f"round {r}: tier_info {kept, current, escaped, variant}"
+            assert escaped == 0, f"round {r}: {escaped} escaped chunks"
+    return check
+
+
 def test_c3_fullsize_steady_state(gs, oracle_mod):
-    """The bench's workload (T_fail = 16): 6 rounds, no detections."""
-    run(gs, oracle_mod, 16, 6, {3, 6}, lambda s: s["detections"] == 0 or pytest.fail("unexpected detections"))
+    """The bench's workload (T_fail = 16) through the rounds the bench times
+    (the driver's --warmup 5 --steps 20 covers rounds 6-25): no detections,
+    full tables equal at r = 6, 12 and 25, the byte path from round 8 on."""
+    run(gs, oracle_mod, 16, 25, {6, 12, 25}, lambda s: s["detections"] == 0 or pytest.fail("unexpected detections"),
+        per_round=byte_path_from(8))
+
+
+def test_c3_fullsize_crash_1pct(gs, oracle_mod):
+    """1% crash in the bench's workload: 655 members (Philox, seed
+    0x5EED0003, tag CRASH) stop at r=8; run through their detection and the
+    REMOVE wave, full tables equal at r=12, the detection round, the round
+    after it and the last round."""
+    from scenarios import crash_ids
+    crashed = crash_ids(N, 0.01, 0x5EED0003)
+    assert len(crashed) == 655
+    sched = {8: [(gs.GH_EV_CRASH, int(c)) for c in crashed]}
+
+    def expect(s):
+        assert s["detections"] > 0 and s["first_detection"] is not None, s
+
+    run(gs, oracle_mod, 16, 32, {12, 32}, expect, sched=sched)
 
 
 def test_c3_fullsize_reference_timeouts(gs, oracle_mod):
