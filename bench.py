@@ -25,26 +25,32 @@ tests cover both regimes.
 
 The JSON line also carries
   roofline: the round kernel (k_round) — achieved = its COMPULSORY bytes per
-            launch, 4*N*ncols (every 2-byte narrow cell read once and written
-            once; DESIGN.md "Kernels"), / its mean duration from HIP events on
-            the engine's stream; peak 8.0 TB/s (MI355X_MICROARCH.md), so
-            frac <= 1 is the share of the HBM peak the round moves. The k
-            sender gathers (2*N*ncols*k more bytes, mostly served by L2 and the
-            Infinity Cache) are reported as gather_bytes_per_launch, SURVEY.md
-            §8d's int32 model 4*N^2*(k+4) as survey_bytes_per_launch;
-            traffic = fabric-side bytes per launch from the rocprofv3 PMC
-            passes of tools/pmc.sh for this configuration and warm-up
-            (profiles/, FETCH_SIZE x2 + WRITE_SIZE, the guide's gfx950
-            correction; they include Infinity-Cache hits), null if none.
+            launch / its mean duration from HIP events on the engine's stream;
+            peak 8.0 TB/s (MI355X_MICROARCH.md), so frac <= 1 is the share of
+            the HBM peak the round moves. Compulsory bytes on the 4-bit tier:
+            2*N*ncols (each cell's lag nibble and age nibble read once and
+            written once; the lag nibbles ARE the sender plane the k gathers
+            read; DESIGN.md "Kernels"); on the 16-bit table 5*N*ncols (cells
+            in and out, the plane out and in). frac_prev_model restates the
+            same time on round 2's 8-bit-tier model (3*N*ncols) so a model
+            change cannot pass for a speed-up. The k sender gathers are
+            gather_bytes_per_launch, SURVEY.md §8d's int32 model
+            4*N^2*(k+4) survey_bytes_per_launch; traffic = fabric-side bytes
+            per launch from the rocprofv3 PMC passes of tools/pmc.sh for this
+            configuration, encoding and warm-up (profiles/, FETCH_SIZE x2 +
+            WRITE_SIZE, the guide's gfx950 correction; Infinity-Cache hits
+            included), null if none was captured at this warm-up.
   cpu_baseline: the CPU restatement (oracle/tablesim.c, "port") timed on this
             host's cores (nproc threads and 1 thread) on the full benched
             configuration, plus N=4,096 and N=10 rates and the literal list
             replay (oracle/listsim.py) at N <= 256 (rank 0, N=1 only).
   secondary: the same engine at the reference's own PERIOD = COOLDOWN = 5
             rounds (slave/slave.go:24-25; the cluster collapses under the <4
-            guard in round 7), the reference's ring push, and BASELINE config
-            2 (N=4,096, k=3, 1% crash at r=8, 64 rounds: the launch-gap
-            regime).
+            guard in round 7), the reference's ring push, BASELINE config 2
+            (N=4,096, k=3, 1% crash at r=8, 64 rounds: the launch-gap regime),
+            and the benched configuration with a 1% crash (655 Philox-drawn
+            members at r=8, through detection, REMOVE and the tombstones'
+            release: rounds/s and the round count of each kernel variant).
 """
 from __future__ import annotations
 
@@ -68,7 +74,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=12)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n", type=int, default=65536)
     ap.add_argument("--fanout", type=int, default=4)
     ap.add_argument("--peer-mode", choices=("pull", "ring"), default="pull",
@@ -89,10 +95,11 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(n, k, world, warmup, plane, tw, cell_bytes):
+def pmc_traffic(n, k, world, warmup, plane, tw, encoding):
     """Fabric-side bytes per k_round launch from the committed PMC summary of
-    the same configuration, layout (sender plane, tile width) and steady state
-    (tools/pmc.sh -> profiles/*k_round_pmc*.json, warm-up >= 5 rounds)."""
+    the same configuration, layout (sender plane, tile width), table encoding
+    and warm-up (tools/pmc.sh -> profiles/*k_round_pmc*.json); a profile taken
+    at another warm-up is refused (its timed rounds are another regime)."""
     best = None
     for f in sorted((REPO / "profiles").glob("*k_round_pmc*.json")):
         try:
@@ -100,8 +107,9 @@ def pmc_traffic(n, k, world, warmup, plane, tw, cell_bytes):
         except (OSError, ValueError):
             continue
         c = d.get("config", {})
-        if (c.get("n") == n and c.get("k") == k and c.get("world", 1) == world and c.get("cell_bytes", 4) == cell_bytes
-                and c.get("warmup", 0) >= min(5, warmup) and "traffic_bytes" in d
+        enc = c.get("encoding", {4: "int32", 2: "u16", 1: "u8"}.get(c.get("cell_bytes", 4)))
+        if (c.get("n") == n and c.get("k") == k and c.get("world", 1) == world and enc == encoding
+                and c.get("warmup") == warmup and "traffic_bytes" in d
                 and c.get("plane", 0) == plane and c.get("tile_width", 64) == tw):
             best = {"traffic_bytes": d["traffic_bytes"], "source": f"profiles/{f.name}",
                     "l2_hit_rate": d.get("l2_hit_rate")}
@@ -252,7 +260,55 @@ def secondary_legs(gs):
                  "at r=8, 64 rounds timed one gh_step call per round",
         **timed(gs.default_config(4096, fanout=3, seed=0x5EED0002), 0, 64,
                 sched={8: [(gs.GH_EV_CRASH, int(c)) for c in crash]}))
+    out["c3_crash_1pct"] = crash_leg(gs, n)
     return out
+
+
+def crash_leg(gs, n, rounds=40):
+    """The benched configuration (N=65,536, k=4 pull, T_fail = T_cleanup = 16,
+    full start) with 1% of the members (655, Philox seed 0x5EED0003, tag
+    CRASH: the set tests/test_gpu_fullsize.py checks against the oracle)
+    crashing at r=8, rounds 1..40 timed one gh_step call per round: the
+    healthy rounds, the crashed members' views ageing past T_fail, the
+    detection round, the REMOVE wave and the tombstones' release. Reports
+    rounds/s over all of them and, per k_round variant (gh_tier_info: 3 the
+    nibble path, 1 storm, 2 / 0 lean 16-bit rule), its round count and mean
+    k_round time (HIP events)."""
+    from gossipsim.scenario import crash_ids
+    crashed = crash_ids(n, 0.01, 0x5EED0003)
+    eng = gs.Engine(gs.default_config(n, fanout=4, seed=0x5EED0003, t_fail=16, t_cleanup=16))
+    eng.init_full(2, 0, 0)
+    eng.set_timing(True)
+    names = {0: "lean_16bit_input", 1: "storm", 2: "lean_tier_input_16bit_rule", 3: "nibble_path"}
+    per = {}
+    tot = {"detections": 0, "tombstoned": 0, "released": 0, "remove_unknown": 0}
+    first_det = None
+    eng.sync()
+    t0 = time.perf_counter()
+    ms_prev = 0.0
+    for r in range(1, rounds + 1):
+        if r == 8:
+            eng.apply_events([(gs.GH_EV_CRASH, int(c)) for c in crashed])
+        st = eng.step(1)
+        ms, _ = eng.read_timing()
+        v = names.get(eng.tier_info(full=True)[3], "?")
+        e = per.setdefault(v, {"rounds": 0, "k_round_ms_sum": 0.0})
+        e["rounds"] += 1
+        e["k_round_ms_sum"] += ms - ms_prev
+        ms_prev = ms
+        for key in tot:
+            tot[key] += st[key]
+        if st["detections"] and first_det is None:
+            first_det = r
+    eng.sync()
+    el = time.perf_counter() - t0
+    eng.close()
+    for e in per.values():
+        e["k_round_ms"] = e.pop("k_round_ms_sum") / max(e["rounds"], 1)
+    return {"workload": f"N={n}, k=4 pull, T_fail=T_cleanup=16, full start, 655 members (1%, Philox seed "
+                        f"0x5eed0003) crash at r=8, rounds 1..{rounds} timed one gh_step call per round "
+                        "(host round trips included)",
+            "rounds_per_s": rounds / el, "first_detection_round": first_det, "variants": per, **tot}
 
 
 def placement_leg(gs, eng, n, files, t_fail):
@@ -380,8 +436,7 @@ def main():
     # rows, every column)
     nrows_r = -(-n // world) if args.layout == "rows" else n
     plane = eng.plane_info()[0]
-    tier8 = eng.tier_info()[0]  # steady-state cells stream at 1 B (escapes: the 16-bit table)
-    cell_bytes = 1 if tier8 else 2
+    tier4 = eng.tier_info()[0]  # steady-state cells: a lag nibble (the plane) + an age nibble (escapes: 16-bit)
     tile_w = int(os.environ.get("GH_TILE_W", "256" if plane else "64"))
     eng.init_full(2, 0, 0)
     if args.warmup:
@@ -410,6 +465,7 @@ def main():
     exch = eng.exchange_info() if args.layout == "rows" else None
     plane_fb = eng.plane_info()[2]
     tier_last = eng.tier_info()
+    tier_last_var = eng.tier_info(full=True)[3]
     placement = None
     if world == 1 and args.files > 0:
         progress("placement and election legs")
@@ -424,14 +480,21 @@ def main():
     value = args.steps / elapsed
     # bytes of one k_round launch (this rank's columns)
     # compulsory bytes of one launch: each table cell read once and written
-    # once, and the sender plane (4 bits per cell) written once and read
-    # once -- the least the round's data structures move through HBM
-    b_table = 2.0 * cell_bytes * nrows_r * ncols
-    b_plane = 1.0 * nrows_r * ncols if plane else 0.0
+    # once -- the least the round's data structures move through HBM. On the
+    # 4-bit tier a cell is its lag nibble (the sender plane itself) and its
+    # age nibble: 1 B in, 1 B out. On the 16-bit table: 2 B in, 2 B out, and
+    # the sender plane (4 bits per cell) written once and read once.
+    if tier4:
+        b_table, b_plane = 2.0 * nrows_r * ncols, 0.0
+    else:
+        b_table = 4.0 * nrows_r * ncols
+        b_plane = 1.0 * nrows_r * ncols if plane else 0.0
     b_compulsory = b_table + b_plane
+    b_prev_model = 3.0 * nrows_r * ncols  # round 2's 8-bit tier: 1-B cells in + out, the plane out + in
     b_gather = 2.0 * nrows_r * ncols * k       # the k sender segments per cell (L2 / Infinity Cache / HBM)
     b_survey = 4.0 * nrows_r * ncols * (k + 4)  # SURVEY.md §8d (int32 hb + ts streams)
-    traffic = pmc_traffic(n, k, world, args.warmup, plane, tile_w, cell_bytes)
+    encoding = "t4" if tier4 else "u16"
+    traffic = pmc_traffic(n, k, world, args.warmup, plane, tile_w, encoding)
     tier_cur, tier_esc = tier_last[1], tier_last[2]
     avg_s = (kern_ms / 1e3) / max(launches, 1)
     achieved = b_compulsory / avg_s / 1e9
@@ -446,7 +509,12 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "u8" if tier8 else "int16",
+        # the arithmetic is int32-exact (heartbeats over the full int32 range
+        # through the 16-bit escapes and the int32 wide arena); "storage" is
+        # the steady-state encoding the round streams
+        "dtype": "int32",
+        "storage": ("4-bit lag + 4-bit age per cell (the lag nibbles are the sender plane); escaped chunks "
+                    "16-bit, wide segments int32") if tier4 else "16-bit narrow codes, wide segments int32",
         "data": "synthetic",
         "config": {
             "workload": f"BASELINE config 3: N={n} members, "
@@ -468,10 +536,13 @@ def main():
             "traffic": traffic["traffic_bytes"] if traffic else None,
             "traffic_source": traffic["source"] if traffic else None,
             "bytes_per_launch": b_compulsory,
-            "bytes_model": (f"compulsory: {2 * cell_bytes + (1 if plane else 0)}*N*ncols ({cell_bytes}-byte cells "
-                            "read + written once" + (" (the 8-bit tier; escaped chunks in 16 bits)" if tier8 else "")
+            "bytes_model": ("compulsory: 2*N*ncols (4-bit tier: lag nibble + age nibble per cell read + written "
+                            "once; the lag nibbles are the sender plane the gathers read)" if tier4 else
+                            "compulsory: " + ("5" if plane else "4") + "*N*ncols (2-byte cells read + written once"
                             + (", 4-bit sender plane written + read once" if plane else "") + ")"),
             "table_bytes_per_launch": b_table, "plane_bytes_per_launch": b_plane,
+            "prev_model_bytes_per_launch": b_prev_model,
+            "frac_prev_model": b_prev_model / avg_s / 1e9 / HBM_PEAK_GBS,
             "avg_launch_ms": avg_s * 1e3, "launches": launches,
             "gather_bytes_per_launch": b_gather, "gather_achieved": b_gather / avg_s / 1e9,
             "survey_bytes_per_launch": b_survey,
@@ -488,8 +559,10 @@ def main():
                    "wide_slots_used": mem["wide_used"]},
         "exchange": exch,
         "layout": {"tile_width": tile_w, "sender_plane": bool(plane), "shards": args.layout,
-                   "plane_fallback_waves_last_round": plane_fb, "tier8": bool(tier8),
-                   "tier8_current": bool(tier_cur), "tier8_escaped_chunks_last_round": tier_esc},
+                   "plane_fallback_waves_last_round": plane_fb, "tier4": bool(tier4),
+                   "tier4_current": bool(tier_cur), "tier4_escaped_chunks_last_round": tier_esc,
+                   "last_variant": {0: "lean_16bit_input", 1: "storm", 2: "lean_tier_input_16bit_rule",
+                                    3: "nibble_path"}.get(tier_last_var, "?")},
         "secondary": secondary,
         "placement": placement,
     }

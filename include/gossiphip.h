@@ -130,7 +130,7 @@ void gh_config_default(gh_config* cfg);
 /* Replaces InitSlave/InitMaster (slave/slave.go:95, master/master.go:38) for
  * N members at once. HBM: the 16-bit narrow table (x2), 4*N*N bytes; in pull
  * mode with 3 <= k <= 4 from N = 16,384 the sender plane (x2, N*N bytes) and
- * the 8-bit tier (x2, 2*N*N bytes); plus the wide-segment arenas
+ * the 4-bit tier's age plane (x2, N*N bytes); plus the wide-segment arenas
  * (gh_config.wide_segments) and a frozen store for stopped rows that grows
  * with them (gh_memory_info). */
 int gh_create(const gh_config* cfg, void** handle);
@@ -203,7 +203,11 @@ int gh_put(void* h, const int32_t* files, int64_t n, int32_t* replicas,
  * path asks for confirmation on a conflict (server/server.go:79-114). */
 int gh_put_conflicts(void* h, const int32_t* files, int64_t n, int32_t window, uint8_t* conflict);
 /* Update_metadata (master/master.go:74) with available = observer's list;
- * plan entries in file order. *n_plan = number of entries (<= cap written). */
+ * plan entries in file order. *n_plan = number of entries (<= cap written).
+ * Every file's metadata is repaired. GH_DETECT_QUIRK engines also keep the
+ * reference's plan-map remake (:118, SPEC D5): the plan holds only the entry
+ * of the highest repaired file id (Go's map order is random, so which file
+ * the reference returns is unpinned). */
 int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap,
               int64_t* n_plan);
 /* get / ls (master/master.go:177-212): versions -1 if absent. */
@@ -286,13 +290,13 @@ int gh_encoding_info(void* h, int64_t* wide_segments, int64_t* slow_segments, in
  * 16-bit sender codes although the plane was valid (a sender code outside
  * the plane's window). Any output may be NULL. No reference counterpart. */
 int gh_plane_info(void* h, int32_t* enabled, int32_t* valid, int64_t* fallback_waves);
-/* 8-bit tier (diagnostic; DESIGN.md "8-bit tier"): whether the engine keeps
+/* 4-bit tier (diagnostic; DESIGN.md "4-bit tier"): whether the engine keeps
  * one (plane mode, column layout; GH_C8=0 drops it), whether the current
- * table is held in it (8-bit chunks, escaped chunks in 16 bits), how many
- * chunks the last round's packed 16-bit path wrote escaped, and the round
- * kernel variant of the last round (0 lean on a 16-bit input, 1 storm, 2
- * lean on an 8-bit input widened to 16 bits, 3 the byte path). Any output may
- * be NULL. No reference counterpart. */
+ * table is held in it (lag and age nibbles, escaped chunks in 16 bits), how
+ * many chunks the last round's packed 16-bit path wrote escaped, and the
+ * round kernel variant of the last round (0 lean on a 16-bit input, 1 storm,
+ * 2 lean on a tier input widened to 16 bits, 3 the nibble path). Any output
+ * may be NULL. No reference counterpart. */
 int gh_tier_info(void* h, int32_t* enabled, int32_t* current_8bit, int64_t* escaped_chunks, int32_t* last_variant);
 /* Row layout (GH_LAYOUT_ROWS): the last ghost-row exchange of this shard --
  * the sender rows it received, and the bytes it sent and received by
@@ -304,6 +308,16 @@ int gh_exchange_info(void* h, int64_t* ghost_rows, int64_t* bytes_out, int64_t* 
  * slots in use / per buffer, and stopped rows in the frozen store. Any
  * output may be NULL. Diagnostic; no reference counterpart. */
 int gh_memory_info(void* h, int64_t* device_bytes, int64_t* wide_used, int64_t* wide_cap, int64_t* frozen_rows);
+/* The HBM one shard (rank of world, layout and sizes from cfg) would hold,
+ * without a device or a communicator (a dry walk of gh_create's
+ * allocations): *create_bytes = everything gh_create allocates;
+ * *exchange_bytes = the row layout's ghost-row exchange buffers at a
+ * healthy pull round's expected distinct remote senders (0 in the column
+ * layout). The frozen store (grows with stopped rows) and per-call staging
+ * are not included. Plans config 4 (N = 262,144 over 8 GPUs) before any
+ * allocation. Any output may be NULL. No reference counterpart. */
+int gh_footprint(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport, int64_t* create_bytes,
+                 int64_t* exchange_bytes);
 
 /* Tuning knobs of the round kernel (k_round): non-temporal stores of the new
  * table and the XCD-aware block->tile map. Results do not depend on them;

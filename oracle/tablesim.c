@@ -406,21 +406,24 @@ static void stats_add(gh_round_stats *a, const gh_round_stats *b) {
   a->tombstoned += b->tombstoned;
 }
 
-/* One round; GH_ERANGE (nothing done) when a running member's own heartbeat
- * is INT32_MAX: Go's int would go on counting (slave/slave.go:446), our
- * int32 cannot (SPEC.md §2). */
+/* One round; GH_ERANGE (nothing done, the round's events stay pending) when
+ * a member that runs this round (alive, not crashing or leaving in its
+ * events) has its own heartbeat at INT32_MAX: Go's int would go on counting
+ * (slave/slave.go:446), our int32 cannot (SPEC.md §2). */
 static int one_round(ors *s, gh_round_stats *acc) {
   int32_t r = s->round + 1;
   int32_t n = s->n;
   int64_t rows = s->rows;
   gh_round_stats st;
   memset(&st, 0, sizeof st);
+  for (int64_t i = 0; i < rows && i < n; ++i) {
+    if (!s->alive[i] || HB(s, i, i) != INT32_MAX) continue;
+    int stops = 0; /* a crash or leave of i in this round's events stops it first */
+    for (int64_t x = 0; x < s->nev; ++x)
+      stops |= s->ev[x].member == i && (s->ev[x].kind == GH_EV_CRASH || s->ev[x].kind == GH_EV_LEAVE);
+    if (!stops) return fail(s, GH_ERANGE, "a heartbeat would pass INT32_MAX");
+  }
   apply_events(s, r, &st);
-  for (int64_t i = 0; i < rows && i < n; ++i)
-    if (s->alive[i] && HB(s, i, i) == INT32_MAX) {
-      stats_add(acc, &st); /* the round's events happened; the round did not */
-      return fail(s, GH_ERANGE, "a heartbeat would pass INT32_MAX");
-    }
   memset(s->det_any, 0, rows);
   for (int32_t c = 0; c < n; ++c) {
     s->ndet_cnt[c] = 0;

@@ -31,10 +31,11 @@ struct GhComm {
   virtual int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
   // Personalized exchange (row layout): send holds one block per
   // destination rank in rank order (sendbytes[r] bytes for rank r), recv
-  // receives one block per source rank in rank order (recvbytes[r] bytes
-  // from rank r). Host arrays of world entries; send and recv must not alias.
+  // receives one block per source rank (recvbytes[r] bytes from rank r) at
+  // byte offset recvdispl[r], or in rank order back to back when recvdispl
+  // is null. Host arrays of world entries; send and recv must not alias.
   virtual int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t* recvbytes,
-                        hipStream_t s) = 0;
+                        hipStream_t s, const size_t* recvdispl = nullptr) = 0;
 };
 
 size_t gh_dtype_size(GhDType dt);

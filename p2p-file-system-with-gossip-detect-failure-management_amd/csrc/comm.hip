@@ -34,8 +34,9 @@ struct SingleComm final : GhComm {
   int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     return copy_if_needed(send, recv, bytes, s);
   }
-  int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t*, hipStream_t s) override {
-    return copy_if_needed(send, recv, sendbytes[0], s);
+  int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t*, hipStream_t s,
+                const size_t* recvdispl) override {
+    return copy_if_needed(send, static_cast<char*>(recv) + (recvdispl ? recvdispl[0] : 0), sendbytes[0], s);
   }
 };
 
@@ -105,12 +106,12 @@ struct RcclComm final : GhComm {
   }
   // ncclAllToAllv (rccl.h:815) over byte counts, displacements = prefix sums
   int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t* recvbytes,
-                hipStream_t s) override {
+                hipStream_t s, const size_t* recvdispl) override {
     std::vector<size_t> sd(world), rd(world);
     size_t so = 0, ro = 0;
     for (int r = 0; r < world; ++r) {
       sd[r] = so;
-      rd[r] = ro;
+      rd[r] = recvdispl ? recvdispl[r] : ro;
       so += sendbytes[r];
       ro += recvbytes[r];
     }
@@ -227,7 +228,7 @@ struct LocalComm final : GhComm {
   // every rank publishes its send buffer and counts; each copies the blocks
   // addressed to it straight from the peers' buffers
   int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t* recvbytes,
-                hipStream_t s) override {
+                hipStream_t s, const size_t* recvdispl) override {
     if (hipStreamSynchronize(s) != hipSuccess) return fail("local comm: stream sync failed");
     g->ptr[rank] = send;
     g->counts[rank] = sendbytes;
@@ -241,7 +242,8 @@ struct LocalComm final : GhComm {
         g->barrier();
         return fail("local comm: alltoallv counts disagree");
       }
-      if (bytes && hipMemcpyPeerAsync(static_cast<char*>(recv) + ro, device, static_cast<const char*>(g->ptr[h]) + off,
+      const size_t at = recvdispl ? recvdispl[h] : ro;
+      if (bytes && hipMemcpyPeerAsync(static_cast<char*>(recv) + at, device, static_cast<const char*>(g->ptr[h]) + off,
                                       g->dev[h], bytes, s) != hipSuccess)
         return fail("local comm: peer copy failed");
       ro += bytes;

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void k_seg(GhDev d, int buf, SegSet set, const
     GhCell v[8];
     uint4 x = {0u, 0u, 0u, 0u}, nx = {0u, 0u, 0u, 0u};
     if (valid) {
-      x = gh_ld16(d, buf, gh_cell(d, i, c));
+      x = gh_ld16(d, buf, i, c);
       gh_dec8(d, buf, i, c, p.r, x, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -263,9 +263,9 @@ __global__ __launch_bounds__(256) void k_freeze_mark(GhDev d, const int32_t* row
     const int64_t off = gh_cell(d, rows[idx / cpr], (idx % cpr) * 8);
     *reinterpret_cast<uint4*>(d.hn[0] + off) = uint4{m, m, m, m};
     *reinterpret_cast<uint4*>(d.hn[1] + off) = uint4{m, m, m, m};
-    if (d.h8[0]) {  // a stopped row's chunks are escaped in both tiers' buffers at all times
-      *reinterpret_cast<uint2*>(d.h8[0] + off) = GH_C8_ESC2;
-      *reinterpret_cast<uint2*>(d.h8[1] + off) = GH_C8_ESC2;
+    if (d.a4[0]) {  // a stopped row's chunks are escaped in both tiers' buffers at all times
+      d.a4[0][off >> 3] = GH_T4_ESC;
+      d.a4[1][off >> 3] = GH_T4_ESC;
     }
     if (d.pl[0]) {  // never a sender: its plane words say unknown
       d.pl[0][off >> 3] = 0u;
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void k_count_wide(GhDev d, int buf, unsigned l
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int64_t t = idx / d.nrows, i = idx - t * d.nrows;
-    const uint32_t h = gh_ld16(d, buf, t * d.tstride + i * d.tw).x & 0xFFFFu;
+    const uint32_t h = gh_ld16s(d, buf, i, t * d.tw, -1).x & 0xFFFFu;  // (a marker is never a tier chunk)
     cw += h == GH_N_WIDE;
     cf += h == GH_N_FROZEN;
   }
@@ -321,7 +321,9 @@ __global__ __launch_bounds__(256) void k_hb_check(GhDev d, int cur, int32_t* fla
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= d.ncol) return;
   const int64_t i = d.col0 + c;
-  if (i < d.n && gh_owned(d, i) && d.alive[i] && gh_get(d, cur, i, c, p.r).x == INT32_MAX) *flag = 1;
+  // und: the rows that run the round (the host's scratch copy of alive
+  // without this round's crashes and leaves)
+  if (i < d.n && gh_owned(d, i) && d.und[i] && gh_get(d, cur, i, c, p.r).x == INT32_MAX) *flag = 1;
 }
 
 // base[buf][c] = v for every local column

@@ -10,10 +10,12 @@
 // Row sharding (GH_LAYOUT_ROWS, north_star; DESIGN.md "Multi-GPU"): rank g
 // holds observer rows [row0, row0 + nrows) for ALL member columns (col0 = 0,
 // ncol = N), plus GHOST rows: the snapshots of the senders its receivers pull
-// this round, copied in from their owners by one alltoallv before the round.
-// Table row SLOTS: owned row i at slot i - row0, ghosts after them; rslot[i]
-// maps a global row to its slot (-1: not held). Column layout: row0 = 0,
-// nrows = nslots = N, rslot = null (slot = row id).
+// this round, received from their owners by alltoallv before the round. Row
+// SLOTS: owned row i at slot i - row0 of the (tiled, double-buffered) table;
+// ghost j at slot nrows + j, held in the single ghost table gcodes / gplane
+// (row-major, [gcap][ld], written by the alltoallv itself); rslot[i] maps a
+// global row to its slot (-1: not held). Column layout: row0 = 0, nrows =
+// nslots = N, rslot = null (slot = row id), no ghosts.
 //
 // Device layout (SPEC.md §1/§3, DESIGN.md "Data layout in HBM"):
 //   The N x ld local membership tables are stored in column TILES of TW
@@ -83,24 +85,32 @@
 //                  chunk keeps its plane word (gh_put8, gh_clearflags8; a
 //                  stopped row's words are 0); pvalid[b] = 0 after whole-table
 //                  rewrites (imports, fill) and the list-order quirk pass.
-//   h8[2]  uint8   8-BIT TIER beside each narrow buffer (c8 engines: plane
-//                  mode, column layout), one byte per cell in the narrow
-//                  table's tiled order. While m8[b] = 1 the 8-cell chunk at
-//                  cell c8 of buffer b is h8[b][c8..c8+7] unless its byte 0 is
-//                  GH_C8_ESC, in which case it is hn[b]'s chunk (escaped); a
-//                  byte holds
-//                    l << 4 | age   visible (present, unflagged), offset =
-//                                   GH_C8_REF - l, l 0..14, age 0..15
-//                    0xFF           absent
-//                  so the steady state streams 1 B per cell, and anything
-//                  else (flags, tombstones, wide and frozen markers, lags or
-//                  ages past the window) keeps its 16-bit chunk. m8[b] = 0:
-//                  hn[b] alone holds the buffer (h8[b] is ignored, except
-//                  that stopped rows' chunks are GH_C8_ESC in both buffers at
-//                  all times). The round that writes buffer b picks its tier
-//                  (k_base: the lean variant writes 8-bit chunks); every
-//                  other reader and writer goes through gh_ld16 / gh_put8 /
-//                  gh_st16, which follow m8.
+//   a4[2]  uint32  4-BIT TIER beside each narrow buffer (tiered engines: plane
+//                  mode, column layout): the AGE plane, one nibble per cell in
+//                  the sender plane's word and nibble order (word gh_cell(i,
+//                  c) >> 3). Together with the sender plane pl[b] it IS the
+//                  table while m8[b] = 1: the cell's plane code u (0..15, see
+//                  pl) and its age a. A chunk whose age word has a zero cell-0
+//                  nibble is ESCAPED: its cells are hn[b]'s 16-bit codes (its
+//                  plane word is their plane_word, as for any chunk). Any
+//                  other chunk holds only
+//                    visible cells  u = GH_P_REF + 1 - offset (exact, 2..13;
+//                                   on the row's own member, u = GH_P_REF -
+//                                   offset, 1..12: the plane's diagonal code)
+//                                   with age 1..15
+//                    absent cells   u = 15, age nibble 15
+//                  so the plane word a round writes for its senders is the
+//                  row's own lag code as well: the steady state streams one
+//                  nibble of lag and one of age per cell each way, and the
+//                  senders gather the same lag nibbles. Flags, tombstones,
+//                  wide and frozen markers, lags or ages outside the window
+//                  keep their 16-bit chunk (escaped). m8[b] = 0: hn[b] alone
+//                  holds the buffer (a4[b] is ignored, except that stopped
+//                  rows' chunks are escaped in both buffers at all times).
+//                  The round that writes buffer b picks its tier (k_base: the
+//                  lean variants write tier chunks); every other reader and
+//                  writer goes through gh_ld16 / gh_put8 / gh_st16, which
+//                  follow m8.
 //   tsat = T_cleanup < 30: a tombstone's age is only ever compared with
 //            T_cleanup (cleanFailList, slave/slave.go:490), so every age
 //            past 30 decides the same; narrow tombstones saturate at 30 and
@@ -134,15 +144,22 @@
 #define GH_P_UNK 0u                        // plane: unknown (read the narrow table)
 #define GH_P_OLD 14u                       // plane: visible, offset below GH_P_REF - 12
 #define GH_P_NONE 15u                      // plane: not in the snapshot
-#define GH_C8_REF (GH_BASE_LAG + 1)        // 8-bit tier: offset of lag l = 0 (an active member's own cell)
-#define GH_C8_ESC 0xF0u                    // 8-bit tier: byte 0 of an escaped chunk (its codes are in hn)
-#define GH_C8_ABSENT 0xFFu                 // 8-bit tier: absent
+#define GH_C8_REF (GH_BASE_LAG + 1)        // 4-bit tier: offset of lag l = 0 (an active member's own cell)
 #define GH_PAD 256               // column padding granule (ld % 256 == 0)
 #ifndef GH_WG_CELLS
 #define GH_WG_CELLS 16384        // round kernel: cells per workgroup tile (rows = GH_WG_CELLS / TW)
 #endif
 #ifndef GH_WG_ROWS_WIDE
 #define GH_WG_ROWS_WIDE 256      // round kernel: rows per workgroup at TW >= 128
+#endif
+#ifndef GH_NIB_CPL
+#define GH_NIB_CPL 8            // nibble path: cells per lane (8, 16, 32: 4-, 8-, 16-B lane accesses)
+#endif
+#ifndef GH_NIB_RS
+#define GH_NIB_RS 0             // nibble path: row steps per iteration (0: 2 for CPL <= 16, else 1)
+#endif
+#ifndef GH_NIB_WAVES
+#define GH_NIB_WAVES 1          // nibble path: min waves per SIMD it is compiled for (1: the compiler picks)
 #endif
 #ifndef GH_STORM_WAVES
 #define GH_STORM_WAVES 5         // storm variant: waves per SIMD it is compiled for (96 VGPRs, SGPR spills only)
@@ -206,12 +223,15 @@ struct GhDev {
   int64_t ntiles;   // ld / tw
   int32_t rowlay;   // GH_LAYOUT_ROWS
   int64_t row0, nrows;  // rows this engine owns (column layout: 0, n)
-  int64_t nslots;   // table rows per tile (owned + ghost slots; column layout: n)
+  int64_t nslots;   // table rows per tile: the owned rows (column layout: n)
   int32_t *rslot;   // row layout: [n] table slot of a global row, -1 = not held
+  uint16_t *gcodes; // row layout: ghost rows' narrow codes [gcap][ld], row-major (null: no ghosts)
+  uint32_t *gplane; // ... their sender plane words [gcap][ld / 8] (null without the plane)
+  int64_t gcap;     // ghost rows the ghost table holds
   int32_t *pvf;     // row layout: [n][k] validity of each receiver's draws (summed over shards)
   uint16_t *hn[2];  // narrow double buffer
-  uint8_t *h8[2];   // 8-bit tier per buffer (null: tier off)
-  int32_t *m8;      // [0..1] buffer b is in the 8-bit tier; [2] this round switches the next buffer's tier;
+  uint32_t *a4[2];  // 4-bit tier: age plane per buffer (null: tier off); with pl[b] it holds buffer b
+  int32_t *m8;      // [0..1] buffer b is in the 4-bit tier; [2] this round switches the next buffer's tier;
                     // [3] escaped chunks the round wrote; [4] the round variant that ran (gh_tier_info)
   uint32_t *pl[2];  // sender snapshot plane per buffer (null: plane off)
   int32_t *pvalid;  // [2]: plane of buffer b written by the round that wrote b
@@ -374,64 +394,99 @@ __device__ __forceinline__ uint32_t plane_word(const v4u& o, int jd) {
   }
   return wd;
 }
-// ---- 8-bit tier (h8) -------------------------------------------------------
-// 16-bit codes of two 8-bit codes t (bytes in bits 0-7 and 16-23):
-// offset GH_C8_REF - l, age; 0xFF -> absent.
-__device__ __forceinline__ uint32_t c8_pair(uint32_t t) {
-  const uint32_t code = ((uint32_t)(GH_C8_REF << 5) * 0x10001u - ((t & 0x00F000F0u) << 1)) | (t & 0x000F000Fu);
-  const uint32_t ab = ((t + 0x00010001u) >> 8) & 0x00010001u;  // 1 per 0xFF half
-  return code | pk_sub_u16(0u, ab);
+// ---- 4-bit tier (a4 + pl) -------------------------------------------------
+// Nibble of cell j (0..7) of a chunk in the plane's order: cell 2m in bits
+// 4m, cell 2m + 1 in bits 16 + 4m (one field per 16-bit half of pair m).
+__host__ __device__ __forceinline__ int gh_nib(int j) { return 4 * (j >> 1) + 16 * (j & 1); }
+// the escape test of a tier chunk's age word
+__host__ __device__ __forceinline__ bool gh_t4_esc(uint32_t age) { return (age & 0xFu) == 0u; }
+// The 16-bit codes of a tier chunk (not escaped): lag plane word u, age word
+// a; jd = the row's own member in the chunk (0..7, its code is the plane's
+// diagonal code) or -1.
+__device__ __forceinline__ v4u c4_dec(uint32_t u, uint32_t a, int jd) {
+  v4u o;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const uint32_t U = (u >> (4 * m)) & 0x000F000Fu, A = (a >> (4 * m)) & 0x000F000Fu;
+    // offset = GH_P_REF + 1 - u; no borrow crosses the halves (u <= 15)
+    const uint32_t code = ((uint32_t)((GH_P_REF + 1) << 5) * 0x10001u - (U << 5)) | A;
+    const uint32_t ab = ((U + 0x00010001u) >> 4) & 0x00010001u;  // 1 per absent half (u = 15)
+    o[m] = code | pk_sub_u16(0u, ab);
+  }
+  if (jd >= 0) {  // the diagonal's code is one offset lower: offset = GH_P_REF - u
+    const int m = jd >> 1, sh = 16 * (jd & 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q == m && ((o[q] >> sh) & 0xFFFFu) != 0xFFFFu) o[q] -= 0x20u << sh;
+  }
+  return o;
 }
-// the 16-bit codes of an 8-bit chunk (not escaped)
-__device__ __forceinline__ v4u c8_dec(uint2 b) {
-  return v4u{c8_pair(__builtin_amdgcn_perm(0u, b.x, 0x0C010C00u)), c8_pair(__builtin_amdgcn_perm(0u, b.x, 0x0C030C02u)),
-             c8_pair(__builtin_amdgcn_perm(0u, b.y, 0x0C010C00u)), c8_pair(__builtin_amdgcn_perm(0u, b.y, 0x0C030C02u))};
+// The age word of 16-bit codes o whose plane word is u = plane_word(o, jd),
+// when the chunk has a tier encoding (every cell absent, or visible with an
+// exact plane code in the window and age 1..15); else false.
+__device__ __forceinline__ bool c4_enc(const v4u& o, int jd, uint32_t& age) {
+  uint32_t a = 0, bad = 0;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const uint32_t y = o[m];
+    const uint32_t ab = pk_zero_mask(pk_add_u16(y, 0x00010001u));  // absent halves
+    // raw plane code GH_P_REF + 1 - offset in 2..13 (the diagonal's 1..12 is
+    // the same range before its - 1); flagged, tombstone and marker codes
+    // have bit 15 or an offset far above the window
+    const uint32_t ur = pk_sub_u16((uint32_t)(GH_P_REF + 1) * 0x10001u, pk_lshr16(y, 5));
+    const uint32_t ag = y & 0x001F001Fu;
+    // per half: bit 15 of (y), (ur - 2), (13 - ur), (ag - 1), (15 - ag)
+    const uint32_t b = y | pk_sub_u16(ur, 0x00020002u) | pk_sub_u16(0x000D000Du, ur) | pk_sub_u16(ag, 0x00010001u) |
+                       pk_sub_u16(0x000F000Fu, ag);
+    bad |= b & ~ab & 0x80008000u;
+    a |= ((ag | ab) & 0x000F000Fu) << (4 * m);  // absent: age nibble 15
+  }
+  (void)jd;
+  age = a;
+  return bad == 0;
 }
-// 8-bit codes of two 16-bit codes y (one per half: bytes 0 and 2); bit 15 /
-// 31 of bad set for a half with no 8-bit code (flagged, tombstone, marker,
-// lag past 14, offset above GH_C8_REF, age past 15)
-__device__ __forceinline__ uint32_t c8_enc_pair(uint32_t y, uint32_t& bad) {
-  const uint32_t ab = pk_zero_mask(pk_add_u16(y, 0x00010001u));         // absent halves
-  const uint32_t L = pk_sub_u16((uint32_t)GH_C8_REF * 0x10001u, pk_lshr16(y, 5));
-  bad |= (y | pk_adds_u16(L, 0x7FF17FF1u) | (y << 11)) & ~ab & 0x80008000u;
-  // (L masked first: an absent or escaped half's L must not shift into the
-  // other half's byte)
-  return (((L & 0x000F000Fu) << 4) | (y & 0x000F000Fu) | ab) & 0x00FF00FFu;
-}
-// the 8-bit chunk of 16-bit codes o; bad != 0 when one has no 8-bit code
-__device__ __forceinline__ uint2 c8_enc(const v4u& o, uint32_t& bad) {
-  const uint32_t p0 = c8_enc_pair(o[0], bad), p1 = c8_enc_pair(o[1], bad);
-  const uint32_t p2 = c8_enc_pair(o[2], bad), p3 = c8_enc_pair(o[3], bad);
-  return uint2{__builtin_amdgcn_perm(p1, p0, 0x06040200u), __builtin_amdgcn_perm(p3, p2, 0x06040200u)};
-}
-#define GH_C8_ESC2 uint2{0xF0F0F0F0u, 0xF0F0F0F0u}
+#define GH_T4_ESC 0u  // the age word of an escaped chunk
 
-// buffer buf is in the 8-bit tier
-__device__ __forceinline__ bool gh_m8(const GhDev& d, int buf) { return d.h8[0] != nullptr && d.m8[buf] != 0; }
-// The 16-bit chunk at cell index `cell` (cell % 8 == 0) of buffer buf: its
-// 8-bit codes widened, or hn's chunk when escaped or the buffer is 16-bit.
-__device__ __forceinline__ uint4 gh_ld16(const GhDev& d, int buf, int64_t cell) {
+// buffer buf is in the 4-bit tier
+__device__ __forceinline__ bool gh_m8(const GhDev& d, int buf) { return d.a4[0] != nullptr && d.m8[buf] != 0; }
+// own-member position of row i in the chunk at local column c: 0..7 or -1
+__device__ __forceinline__ int gh_jd(const GhDev& d, int64_t i, int64_t c) {
+  const int64_t jd = i - (d.col0 + c);
+  return (uint64_t)jd < 8u ? (int)jd : -1;
+}
+// The 16-bit chunk of table slot s, local column c (c % 8 == 0) of buffer
+// buf: its tier codes decoded, or hn's chunk when escaped or the buffer is
+// 16-bit. jd: the row's own member in the chunk (gh_jd) or -1.
+__device__ __forceinline__ uint4 gh_ld16s(const GhDev& d, int buf, int64_t s, int64_t c, int jd) {
+  if (d.gcodes && s >= d.nrows)  // a ghost row (row layout: 16-bit, single-buffered)
+    return *reinterpret_cast<const uint4*>(d.gcodes + (s - d.nrows) * d.ld + c);
+  const int64_t cell = gh_cell_slot(d, s, c);
   if (gh_m8(d, buf)) {
-    const uint2 b = *reinterpret_cast<const uint2*>(d.h8[buf] + cell);
-    if ((b.x & 0xFFu) != GH_C8_ESC) {
-      const v4u w = c8_dec(b);
+    const uint32_t a = d.a4[buf][cell >> 3];
+    if (!gh_t4_esc(a)) {
+      const v4u w = c4_dec(d.pl[buf][cell >> 3], a, jd);
       return uint4{w[0], w[1], w[2], w[3]};
     }
   }
   return *reinterpret_cast<const uint4*>(d.hn[buf] + cell);
 }
-// Stores a 16-bit chunk (narrow codes or a marker) at cell `cell` of buffer
-// buf: in the 8-bit tier as 8-bit codes when every cell has one (c8 =
-// allowed), else escaped.
-__device__ __forceinline__ void gh_st16(const GhDev& d, int buf, int64_t cell, const uint4& x, bool c8 = true) {
+// ... of global row i (held by this engine)
+__device__ __forceinline__ uint4 gh_ld16(const GhDev& d, int buf, int64_t i, int64_t c) {
+  return gh_ld16s(d, buf, gh_slot(d, i), c, gh_jd(d, i, c));
+}
+// Stores the 16-bit chunk x (narrow codes or a marker) of row i, local
+// column c of buffer buf whose plane word the caller writes (gh_put8): in the
+// 4-bit tier as its age word when the chunk has a tier encoding (t4 =
+// allowed), else escaped with x in hn.
+__device__ __forceinline__ void gh_st16(const GhDev& d, int buf, int64_t i, int64_t c, const uint4& x, bool t4 = true) {
+  const int64_t cell = gh_cell(d, i, c);
   if (gh_m8(d, buf)) {
-    uint32_t bad = 0;
-    const uint2 b = c8_enc(v4u{x.x, x.y, x.z, x.w}, bad);
-    if (c8 && bad == 0) {
-      *reinterpret_cast<uint2*>(d.h8[buf] + cell) = b;
+    uint32_t a = 0;
+    if (t4 && c4_enc(v4u{x.x, x.y, x.z, x.w}, gh_jd(d, i, c), a)) {
+      d.a4[buf][cell >> 3] = a;
       return;
     }
-    *reinterpret_cast<uint2*>(d.h8[buf] + cell) = GH_C8_ESC2;
+    d.a4[buf][cell >> 3] = GH_T4_ESC;
   }
   *reinterpret_cast<uint4*>(d.hn[buf] + cell) = x;
 }
@@ -508,14 +563,14 @@ __device__ __forceinline__ void gh_dec8(const GhDev& d, int buf, int64_t i, int6
   }
 }
 __device__ __forceinline__ void gh_get8(const GhDev& d, int buf, int64_t i, int64_t c, int32_t r, GhCell out[8]) {
-  const uint4 x = gh_ld16(d, buf, gh_cell(d, i, c));
+  const uint4 x = gh_ld16(d, buf, i, c);
   gh_dec8(d, buf, i, c, r, x, out);
 }
 
 // Cell (i, local c) of buffer buf (for round r).
 __device__ __forceinline__ GhCell gh_get(const GhDev& d, int buf, int64_t i, int64_t c, int32_t r) {
   const int64_t c8 = c & ~(int64_t)7;
-  const uint4 hd = gh_ld16(d, buf, gh_cell(d, i, c8));
+  const uint4 hd = gh_ld16(d, buf, i, c8);
   const uint32_t h0 = hd.x & 0xFFFFu;
   if (h0 == GH_N_WIDE) {
     if (gh_wide_slot(hd.x, hd.y) >= d.wcap) return gh_absent();
@@ -537,7 +592,7 @@ __device__ __forceinline__ GhCell gh_get(const GhDev& d, int buf, int64_t i, int
 // bit j = present, bit 8 + j = present and flagged. Narrow codes answer
 // directly (no base, no round).
 __device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, int64_t c) {
-  const uint4 x = gh_ld16(d, buf, gh_cell(d, i, c));
+  const uint4 x = gh_ld16(d, buf, i, c);
   const uint32_t h0 = x.x & 0xFFFFu;
   uint32_t out = 0;
   if (h0 == GH_N_WIDE || h0 == GH_N_FROZEN) {
@@ -560,8 +615,8 @@ __device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, i
 // A stopped row has no flags.
 __device__ __forceinline__ void gh_clearflags8(const GhDev& d, int buf, int64_t i, int64_t c, uint32_t m) {
   const int64_t cell = gh_cell(d, i, c);
-  // an 8-bit chunk holds no flag; an escaped one is hn's
-  if (gh_m8(d, buf) && (d.h8[buf][cell] != GH_C8_ESC)) return;
+  // a tier chunk holds no flag; an escaped one is hn's
+  if (gh_m8(d, buf) && !gh_t4_esc(d.a4[buf][cell >> 3])) return;
   uint4* np = reinterpret_cast<uint4*>(d.hn[buf] + cell);
   uint4 x = *np;
   const uint32_t h0 = x.x & 0xFFFFu;
@@ -596,10 +651,10 @@ __device__ __forceinline__ void gh_put8(const GhDev& d, int buf, int64_t i, int6
     d.pl[buf][cell >> 3] = narrow ? plane_word(v4u{nx.x, nx.y, nx.z, nx.w}, (uint64_t)jd < 8u ? (int)jd : -1) : 0u;
   }
   if (narrow) {
-    gh_st16(d, buf, cell, nx);
+    gh_st16(d, buf, i, c, nx);
     return;
   }
-  if (gh_m8(d, buf)) *reinterpret_cast<uint2*>(d.h8[buf] + cell) = GH_C8_ESC2;
+  if (gh_m8(d, buf)) d.a4[buf][cell >> 3] = GH_T4_ESC;
   uint4* np = reinterpret_cast<uint4*>(d.hn[buf] + cell);
   const int64_t w = gh_wcell(d, slot, c);
   *reinterpret_cast<int4*>(d.wh[buf] + w) = int4{v[0].x, v[1].x, v[2].x, v[3].x};
@@ -673,6 +728,8 @@ struct GhRound {
   int32_t plane;        // the round writes the next buffer's sender plane (and may read cur's)
   int32_t ring_whole;   // ring mode: one engine and a current flag count, so the targets may come
                         // from whole lists when no REMOVE / flag is pending (k_ring_fast)
+  int32_t gpo;          // row layout: this round's ghost rows carry only their sender plane (the
+                        // 16-bit codes arrive after k_round, before k_round_slow, if any segment needs them)
 };
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------
@@ -722,7 +779,8 @@ void launch_unpack(const GhDev& d, int cur, int32_t* dst_rows, int64_t row0, int
 void launch_freeze(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p, hipStream_t s);
 // segments of buffer buf: wide (arena) -> out[0], frozen -> out[1] (device)
 void launch_count_wide(const GhDev& d, int buf, unsigned long long* out, hipStream_t s);
-// 1 -> *flag if an alive row's own heartbeat is INT32_MAX (the round would
+// 1 -> *flag if a row that runs the round (und: alive, not stopping in its
+// events) has its own heartbeat at INT32_MAX (the round would
 // overflow it, slave/slave.go:446); *flag is zeroed by the caller
 void launch_hb_check(const GhDev& d, int cur, int32_t* flag, const GhRound& p, hipStream_t s);
 // presence bitmaps of rows[0..nr) over the local columns -> rbits + rank*nr*ncsw
@@ -739,18 +797,20 @@ void launch_merge_list(const GhDev& d, int cur, int32_t obs, const int32_t* ids,
                        const GhRound& p, hipStream_t s);
 void launch_join_reset(const GhDev& d, int cur, const int32_t* rows, int32_t nr, const GhRound& p,
                        hipStream_t s);
-// rows.hip (row layout): ghost rows. pack: rows[0..ns) (owned) with their
-// destination ranks dest[] -> out (ghost_row_bytes each), wcnt[dest] += the
-// wide segments; wide: their exact cells -> out records (ghost_wide_record_bytes
-// each) at wcur[dest]++; unpack: nr received rows -> slots slot0..; unwide:
-// nrec records -> fresh arena slots of buffer cur
-int64_t ghost_row_bytes(const GhDev& d);
+// rows.hip (row layout): ghost rows, in two parts (GH_GX_PLANE: the sender
+// plane words, GH_GX_CODES: the 16-bit codes). pack: rows[0..ns) (owned)
+// -> out back to back (ghost_part_bytes each), codes: wcnt[dest[e]] += the
+// row's wide segments; wide: their exact cells -> out records
+// (ghost_wide_record_bytes each) at wcur[dest]++; unwide: nrec records ->
+// fresh arena slots of buffer cur, the ghost rows' markers rewritten
+#define GH_GX_PLANE 1
+#define GH_GX_CODES 2
+int64_t ghost_part_bytes(const GhDev& d, int part);
 int64_t ghost_wide_record_bytes(const GhDev& d);
-void launch_ghost_pack(const GhDev& d, int cur, const int32_t* rows, const int32_t* dest, int64_t ns, char* out,
-                       int32_t* wcnt, hipStream_t s);
+void launch_ghost_pack(const GhDev& d, int cur, const int32_t* rows, const int32_t* dest, int64_t ns, int part,
+                       char* out, int32_t* wcnt, hipStream_t s);
 void launch_ghost_wide(const GhDev& d, int cur, const int32_t* rows, const int32_t* dest, int64_t ns, int32_t* wcur,
                        char* out, hipStream_t s);
-void launch_ghost_unpack(const GhDev& d, int cur, const char* in, int64_t nr, int64_t slot0, hipStream_t s);
 void launch_ghost_unwide(const GhDev& d, int cur, const char* in, int64_t nrec, hipStream_t s);
 // order.hip (GH_ORDER_APPEND): list generation lin -> lin ^ 1 (events: rows
 // or all; added members in the order of src_ids, else of src_row's new list);

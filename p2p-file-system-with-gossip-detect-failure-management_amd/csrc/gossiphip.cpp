@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -64,8 +65,17 @@ struct Engine {
   // current ghost rows, exchange buffers (grown on demand)
   bool rowlay = false;
   int64_t nrs = 0;
+  int64_t segs_g = 0;    // wide-arena sizing: segments of owned rows + the ghost table, the largest over the shards
+  int64_t segs_all = 0;  // segments the arena may ever have to hold (row layout: every row as a ghost)
+  bool dry = false;       // gh_footprint: create() only counts its allocations
+  int64_t dry_bytes = 0;
   std::vector<int32_t> rslot_h;
   std::vector<int32_t> ghosts;
+  std::vector<std::vector<int32_t>> gx_send;  // rows this shard sends each rank this round
+  std::vector<int64_t> gx_rcnt, gx_rbeg;      // ghosts from each owner: count, first ghost index
+  int64_t gx_maxsend = 0;                     // the most rows any shard sends (the chunk count)
+  bool gpo = false;                           // this round's ghosts carry only their plane (GhRound.gpo)
+  bool plane_valid = false;                   // the current buffer's plane was written by a round
   int32_t* gwcnt = nullptr;  // [2 * world] wide counts / cursors per destination
   void* gbuf[4] = {nullptr, nullptr, nullptr, nullptr};  // send, recv, wide send, wide recv
   size_t gcap_bytes[4] = {0, 0, 0, 0};
@@ -73,7 +83,7 @@ struct Engine {
   int64_t gidx_cap = 0;
   int64_t gx_rows = 0, gx_out = 0, gx_in = 0;  // the last exchange: ghost rows, bytes sent / received
   int plane = 0;         // sender snapshot plane (pull mode, 3 <= k <= 4, N >= GH_PLANE_MIN_N; GH_PLANE=0/1)
-  int c8 = 0;            // 8-bit tier (plane mode, column layout; GH_C8=0 drops it)
+  int c8 = 0;            // 4-bit tier (plane mode, column layout; GH_C8=0 drops it)
   // GH_ORDER_APPEND: per-row list order kept beside the table (order.hip);
   // lcur = the list buffer of the current state
   bool lorder = false;
@@ -117,6 +127,11 @@ template <class T>
 int dalloc(Engine* e, T** p, size_t count, int fill_byte) {
   void* q = nullptr;
   const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+  if (e->dry) {  // gh_footprint: count the bytes, allocate nothing
+    e->dry_bytes += (int64_t)bytes;
+    *p = nullptr;
+    return GH_OK;
+  }
   if (hipMalloc(&q, bytes) != hipSuccess) {
     (void)hipGetLastError();
     return set_err(e, GH_ENOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
@@ -166,7 +181,8 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.force_storm = e->force_storm;
   p.force_slow = e->force_slow;
   p.plane = e->plane;
-  p.ring_whole = e->world == 1 && e->flags_known && !e->rowlay;
+  // (a row shard holds its senders' whole rows: their lists)
+  p.ring_whole = (e->world == 1 || e->rowlay) && e->flags_known;
   return p;
 }
 
@@ -302,25 +318,31 @@ int grow_arena(Engine* e, int64_t cap) {
   return GH_OK;
 }
 
-// Before and between rounds: grow the arena when the current buffer uses
-// more than half of it (all shards take the same decision). *busy = more
-// than a quarter is in use (gh_step then checks after every round).
-int maybe_grow(Engine* e, bool* busy = nullptr) {
+// Before and between rounds: grow the arena when the current buffer of any
+// shard uses more than half of it. Every decision is collective (one
+// allreduce(max) of the shards' flags), so all shards run the same
+// collectives after it: *busy = some shard uses more than a quarter (gh_step
+// then checks after every round); check_err: an arena overflow of the last
+// round on any shard loses the state on every shard. The arena caps and
+// segs_all are the same on every shard, so the early return is too.
+int maybe_grow(Engine* e, bool* busy = nullptr, bool check_err = false) {
   GhDev& d = e->d;
-  const int64_t segs = d.ntiles * d.nslots;
+  const int64_t segs = e->segs_all;
   if (busy) *busy = false;
-  if (d.wcap >= segs) return GH_OK;
-  int32_t used = 0;
+  if (d.wcap >= segs) return GH_OK;  // every segment fits: no overflow, nothing to grow
+  int32_t used = 0, err = 0;
   HIPCHK(e, hipMemcpyAsync(&used, d.wn + e->cur, sizeof used, hipMemcpyDeviceToHost, e->stream));
+  if (check_err) HIPCHK(e, hipMemcpyAsync(&err, d.err, sizeof err, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  if (busy) *busy = 4 * (int64_t)used > d.wcap;
-  int32_t* flag = d.wn + 2;
-  int32_t want = 2 * (int64_t)used > d.wcap ? 1 : 0;
-  HIPCHK(e, hipMemcpyAsync(flag, &want, sizeof want, hipMemcpyHostToDevice, e->stream));
-  COMMCHK(e, e->comm->allreduce(flag, flag, 1, GH_DT_I32, GH_OP_MAX, e->stream));
-  HIPCHK(e, hipMemcpyAsync(&want, flag, sizeof want, hipMemcpyDeviceToHost, e->stream));
+  int32_t v[3] = {2 * (int64_t)used > d.wcap ? 1 : 0, 4 * (int64_t)used > d.wcap ? 1 : 0, err == GH_ENOMEM ? 1 : 0};
+  int32_t* flag = d.wn + 4;
+  HIPCHK(e, hipMemcpyAsync(flag, v, sizeof v, hipMemcpyHostToDevice, e->stream));
+  COMMCHK(e, e->comm->allreduce(flag, flag, 3, GH_DT_I32, GH_OP_MAX, e->stream));
+  HIPCHK(e, hipMemcpyAsync(v, flag, sizeof v, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  if (!want) return GH_OK;
+  if (v[2]) return lose(e, "gh_step");
+  if (busy) *busy = v[1] != 0;
+  if (!v[0]) return GH_OK;
   return grow_arena(e, std::min<int64_t>(segs, 2 * d.wcap));
 }
 
@@ -388,33 +410,58 @@ int gbuf_reserve(Engine* e, int b, size_t bytes) {
   return GH_OK;
 }
 
-// Every shard calls this with the same `want` (want[r]: the rows rank r
-// needs and does not own, ascending): the rows it owns go to the ranks that
-// want them, and its own wants land in ghost slots nrows, nrows + 1, ... of
-// the current buffer (in owner order, ascending within), wide segments
-// included. The previous ghosts are dropped.
-int ghost_exchange(Engine* e, const std::vector<std::vector<int32_t>>& want) {
+// Send staging of one ghost_move chunk (the parts travel in chunks of at
+// most this many bytes per shard).
+constexpr int64_t kGhostChunk = (int64_t)1 << 30;
+
+// Every shard calls this with the same `want` (want[r]: the rows rank r needs
+// and does not own, ascending). Its own wants become ghost j = slot nrows + j
+// (ascending, so grouped by owner); the rows it owns that other ranks want
+// are its send lists. The previous ghosts are dropped; nothing moves yet
+// (ghost_move).
+int ghost_setup(Engine* e, const std::vector<std::vector<int32_t>>& want) {
   GhDev& d = e->d;
   const int G = e->world, me = e->rank;
   for (int32_t s : e->ghosts) e->rslot_h[s] = -1;
   e->ghosts = want[me];
-  if ((int64_t)e->ghosts.size() > d.nslots - d.nrows) return set_err(e, GH_ENOMEM, "ghost rows exceed their slots");
-  std::vector<size_t> rcnt(G, 0), scnt(G, 0);
-  for (size_t j = 0; j < e->ghosts.size(); ++j) {
-    e->rslot_h[e->ghosts[j]] = (int32_t)(d.nrows + (int64_t)j);
-    rcnt[row_owner(e, e->ghosts[j])]++;
+  const int64_t nr = (int64_t)e->ghosts.size();
+  if (nr > d.gcap) {  // the ghost table grows (its rows are rewritten every round)
+    const int64_t cap = std::max<int64_t>(nr, d.gcap + d.gcap / 4);
+    dfree(e, d.gcodes);
+    dfree(e, d.gplane);
+    d.gcodes = nullptr;
+    d.gplane = nullptr;
+    d.gcap = 0;
+    int rc;
+    if ((rc = dalloc(e, &d.gcodes, (size_t)cap * e->ld, 0xFF))) return rc;
+    if (e->plane && (rc = dalloc(e, &d.gplane, (size_t)cap * e->ld / 8, 0xFF))) return rc;
+    d.gcap = cap;
   }
-  std::vector<int32_t> idx;  // rows to send, then their destinations
-  std::vector<int32_t> dst;
+  e->gx_rcnt.assign(G, 0);
+  e->gx_rbeg.assign(G, 0);
+  for (int64_t j = 0; j < nr; ++j) {
+    e->rslot_h[e->ghosts[j]] = (int32_t)(d.nrows + j);
+    e->gx_rcnt[row_owner(e, e->ghosts[j])]++;
+  }
+  for (int r = 1; r < G; ++r) e->gx_rbeg[r] = e->gx_rbeg[r - 1] + e->gx_rcnt[r - 1];
+  e->gx_send.assign(G, {});
+  std::vector<int64_t> sends(G, 0);  // every shard's send rows (replicated wants: the same everywhere)
   for (int r = 0; r < G; ++r)
-    if (r != me)
-      for (int32_t s : want[r])
-        if (row_owner(e, s) == me) {
-          idx.push_back(s);
-          dst.push_back(r);
-          scnt[r]++;
-        }
-  const int64_t ns = (int64_t)idx.size(), nr = (int64_t)e->ghosts.size();
+    for (int32_t s : want[r]) {
+      const int o = row_owner(e, s);
+      sends[o]++;
+      if (o == me) e->gx_send[r].push_back(s);
+    }
+  e->gx_maxsend = *std::max_element(sends.begin(), sends.end());
+  e->gx_rows = nr;
+  e->gx_out = e->gx_in = 0;
+  HIPCHK(e, hipMemcpyAsync(d.rslot, e->rslot_h.data(), sizeof(int32_t) * e->n, hipMemcpyHostToDevice, e->stream));
+  return GH_OK;
+}
+
+// device list of rows (and their destinations) in gidx
+int upload_rows(Engine* e, const std::vector<int32_t>& rows, const std::vector<int32_t>& dst) {
+  const int64_t ns = (int64_t)rows.size();
   if (ns > e->gidx_cap) {
     dfree(e, e->gidx);
     e->gidx = nullptr;
@@ -423,33 +470,55 @@ int ghost_exchange(Engine* e, const std::vector<std::vector<int32_t>>& want) {
     if ((rc = dalloc(e, &e->gidx, 2 * std::max<int64_t>(ns, 1024), 0))) return rc;
     e->gidx_cap = std::max<int64_t>(ns, 1024);
   }
-  int32_t* drows = e->gidx;
-  int32_t* ddest = e->gidx + e->gidx_cap;
-  HIPCHK(e, hipMemcpyAsync(d.rslot, e->rslot_h.data(), sizeof(int32_t) * e->n, hipMemcpyHostToDevice, e->stream));
   if (ns) {
-    HIPCHK(e, hipMemcpyAsync(drows, idx.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(ddest, dst.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->gidx, rows.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->gidx + e->gidx_cap, dst.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice,
+                             e->stream));
   }
-  const int64_t RB = ghost_row_bytes(d);
+  return GH_OK;
+}
+
+// Moves one part of the set-up ghost rows (GH_GX_PLANE: sender plane words,
+// GH_GX_CODES: 16-bit codes and then the wide segments' exact cells) from
+// their owners straight into the ghost table, by alltoallv with receive
+// displacements, in C chunks (the same C on every shard): chunk c carries
+// rows [c*n/C, (c+1)*n/C) of every (source, destination) list.
+int ghost_move(Engine* e, int part) {
+  GhDev& d = e->d;
+  const int G = e->world;
+  const int64_t B = ghost_part_bytes(d, part);
+  const int64_t C = std::max<int64_t>(1, (e->gx_maxsend * B + kGhostChunk - 1) / kGhostChunk);
+  char* region = part == GH_GX_PLANE ? reinterpret_cast<char*>(d.gplane) : reinterpret_cast<char*>(d.gcodes);
   int rc;
-  if ((rc = gbuf_reserve(e, 0, (size_t)std::max<int64_t>(ns, 1) * RB)) ||
-      (rc = gbuf_reserve(e, 1, (size_t)std::max<int64_t>(nr, 1) * RB)))
-    return rc;
-  HIPCHK(e, hipMemsetAsync(e->gwcnt, 0, sizeof(int32_t) * G, e->stream));
-  launch_ghost_pack(d, e->cur, drows, ddest, ns, static_cast<char*>(e->gbuf[0]), e->gwcnt, e->stream);
-  HIPCHK(e, hipGetLastError());
-  std::vector<size_t> sb(G), rbv(G);
-  for (int r = 0; r < G; ++r) {
-    sb[r] = scnt[r] * RB;
-    rbv[r] = rcnt[r] * RB;
+  if (part == GH_GX_CODES) HIPCHK(e, hipMemsetAsync(e->gwcnt, 0, sizeof(int32_t) * G, e->stream));
+  std::vector<size_t> sb(G), rb(G), rd(G);
+  for (int64_t c = 0; c < C; ++c) {
+    std::vector<int32_t> rows, dst;
+    for (int r = 0; r < G; ++r) {
+      const int64_t m = (int64_t)e->gx_send[r].size(), lo = c * m / C, hi = (c + 1) * m / C;
+      for (int64_t x = lo; x < hi; ++x) {
+        rows.push_back(e->gx_send[r][x]);
+        dst.push_back(r);
+      }
+      sb[r] = (size_t)(hi - lo) * B;
+      const int64_t q = e->gx_rcnt[r], qlo = c * q / C, qhi = (c + 1) * q / C;
+      rb[r] = (size_t)(qhi - qlo) * B;
+      rd[r] = (size_t)(e->gx_rbeg[r] + qlo) * B;
+    }
+    if ((rc = upload_rows(e, rows, dst)) || (rc = gbuf_reserve(e, 0, (size_t)std::max<size_t>(rows.size(), 1) * B)))
+      return rc;
+    launch_ghost_pack(d, e->cur, e->gidx, e->gidx + e->gidx_cap, (int64_t)rows.size(), part,
+                      static_cast<char*>(e->gbuf[0]), e->gwcnt, e->stream);
+    HIPCHK(e, hipGetLastError());
+    COMMCHK(e, e->comm->alltoallv(e->gbuf[0], sb.data(), region, rb.data(), e->stream, rd.data()));
+    for (int r = 0; r < G; ++r) {
+      e->gx_out += (int64_t)sb[r];
+      e->gx_in += (int64_t)rb[r];
+    }
   }
-  COMMCHK(e, e->comm->alltoallv(e->gbuf[0], sb.data(), e->gbuf[1], rbv.data(), e->stream));
-  e->gx_rows = nr;
-  e->gx_out = ns * RB;
-  e->gx_in = nr * RB;
-  launch_ghost_unpack(d, e->cur, static_cast<const char*>(e->gbuf[1]), nr, d.nrows, e->stream);
-  HIPCHK(e, hipGetLastError());
+  if (part != GH_GX_CODES) return GH_OK;
   // wide segments of the sent rows: every shard's per-destination counts
+  const int me = e->rank;
   int32_t* mat = e->gwcnt + 2 * G;
   COMMCHK(e, e->comm->allgather(e->gwcnt, mat, sizeof(int32_t) * G, e->stream));
   std::vector<int32_t> m((size_t)G * G);
@@ -459,22 +528,27 @@ int ghost_exchange(Engine* e, const std::vector<std::vector<int32_t>>& want) {
   for (int32_t v : m) any += v;
   if (any == 0) return GH_OK;
   const int64_t REC = ghost_wide_record_bytes(d);
-  std::vector<int32_t> cur0(G);
+  std::vector<int32_t> cur0(G), rows, dst;
   int64_t ws = 0, wr = 0;
   for (int r = 0; r < G; ++r) {
     cur0[r] = (int32_t)ws;
     ws += m[(size_t)me * G + r];  // my records to r
     wr += m[(size_t)r * G + me];  // r's records to me
     sb[r] = (size_t)m[(size_t)me * G + r] * REC;
-    rbv[r] = (size_t)m[(size_t)r * G + me] * REC;
+    rb[r] = (size_t)m[(size_t)r * G + me] * REC;
+    for (int32_t s : e->gx_send[r]) {
+      rows.push_back(s);
+      dst.push_back(r);
+    }
   }
-  if ((rc = gbuf_reserve(e, 2, (size_t)std::max<int64_t>(ws, 1) * REC)) ||
+  if ((rc = upload_rows(e, rows, dst)) || (rc = gbuf_reserve(e, 2, (size_t)std::max<int64_t>(ws, 1) * REC)) ||
       (rc = gbuf_reserve(e, 3, (size_t)std::max<int64_t>(wr, 1) * REC)))
     return rc;
   HIPCHK(e, hipMemcpyAsync(e->gwcnt + G, cur0.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, e->stream));
-  launch_ghost_wide(d, e->cur, drows, ddest, ns, e->gwcnt + G, static_cast<char*>(e->gbuf[2]), e->stream);
+  launch_ghost_wide(d, e->cur, e->gidx, e->gidx + e->gidx_cap, (int64_t)rows.size(), e->gwcnt + G,
+                    static_cast<char*>(e->gbuf[2]), e->stream);
   HIPCHK(e, hipGetLastError());
-  COMMCHK(e, e->comm->alltoallv(e->gbuf[2], sb.data(), e->gbuf[3], rbv.data(), e->stream));
+  COMMCHK(e, e->comm->alltoallv(e->gbuf[2], sb.data(), e->gbuf[3], rb.data(), e->stream));
   e->gx_out += ws * REC;
   e->gx_in += wr * REC;
   launch_ghost_unwide(d, e->cur, static_cast<const char*>(e->gbuf[3]), wr, e->stream);
@@ -482,27 +556,81 @@ int ghost_exchange(Engine* e, const std::vector<std::vector<int32_t>>& want) {
   return GH_OK;
 }
 
+// The whole ghost rows (plane and codes).
+int ghost_exchange(Engine* e, const std::vector<std::vector<int32_t>>& want) {
+  int rc;
+  if ((rc = ghost_setup(e, want))) return rc;
+  if (e->plane && (rc = ghost_move(e, GH_GX_PLANE))) return rc;
+  return ghost_move(e, GH_GX_CODES);
+}
+
+// Row layout: the exchange staging ghost_move grows during the rounds, at
+// the expected size of a healthy Philox-pull round: each of the shard's
+// nrows receivers draws k senders uniformly from the N - 1 others, so the
+// distinct remote senders (the ghost rows received, and by symmetry the rows
+// sent) are (N - nrows) * (1 - (1 - 1/(N-1))^(k * nrows)); the send side is
+// staged one chunk at a time. Column layout: 0 (its exchanges are O(N)
+// vectors allocated by create).
+int64_t exchange_footprint(const Engine* e) {
+  if (!e->rowlay || e->world < 2) return 0;
+  const double n = (double)e->n, nr = (double)e->d.nrows, k = (double)e->cfg.fanout;
+  const int64_t distinct = (int64_t)std::ceil((n - nr) * (1.0 - std::pow(1.0 - 1.0 / (n - 1.0), k * nr)));
+  // one chunk of send staging (the ghost table is allocated by create)
+  return std::min<int64_t>(kGhostChunk, distinct * e->ld * 2);
+}
+
 // The round's ghosts: the senders of each shard's receivers that other
-// shards own, from the (replicated) pull inboxes.
+// shards own, from the (replicated) pull inboxes. A healthy round (no shard
+// in the storm variant, the plane valid) moves only their sender planes
+// (e->gpo; the codes follow after k_round if a segment needs the per-cell
+// rule), any other round the whole rows.
 int round_ghosts(Engine* e) {
   const int G = e->world;
   const int k = e->cfg.fanout;
-  std::vector<int32_t> inbox((size_t)e->n * (k + 1));
+  const bool pull = e->cfg.peer_mode == GH_PEER_PULL;
+  // pull: [n][k + 1] (count, senders); ring: CSR (beg, cnt) into <= 3N senders
+  std::vector<int32_t> inbox(pull ? (size_t)e->n * (k + 1) : 3 * (size_t)e->n), beg, cnt;
+  int32_t storm = 0;  // shards in the storm variant (summed by decide_active)
   HIPCHK(e, hipMemcpyAsync(inbox.data(), e->d.inbox, sizeof(int32_t) * inbox.size(), hipMemcpyDeviceToHost,
                            e->stream));
+  if (!pull) {
+    beg.resize(e->n);
+    cnt.resize(e->n);
+    HIPCHK(e, hipMemcpyAsync(beg.data(), e->d.inbox_beg, sizeof(int32_t) * e->n, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(cnt.data(), e->d.inbox_cnt, sizeof(int32_t) * e->n, hipMemcpyDeviceToHost, e->stream));
+  }
+  HIPCHK(e, hipMemcpyAsync(&storm, e->d.cntg + e->n + 2, sizeof storm, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
   std::vector<std::vector<uint8_t>> mark(G, std::vector<uint8_t>(e->n, 0));
   for (int64_t i = 0; i < e->n; ++i) {
     const int r = row_owner(e, i);
-    const int32_t* b = inbox.data() + i * (k + 1);
-    for (int q = 0; q < b[0]; ++q)
-      if (row_owner(e, b[1 + q]) != r) mark[r][b[1 + q]] = 1;
+    const int32_t* b = pull ? inbox.data() + i * (k + 1) + 1 : inbox.data() + beg[i];
+    const int nb = pull ? b[-1] : cnt[i];
+    for (int q = 0; q < nb; ++q)
+      if (row_owner(e, b[q]) != r) mark[r][b[q]] = 1;
   }
   std::vector<std::vector<int32_t>> want(G);
   for (int r = 0; r < G; ++r)
     for (int32_t s = 0; s < e->n; ++s)
       if (mark[r][s]) want[r].push_back(s);
-  return ghost_exchange(e, want);
+  e->gpo = e->plane && e->plane_valid && storm == 0;
+  if (!e->gpo) return ghost_exchange(e, want);
+  int rc;
+  if ((rc = ghost_setup(e, want))) return rc;
+  return ghost_move(e, GH_GX_PLANE);
+}
+
+// After k_round in a plane-only round: the ghosts' 16-bit codes, when any
+// shard's k_round listed segments for k_round_slow (one collective decision).
+int ghost_codes_if_slow(Engine* e) {
+  if (!e->rowlay || e->world < 2 || !e->gpo) return GH_OK;
+  int32_t* flag = e->d.wn + 4;
+  HIPCHK(e, hipMemcpyAsync(flag, e->d.slow_n, sizeof(int32_t), hipMemcpyDeviceToDevice, e->stream));
+  COMMCHK(e, e->comm->allreduce(flag, flag, 1, GH_DT_I32, GH_OP_MAX, e->stream));
+  int32_t any = 0;
+  HIPCHK(e, hipMemcpyAsync(&any, flag, sizeof any, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return any > 0 ? ghost_move(e, GH_GX_CODES) : GH_OK;
 }
 
 int allreduce_i32(Engine* e, int32_t* send, int32_t* recv, size_t count) {
@@ -687,8 +815,21 @@ int export_table(Engine* e, int32_t* out, int what, int64_t row0, int64_t n_rows
   return GH_OK;
 }
 
+// Ghost table rows of a row shard of nrows receivers: the distinct remote
+// senders of a healthy pull round, (N - nrows)(1 - (1 - 1/(N-1))^(k nrows))
+// expected, with 5% to spare (ghost_setup grows the table when a round needs
+// more).
+int64_t ghost_cap(int64_t n, int64_t nrows, int k) {
+  const double nn = (double)n, nr = (double)nrows;
+  const double dist = (nn - nr) * (1.0 - std::pow(1.0 - 1.0 / std::max(nn - 1.0, 1.0), (double)k * nr));
+  return std::min<int64_t>(n - nrows, (int64_t)std::ceil(dist * 1.05) + 64);
+}
+
+// dry: gh_footprint's walk of the same allocations with no device, no
+// communicator and no memory (*handle = the Engine holding dry_bytes; the
+// caller deletes it)
 int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport, const uint8_t* comm_id,
-           void** handle) {
+           void** handle, bool dry = false) {
   if (!cfg || !handle) return GH_EINVAL;
   *handle = nullptr;
   if (cfg->n_members < 1 || cfg->fanout < 1 || cfg->fanout > GH_MAXK || cfg->replicas < 1 ||
@@ -702,19 +843,22 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (world < 1 || rank < 0 || rank >= world) return GH_EINVAL;
   // the list order of a row spans every member column: one engine holds it
   if (cfg->list_order == GH_ORDER_APPEND && world > 1) return GH_EINVAL;
-  if (world > 1 && !comm_id) return GH_EINVAL;
+  if (world > 1 && !comm_id && !dry) return GH_EINVAL;
   if (transport != GH_COMM_RCCL && transport != GH_COMM_LOCAL) return GH_EINVAL;
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device || cfg->device < 0) {
-    (void)hipGetLastError();
-    return GH_ENODEV;
+  if (!dry) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= cfg->device || cfg->device < 0) {
+      (void)hipGetLastError();
+      return GH_ENODEV;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) return GH_ENODEV;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return GH_ENODEV;
+    if (hipSetDevice(cfg->device) != hipSuccess) return GH_ENODEV;
   }
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess) return GH_ENODEV;
-  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return GH_ENODEV;
-  if (hipSetDevice(cfg->device) != hipSuccess) return GH_ENODEV;
 
   Engine* e = new Engine();
+  e->dry = dry;
   e->cfg = *cfg;
   e->n = cfg->n_members;
   e->rank = rank;
@@ -741,20 +885,21 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
     return GH_EINVAL;
   }
   if (e->tpw != 1 && e->tpw != 2 && e->tpw != 4 && e->tpw != 8) e->tpw = 1;
-  // the 8-bit tier streams the steady state the plane serves at 1 B per cell
-  // (its window is the plane's: lags of healthy pull dissemination); the row
-  // layout ships 16-bit ghost rows
+  // the 4-bit tier streams the steady state the plane serves at 1 B per cell,
+  // half of it the plane itself (its window is the plane's: lags of healthy
+  // pull dissemination); the row layout ships 16-bit ghost rows
   e->c8 = e->plane && cfg->shard_layout == GH_LAYOUT_COLUMNS && e->tpw == 1 && tw >= 64;
   if (const char* v = std::getenv("GH_C8")) e->c8 = e->c8 && std::atoi(v) != 0;
-  if (cfg->shard_layout != GH_LAYOUT_COLUMNS &&
-      (cfg->shard_layout != GH_LAYOUT_ROWS || cfg->peer_mode != GH_PEER_PULL)) {
-    delete e;  // the row layout is the pull-mode path (ring targets need every sender's list order)
+  if (cfg->shard_layout != GH_LAYOUT_COLUMNS && cfg->shard_layout != GH_LAYOUT_ROWS) {
+    delete e;
     return GH_EINVAL;
   }
   // communicator
   std::string cerr;
   GhComm* c = nullptr;
-  if (world == 1 && transport != GH_COMM_RCCL)
+  if (dry)
+    c = gh_comm_single();
+  else if (world == 1 && transport != GH_COMM_RCCL)
     c = gh_comm_single();
   else if (world == 1 && !comm_id)
     c = gh_comm_single();
@@ -780,15 +925,14 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   const int64_t nrs = rowlay ? ((int64_t)e->n + world - 1) / world : e->n;
   const int64_t row0 = rowlay ? std::min<int64_t>((int64_t)rank * nrs, e->n) : 0;
   const int64_t nrows = rowlay ? std::min<int64_t>(nrs, e->n - row0) : e->n;
-  // ghost slots: every distinct remote sender of the owned receivers, and
-  // the introducer's row for a join broadcast
-  const int64_t gcap = rowlay && world > 1 ? std::min<int64_t>(e->n - nrows, nrows * cfg->fanout + 1) : 0;
+  // ghost rows (row layout)
+  const int64_t gcap = rowlay && world > 1 ? ghost_cap(e->n, nrows, cfg->fanout) : 0;
   e->rowlay = rowlay;
   e->nrs = nrs;
   e->lorder = cfg->list_order == GH_ORDER_APPEND;
   const int64_t pad = std::max<int64_t>(GH_PAD, 8 * (int64_t)tw);
   e->ld = (ncs + pad - 1) / pad * pad;
-  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (!dry && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return GH_EHIP;
   }
@@ -800,7 +944,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   d.rowlay = rowlay;
   d.row0 = row0;
   d.nrows = nrows;
-  d.nslots = nrows + gcap;
+  d.nslots = nrows;  // ghosts live in the ghost table (gcodes / gplane)
   d.tstride = d.nslots * tw;
   d.ntiles = e->ld / tw;
   d.col0 = col0;
@@ -810,7 +954,18 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   d.rank = rank;
   d.world = world;
   d.tsat = cfg->t_cleanup < GH_TSAT_T;
-  d.wcap = arena_slots(cfg, d.ntiles * d.nslots, tw);
+  // every shard sizes (and grows) its arena from the same segment count, the
+  // largest over the shards, so the grow and lose decisions are collective
+  // (ghost rows' wide segments take arena slots of the current buffer too)
+  int64_t slots_max = d.nslots + gcap;
+  if (rowlay)
+    for (int32_t g = 0; g < world; ++g) {
+      const int64_t r0 = std::min<int64_t>((int64_t)g * nrs, e->n), nr = std::min<int64_t>(nrs, e->n - r0);
+      slots_max = std::max<int64_t>(slots_max, nr + (world > 1 ? ghost_cap(e->n, nr, cfg->fanout) : 0));
+    }
+  e->segs_g = d.ntiles * slots_max;
+  e->segs_all = rowlay ? d.ntiles * (int64_t)e->n : e->segs_g;
+  d.wcap = arena_slots(cfg, e->segs_g, tw);
   e->cfg.tile_width = tw;
   const int64_t cells = d.nslots * e->ld;
   const int64_t nch = e->ld / tw;  // tiles: per-(tile, row) ring / quirk summaries
@@ -820,9 +975,9 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   do {
     if ((rc = dalloc(e, &d.hn[0], cells, 0xFF)) || (rc = dalloc(e, &d.hn[1], cells, 0xFF)) ||
         (rc = dalloc(e, &d.base[0], e->ld, 0)) || (rc = dalloc(e, &d.base[1], e->ld, 0)) ||
-        (rc = dalloc(e, &d.colq, e->ld, 0)) || (rc = dalloc(e, &d.wn, 4, 0)) || (rc = dalloc(e, &d.err, 1, 0)) ||
+        (rc = dalloc(e, &d.colq, e->ld, 0)) || (rc = dalloc(e, &d.wn, 8, 0)) || (rc = dalloc(e, &d.err, 1, 0)) ||
         (rc = dalloc(e, &d.frow, e->n, 0xFF)) ||
-        (rc = dalloc(e, &d.slow, (size_t)(e->ld / tw) * e->n, 0)) || (rc = dalloc(e, &d.slow_n, 4, 0)) ||
+        (rc = dalloc(e, &d.slow, (size_t)(e->ld / tw) * nrows, 0)) || (rc = dalloc(e, &d.slow_n, 4, 0)) ||
         (rc = dalloc(e, &d.mode, 4, 0)) || (rc = dalloc(e, &d.nstorm, 4, 0)) ||
         (rc = dalloc(e, &d.nflag, 2, 0)) || (rc = dalloc(e, &d.pvalid, 2, 0)) ||
         (rc = dalloc(e, &d.pfb, 1, 0)) ||
@@ -831,10 +986,10 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
       break;
     if (e->plane && ((rc = dalloc(e, &d.pl[0], cells / 8, 0xFF)) || (rc = dalloc(e, &d.pl[1], cells / 8, 0xFF))))
       break;
-    // 8-bit tier: every chunk escaped, both buffers 16-bit until a round
-    // writes one
+    // 4-bit tier: every chunk escaped (age word 0), both buffers 16-bit
+    // until a round writes one
     if ((rc = dalloc(e, &d.m8, 8, 0))) break;
-    if (e->c8 && ((rc = dalloc(e, &d.h8[0], cells, GH_C8_ESC)) || (rc = dalloc(e, &d.h8[1], cells, GH_C8_ESC))))
+    if (e->c8 && ((rc = dalloc(e, &d.a4[0], cells / 8, 0)) || (rc = dalloc(e, &d.a4[1], cells / 8, 0))))
       break;
     if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
         (rc = dalloc(e, &d.det_any, e->n, 0)) || (rc = dalloc(e, &d.und, e->n, 0)) ||
@@ -877,8 +1032,12 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
       if ((rc = dalloc(e, &d.rslot, e->n, 0xFF)) || (rc = dalloc(e, &d.pvf, (int64_t)e->n * cfg->fanout, 0)) ||
           (rc = dalloc(e, &e->gwcnt, 2 * (int64_t)world + (int64_t)world * world, 0)))
         break;
-      if (hipMemcpyAsync(d.rslot, e->rslot_h.data(), sizeof(int32_t) * e->n, hipMemcpyHostToDevice, e->stream) !=
-          hipSuccess) {
+      if (gcap > 0 && ((rc = dalloc(e, &d.gcodes, (size_t)gcap * e->ld, 0xFF)) ||
+                       (e->plane && (rc = dalloc(e, &d.gplane, (size_t)gcap * e->ld / 8, 0xFF)))))
+        break;
+      d.gcap = gcap;
+      if (!dry && hipMemcpyAsync(d.rslot, e->rslot_h.data(), sizeof(int32_t) * e->n, hipMemcpyHostToDevice,
+                                 e->stream) != hipSuccess) {
         rc = GH_EHIP;
         break;
       }
@@ -903,6 +1062,10 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
     gh_destroy(e);
     return rc;
   }
+  if (dry) {
+    *handle = e;
+    return GH_OK;
+  }
   if (hipDeviceSynchronize() != hipSuccess) {
     gh_destroy(e);
     return GH_EHIP;
@@ -916,7 +1079,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
 int decide_active(Engine* e, const GhRound& p) {
   GhDev& d = e->d;
   int rc;
-  if ((rc = allreduce_i32(e, d.cntl, d.cntg, (size_t)e->n + 2))) return rc;
+  if ((rc = allreduce_i32(e, d.cntl, d.cntg, (size_t)e->n + 3))) return rc;
   launch_active_pre(d, e->cur, e->dcur, p, e->stream);
   HIPCHK(e, hipGetLastError());
   if (e->world > 1 && (rc = allreduce_i32(e, d.post, d.post, (size_t)e->n))) return rc;
@@ -948,12 +1111,30 @@ int quirk_flags(Engine* e, const GhRound& p) {
 int build_inboxes(Engine* e, const GhRound& p) {
   GhDev& d = e->d;
   if (e->rowlay) {
-    // validity at the senders' owners, summed; every shard builds all inboxes
-    launch_peers_rows(d, e->cur, e->dcur, p, e->stream);
-    HIPCHK(e, hipGetLastError());
-    int rc;
-    if (e->world > 1 && (rc = allreduce_i32(e, d.pvf, d.pvf, (size_t)e->n * e->cfg.fanout))) return rc;
-    launch_inbox_rows(d, p, e->stream);
+    if (e->cfg.peer_mode == GH_PEER_PULL) {
+      // validity at the senders' owners, summed; every shard builds all inboxes
+      launch_peers_rows(d, e->cur, e->dcur, p, e->stream);
+      HIPCHK(e, hipGetLastError());
+      int rc;
+      if (e->world > 1 && (rc = allreduce_i32(e, d.pvf, d.pvf, (size_t)e->n * e->cfg.fanout))) return rc;
+      launch_inbox_rows(d, p, e->stream);
+    } else {
+      // ring (slave/slave.go:515-524): each sender's owner holds its whole
+      // row, its list, so it finds the 3 targets alone (the ring kernels on
+      // a one-shard view of the columns, skipping rows it does not own);
+      // allreduce(max) of the targets, then every shard builds every CSR
+      // inbox. In a healthy cluster the targets are the adjacent members,
+      // so the want lists below are a halo of a few rows per shard boundary.
+      GhDev v = d;
+      v.rank = 0;
+      v.world = 1;
+      launch_ring_count(v, e->cur, e->dcur, p, e->stream);
+      launch_ring_select(v, e->cur, e->dcur, p, e->stream);
+      HIPCHK(e, hipGetLastError());
+      if (e->world > 1)
+        COMMCHK(e, e->comm->allreduce(d.targets, d.targets, 3 * (size_t)e->n, GH_DT_I32, GH_OP_MAX, e->stream));
+      launch_inbox(d, p, e->stream);
+    }
     HIPCHK(e, hipGetLastError());
     return e->world > 1 ? round_ghosts(e) : GH_OK;
   }
@@ -992,7 +1173,7 @@ int build_inboxes(Engine* e, const GhRound& p) {
 // idempotent rewrites of whole rows).
 template <class F>
 int encode_rows(Engine* e, const char* what, F launch) {
-  const int64_t segs = e->d.ntiles * e->d.nslots;
+  const int64_t segs = e->segs_all;
   for (;;) {
     launch();
     HIPCHK(e, hipGetLastError());
@@ -1073,6 +1254,10 @@ const char* gh_last_error(void* h) {
 void gh_destroy(void* h) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return;
+  if (e->dry) {  // (gh_footprint: nothing on a device)
+    delete e;
+    return;
+  }
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   e->comm.reset();
@@ -1089,6 +1274,18 @@ int gh_create(const gh_config* cfg, void** handle) {
 int gh_create_sharded(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
                       const uint8_t* comm_id, void** handle) {
   return create(cfg, rank, world, transport, comm_id, handle);
+}
+
+int gh_footprint(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport, int64_t* create_bytes,
+                 int64_t* exchange_bytes) {
+  void* h = nullptr;
+  const int rc = create(cfg, rank, world, transport, nullptr, &h, true);
+  if (rc != GH_OK) return rc;
+  Engine* e = static_cast<Engine*>(h);
+  if (create_bytes) *create_bytes = e->dry_bytes;
+  if (exchange_bytes) *exchange_bytes = exchange_footprint(e);
+  delete e;
+  return GH_OK;
 }
 
 int gh_comm_unique_id(uint8_t* id) {
@@ -1187,8 +1384,9 @@ int gh_memory_info(void* h, int64_t* device_bytes, int64_t* wide_used, int64_t* 
     // per-column vectors and the file table are counted by hipMemGetInfo
     // callers, not here
     const int64_t cells = d.nslots * e->ld;
-    *device_bytes = 2 * cells * 2 + (e->plane ? cells : 0) + (e->c8 ? 2 * cells : 0) + 2 * d.wcap * ((int64_t)d.tw * 8 + d.tw / 8) +
-                    e->fzcap * e->ld * 8 + (e->lorder ? 2 * (int64_t)e->n * e->ld * 4 : 0);
+    *device_bytes = 2 * cells * 2 + (e->plane ? cells : 0) + (e->c8 ? cells : 0) + 2 * d.wcap * ((int64_t)d.tw * 8 + d.tw / 8) +
+                    e->fzcap * e->ld * 8 + (e->lorder ? 2 * (int64_t)e->n * e->ld * 4 : 0) +
+                    d.gcap * (e->ld * 2 + (e->plane ? e->ld / 2 : 0));  // row layout: the ghost table
   }
   if (wide_used) *wide_used = std::min<int64_t>(used, d.wcap);
   if (wide_cap) *wide_cap = d.wcap;
@@ -1321,24 +1519,20 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   for (int32_t q = 0; q < rounds; ++q) {
     const int32_t r = e->round + 1;
     int rc;
-    if ((rc = process_events(e, r))) return rc;
-    if (e->pforce) {  // the table was rewritten outside a round: no valid plane
-      HIPCHK(e, hipMemsetAsync(e->d.pvalid + e->cur, 0, sizeof(int32_t), e->stream));
-      e->pforce = false;
-      e->sforce = true;
-    }
-    if (e->sforce) {  // written outside a round: no quiet rows
-      for (int b = 0; b < 2; ++b) HIPCHK(e, hipMemsetAsync(e->d.stab[b], 0, e->n, e->stream));
-      e->sforce = false;
-    }
-    const GhRound p = round_params(e, r);
     if (e->hb_bound >= INT32_MAX) {
       // a heartbeat may sit at INT32_MAX: the round would overflow Go's
       // HeartbeatCount (slave/slave.go:446) in our int32; refused (SPEC §2)
+      // before its events are applied, so they stay pending. The rows that
+      // run it: alive and not crashing or leaving in its events (und is the
+      // round's scratch, rewritten by decide_active)
+      std::vector<uint8_t> runs(e->alive.begin(), e->alive.end());
+      for (const auto& x : e->pending)
+        if (x.kind == GH_EV_CRASH || x.kind == GH_EV_LEAVE) runs[x.member] = 0;
+      HIPCHK(e, hipMemcpyAsync(e->d.und, runs.data(), e->n, hipMemcpyHostToDevice, e->stream));
       int32_t* flag = e->d.wn + 2;
       int32_t hit = 0;
       HIPCHK(e, hipMemsetAsync(flag, 0, sizeof(int32_t), e->stream));
-      launch_hb_check(e->d, e->cur, flag, p, e->stream);
+      launch_hb_check(e->d, e->cur, flag, round_params(e, r), e->stream);
       HIPCHK(e, hipGetLastError());
       COMMCHK(e, e->comm->allreduce(flag, flag, 1, GH_DT_I32, GH_OP_MAX, e->stream));
       HIPCHK(e, hipMemcpyAsync(&hit, flag, sizeof hit, hipMemcpyDeviceToHost, e->stream));
@@ -1348,6 +1542,18 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
         break;
       }
     }
+    if ((rc = process_events(e, r))) return rc;
+    if (e->pforce) {  // the table was rewritten outside a round: no valid plane
+      HIPCHK(e, hipMemsetAsync(e->d.pvalid + e->cur, 0, sizeof(int32_t), e->stream));
+      e->pforce = false;
+      e->sforce = true;
+      e->plane_valid = false;
+    }
+    if (e->sforce) {  // written outside a round: no quiet rows
+      for (int b = 0; b < 2; ++b) HIPCHK(e, hipMemsetAsync(e->d.stab[b], 0, e->n, e->stream));
+      e->sforce = false;
+    }
+    const GhRound p = round_params(e, r);
     launch_base(e->d, e->cur, e->dcur, p, e->stream);
     if (e->rowlay && e->world > 1)  // each column's base from its owner row's shard
       COMMCHK(e, e->comm->allreduce(e->d.base[e->cur ^ 1], e->d.base[e->cur ^ 1], e->ld, GH_DT_I32, GH_OP_MAX,
@@ -1362,15 +1568,19 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       if ((rc = quirk_flags(e, pq))) return rc;
       e->qforce = false;
     }
+    e->gpo = false;
     if ((rc = build_inboxes(e, p))) return rc;
+    GhRound pr = p;
+    pr.gpo = e->gpo;  // row layout: the ghosts carry only their plane so far
     // the variants of k_round; the ones not selected return at once
-    const int nvar = e->c8 ? 4 : 2;  // lean 16-bit input, storm, lean 8-bit input (16-bit rule, byte path)
+    const int nvar = e->c8 ? 4 : 2;  // lean 16-bit input, storm, lean tier input (16-bit rule, nibble path)
     for (int v = 0; v < nvar; ++v) {
       if (e->timing) HIPCHK(e, hipEventRecord(e->evs[5 * q + v], e->stream));
-      launch_round(e->d, e->cur, e->dcur, p, e->stream, e->nt, v);
+      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v);
     }
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[5 * q + nvar], e->stream));
-    launch_round_slow(e->d, e->cur, e->dcur, p, e->stream);
+    if ((rc = ghost_codes_if_slow(e))) return rc;
+    launch_round_slow(e->d, e->cur, e->dcur, pr, e->stream);
     if (e->rowlay && e->world > 1) {
       // every shard detected in its own rows: D_r's counts and first
       // detectors over all of them (MIN as the MAX of negations)
@@ -1391,16 +1601,15 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     e->cur ^= 1;
     e->dcur ^= 1;
     e->round = r;
+    e->plane_valid = e->plane;  // the round wrote the next buffer's plane
     e->flags_known = true;
     e->hb_bound = std::min<int64_t>(INT32_MAX, e->hb_bound + 1);
     done++;
     if (busy && q + 1 < rounds) {
-      // a quarter of the arena in use: check and grow after every round, so
-      // only a jump from under 1/4 to over 1/1 in one round can overflow it
-      int32_t err = 0;
-      if ((rc = read_err(e, &err))) return rc;
-      if (err == GH_ENOMEM) return lose(e, "gh_step");
-      if ((rc = maybe_grow(e, &busy))) return rc;
+      // a quarter of the arena in use on some shard: check and grow after
+      // every round (collectively), so only a jump from under 1/4 to over
+      // 1/1 in one round can overflow it
+      if ((rc = maybe_grow(e, &busy, true))) return rc;
     }
   }
   unsigned long long st[ST_COUNT];
@@ -1412,7 +1621,12 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     int rc;
     if ((rc = read_err(e, &err))) return rc;
     if (err == GH_ENOMEM) return lose(e, "gh_step");
-    if (err) return set_err(e, err, "device error in a round");
+    if (err) {
+      // reported once: the flag is cleared, so the next call starts clean
+      HIPCHK(e, hipMemsetAsync(e->d.err, 0, sizeof(int32_t), e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+      return set_err(e, err, "device error in a round");
+    }
   }
   if (e->timing) {
     for (int32_t q = 0; q < done; ++q) {
@@ -1792,17 +2006,20 @@ int gh_debug_raw(void* h, int32_t row, int64_t c0, int64_t n, uint16_t* codes, i
   HIPCHK(e, hipSetDevice(e->cfg.device));
   for (int64_t c = c0; c < c0 + n; ++c) {
     const int64_t slot = e->rowlay ? e->rslot_h[row] : row;
-    if (slot < 0) return set_err(e, GH_EINVAL, "row not held by this shard");
+    if (slot < 0 || slot >= e->d.nrows) return set_err(e, GH_EINVAL, "row not owned by this shard");
     const int64_t cell = gh_cell_slot(e->d, slot, c);
     int32_t m8 = 0;
-    uint8_t b8[8] = {0};
+    uint32_t a4 = 0, u4 = 0;
     if (e->c8) {
       HIPCHK(e, hipMemcpy(&m8, e->d.m8 + e->cur, 4, hipMemcpyDeviceToHost));
-      HIPCHK(e, hipMemcpy(b8, e->d.h8[e->cur] + (cell & ~(int64_t)7), 8, hipMemcpyDeviceToHost));
+      HIPCHK(e, hipMemcpy(&a4, e->d.a4[e->cur] + (cell >> 3), 4, hipMemcpyDeviceToHost));
+      HIPCHK(e, hipMemcpy(&u4, e->d.pl[e->cur] + (cell >> 3), 4, hipMemcpyDeviceToHost));
     }
-    if (m8 && b8[0] != GH_C8_ESC) {  // the 16-bit code of an 8-bit one
-      const uint32_t b = b8[c & 7];
-      codes[c - c0] = b == GH_C8_ABSENT ? (uint16_t)GH_N_ABSENT : (uint16_t)(((GH_C8_REF - (b >> 4)) << 5) | (b & 15));
+    if (m8 && !gh_t4_esc(a4)) {  // the 16-bit code of a tier cell
+      const int sh = gh_nib((int)(c & 7));
+      const uint32_t u = (u4 >> sh) & 15u, a = (a4 >> sh) & 15u;
+      const int diag = e->d.col0 + c == row;  // the plane's diagonal code
+      codes[c - c0] = u == 15u ? (uint16_t)GH_N_ABSENT : (uint16_t)(((GH_P_REF + 1 - diag - (int)u) << 5) | a);
     } else {
       HIPCHK(e, hipMemcpy(codes + (c - c0), e->d.hn[e->cur] + cell, 2, hipMemcpyDeviceToHost));
     }

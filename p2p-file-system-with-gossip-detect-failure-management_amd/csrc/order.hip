@@ -33,7 +33,7 @@
 
 namespace {
 
-constexpr int kMaxSenders = 128;  // distinct senders of one receiver per round
+constexpr int kMaxSenders = 128;  // distinct senders of one receiver per batch (k_list_round)
 
 // REMOVE of member c delivered to row j at step 1 (D_{r-1}; the sole
 // detector does not message itself, slave/slave.go:344-346)
@@ -223,37 +223,43 @@ __global__ __launch_bounds__(256) void k_list_round(GhDev d, int cur, int dcur, 
   int need = target - pos;
   if (need > 0) {
     need = mark_added(d, nxt, cur, i, rem ? stay : nullptr, app, s_w);
-    if (threadIdx.x == 0) {
-      // the receiver's senders, ascending and distinct (SPEC §2 delivery order)
-      const bool pull = p.peer_mode == GH_PEER_PULL;
-      const int cnt = gh_in_cnt(d, pull, p.k, i);
-      const int64_t beg = gh_in_beg(d, pull, p.k, i);
-      int ns = 0;
-      for (int q = 0; q < cnt; ++q) {
-        const int s = d.inbox[beg + q];
-        int at = ns;
-        bool dup = false;
-        for (int x = 0; x < ns; ++x) {
-          if (s_snd[x] == s) dup = true;
-          if (s_snd[x] > s && at == ns) at = x;
+    // the receiver's senders, ascending and distinct (SPEC §2 delivery order),
+    // taken kMaxSenders at a time: each batch holds the smallest distinct
+    // senders above the last batch's largest (a ring inbox has no bound)
+    const bool pull = p.peer_mode == GH_PEER_PULL;
+    const int cnt = gh_in_cnt(d, pull, p.k, i);
+    const int64_t beg = gh_in_beg(d, pull, p.k, i);
+    int last = -1;
+    for (;;) {
+      if (threadIdx.x == 0) {
+        int ns = 0;
+        for (int q = 0; q < cnt; ++q) {
+          const int s = d.inbox[beg + q];
+          if (s <= last) continue;
+          int at = ns;
+          bool dup = false;
+          for (int x = 0; x < ns; ++x) {
+            if (s_snd[x] == s) dup = true;
+            if (s_snd[x] > s && at == ns) at = x;
+          }
+          if (dup || at == kMaxSenders) continue;  // a duplicate, or above a full batch
+          for (int x = (ns < kMaxSenders ? ns : kMaxSenders - 1); x > at; --x) s_snd[x] = s_snd[x - 1];
+          s_snd[at] = s;
+          if (ns < kMaxSenders) ns++;
         }
-        if (dup) continue;
-        if (ns == kMaxSenders) {
-          atomicExch(d.err, GH_EINVAL);
-          break;
-        }
-        for (int x = ns; x > at; --x) s_snd[x] = s_snd[x - 1];
-        s_snd[at] = s;
-        ns++;
+        s_ns = ns;
       }
-      s_ns = ns;
-    }
-    __syncthreads();
-    for (int q = 0; q < s_ns && need > 0; ++q) {
-      const int s = s_snd[q];
-      // s's snapshot: its list (generation g) after REMOVE delivery and detection
-      append_from(list_of(d, g, s), d.llen[g][s], app, dst, pos, need, s_w, i, &s_self,
-                  [&](int c) { return !gh_get(d, cur, s, c, 0).f && !removed_at(d, dcur, c, s); });
+      __syncthreads();
+      const int ns = s_ns;
+      for (int q = 0; q < ns && need > 0; ++q) {
+        const int s = s_snd[q];
+        // s's snapshot: its list (generation g) after REMOVE delivery and detection
+        append_from(list_of(d, g, s), d.llen[g][s], app, dst, pos, need, s_w, i, &s_self,
+                    [&](int c) { return !gh_get(d, cur, s, c, 0).f && !removed_at(d, dcur, c, s); });
+      }
+      if (ns < kMaxSenders || need <= 0) break;  // (uniform: ns and need are the same in every thread)
+      last = s_snd[kMaxSenders - 1];
+      __syncthreads();  // s_snd is refilled
     }
   }
   __syncthreads();
@@ -419,8 +425,8 @@ __device__ __forceinline__ int run_apply(int f, int s) { return (f & 1) ? ((f >>
 __device__ void clear_flag(const GhDev& d, int buf, int64_t i, int64_t c) {
   const int64_t c8 = c & ~(int64_t)7;
   const int64_t cell0 = gh_cell(d, i, c8);
-  // an 8-bit chunk holds no flag; an escaped one is hn's
-  if (gh_m8(d, buf) && d.h8[buf][cell0] != GH_C8_ESC) return;
+  // a tier chunk holds no flag; an escaped one is hn's
+  if (gh_m8(d, buf) && !gh_t4_esc(d.a4[buf][cell0 >> 3])) return;
   const uint2 hd = *reinterpret_cast<const uint2*>(d.hn[buf] + cell0);
   const uint32_t h0 = hd.x & 0xFFFFu;
   if (h0 == GH_N_FROZEN) return;

@@ -292,7 +292,9 @@ __global__ __launch_bounds__(256) void k_ring_fast(GhDev d, int cur, GhRound p) 
   const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= p.n) return;
   int tg[3] = {-1, -1, -1};
-  if (d.alive[s] && d.active[s]) {
+  // (row layout: the sender's owner finds its targets, the other shards'
+  // targets arrive by allreduce(max))
+  if (gh_owned(d, s) && d.alive[s] && d.active[s]) {
     if (d.cntl[s] == 0) {
       if ((threadIdx.x & 63) == 0) atomicAdd(&d.stats[ST_RING_EMPTY], 1ull);  // slave.go:517 division by zero
     } else if (gh_pf8(d, cur, s, s & ~7) >> (s & 7) & 1u) {
@@ -356,7 +358,8 @@ __global__ __launch_bounds__(256) void k_ring_count(GhDev d, int cur, int dcur, 
   const int sdr = blockIdx.x * blockDim.x + threadIdx.x;
   if (sdr >= p.n) return;
   int32_t* out = d.ring + ((int64_t)d.rank * p.n + sdr) * 2;
-  if (!(d.alive[sdr] && d.active[sdr])) {
+  // (row layout, one shard's view of the columns: the owner counts its rows)
+  if (!(gh_owned(d, sdr) && d.alive[sdr] && d.active[sdr])) {
     out[0] = 0;
     out[1] = -1;
     return;
@@ -395,7 +398,7 @@ __global__ __launch_bounds__(256) void k_ring_select(GhDev d, int cur, int dcur,
   const int sdr = blockIdx.x * blockDim.x + threadIdx.x;
   if (sdr >= p.n) return;
   int32_t tg[3] = {-1, -1, -1};
-  if (d.alive[sdr] && d.active[sdr]) {
+  if (gh_owned(d, sdr) && d.alive[sdr] && d.active[sdr]) {
     int64_t L = 0, before_me = 0, before_owner = 0;
     const int owner = (int)(sdr / d.ncs);
     for (int g = 0; g < d.world; ++g) {
@@ -543,8 +546,8 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
     // seen the round before it happens
     const int64_t measure = (int64_t)*d.nstorm + *d.slow_n;
     *d.mode = p.force_storm || measure * 32 > d.ntiles * (int64_t)d.n;
-    if (d.h8[0]) {
-      // the lean variant writes the next buffer in the 8-bit tier, the storm
+    if (d.a4[0]) {
+      // the lean variant writes the next buffer in the 4-bit tier, the storm
       // one in 16 bits; a buffer that changes tier is written whole (no
       // quiet row keeps its old chunks)
       const int w8 = *d.mode == 0;
@@ -561,6 +564,7 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
     // (row layout: every shard holds all of D, rank 0 counts it)
     d.cntl[d.n] = (d.rowlay && d.rank != 0) ? 0 : d.nd[dcur];
     d.cntl[d.n + 1] = d.nflag[cur];  // flagged segments of this shard's table (quirk gate, summed)
+    d.cntl[d.n + 2] = *d.mode;       // shards running the storm variant (row layout: the ghosts' codes, summed)
     d.pvalid[cur ^ 1] = p.plane;  // this round writes the next buffer's plane
     *d.pfb = 0;
   }
@@ -608,9 +612,291 @@ constexpr int round_rb() {
   return rb < 2048 / TW ? 2048 / TW : rb;
 }
 
-// IN: 0 = a 16-bit input (full grid), 1 = an 8-bit input by the 16-bit rule
-// (widened), 2 = an 8-bit input by the byte path, 3 = a 16-bit input in a
-// tiered engine (rarely selected: a persistent 1/8 grid)
+// THE NIBBLE PATH (k_round with IN = 2): a healthy round of a tiered engine
+// whose input buffer is in the 4-bit tier with a valid plane (column layout,
+// pull k <= 4). The lean rule runs on the tier's nibbles themselves: a cell
+// is q = its plane code (lag + 2; the row's own member: lag + 1; 15 absent)
+// and a = its age; u = the senders' minimum plane code, the freshest entry
+// (gh_internal.h: pl). A sender's heartbeat beats the own one iff u < q (an
+// absent own cell takes any sender; u = 15 = no entry), and the own member's
+// rule (step 3: hb + 1, merged only by a larger snapshot) is the same
+// comparison on its diagonal code. Merged: code u, age 1; else age + 1; then
+// the rebase q += base move. The written code is the row's next plane word
+// as it stands: the senders of the next round read exactly it.
+//
+// A lane owns CPL consecutive cells: W = CPL / 8 dwords of the plane and of
+// the age plane, and the same W dwords of each of its k senders' plane rows;
+// a row segment of 256 members is 256 / CPL lanes (one 128-B line per plane
+// row segment). Per dword (8 cells) the rule is SWAR on bytes after splitting
+// the even and odd nibbles. RS row steps per iteration: all their loads are
+// issued before any is computed. A row segment whose every lane stays in the
+// tier (codes 2..13, age <= min(T_fail, 15): no flag, no REMOVE, no guard
+// row, no escape, sender codes exact) is written here; any other goes to the
+// slow list (k_round_slow, the per-cell rule).
+template <int W>
+struct NibWords {
+  uint32_t v[W];
+};
+template <int W, bool NTL>
+__device__ __forceinline__ NibWords<W> nib_load(const char* p) {
+  NibWords<W> o;
+  if constexpr (W == 1) {
+    o.v[0] = NTL ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p)) : *reinterpret_cast<const uint32_t*>(p);
+  } else if constexpr (W == 2) {
+    const uint64_t x = NTL ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p))
+                           : *reinterpret_cast<const uint64_t*>(p);
+    o.v[0] = (uint32_t)x;
+    o.v[1] = (uint32_t)(x >> 32);
+  } else {
+    const v4u x = NTL ? __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p)) : *reinterpret_cast<const v4u*>(p);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o.v[j] = x[j];
+  }
+  return o;
+}
+template <int W, bool NTS>
+__device__ __forceinline__ void nib_store(char* p, const uint32_t* v) {
+  if constexpr (W == 1) {
+    if constexpr (NTS) __builtin_nontemporal_store(v[0], reinterpret_cast<uint32_t*>(p));
+    else *reinterpret_cast<uint32_t*>(p) = v[0];
+  } else if constexpr (W == 2) {
+    const uint64_t x = ((uint64_t)v[1] << 32) | v[0];
+    if constexpr (NTS) __builtin_nontemporal_store(x, reinterpret_cast<uint64_t*>(p));
+    else *reinterpret_cast<uint64_t*>(p) = x;
+  } else {
+    const v4u x = {v[0], v[1], v[2], v[3]};
+    if constexpr (NTS) __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(p));
+    else *reinterpret_cast<v4u*>(p) = x;
+  }
+}
+
+template <int TW, bool NT, int CPL>
+__device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, const GhRound& p, const int bid) {
+  constexpr int W = CPL / 8;         // dwords per lane and plane
+  constexpr int SEG = TW / CPL;      // lanes per row segment
+  constexpr int RPW = 64 / SEG;      // rows per wave instruction
+  constexpr int RSTEP = 4 * RPW;     // rows per workgroup step
+  constexpr int RB = round_rb<TW>();
+  constexpr int KB = 4;
+  constexpr int RS = GH_NIB_RS > 0 ? GH_NIB_RS : (CPL <= 16 ? 2 : 1);  // row steps per iteration
+  static_assert(SEG >= 2 && SEG <= 64 && RB % (RSTEP * RS) == 0, "nibble path: whole row steps");
+  __shared__ unsigned long long s_merged;
+  __shared__ int s_quiet, s_nslow, s_slowbase, s_bmove;
+  __shared__ unsigned long long s_d8bad;  // bit l: lane l's columns hold a base move outside 0..15
+  // per column the base move, one byte each, a lane's CPL bytes in its dword
+  // order, even nibbles (cells 0,4,1,5) then odd ones (2,6,3,7) per dword
+  __shared__ __attribute__((aligned(16))) uint32_t s_d8[TW / 4];
+  __shared__ int s_slow[RB];
+  __shared__ int s_meta[RB];
+  __shared__ __attribute__((aligned(16))) int s_inb[RB * KB];
+
+  const int nrb = (int)((d.nrows + RB - 1) / RB);
+  const int ngroups = (int)(p.ld / TW);
+  const int rowend = (int)(d.row0 + d.nrows);
+  int tile, rb;
+  if (p.xmap && ngroups % 8 == 0) {  // XCD-aware: XCD x = bid % 8 sweeps tiles x, x + 8, ...
+    const int x = bid & 7, j = bid >> 3;
+    tile = x + 8 * (j / nrb);
+    rb = j - (j / nrb) * nrb;
+  } else {
+    tile = bid / nrb;
+    rb = bid - tile * nrb;
+  }
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = uni(tid >> 6);
+  const int sub = lane / SEG, lc = lane % SEG;
+  const unsigned long long gmask = (SEG == 64 ? ~0ull : ((1ull << SEG) - 1)) << (sub * SEG);
+  if (tid == 0) {
+    s_merged = 0;
+    s_quiet = s_nslow = s_bmove = 0;
+    s_d8bad = 0ull;
+  }
+  const bool pull = p.peer_mode == GH_PEER_PULL;
+  const bool quiet = d.cntg[p.n] == 0 && !p.force_slow && !d.m8[2];
+  const uint8_t* __restrict__ stab_cur = d.stab[p.r & 1];
+  __syncthreads();
+  for (int t = tid; t < RB * KB; t += 256) {
+    const int row = t / KB, q = t - row * KB;
+    const int i = (int)d.row0 + rb * RB + row;
+    int meta = 0, sv = 0;
+    if (i < rowend) {
+      const int al = d.alive[i];
+      const int cnt = al ? gh_in_cnt(d, pull, p.k, i) : 0;
+      const int act = d.active[i];
+      meta = al | (act << 1) | (cnt << 2) | ((quiet && al && !act && cnt == 0 && stab_cur[i]) ? 1 << 30 : 0);
+      if (q < cnt) sv = d.inbox[gh_in_beg(d, pull, p.k, i) + q];
+    }
+    if (q == 0) s_meta[row] = meta;
+    s_inb[t] = sv;
+  }
+  const int32_t* __restrict__ bo = d.base[cur];
+  const int32_t* __restrict__ bn = d.base[cur ^ 1];
+  for (int cc = tid; cc < TW; cc += 256) {
+    const int64_t c = (int64_t)tile * TW + cc;
+    const int64_t delta = (int64_t)bn[c] - bo[c];
+    const int j = cc & 7;
+    reinterpret_cast<uint8_t*>(s_d8)[(cc & ~7) + (j >> 2) + 2 * (j & 1) + 4 * ((j >> 1) & 1)] = (uint8_t)(delta & 0xFF);
+    if (delta < 0 || delta > 15) atomicOr(&s_d8bad, 1ull << (cc / CPL));
+    if (delta) s_bmove = 1;
+  }
+  __syncthreads();
+
+  const int64_t l0 = (int64_t)tile * TW + lc * CPL;  // local column of this lane's first cell
+  const int c0 = (int)(d.col0 + l0);
+  const int64_t tcell = (int64_t)tile * d.tstride;
+  const char* plo_t = reinterpret_cast<const char*>(d.pl[cur]) + tcell / 2;
+  char* pln_t = reinterpret_cast<char*>(d.pl[cur ^ 1]) + tcell / 2;
+  const char* a4o_t = reinterpret_cast<const char*>(d.a4[cur]) + tcell / 2;
+  char* a4n_t = reinterpret_cast<char*>(d.a4[cur ^ 1]) + tcell / 2;
+  const uint32_t lbp = (uint32_t)lc * (CPL / 2);  // the lane's byte offset in a plane row segment
+  const bool tile_still = s_bmove == 0;
+  // the lane: no REMOVE'd member (REMOVE needs the per-cell rule), base
+  // moves of its columns in 0..15
+  uint32_t rm = 0;
+#pragma unroll
+  for (int w = 0; w < (CPL + 31) / 32; ++w) rm |= d.dbits[(l0 >> 5) + w];
+  if constexpr (CPL < 32) rm = (rm >> (l0 & 31)) & ((1u << CPL) - 1u);
+  const bool lane_ok = !p.force_slow && rm == 0u && ((s_d8bad >> lc) & 1ull) == 0;
+  uint32_t D8[2 * W];  // [2w + h]: the base moves of dword w's even / odd nibbles
+#pragma unroll
+  for (int x = 0; x < 2 * W; ++x) D8[x] = s_d8[lc * 2 * W + x];
+  const uint32_t tfb = (uint32_t)(0x7F - min(p.t_fail, 15)) * 0x01010101u;  // age + tfb: bit 7 iff age > T_fail
+  uint32_t n_mrg = 0;
+
+#pragma unroll 1
+  for (int it = 0; it < RB / RSTEP; it += RS) {
+    int iu[RS];
+    bool alu[RS], oku[RS];
+    uint32_t owu[RS];
+    NibWords<W> awu[RS], qwu[RS], pwu[RS][4];
+#pragma unroll
+    for (int u = 0; u < RS; ++u) {
+      const int rr = wave * RPW + (it + u) * RSTEP + sub;
+      const int i_raw = (int)d.row0 + rb * RB + rr;
+      const bool valid = i_raw < rowend;
+      const int i = valid ? i_raw : rowend - 1;  // in-range row for the loads of idle lanes
+      const int rs = valid ? rr : 0;
+      const int meta = s_meta[rs];
+      const bool skip = ((meta >> 30) & 1) && tile_still;  // quiet row, bases still
+      if (valid && skip && lc == 0) atomicAdd(&s_quiet, 1);
+      const int cntv = (meta >> 2) & 0xFFFF;
+      alu[u] = (meta & 1) && valid && !skip;
+      oku[u] = ((meta >> 1) & 1) && cntv <= KB;  // active (not a guard row), at most KB senders
+      iu[u] = i;
+      const uint32_t islot = (uint32_t)(i - d.row0);
+      const uint32_t ow = islot * (TW / 2) + lbp;
+      owu[u] = ow;
+      // the age words are read once (no peer reads them): they stream past
+      // the caches the plane lines live in; the own plane words are a line
+      // the row's receivers gather too
+      awu[u] = nib_load<W, true>(a4o_t + ow);
+      qwu[u] = nib_load<W, false>(plo_t + ow);
+      const int4 sv4 = *reinterpret_cast<const int4*>(&s_inb[rs * KB]);
+      const int sv[4] = {sv4.x, sv4.y, sv4.z, sv4.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        // unused slots read the own row's codes (a no-op under the merge)
+        const uint32_t sq = q < cntv ? (uint32_t)sv[q] : islot;
+        pwu[u][q] = nib_load<W, false>(plo_t + (sq * (TW / 2) + lbp));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RS; ++u) {
+      const int i = iu[u];
+      const bool al = alu[u];
+      uint32_t QO[W], AO[W], Bm = 0, Lz = 0;
+      int mrg = 0, gain = 0;
+      bool esc = false;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const uint32_t qw = qwu[u].v[w], aw = awu[u].v[w];
+        esc |= gh_t4_esc(aw);
+        uint32_t Lw = 0;  // per nibble the min over senders (fields at their bit position)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t M = 0x000F000Fu << (4 * j);
+          Lw |= pk_min_u16(pk_min_u16(pwu[u][0].v[w] & M, pwu[u][1].v[w] & M),
+                           pk_min_u16(pwu[u][2].v[w] & M, pwu[u][3].v[w] & M));
+        }
+        Lz |= nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu);  // a sender code unknown (0) or old (14)
+        const uint32_t QQ[2] = {qw & 0x0F0F0F0Fu, (qw >> 4) & 0x0F0F0F0Fu};
+        const uint32_t GG[2] = {aw & 0x0F0F0F0Fu, (aw >> 4) & 0x0F0F0F0Fu};
+        const uint32_t UU[2] = {Lw & 0x0F0F0F0Fu, (Lw >> 4) & 0x0F0F0F0Fu};
+        uint32_t qo[2], ao[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t Q = QQ[h], G = GG[h], U = UU[h], dd = D8[2 * w + h];
+          const uint32_t A = (Q + 0x01010101u) & 0x10101010u;                 // own absent (0x10)
+          const uint32_t Mg = ((Q + 0x7F7F7F7Fu) - U) & 0x80808080u;          // merged: u < q (0x80)
+          const uint32_t MM = bmask(Mg);
+          const uint32_t qn = ((U & MM) | (Q & ~MM)) + dd;                     // next code, rebased
+          const uint32_t ANm = bmask((A & ~(Mg >> 3)) << 3);                  // absent next
+          const uint32_t an = (0x01010101u & MM) | ((G + 0x01010101u) & ~MM);  // next age
+          // a running cell outside the tier: code above 13 or below 2, age
+          // above min(T_fail, 15)
+          Bm |= ((qn + 0x72727272u) | ~(qn + 0x7E7E7E7Eu) | (an + tfb)) & ~ANm & 0x80808080u;
+          qo[h] = (qn | ANm) & 0x0F0F0F0Fu;  // absent: 15
+          ao[h] = (an | ANm) & 0x0F0F0F0Fu;  // absent: age nibble 15
+          mrg += __builtin_popcount(Mg);
+          gain += __builtin_popcount(Mg & (A << 3));
+        }
+        QO[w] = qo[0] | (qo[1] << 4);
+        AO[w] = ao[0] | (ao[1] << 4);
+      }
+      bool ob = false;
+      const int jd = i - c0;
+      // (a wave-uniform branch: 1 wave in TW / CPL... holds an own member)
+      if (__ballot((unsigned)jd < (unsigned)CPL) != 0 && (unsigned)jd < (unsigned)CPL) {
+        // the row's own member (step 3, :443-448): hb + 1 with a fresh
+        // stamp, never flagged; the rule above merged and rebased it on its
+        // diagonal code, whose written code is one lower (the snapshot
+        // carries hb + 1) and whose age is 1. Absent, a guard row or at the
+        // heartbeat cap: the per-cell rule
+        const int wj = jd >> 3, sh = gh_nib(jd & 7);
+#pragma unroll
+        for (int x = 0; x < W; ++x)
+          if (x == wj) {
+            const int qd = (int)((qwu[u].v[x] >> sh) & 0xFu);
+            ob = qd == 15 || (int64_t)bo[l0 + jd] + (GH_P_REF - qd) >= INT32_MAX;
+            QO[x] -= 1u << sh;
+            AO[x] = (AO[x] & ~(0xFu << sh)) | (1u << sh);
+          }
+      }
+      const bool okb = lane_ok && oku[u] && !esc && !ob && Bm == 0 && Lz == 0;
+      const bool seg_okb = (__ballot(al && !okb) & gmask) == 0;
+      int dpres = 0;
+      if (al && seg_okb) {
+        nib_store<W, NT>(pln_t + owu[u], QO);
+        nib_store<W, NT>(a4n_t + owu[u], AO);
+        n_mrg += (uint32_t)mrg;
+        dpres = gain;
+      } else if (al && lc == 0) {
+        s_slow[atomicAdd(&s_nslow, 1)] = i;
+      }
+      if (__ballot(dpres != 0) != 0) {  // absent cells merged: the row's count moves
+#pragma unroll
+        for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) dpres += __shfl_xor(dpres, o2);
+        if (lc == 0 && dpres) atomicAdd(&d.cntl[i], dpres);
+      }
+    }
+  }
+
+  if (n_mrg) atomicAdd(&s_merged, (unsigned long long)n_mrg);
+  __syncthreads();
+  if (tid == 0) {
+    if (s_nslow) s_slowbase = atomicAdd(d.slow_n, s_nslow);
+    if (s_merged) atomicAdd(&d.stats[ST_MERGED], s_merged);
+    if (s_quiet) atomicAdd(d.nquiet, s_quiet);
+  }
+  __syncthreads();
+  for (int t = tid; t < s_nslow; t += 256) d.slow[s_slowbase + t] = ((int64_t)tile << 32) | (uint32_t)s_slow[t];
+}
+
+// IN: 0 = a 16-bit input (full grid), 1 = a tier input by the 16-bit rule
+// (widened), 3 = a 16-bit input in a tiered engine (rarely selected: a
+// persistent 1/8 grid); IN = 2 (a tier input by the nibble path) is
+// round_block_nib above
 template <int KB, int TW, int TPW, bool NT, bool STORM, int IN>
 __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const int dcur, const GhRound& p,
                                             const int bid) {
@@ -636,11 +922,6 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   // this tile's segments for the slow list, appended with one global atomic
   __shared__ int s_nslow, s_slowbase;
   __shared__ int s_bmove;  // a column base of the tile moved this round
-  // 8-bit tier: per column of the tile the base move (base_next - base_cur,
-  // one byte each; the byte path's rebase), s_d8bad bit l = lane l's 8
-  // columns hold a move outside 0..15
-  __shared__ uint32_t s_d8[TW / 4];
-  __shared__ uint32_t s_d8bad;
   __shared__ int s_slow[RB];
   // per-row metadata of the workgroup's rows, staged once for its TPW tiles:
   // s_meta = alive | active << 1 | inbox count << 2; s_inb = first KB senders
@@ -678,11 +959,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     s_merged = s_det = s_rel = s_storm = s_tomb = s_unk = 0;
     s_quiet = 0;
     s_bmove = 0;  // set by the first tile's setup after the staging barrier
-    s_d8bad = 0u;
   }
   const bool pull = p.peer_mode == GH_PEER_PULL;
   // quiet rows may be skipped: no REMOVE pending anywhere (|D_{r-1}| = 0)
-  const bool quiet = d.cntg[p.n] == 0 && !p.force_slow && !(d.h8[0] && d.m8[2]);
+  const bool quiet = d.cntg[p.n] == 0 && !p.force_slow && !(d.a4[0] && d.m8[2]);
   const uint8_t* __restrict__ stab_cur = d.stab[p.r & 1];
   uint8_t* __restrict__ stab_nxt = d.stab[(p.r + 1) & 1];
   if constexpr (STORM) {
@@ -733,18 +1013,17 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   uint16_t* __restrict__ hnn = d.hn[cur ^ 1];
   const int32_t* __restrict__ bo = d.base[cur];
   const int32_t* __restrict__ bn = d.base[cur ^ 1];
-  // 8-bit tier of the buffer read / written (gh_internal.h: h8): a lane's 8
-  // cells are one 8-B load / store, widened to packed 16-bit codes in
-  // registers; an escaped chunk is read from / written to hn
+  // 4-bit tier of the buffer read / written (gh_internal.h: a4): a lane's 8
+  // cells are its plane word and its age word (4 B each), widened to packed
+  // 16-bit codes in registers; an escaped chunk is read from / written to hn
   // (lean variants: one instantiation per input tier)
   constexpr bool RD8 = IN == 1 || IN == 2;
-  constexpr bool BYTE = IN == 2;
-  // (the 8-bit write path only where a tiered engine runs: pull k <= 4, one
+  // (the tier write path only where a tiered engine runs: pull k <= 4, one
   // tile per workgroup)
   constexpr bool W8 = !STORM && KB == 4 && TPW == 1;
   const bool m8c = STORM ? gh_m8(d, cur) : RD8, m8n = W8 && gh_m8(d, cur ^ 1);
-  const uint8_t* __restrict__ h8o = d.h8[cur];
-  uint8_t* __restrict__ h8n = d.h8[cur ^ 1];
+  const uint32_t* __restrict__ a4o = d.a4[cur];
+  uint32_t* __restrict__ a4n = d.a4[cur ^ 1];
   int n_esc = 0;  // escaped chunks written
   // sender plane: read by the lean 4-slot variant when valid, written by
   // every variant in plane mode
@@ -768,11 +1047,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   char* hnn_t = reinterpret_cast<char*>(hnn + tcell);
   const char* plo_t = reinterpret_cast<const char*>(plo) + (plo ? tcell / 2 : 0);
   char* pln_t = reinterpret_cast<char*>(pln) + (pln ? tcell / 2 : 0);
-  const char* h8o_t = reinterpret_cast<const char*>(h8o) + (h8o ? tcell : 0);
-  char* h8n_t = reinterpret_cast<char*>(h8n) + (h8n ? tcell : 0);
+  const char* a4o_t = reinterpret_cast<const char*>(a4o) + (a4o ? tcell / 2 : 0);
+  char* a4n_t = reinterpret_cast<char*>(a4n) + (a4n ? tcell / 2 : 0);
   const uint32_t lb = (uint32_t)lc * (CPL * 2);  // lane's byte offset in a row segment (narrow)
-  const uint32_t lbp = (uint32_t)lc * 4;         // ... in a plane row segment
-  const uint32_t lb8 = (uint32_t)lc * CPL;       // ... in an 8-bit row segment
+  const uint32_t lbp = (uint32_t)lc * 4;         // ... in a plane (or age plane) row segment
   if (tid == 0) s_nslow = 0;
   for (int t = tid; t < TW; t += 256) {
     s_dcnt[t] = 0;
@@ -794,10 +1072,6 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       }
       const int64_t delta = (int64_t)bn[c] - bo[c];
       const uint32_t d5h = (delta > 1023 || delta < -1023) ? 0x8000u : ((uint32_t)(delta << 5) & 0xFFFFu);
-      if constexpr (BYTE) {
-        reinterpret_cast<uint8_t*>(s_d8)[2 * pp + h] = (uint8_t)(delta & 0xFF);
-        if (delta < 0 || delta > 15) atomicOr(&s_d8bad, 1u << ((2 * pp + h) >> 3));
-      }
       const int64_t thr = 1 - (int64_t)bn[c];
       const uint32_t tc = thr < 0 ? 0xFFFFu : thr > 1023 ? 0x7FFFu : (uint32_t)((thr << 5) | 31);
       dd |= d5h << (16 * h);
@@ -813,10 +1087,6 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   const uint32_t tcp = (uint32_t)min(p.t_cleanup, 31) * 0x10001u;
   __syncthreads();
   const bool tile_still = s_bmove == 0;
-  // the byte path (below) needs the base moves of the lane's columns in 0..15
-  const bool byte_lane = BYTE && ((s_d8bad >> lc) & 1u) == 0;
-  const uint2 d8 = BYTE ? *reinterpret_cast<const uint2*>(&s_d8[lc * 2]) : uint2{0u, 0u};
-  const uint32_t tfb = (uint32_t)(0x7F - min(p.t_fail, 15)) * 0x01010101u;  // age + tfb: bit 7 iff age > T_fail
   // lean: no REMOVE in the lane; storm: REMOVE applied in the packed path
   // unless a column has a single detector (that row keeps the member)
   bool lane_ok = !p.force_slow;
@@ -828,155 +1098,6 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   }
 
   constexpr int NIT = RB / RSTEP;
-  if constexpr (BYTE) {
-    // THE BYTE PATH (IN = 2: 8-bit tier in and out with a valid plane, the
-    // column layout, KB = 4; the 16-bit rule is not compiled into this
-    // instantiation): the lean rule on the one-byte cells themselves, four
-    // per dword (SWAR), no widening. Per cell: l = lag (GH_C8_REF - offset),
-    // a = age; the freshest sender's plane code u = l_s + 2 (gh_internal.h:
-    // GH_P_REF = GH_C8_REF + 1) merges iff l_s < l (u <= l + 1; an absent own
-    // cell, l = 15, takes any sender; u = 15 = no sender entry). Merged: lag
-    // u - 2, age 1; else age + 1; then the rebase l += base move. The row's
-    // own member (step 3): hb + 1, age 1, merged only by a larger snapshot
-    // (u <= l). A row segment whose every lane stays in the byte codes (lag
-    // 0..14, age <= min(T_fail, 15): no flag, no REMOVE, no guard row, no
-    // escape, plane codes exact) is written here; any other goes to the slow
-    // list (k_round_slow, the per-cell rule). Two row steps per iteration:
-    // both steps' loads are issued before either is computed.
-    static_assert(KB == 4 && NIT % 2 == 0, "byte path: 4 senders, an even row-step count");
-#pragma unroll 1
-    for (int it = 0; it < NIT; it += 2) {
-      int iu[2];
-      bool alu[2], oku[2];
-      uint32_t slu[2];
-      uint2 w8u[2];
-      uint32_t pwu[2][4];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int rr = wave * RPW + (it + u) * RSTEP + sub;
-        const int i_raw = (int)d.row0 + rb * RB + rr;
-        const bool valid = i_raw < rowend;
-        const int i = valid ? i_raw : rowend - 1;  // in-range row for the loads of idle lanes
-        const int rs = valid ? rr : 0;
-        const int meta = s_meta[rs];
-        const bool skip = ((meta >> 30) & 1) && tile_still;  // quiet row, bases still
-        if (valid && skip && lc == 0) atomicAdd(&s_quiet, 1);
-        const int cntv = (meta >> 2) & 0xFFFF;
-        alu[u] = (meta & 1) && valid && !skip;
-        oku[u] = ((meta >> 1) & 1) && cntv <= KB;  // active (not a guard row), at most KB senders
-        iu[u] = i;
-        const uint32_t islot = (uint32_t)(i - d.row0);
-        slu[u] = islot;
-        // the own bytes are read once (no peer reads them: senders come from
-        // the plane), so they stream past the caches the plane lines live in
-        const uint64_t w8v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(h8o_t + (islot * TW + lb8)));
-        w8u[u] = uint2{(uint32_t)w8v, (uint32_t)(w8v >> 32)};
-        const int4 v = *reinterpret_cast<const int4*>(&s_inb[rs * KB]);
-        const int sv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          // unused slots read the own row's codes (a no-op under the merge)
-          const uint32_t sq = q < cntv ? (uint32_t)sv[q] : islot;
-          pwu[u][q] = *reinterpret_cast<const uint32_t*>(plo_t + (sq * (TW / 2) + lbp));
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int i = iu[u];
-        const bool al = alu[u];
-        const uint2 w8 = w8u[u];
-        const uint32_t* pw = pwu[u];
-        uint32_t Lw = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t M = 0x000F000Fu << (4 * j);
-          uint32_t L = pw[0] & M;
-#pragma unroll
-          for (int q = 1; q < 4; ++q) L = pk_min_u16(L, pw[q] & M);
-          Lw |= L;
-        }
-        const uint32_t lo = Lw & 0x0F0F0F0Fu, hi = (Lw >> 4) & 0x0F0F0F0Fu;
-        const uint32_t U[2] = {__builtin_amdgcn_perm(hi, lo, 0x06040200u), __builtin_amdgcn_perm(hi, lo, 0x07050301u)};
-        const uint32_t X[2] = {w8.x, w8.y};
-        const uint32_t D[2] = {d8.x, d8.y};
-        uint32_t O[2], P[2], B[2];
-        int mrg = 0, gain = 0;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t x = X[h], uu = U[h], dd = D[h];
-          const uint32_t L = (x >> 4) & 0x0F0F0F0Fu, Ag = x & 0x0F0F0F0Fu;
-          const uint32_t A = (L + 0x01010101u) & 0x10101010u;                      // own absent (0x10)
-          const uint32_t N = (uu + 0x01010101u) & 0x10101010u;                     // no sender entry
-          const uint32_t Mg = ((L + 0x81818181u) - uu) & ~(N << 3) & 0x80808080u;  // merged (0x80)
-          const uint32_t MM = bmask(Mg);
-          const uint32_t V = uu + dd;
-          const uint32_t ln = ((V - 0x02020202u) & MM) | ((L + dd) & ~MM);         // next lag
-          const uint32_t an = (0x01010101u & MM) | ((Ag + 0x01010101u) & ~MM);     // next age
-          const uint32_t AN = bmask((A & ~(Mg >> 3)) << 3);                        // absent next
-          // a running cell outside the byte codes: lag above 14, a merged
-          // lag below 0 (V < 2), age above min(T_fail, 15)
-          B[h] = (((ln + 0x71717171u) | (an + tfb)) & ~AN & 0x80808080u) | (Mg & ~(V + 0x7E7E7E7Eu));
-          O[h] = (((ln & 0x0F0F0F0Fu) << 4) | an) | AN;
-          // plane code of the written cell: l + 2 (14 = older), absent 15
-          const uint32_t pq = ln + 0x02020202u;
-          const uint32_t OM = bmask((pq + 0x71717171u) & 0x80808080u);
-          P[h] = ((pq & ~OM) | (0x0E0E0E0Eu & OM) | AN) & 0x0F0F0F0Fu;
-          mrg += __builtin_popcount(Mg);
-          gain += __builtin_popcount(Mg & (A << 3));
-        }
-        const int jd8 = i - c0;
-        // (a wave-uniform branch: 1 wave in 256 holds an own member)
-        if (__ballot((unsigned)jd8 < 8u) != 0 && (unsigned)jd8 < 8u) {
-          // the row's own member (step 3, :443-448): hb + 1 with a fresh
-          // stamp, never flagged; its snapshot entry carries hb + 1 (plane
-          // code - 1). Not visible, a guard row or at the heartbeat cap: the
-          // per-cell rule
-          const int h = jd8 >> 2, sh = 8 * (jd8 & 3);
-          const int xb = (int)((X[h] >> sh) & 0xFFu), ub = (int)((U[h] >> sh) & 0xFFu),
-                    db = (int)((D[h] >> sh) & 0xFFu);
-          const int lo8 = xb >> 4;
-          const bool mo = ub <= 13 && ub <= lo8;
-          const int ln8 = (mo ? ub - 2 : lo8 - 1) + db;
-          const bool ob8b = xb == 0xFF || !oku[u] || ln8 < 0 || ln8 > 14 ||
-                            (int64_t)bo[l0 + jd8] + (GH_C8_REF - lo8) >= INT32_MAX;
-          const uint32_t m8b = 0xFFu << sh;
-          const int c = min(ln8 + 2, 14);
-          O[h] = (O[h] & ~m8b) | ((uint32_t)(((ln8 & 15) << 4) | 1) << sh);
-          P[h] = (P[h] & ~m8b) | ((uint32_t)(c <= 13 ? c - 1 : c) << sh);
-          B[h] = (B[h] & ~m8b) | (ob8b ? 0x80u << sh : 0u);
-          mrg += (int)mo - (int)(ub <= lo8 + 1 && ub != 15);
-        }
-        const bool okb = lane_ok && oku[u] && byte_lane && (w8.x & 0xFFu) != GH_C8_ESC && (B[0] | B[1]) == 0 &&
-                         (nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu)) == 0;
-        const bool seg_okb = (__ballot(al && !okb) & gmask) == 0;
-        int dpres = 0;
-        if (al && seg_okb) {
-          const uint64_t v8 = ((uint64_t)O[1] << 32) | O[0];
-          uint64_t* hp = reinterpret_cast<uint64_t*>(h8n_t + (slu[u] * TW + lb8));
-          const uint32_t E = __builtin_amdgcn_perm(P[1], P[0], 0x06040200u);
-          const uint32_t Od = __builtin_amdgcn_perm(P[1], P[0], 0x07050301u);
-          const uint32_t pwd = __builtin_amdgcn_perm(Od | (Od >> 4), E | (E >> 4), 0x06040200u);
-          uint32_t* pp = reinterpret_cast<uint32_t*>(pln_t + (slu[u] * (TW / 2) + lbp));
-          if constexpr (NT) {
-            __builtin_nontemporal_store(v8, hp);
-            __builtin_nontemporal_store(pwd, pp);
-          } else {
-            *hp = v8;
-            *pp = pwd;
-          }
-          n_mrg16 += 16u * (uint32_t)mrg;
-          dpres = gain;
-        } else if (al && lc == 0) {
-          s_slow[atomicAdd(&s_nslow, 1)] = i;
-        }
-        if (__ballot(dpres != 0) != 0) {  // absent cells merged: the row's count moves
-#pragma unroll
-          for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) dpres += __shfl_xor(dpres, o2);
-          if (lc == 0 && dpres) atomicAdd(&d.cntl[i], dpres);
-        }
-      }
-    }
-  } else {
 #pragma unroll 1
   for (int it = 0; it < NIT; ++it) {
     const int rr = wave * RPW + it * RSTEP + sub;
@@ -998,13 +1119,17 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     // own segment and the senders' snapshots, issued together: plane words
     // when the plane is valid, else the first KB senders' 16-bit segments
     // (slots q >= cntv hold the own row, a no-op under the max)
-    const uint32_t ob8 = islot * TW + lb8;      // ... in the 8-bit tier
+    const uint32_t obp = islot * (TW / 2) + lbp;  // ... in the plane and the age plane
     v4u w = {0u, 0u, 0u, 0u};
-    uint2 w8 = {0u, 0u};
-    if (m8c)
-      w8 = *reinterpret_cast<const uint2*>(h8o_t + ob8);
-    else
+    uint32_t a4w = 0u, q4w = 0u;
+    if (m8c) {
+      a4w = *reinterpret_cast<const uint32_t*>(a4o_t + obp);
+      q4w = *reinterpret_cast<const uint32_t*>(plo_t + obp);
+    } else {
       w = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + ob));  // re-read by peers: keep it cached
+    }
+    const int jd = i - c0;
+    const bool own_in = (unsigned)jd < 8u;
     int ps[KB];
     const bool act = (meta >> 1) & 1;  // else the row is under the <4 guard (step 2)
     // guard rows in the lean variant: the 8-slot instantiation (ring
@@ -1043,6 +1168,16 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 #pragma unroll
       for (int q = 0; q < KB; ++q) psl[q] = (uint32_t)ps[q];
     }
+    // a sender's segment: an owned row's in this tile of the table, a ghost
+    // row's (row layout, slot >= nrows) in the row-major ghost table
+    auto snd16 = [&](uint32_t sl) -> const uint16_t* {
+      if (d.gcodes && (int64_t)sl >= d.nrows) return d.gcodes + ((int64_t)sl - d.nrows) * d.ld + l0;
+      return reinterpret_cast<const uint16_t*>(hno_t + (sl * (TW * 2) + lb));
+    };
+    auto sndp = [&](uint32_t sl) -> const uint32_t* {
+      if (d.gplane && (int64_t)sl >= d.nrows) return d.gplane + ((((int64_t)sl - d.nrows) * d.ld + l0) >> 3);
+      return reinterpret_cast<const uint32_t*>(plo_t + (sl * (TW / 2) + lbp));
+    };
     uint32_t pw[KB];
     if constexpr (PLANE_RD) {
       if (use_plane) {
@@ -1050,22 +1185,19 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         // above the own cell, so a no-op under the merge (an unknown or old
         // code there only costs a fallback)
 #pragma unroll
-        for (int q = 0; q < KB; ++q)
-          pw[q] = *reinterpret_cast<const uint32_t*>(plo_t + (psl[q] * (TW / 2) + lbp));
+        for (int q = 0; q < KB; ++q) pw[q] = *sndp(psl[q]);
       }
     }
     if (m8c) {  // widen the own chunk (an escaped one is hn's)
-      if ((w8.x & 0xFFu) == GH_C8_ESC)
+      if (gh_t4_esc(a4w))
         w = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + ob));
       else
-        w = c8_dec(w8);
+        w = c4_dec(q4w, a4w, own_in ? jd : -1);
     }
     bad |= (w[0] & 0xFFFFu) == GH_N_WIDE;  // own segment wide
     // The row's own member in the lane (step 3, :443-448): hb + 1 with a
     // fresh stamp (age 0, so age 1 after the round's +1), never flagged.
     // An own cell that is not visible, or at the heartbeat cap, is slow.
-    const int jd = i - c0;
-    const bool own_in = (unsigned)jd < 8u;
     if (own_in && act) {
       const int sh = 16 * (jd & 1);
 #pragma unroll
@@ -1128,27 +1260,26 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
           for (int j = 0; j < 4; ++j) ms[j] = q == 0 ? pv[j] : pk_max_i16(ms[j], pv[j]);
         };
         if (m8c) {
-          // 8-bit sender chunks (absent: 0xFF bytes), all four issued, then
-          // widened one at a time (an escaped one is read from hn)
-          uint2 b8[4];
+          // tier sender chunks (plane and age words; unused slots: all
+          // absent), all four issued, then widened one at a time (an escaped
+          // one is read from hn)
+          uint32_t su[4], sa[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int q = g + u;
-            const uint2* src = reinterpret_cast<const uint2*>(h8o_t + (psl[q] * TW + lb8));
-            if constexpr (STORM)
-              b8[u] = q < cntv ? *src : uint2{~0u, ~0u};
-            else if constexpr (KB > 4)
-              b8[u] = __ballot(q < cntv) != 0 ? *src : uint2{~0u, ~0u};
-            else
-              b8[u] = *src;
+            const uint32_t off = psl[q] * (TW / 2) + lbp;
+            const bool ld = STORM ? q < cntv : KB > 4 ? __ballot(q < cntv) != 0 : true;
+            su[u] = ld ? *reinterpret_cast<const uint32_t*>(plo_t + off) : ~0u;
+            sa[u] = ld ? *reinterpret_cast<const uint32_t*>(a4o_t + off) : ~0u;
           }
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             v4u pv;
-            if ((b8[u].x & 0xFFu) == GH_C8_ESC)
+            const int js = ps[g + u] - c0;
+            if (gh_t4_esc(sa[u]))
               pv = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + (psl[g + u] * (TW * 2) + lb)));
             else
-              pv = c8_dec(b8[u]);
+              pv = c4_dec(su[u], sa[u], (unsigned)js < 8u ? js : -1);
             fold(pv, g + u);
           }
         } else {
@@ -1156,7 +1287,13 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int q = g + u;
-            const uint16_t* src = reinterpret_cast<const uint16_t*>(hno_t + (psl[q] * (TW * 2) + lb));
+            // row layout, a round whose ghosts carry only their plane
+            // (p.gpo): a ghost sender's 16-bit codes are not here yet, so
+            // the lane goes to the slow list (k_round_slow runs after they
+            // arrive) and reads the own row instead
+            const bool gq = p.gpo && q < cntv && (int64_t)psl[q] >= d.nrows;
+            bad |= gq;
+            const uint16_t* src = snd16(gq ? islot : psl[q]);
             if constexpr (STORM) {
               // storms hold few senders (guard rows none): load only the used
               // slots, the rest are absent (-1, a no-op under the max)
@@ -1304,15 +1441,15 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     if (al) {
       if (seg_ok) {
         if (m8n) {
-          uint32_t bad8 = 0;
-          const uint2 e8 = c8_enc(o, bad8);
-          uint64_t* hp = reinterpret_cast<uint64_t*>(h8n_t + ob8);
-          const uint64_t v8 = bad8 ? 0xF0F0F0F0F0F0F0F0ull : ((uint64_t)e8.y << 32) | e8.x;
+          // the tier: the age word, the plane word below is the lag
+          uint32_t age = 0;
+          const bool t4 = c4_enc(o, own_in ? jd : -1, age);
+          uint32_t* ap = reinterpret_cast<uint32_t*>(a4n_t + obp);
           if constexpr (NT)
-            __builtin_nontemporal_store(v8, hp);
+            __builtin_nontemporal_store(t4 ? age : GH_T4_ESC, ap);
           else
-            *hp = v8;
-          if (bad8) {  // escaped: the 16-bit chunk
+            *ap = t4 ? age : GH_T4_ESC;
+          if (!t4) {  // escaped: the 16-bit chunk
             stn<NT>(reinterpret_cast<uint16_t*>(hnn_t + ob), o);
             n_esc++;
           }
@@ -1364,13 +1501,9 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     // hold next round (flagged results) cells the lean variant cannot take
     if (al && seg_ok && (__ballot(stb != 0 || fo != 0) & gmask) != 0 && lc == 0) atomicAdd(&s_storm, 1ull);
   }
-  }  // the 16-bit rule's row loop
 
   __syncthreads();
-  if (tid == 0) {  // read before the barrier above; the next tile's setup writes them after two more
-    s_bmove = 0;
-    s_d8bad = 0u;
-  }
+  if (tid == 0) s_bmove = 0;  // read before the barrier above; the next tile's setup writes it after two more
   for (int t = tid; t < TW; t += 256) {
     if (s_dcnt[t]) {
       const int64_t c = (int64_t)tile * TW + t;
@@ -1414,11 +1547,11 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 // of the workgroups, each taking blocks a multiple of 8 apart (same XCD), so
 // idle they are a small dispatch.
 template <int KB, int TW, int TPW, bool NT, bool STORM, int IN>
-__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
+__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : IN == 2 ? GH_NIB_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
   if (*d.mode != (int)STORM) return;
   if constexpr (!STORM) {
     int want = 0;
-    if (d.h8[0])
+    if (d.a4[0])
       want = !gh_m8(d, cur) ? 3 : (KB == 4 && p.plane && d.pvalid[cur] && gh_m8(d, cur ^ 1)) ? 2 : 1;
     if (want != IN) return;
   }
@@ -1430,6 +1563,8 @@ __global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM 
       round_block<KB, TW, TPW, NT, STORM, IN>(d, cur, dcur, p, b);
       __syncthreads();  // LDS of this block before the next
     }
+  } else if constexpr (IN == 2) {
+    round_block_nib<TW, NT, GH_NIB_CPL>(d, cur, p, blockIdx.x);  // one block per workgroup
   } else {
     // one block per workgroup (a loop here costs the lean variants 20+ VGPRs)
     round_block<KB, TW, TPW, NT, STORM, IN>(d, cur, dcur, p, blockIdx.x);
@@ -1477,7 +1612,7 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
     uint4 nx = {0u, 0u, 0u, 0u};
     uint4 raw = {0u, 0u, 0u, 0u};  // the chunk as read (narrow codes or a wide marker)
     if (valid) {
-      raw = gh_ld16(d, cur, gh_cell(d, i, l0));
+      raw = gh_ld16(d, cur, i, l0);
       GhCell A[8], X[8];
       gh_dec8(d, cur, i, l0, r, raw, A);
       int64_t m[8];
@@ -1846,7 +1981,7 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
   const int64_t nrb = (d.nrows + RB - 1) / RB;
   const int64_t nblk = nrb * (p.ld / TW / TPW);
   if (nblk == 0) return;
-  const bool tiered = d.h8[0] != nullptr;
+  const bool tiered = d.a4[0] != nullptr;
   const bool few = variant == 1 || variant == 2 || (variant == 0 && tiered);
   const dim3 grid((unsigned)(few ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
 #define GH_ROUND_LAUNCH(NT, ST, IN) \

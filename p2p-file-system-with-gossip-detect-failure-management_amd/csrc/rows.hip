@@ -1,36 +1,41 @@
 // Row layout (GH_LAYOUT_ROWS, north_star; DESIGN.md "Multi-GPU"): the ghost
 // rows a shard's receivers pull. Before a round, each owner packs the rows
 // other shards asked for (their senders this round) into per-destination
-// blocks, one alltoallv moves them (comm.h: ncclAllToAllv), and the receiver
-// writes them into its ghost table slots, so k_round / k_round_slow read a
-// sender through the same tiled table as an owned row (gh_internal.h
-// rslot). The replaced reference step is the UDP list push between hosts,
+// blocks and alltoallv moves them (comm.h: ncclAllToAllv) straight into the
+// receivers' ghost tables (gh_internal.h gcodes / gplane, row-major, ghost j
+// = slot nrows + j), so k_round / k_round_slow read a sender by its slot.
+// Two parts travel separately: a ghost's sender plane (0.5 B per cell, all
+// a healthy round's k_round reads) and its 16-bit codes (2 B per cell, for
+// storm rounds and for the segments k_round leaves to k_round_slow). The
+// replaced reference step is the UDP list push between hosts,
 // slave/slave.go:527-542.
-//   k_ghost_pack    row-major narrow codes (+ plane words) of the rows to
-//                   send; counts the wide segments per destination
+//   k_ghost_pack    rows to send -> back-to-back plane words or codes;
+//                   the codes part counts the wide segments per destination
 //   k_ghost_wide    the exact cells of those wide segments (rare)
-//   k_ghost_unpack  received rows -> ghost slots of the current buffer
 //   k_ghost_unwide  received wide segments -> fresh arena slots of the
-//                   current buffer, marker chunks rewritten to them
+//                   current buffer, the ghost rows' marker chunks rewritten
 #include "gh_internal.h"
 
 namespace {
 
-// one thread per 8-cell chunk of a sent row: rowbytes = ld * 2 (+ ld / 2 with
-// the plane)
+// one thread per 8-cell chunk of a sent row; part GH_GX_PLANE: the row's
+// plane words (ld / 2 bytes per row), GH_GX_CODES: its narrow codes (ld * 2
+// bytes per row), counting its wide segments in wcnt[dest[e]]
 __global__ __launch_bounds__(256) void k_ghost_pack(GhDev d, int cur, const int32_t* rows, const int32_t* dest,
-                                                    int64_t ns, char* out, int64_t rowbytes, int32_t* wcnt) {
+                                                    int64_t ns, int part, char* out, int32_t* wcnt) {
   const int64_t cpr = d.ld >> 3;
   const int64_t total = ns * cpr;
   for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = idx / cpr, k = idx - e * cpr, c = k * 8;
     const int64_t cell = gh_cell(d, rows[e], c);
-    const uint4 x = *reinterpret_cast<const uint4*>(d.hn[cur] + cell);
-    char* o = out + e * rowbytes;
-    *reinterpret_cast<uint4*>(o + c * 2) = x;
-    if (d.pl[cur]) *reinterpret_cast<uint32_t*>(o + d.ld * 2 + k * 4) = d.pl[cur][cell >> 3];
-    if ((c & (d.tw - 1)) == 0 && (x.x & 0xFFFFu) == GH_N_WIDE) atomicAdd(&wcnt[dest[e]], 1);
+    if (part == GH_GX_PLANE) {
+      reinterpret_cast<uint32_t*>(out)[e * cpr + k] = d.pl[cur][cell >> 3];
+    } else {
+      const uint4 x = *reinterpret_cast<const uint4*>(d.hn[cur] + cell);
+      *reinterpret_cast<uint4*>(out + (e * d.ld + c) * 2) = x;
+      if ((c & (d.tw - 1)) == 0 && (x.x & 0xFFFFu) == GH_N_WIDE) atomicAdd(&wcnt[dest[e]], 1);
+    }
   }
 }
 
@@ -62,22 +67,8 @@ __global__ __launch_bounds__(256) void k_ghost_wide(GhDev d, int cur, const int3
   }
 }
 
-// one thread per chunk of a received row; row e goes to table slot slot0 + e
-__global__ __launch_bounds__(256) void k_ghost_unpack(GhDev d, int cur, const char* in, int64_t nr, int64_t rowbytes,
-                                                      int64_t slot0) {
-  const int64_t cpr = d.ld >> 3;
-  const int64_t total = nr * cpr;
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t e = idx / cpr, k = idx - e * cpr, c = k * 8;
-    const int64_t cell = gh_cell_slot(d, slot0 + e, c);
-    const char* o = in + e * rowbytes;
-    *reinterpret_cast<uint4*>(d.hn[cur] + cell) = *reinterpret_cast<const uint4*>(o + c * 2);
-    if (d.pl[cur]) d.pl[cur][cell >> 3] = *reinterpret_cast<const uint32_t*>(o + d.ld * 2 + k * 4);
-  }
-}
-
-// one thread per received wide record
+// one thread per received wide record: the ghost row's segment gets a fresh
+// arena slot of buffer cur (the round reads ghosts with cur's arena)
 __global__ __launch_bounds__(256) void k_ghost_unwide(GhDev d, int cur, const char* in, int64_t nrec) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (x >= nrec) return;
@@ -86,6 +77,8 @@ __global__ __launch_bounds__(256) void k_ghost_unwide(GhDev d, int cur, const ch
   const int64_t t = reinterpret_cast<const int32_t*>(o)[1];
   const int32_t* xs = reinterpret_cast<const int32_t*>(o + 8);
   const uint8_t* fs = reinterpret_cast<const uint8_t*>(o + 8 + 4 * (int64_t)d.tw);
+  const int64_t g = (int64_t)d.rslot[s] - d.nrows;  // its ghost row
+  if (g < 0 || g >= d.gcap) return;
   const int64_t a = gh_wide_alloc(d, cur);
   if (a < 0) return;  // arena full: the state is lost (d.err)
   for (int j = 0; j < d.tw; ++j) {
@@ -94,7 +87,7 @@ __global__ __launch_bounds__(256) void k_ghost_unwide(GhDev d, int cur, const ch
   }
   for (int j = 0; j < d.tw / 8; ++j) d.wf[cur][(a * d.tw >> 3) + j] = fs[j];
   const uint4 m = gh_wide_chunk(a);
-  for (int j = 0; j < d.tw; j += 8) *reinterpret_cast<uint4*>(d.hn[cur] + gh_cell(d, s, t * d.tw + j)) = m;
+  for (int j = 0; j < d.tw; j += 8) *reinterpret_cast<uint4*>(d.gcodes + g * d.ld + t * d.tw + j) = m;
 }
 
 unsigned ghost_grid(int64_t work) {
@@ -103,14 +96,14 @@ unsigned ghost_grid(int64_t work) {
 
 }  // namespace
 
-int64_t ghost_row_bytes(const GhDev& d) { return d.ld * 2 + (d.pl[0] ? d.ld / 2 : 0); }
+int64_t ghost_part_bytes(const GhDev& d, int part) { return part == GH_GX_PLANE ? d.ld / 2 : d.ld * 2; }
 int64_t ghost_wide_record_bytes(const GhDev& d) { return ghost_wide_bytes(d.tw); }
 
-void launch_ghost_pack(const GhDev& d, int cur, const int32_t* rows, const int32_t* dest, int64_t ns, char* out,
-                       int32_t* wcnt, hipStream_t s) {
+void launch_ghost_pack(const GhDev& d, int cur, const int32_t* rows, const int32_t* dest, int64_t ns, int part,
+                       char* out, int32_t* wcnt, hipStream_t s) {
   if (ns == 0) return;
-  hipLaunchKernelGGL(k_ghost_pack, dim3(ghost_grid(ns * (d.ld >> 3))), dim3(256), 0, s, d, cur, rows, dest, ns, out,
-                     ghost_row_bytes(d), wcnt);
+  hipLaunchKernelGGL(k_ghost_pack, dim3(ghost_grid(ns * (d.ld >> 3))), dim3(256), 0, s, d, cur, rows, dest, ns, part,
+                     out, wcnt);
 }
 
 void launch_ghost_wide(const GhDev& d, int cur, const int32_t* rows, const int32_t* dest, int64_t ns, int32_t* wcur,
@@ -118,12 +111,6 @@ void launch_ghost_wide(const GhDev& d, int cur, const int32_t* rows, const int32
   if (ns == 0) return;
   hipLaunchKernelGGL(k_ghost_wide, dim3(ghost_grid(ns * d.ntiles)), dim3(256), 0, s, d, cur, rows, dest, ns, wcur,
                      out);
-}
-
-void launch_ghost_unpack(const GhDev& d, int cur, const char* in, int64_t nr, int64_t slot0, hipStream_t s) {
-  if (nr == 0) return;
-  hipLaunchKernelGGL(k_ghost_unpack, dim3(ghost_grid(nr * (d.ld >> 3))), dim3(256), 0, s, d, cur, in, nr,
-                     ghost_row_bytes(d), slot0);
 }
 
 void launch_ghost_unwide(const GhDev& d, int cur, const char* in, int64_t nrec, hipStream_t s) {

@@ -49,6 +49,19 @@ def default_config(n, **kw) -> Config:
     return cfg
 
 
+def footprint(cfg: Config, rank: int = 0, world: int = 1, transport: int = GH_COMM_RCCL) -> dict:
+    """HBM one shard of `cfg` would hold (gh_footprint: a dry walk of
+    gh_create's allocations, no device needed): create_bytes (tables, plane,
+    tier, arenas, per-row / per-column vectors, files) and exchange_bytes
+    (the row layout's ghost-row buffers at the expected distinct senders of
+    a healthy pull round; 0 for column shards)."""
+    cb, xb = C.c_int64(), C.c_int64()
+    rc = _abi.load().gh_footprint(C.byref(cfg), rank, world, transport, C.byref(cb), C.byref(xb))
+    if rc != GH_OK:
+        raise GossipError(rc, "gh_footprint failed")
+    return {"create_bytes": cb.value, "exchange_bytes": xb.value, "total_bytes": cb.value + xb.value}
+
+
 def comm_unique_id() -> bytes:
     """RCCL unique id for a sharded cluster (rank 0 makes it, every rank uses it)."""
     buf = (C.c_uint8 * _abi.GH_COMM_ID_BYTES)()
@@ -387,12 +400,16 @@ class Cluster:
     """The reference's per-node commands over one Engine (member IDs stand in
     for the VM addresses). Repairs follow Fail_recover: every row that detects
     a failure in round r triggers Update_metadata with its own list as
-    `available` at round r + repair_delay (slave/slave.go:1122-1133). Lists
-    keep the reference's append order (GH_ORDER_APPEND) unless list_order is
-    given: lsm, ring targets, quirk runs, MemberList[0] and the placement
-    candidates read them as the reference's slices do (SPEC D1)."""
+    `available` at round r + repair_delay (slave/slave.go:1122-1133). The
+    defaults are the reference's own topology: gossip is the 3-neighbour ring
+    push (GH_PEER_RING, slave/slave.go:515-542) unless peer_mode is given,
+    and lists keep the reference's append order (GH_ORDER_APPEND) unless
+    list_order is given: lsm, ring targets, quirk runs, MemberList[0] and the
+    placement candidates read them as the reference's slices do (SPEC D1).
+    (Engine / gh_config_default keep Philox pull: the batched bench mode.)"""
 
     def __init__(self, n, repair_delay=8, addresses=None, elect=False, **cfg_kw):
+        cfg_kw.setdefault("peer_mode", GH_PEER_RING)
         cfg_kw.setdefault("list_order", GH_ORDER_APPEND)
         self.engine = Engine(default_config(n, **cfg_kw))
         self.n = n

@@ -126,20 +126,154 @@ kats.append(dict(
     expect_stats=dict(remove_unknown=3, tombstoned=1, detections=2, failed_members=1)))
 
 
+# ---- round 3: ring neighbours, JOIN broadcast, LEAVE lifetime, sole detector
+
+def ring_kat(name, sender, lst, own_hb, fresh_col, fresh_hb, targets, n=8):
+    """HeartBeat's ring (slave/slave.go:515-524): row `sender` holds `lst`
+    (ID order = list order) and is the only active row; every other alive
+    row holds 2 members (itself and `fresh_col`, stale hb 10), so it sits
+    under the <4 guard (:504-509): it stamps ts = now and sends nothing, but
+    still merges what it receives. The sender's snapshot carries `fresh_hb`
+    in column `fresh_col`; exactly the 3 neighbours `targets` take it."""
+    hb, ts, alive = blank(n)
+    for j in range(n):
+        alive[j] = 1
+        if j == sender:
+            continue
+        hb[j][j], ts[j][j] = 5, 99
+        hb[j][fresh_col], ts[j][fresh_col] = 10, 99
+    hb[sender] = [A] * n
+    for c in lst:
+        hb[sender][c], ts[sender][c] = 5, 99
+    if sender in lst:
+        hb[sender][sender] = own_hb
+    hb[sender][fresh_col] = fresh_hb - (1 if fresh_col == sender else 0)  # own hb++ first (:443-448)
+    more = []
+    for j in range(n):
+        if j == sender:
+            continue
+        got = j in targets
+        row_hb = [A] * n
+        row_ts = [0] * n
+        row_hb[j], row_ts[j] = 5, 100  # guard: ts = now, no hb++
+        row_hb[fresh_col], row_ts[fresh_col] = (fresh_hb, 100) if got else (10, 100)
+        if got:  # absent members of the snapshot are appended with ts = now (:430-439)
+            for c in lst:
+                if row_hb[c] == A:
+                    row_hb[c], row_ts[c] = (fresh_hb if c == fresh_col else (own_hb + 1 if c == sender else 5)), 100
+        more.append(dict(row=j, hb=row_hb, ts=row_ts))
+    return dict(name=name, n=n, round=99, detect_mode=0, peer_mode=1, fanout=3, seed=1, t_fail=1000,
+                t_cleanup=1000, hb=hb, ts=ts, alive=alive, events=[], expect_row=more[0]["row"],
+                expect_hb=more[0]["hb"], expect_ts=more[0]["ts"], expect_more=more[1:], expect_failed=[],
+                expect_detectors=[], expect_stats=dict(detections=0, active_rows=1))
+
+
+# KAT-9 ring, self at index 0: list [0, 2, 4, 6], idx 0 -> list[(0-1) mod 4]
+# = 6, list[1] = 2, list[2] = 4. Member 0's hb 50 -> 51 reaches rows 6, 2, 4
+# only.
+kats.append(ring_kat("kat9_ring_self_first", 0, [0, 2, 4, 6], 50, 0, 51, {6, 2, 4}))
+# KAT-10 ring, self at the last slot: list [1, 2, 3, 5, 6], idx 4 ->
+# list[3] = 5, list[5 mod 5] = 1, list[6 mod 5] = 2; row 3 is not a target.
+kats.append(ring_kat("kat10_ring_self_last", 6, [1, 2, 3, 5, 6], 50, 6, 51, {5, 1, 2}))
+# KAT-11 ring, self absent (removed from its own list): idx = -1 -> Go's
+# (-2) % 5 = -2, fixed to 3 (:520-522): list[3] = 4, list[0] = 0, list[1] = 1.
+# No own hb++; the sender's fresh view of member 7 (hb 40) reaches 4, 0, 1.
+kats.append(ring_kat("kat11_ring_self_absent", 6, [0, 1, 3, 4, 7], None, 7, 40, {4, 0, 1}))
+
+# KAT-12 JOIN broadcast (slave/slave.go:224-231, 250-272). Round 10: member 6
+# (a fresh process, empty list) joins through introducer 0, whose list is
+# [0(5), 1(5)]: 0 appends (6, hb 0, ts now) and sends its whole list to every
+# member of it, itself and the joiner included. Row 1 [1(7)] appends 0 (5)
+# and 6 (0); its own 7 > 5 stays. Row 2 [2(8), 0(5)] is not in 0's
+# list: it gets nothing. Row 6 takes the whole list with ts = now. After the
+# adds every row holds < 4 members, so the round itself only stamps ts = now
+# (guard, :504-509): no hb++, nothing sent.
+hb, ts, alive = blank(8)
+hb[0][0], hb[0][1] = 5, 5
+hb[1][1] = 7
+hb[2][2], hb[2][0] = 8, 5
+for j in (0, 1, 2):
+    alive[j] = 1
+    for c in range(8):
+        if hb[j][c] != A:
+            ts[j][c] = 9
+kats.append(dict(
+    name="kat12_join_broadcast", n=8, round=9, detect_mode=0, peer_mode=1, fanout=3, seed=1, t_fail=1000,
+    t_cleanup=1000, hb=hb, ts=ts, alive=alive, events=[[1, 6]], expect_row=1,
+    expect_hb=[5, 7, A, A, A, A, 0, A], expect_ts=[10, 10, 0, 0, 0, 0, 10, 0],
+    expect_more=[dict(row=6, hb=[5, 5, A, A, A, A, 0, A], ts=[10, 10, 0, 0, 0, 0, 10, 0]),
+                 dict(row=2, hb=[5, A, 8, A, A, A, A, A], ts=[10, 0, 10, 0, 0, 0, 0, 0]),
+                 dict(row=0, hb=[5, 5, A, A, A, A, 0, A], ts=[10, 10, 0, 0, 0, 0, 10, 0])],
+    expect_failed=[], expect_detectors=[], expect_stats=dict(detections=0, active_rows=0)))
+
+# KAT-13 LEAVE tombstone lifetime (slave/slave.go:232-235, 276-286, 484-497).
+# Members 0..4 fully connected and fresh (ts 19); member 4 leaves in round 20:
+# every other alive row tombstones it with its last ts 19 (removeMember keeps
+# the Member). cleanFailList drops it once ts < now - COOLDOWN (5): it lives
+# through rounds 20..24 and is released in round 25. Nothing re-adds it (a
+# tombstoned cell ignores merges; no snapshot lists it). T_fail = 1000.
+hb, ts, alive = blank(5)
+for j in range(5):
+    alive[j] = 1
+    for c in range(5):
+        hb[j][c], ts[j][c] = 5, 19
+for rounds, col4, t4, rel in ((5, T, 19, 0), (6, A, 0, 4)):
+    kats.append(dict(
+        name=f"kat13_leave_tombstone_{rounds}r", n=5, round=19, detect_mode=0, peer_mode=0, fanout=3, seed=3,
+        t_fail=1000, t_cleanup=5, hb=hb, ts=ts, alive=alive, events=[[2, 4]], rounds=rounds, expect_row=0,
+        expect_hb=[5 + rounds, None, None, None, col4], expect_ts=[19 + rounds, None, None, None, t4],
+        expect_failed=[], expect_detectors=[], expect_stats=dict(tombstoned=4, released=rel, detections=0)))
+
+# KAT-14 REMOVE sole-detector exception (slave/slave.go:338-363, 344-346):
+# KAT-8's layout, but only row 1 holds member 3 stale (ts 10; rows 0 and 2
+# hold it fresh, ts 19). Round 20: row 1 alone detects 3 and releases it at
+# once. Round 21: REMOVE(3) reaches every alive row except its only detector
+# (the detector does not message itself): rows 0 and 2 tombstone it (ts 19
+# kept), row 4 never knew it (remove_unknown 1), row 1 gets nothing (KAT-8,
+# with two detectors: remove_unknown 3).
+hb, ts, alive = blank(8)
+for i in (0, 1, 2, 4):
+    alive[i] = 1
+    for c in (i, 5, 6, 7):
+        hb[i][c] = 5
+        ts[i][c] = 19
+hb[0][3], ts[0][3] = 6, 19
+hb[1][3], ts[1][3] = 6, 10
+hb[2][3], ts[2][3] = 6, 19
+kats.append(dict(
+    name="kat14_remove_sole_detector", n=8, round=19, detect_mode=0, peer_mode=0, fanout=3, seed=1, t_fail=5,
+    t_cleanup=5, hb=hb, ts=ts, alive=alive, events=[], rounds=2, expect_row=1,
+    expect_hb=[A, 7, A, A, A, 5, 5, 5], expect_ts=[0, 21, 0, 0, 0, 19, 19, 19],
+    expect_more=[dict(row=2, hb=[A, A, 7, T, A, 5, 5, 5], ts=[0, 0, 21, 19, 0, 19, 19, 19]),
+                 dict(row=0, hb=[7, A, A, T, A, 5, 5, 5], ts=[21, 0, 0, 19, 0, 19, 19, 19])],
+    expect_failed=[], expect_detectors=[],
+    expect_stats=dict(remove_unknown=1, tombstoned=2, detections=1, failed_members=1)))
+
+
+def row_matches(name, hb, ts, i, exp_hb, exp_ts):
+    """hb of row i equals exp_hb (None = any), ts where present"""
+    for c, v in enumerate(exp_hb):
+        if v is None:
+            continue
+        assert hb[i][c] == v, (name, i, c, list(hb[i]))
+        if v != A:
+            assert ts[i][c] == exp_ts[c], (name, i, c, list(ts[i]))
+
+
 def check_with_listsim(k):
     import oracle.listsim as L
     L.T_FAIL, L.T_CLEANUP = k["t_fail"], k["t_cleanup"]
     sim = ListSim.from_dense(k["hb"], k["ts"], k["alive"], k["round"], seed=k["seed"],
                              peer_mode="ring" if k["peer_mode"] else "pull", fanout=k["fanout"],
                              quirk=bool(k["detect_mode"]))
+    if k["events"]:
+        sim.apply_events([tuple(e) for e in k["events"]])
     st = sim.step(k.get("rounds", 1))
     hb, ts, _ = sim.dense()
-    i = k["expect_row"]
     if k["expect_hb"] is not None:
-        assert list(hb[i]) == k["expect_hb"], (k["name"], list(hb[i]))
-        for c, v in enumerate(k["expect_hb"]):
-            if v != A:
-                assert ts[i][c] == k["expect_ts"][c], (k["name"], c, list(ts[i]))
+        row_matches(k["name"], hb, ts, k["expect_row"], k["expect_hb"], k["expect_ts"])
+    for m in k.get("expect_more", []):
+        row_matches(k["name"], hb, ts, m["row"], m["hb"], m["ts"])
     for key, v in k["expect_stats"].items():
         assert st[key] == v, (k["name"], key, st[key], v)
     if k.get("rounds", 1) == 1:

@@ -14,17 +14,27 @@ def kat_config(mod, k):
                               t_cleanup=k["t_cleanup"])
 
 
+def check_row(k, hb, ts, i, exp_hb, exp_ts):
+    """row i of (hb, ts) equals exp_hb (None = not checked), ts where present"""
+    for c, v in enumerate(exp_hb):
+        if v is None:
+            continue
+        assert hb[i][c] == v, (k["name"], i, c, list(hb[i]))
+        if v != -1:
+            assert ts[i][c] == exp_ts[c], (k["name"], i, c, list(ts[i]))
+
+
 def run_kat(engine, k):
     engine.import_state(np.array(k["hb"], np.int32), np.array(k["ts"], np.int32),
                         np.array(k["alive"], np.uint8), k["round"])
+    if k["events"]:  # applied at the first round (its events phase)
+        engine.apply_events([tuple(e) for e in k["events"]])
     st = engine.step(k.get("rounds", 1))
     hb, ts, _ = engine.export_state()
-    i = k["expect_row"]
     if k["expect_hb"] is not None:
-        assert list(hb[i]) == k["expect_hb"], (k["name"], list(hb[i]))
-        exp_ts = np.array(k["expect_ts"])
-        keep = np.array(k["expect_hb"]) != -1
-        assert list(ts[i][keep]) == list(exp_ts[keep]), (k["name"], list(ts[i]))
+        check_row(k, hb, ts, k["expect_row"], k["expect_hb"], k["expect_ts"])
+    for m in k.get("expect_more", []):
+        check_row(k, hb, ts, m["row"], m["hb"], m["ts"])
     for key, v in k["expect_stats"].items():
         assert st[key] == v, (k["name"], key, st[key], v)
     if k.get("rounds", 1) == 1:

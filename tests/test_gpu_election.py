@@ -176,7 +176,7 @@ def test_cluster_rebuild_fatal_and_self_votes(gs):
     ts = np.zeros((n, n), np.int32)
     alive = np.ones(n, np.uint8)
     alive[0] = 0
-    cl = gs.Cluster(n, elect=True, t_fail=8, t_cleanup=30, fanout=2)
+    cl = gs.Cluster(n, elect=True, t_fail=8, t_cleanup=30, fanout=2, peer_mode=gs.GH_PEER_PULL)
     cl.engine.import_state(hb, ts, alive, 0)
     cl.dead.add(0)
     cl.tick(1)
@@ -220,7 +220,7 @@ def test_crash_join_then_master_crash(gs):
     configured one, VoteStatus off; when the master then crashes it votes
     like everyone else and is not taken for a dead process."""
     n = 32
-    cl = gs.Cluster(n, elect=True, max_files=64, seed=0x5EED0F36, t_fail=8, t_cleanup=8)
+    cl = gs.Cluster(n, elect=True, max_files=64, seed=0x5EED0F36, t_fail=8, t_cleanup=8, peer_mode=gs.GH_PEER_PULL)
     cl.engine.import_state(*sc.full_state(n), 0)
     cl.tick(2)
     cl.put(range(64))

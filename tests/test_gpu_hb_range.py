@@ -90,13 +90,20 @@ def test_int32_overflow_refused_like_the_oracle(gs, oracle_mod):
     compare(eng, orc, 3)
     h, _, _ = eng.export_state()
     assert h[5, 5] == I32MAX
-    # refused again, nothing runs; member 5 leaving lets the cluster go on
+    # refused again, nothing runs, and a refused round's events stay pending
+    # (member 9's leave); member 5 crashing in the same round lets it run
+    eng.apply_events([(sc.LEAVE, 9)])
+    orc.apply_events([(sc.LEAVE, 9)])
     rc1, s1 = eng.step_rc(1)
-    assert rc1 == gs._abi.GH_ERANGE and s1["rounds"] == 0
+    rc2, s2 = orc.step_rc(1)
+    assert rc1 == rc2 == gs._abi.GH_ERANGE and s1 == s2 and s1["rounds"] == 0
+    compare(eng, orc, 3)
     eng.apply_events([(sc.CRASH, 5)])
     orc.apply_events([(sc.CRASH, 5)])
     assert eng.step(4) == orc.step(4)
     compare(eng, orc, 7)
+    h, _, al = eng.export_state()
+    assert not al[5] and not al[9] and h[0, 9] == -2  # both events ran in round 4
     eng.close()
 
 

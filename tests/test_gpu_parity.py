@@ -264,6 +264,7 @@ def test_cluster_datagram_roundtrip(gs):
     """Cluster.datagram/receive: a member's list in the reference's wire
     format merged at another member (10 VMs, config 1 shape)."""
     cl = gs.Cluster(10, max_files=16)
+    assert cl.engine.cfg.peer_mode == gs.GH_PEER_RING  # the facade gossips the reference's ring (SURVEY §8 f1)
     for m in range(10):
         cl.join(m)
         cl.tick()

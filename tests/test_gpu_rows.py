@@ -28,18 +28,17 @@ def rows_cfg(**kw):
 
 
 def test_row_layout_shapes(gs):
-    """Shards own contiguous row ranges, every column; ring mode is refused."""
-    grp = gs.ShardGroup(gs.default_config(100, shard_layout=ROWS), 3)
-    try:
-        assert [x[2:] for x in grp.run("shard_info")] == [(0, 100)] * 3
-    finally:
-        grp.close()
-    with pytest.raises(gs.GossipError):
-        gs.ShardGroup(gs.default_config(100, shard_layout=ROWS, peer_mode=gs.GH_PEER_RING), 2)
+    """Shards own contiguous row ranges, every column, in pull and ring mode."""
+    for pm in (gs.GH_PEER_PULL, gs.GH_PEER_RING):
+        grp = gs.ShardGroup(gs.default_config(100, shard_layout=ROWS, peer_mode=pm), 3)
+        try:
+            assert [x[2:] for x in grp.run("shard_info")] == [(0, 100)] * 3
+        finally:
+            grp.close()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("k", [k for k in KATS if k["peer_mode"] == 0], ids=lambda k: k["name"])
+@pytest.mark.parametrize("k", KATS, ids=lambda k: k["name"])
 def test_kats_rows(gs, k, world):
     cfg = kat_config(gs, k)
     cfg.shard_layout = ROWS
@@ -155,3 +154,79 @@ def test_rows_match_columns_and_single(gs):
         np.testing.assert_array_equal(a[1], b[1])
         np.testing.assert_array_equal(a[2], b[2])
         np.testing.assert_array_equal(a[2], c[2])
+
+
+@pytest.mark.parametrize("world,n,seed", [(2, 64, 1), (3, 300, 2), (5, 200, 3), (8, 300, 4)])
+def test_ring_rows(gs, oracle_mod, world, n, seed):
+    """The reference's ring push (slave/slave.go:515-524) over row shards:
+    each sender's owner finds its 3 targets in its own row, the targets are
+    reduced, and the senders' rows travel to their receivers' owners; churn
+    makes lists differ, so targets jump across shards."""
+    sched = sc.random_churn(n, 30, 0x60 + seed, p_crash=0.03, p_leave=0.01, p_join=0.05)
+    run_group(gs, oracle_mod, world, rows_cfg(peer_mode=gs.GH_PEER_RING, seed=0x5EED0900 + seed, t_fail=5,
+                                              t_cleanup=5), n, 30, sched, init=sc.full_state(n))
+
+
+def test_ring_rows_quirk(gs, oracle_mod):
+    """Ring push and the reference's quirk detection over 3 row shards."""
+    n = 120
+    sched = sc.random_churn(n, 30, 0x6A, p_crash=0.06, p_leave=0.02, p_join=0.05)
+    run_group(gs, oracle_mod, 3, rows_cfg(peer_mode=gs.GH_PEER_RING, detect_mode=1, seed=0x5EED0910, t_fail=3,
+                                          t_cleanup=5), n, 30, sched, init=sc.full_state(n))
+
+
+def test_ring_rows_halo(gs, oracle_mod):
+    """in a healthy ring the targets of a sender are its adjacent
+    members, so each row shard needs only the few rows across its two
+    boundaries (a halo), not k * rows / G ghost rows."""
+    n, world = 4096, 4
+    cfg = rows_cfg(peer_mode=gs.GH_PEER_RING, seed=0x5EED0920, t_fail=40, t_cleanup=40)
+    grp = gs.ShardGroup(gs.default_config(n, **cfg), world)
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    try:
+        init = sc.full_state(n)
+        grp.import_state(*init, 0)
+        orc.import_state(*init, 0)
+        for r in range(1, 9):
+            assert grp.step(1) == orc.step(1)
+            for x in grp.run("exchange_info"):
+                assert 0 < x["ghost_rows"] <= 4, x
+        h1, t1, _ = grp.export_state()
+        h2, t2, _ = orc.export_state()
+        assert np.array_equal(h1, h2) and np.array_equal(t1, t2)
+    finally:
+        grp.close()
+        orc.close()
+
+
+def test_plane_only_ghosts(gs, oracle_mod, monkeypatch):
+    """A healthy pull round moves only the ghosts' sender plane (0.5 B per
+    cell): the 16-bit codes follow only when a segment needs the per-cell
+    rule, so a storm round still moves them; parity either way."""
+    monkeypatch.setenv("GH_PLANE", "1")
+    n, world = 2048, 4
+    cfg = rows_cfg(fanout=4, seed=0x5EED0930, t_fail=16, t_cleanup=16)
+    grp = gs.ShardGroup(gs.default_config(n, **cfg), world)
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    try:
+        init = sc.full_state(n)
+        grp.import_state(*init, 0)
+        orc.import_state(*init, 0)
+        ld = n  # padded columns (n is a multiple of 8 * 256)
+        plane_only = 0
+        for r in range(1, 21):
+            if r == 12:
+                ev = [(sc.CRASH, c) for c in sc.crash_ids(n, 0.02, 0x5EED0931)]
+                grp.apply_events(ev)
+                orc.apply_events(ev)
+            assert grp.step(1) == orc.step(1), r
+            for x in grp.run("exchange_info"):
+                if x["ghost_rows"] and x["bytes_in"] == x["ghost_rows"] * ld // 2:
+                    plane_only += 1
+        h1, t1, _ = grp.export_state()
+        h2, t2, _ = orc.export_state()
+        assert np.array_equal(h1, h2) and np.array_equal(t1, t2)
+        assert plane_only >= world * 5, plane_only  # the healthy rounds moved planes only
+    finally:
+        grp.close()
+        orc.close()

@@ -4,8 +4,8 @@
 # separate passes), then a kernel-trace --stats run of the same command.
 #   tools/pmc.sh [warmup] [steps]   -> gpurun_out/pmc/summary.json, gpurun_out/pmc/stats/
 set -o pipefail
-W=${1:-12}
-S=${2:-5}
+W=${1:-5}
+S=${2:-20}
 CMD="python3 bench.py --steps $S --warmup $W --no-cpu-baseline --no-secondary --files 0"
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp

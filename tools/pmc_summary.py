@@ -39,14 +39,17 @@ import os  # noqa: E402
 # say otherwise
 plane = int(3 <= k <= 4 and (os.environ["GH_PLANE"] != "0" if "GH_PLANE" in os.environ else n >= 16384))
 tw = int(os.environ.get("GH_TILE_W", "256" if plane else "64"))
-# the 8-bit tier comes with the plane (column layout, one tile per workgroup)
-tier8 = int(plane and os.environ.get("GH_C8", "1") != "0" and os.environ.get("GH_ROUND_TPW", "1") == "1")
-cb = 1 if tier8 else 2
-out["config"] = {"n": n, "k": k, "world": 1, "cell_bytes": cb, "warmup": warmup, "steps": steps,
+# the 4-bit tier comes with the plane (column layout, one tile per workgroup)
+tier4 = int(plane and os.environ.get("GH_C8", "1") != "0" and os.environ.get("GH_ROUND_TPW", "1") == "1")
+enc = "t4" if tier4 else "u16"
+out["config"] = {"n": n, "k": k, "world": 1, "encoding": enc, "warmup": warmup, "steps": steps,
                  "plane": plane, "tile_width": tw,
                  "command": f"python3 bench.py --steps {steps} --warmup {warmup} --no-cpu-baseline --no-secondary "
                             "--files 0"}
-out["compulsory_bytes"] = (2.0 * cb + (1.0 if plane else 0.0)) * n * n  # table in + out, plane out + in
+# compulsory bytes: t4 = lag + age nibbles in and out (the lag nibbles are the
+# plane); u16 = 2-B cells in and out, the plane out and in
+out["compulsory_bytes"] = (2.0 if tier4 else (4.0 + (1.0 if plane else 0.0))) * n * n
+out["prev_model_bytes"] = 3.0 * n * n  # round 2's 8-bit tier model (1-B cells + the plane)
 out["gather_bytes"] = 2.0 * n * n * k
 if "traffic_bytes" in out:
     out["traffic_over_compulsory"] = out["traffic_bytes"] / out["compulsory_bytes"]

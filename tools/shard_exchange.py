@@ -14,8 +14,9 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 G = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 out = {"n": n, "world": G, "k": 4, "transport": "LOCAL (one GPU)"}
-for layout in ("columns", "rows"):
+for layout, pm in (("columns", "pull"), ("rows", "pull"), ("rows", "ring")):
     cfg = gs.default_config(n, fanout=4, seed=0x5EED0003, t_fail=16, t_cleanup=16,
+                            peer_mode=gs.GH_PEER_RING if pm == "ring" else gs.GH_PEER_PULL,
                             shard_layout=gs.GH_LAYOUT_ROWS if layout == "rows" else gs.GH_LAYOUT_COLUMNS)
     grp = gs.ShardGroup(cfg, G)
     try:
@@ -32,8 +33,8 @@ for layout in ("columns", "rows"):
             rec["ghost_rows_per_shard"] = [x["ghost_rows"] for x in ex]
             rec["bytes_in_per_shard"] = [x["bytes_in"] for x in ex]
             rec["bytes_in_total_per_round"] = sum(x["bytes_in"] for x in ex)
-        out[layout] = rec
-        print(layout, json.dumps(rec), flush=True)
+        out[f"{layout}_{pm}"] = rec
+        print(layout, pm, json.dumps(rec), flush=True)
     finally:
         grp.close()
 print(json.dumps(out))
