@@ -2,5 +2,5 @@
 # The whole -m gpu suite (one process), then the smoke test.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread -s > gpurun_out/r03_pytest_gpu.log 2>&1 &&
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_smoke.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -s > gpurun_out/r03_pytest_gpu.log 2>&1 &&
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_smoke.log 2>&1
