@@ -637,36 +637,47 @@ template <int W>
 struct NibWords {
   uint32_t v[W];
 };
+// Buffer resource over one tile slice of a plane (gfx9 descriptor word 3):
+// the lanes then address it by 32-bit byte offsets (buffer_load ... offen,
+// the base in SGPRs), with no 64-bit address arithmetic per load; an offset
+// past the slice reads 0 and a store past it is dropped.
+// The base is made wave-uniform explicitly: a by-value GhDev's arrays indexed
+// by the runtime buffer number read as divergent, and a divergent resource
+// costs a waterfall loop per access.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t nib_rsrc(const void* p, int64_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint64_t u = ((uint64_t)(uint32_t)uni((int)(a >> 32)) << 32) | (uint32_t)uni((int)(uint32_t)a);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(u), (short)0,
+                                           uni((int)min(bytes, (int64_t)INT_MAX)), 0x00020000);
+}
+// cache policy of a buffer access on gfx950: 2 = nt (streamed once)
 template <int W, bool NTL>
-__device__ __forceinline__ NibWords<W> nib_load(const char* p) {
+__device__ __forceinline__ NibWords<W> nib_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  constexpr int aux = NTL ? 2 : 0;
   NibWords<W> o;
   if constexpr (W == 1) {
-    o.v[0] = NTL ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(p)) : *reinterpret_cast<const uint32_t*>(p);
+    o.v[0] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, aux);
   } else if constexpr (W == 2) {
-    const uint64_t x = NTL ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p))
-                           : *reinterpret_cast<const uint64_t*>(p);
-    o.v[0] = (uint32_t)x;
-    o.v[1] = (uint32_t)(x >> 32);
+    const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, aux);
+    o.v[0] = x[0];
+    o.v[1] = x[1];
   } else {
-    const v4u x = NTL ? __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p)) : *reinterpret_cast<const v4u*>(p);
+    const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, aux);
 #pragma unroll
     for (int j = 0; j < 4; ++j) o.v[j] = x[j];
   }
   return o;
 }
 template <int W, bool NTS>
-__device__ __forceinline__ void nib_store(char* p, const uint32_t* v) {
+__device__ __forceinline__ void nib_store(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint32_t* v) {
+  constexpr int aux = NTS ? 2 : 0;
   if constexpr (W == 1) {
-    if constexpr (NTS) __builtin_nontemporal_store(v[0], reinterpret_cast<uint32_t*>(p));
-    else *reinterpret_cast<uint32_t*>(p) = v[0];
+    __builtin_amdgcn_raw_buffer_store_b32(v[0], r, (int)off, 0, aux);
   } else if constexpr (W == 2) {
-    const uint64_t x = ((uint64_t)v[1] << 32) | v[0];
-    if constexpr (NTS) __builtin_nontemporal_store(x, reinterpret_cast<uint64_t*>(p));
-    else *reinterpret_cast<uint64_t*>(p) = x;
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(u32x2{v[0], v[1]}, r, (int)off, 0, aux);
   } else {
-    const v4u x = {v[0], v[1], v[2], v[3]};
-    if constexpr (NTS) __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(p));
-    else *reinterpret_cast<v4u*>(p) = x;
+    __builtin_amdgcn_raw_buffer_store_b128(v4u{v[0], v[1], v[2], v[3]}, r, (int)off, 0, aux);
   }
 }
 
@@ -725,7 +736,9 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       const int cnt = al ? gh_in_cnt(d, pull, p.k, i) : 0;
       const int act = d.active[i];
       meta = al | (act << 1) | (cnt << 2) | ((quiet && al && !act && cnt == 0 && stab_cur[i]) ? 1 << 30 : 0);
-      if (q < cnt) sv = d.inbox[gh_in_beg(d, pull, p.k, i) + q];
+      // the sender's plane row segment as a byte offset in the tile slice;
+      // unused slots read the own row's (a no-op under the merge)
+      sv = (q < cnt ? d.inbox[gh_in_beg(d, pull, p.k, i) + q] : (int)(i - d.row0)) * (TW / 2);
     }
     if (q == 0) s_meta[row] = meta;
     s_inb[t] = sv;
@@ -745,10 +758,11 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const int64_t l0 = (int64_t)tile * TW + lc * CPL;  // local column of this lane's first cell
   const int c0 = (int)(d.col0 + l0);
   const int64_t tcell = (int64_t)tile * d.tstride;
-  const char* plo_t = reinterpret_cast<const char*>(d.pl[cur]) + tcell / 2;
-  char* pln_t = reinterpret_cast<char*>(d.pl[cur ^ 1]) + tcell / 2;
-  const char* a4o_t = reinterpret_cast<const char*>(d.a4[cur]) + tcell / 2;
-  char* a4n_t = reinterpret_cast<char*>(d.a4[cur ^ 1]) + tcell / 2;
+  const int64_t tbytes = d.tstride / 2;  // one tile slice of a plane
+  const auto plo_t = nib_rsrc(reinterpret_cast<const char*>(d.pl[cur]) + tcell / 2, tbytes);
+  const auto pln_t = nib_rsrc(reinterpret_cast<const char*>(d.pl[cur ^ 1]) + tcell / 2, tbytes);
+  const auto a4o_t = nib_rsrc(reinterpret_cast<const char*>(d.a4[cur]) + tcell / 2, tbytes);
+  const auto a4n_t = nib_rsrc(reinterpret_cast<const char*>(d.a4[cur ^ 1]) + tcell / 2, tbytes);
   const uint32_t lbp = (uint32_t)lc * (CPL / 2);  // the lane's byte offset in a plane row segment
   const bool tile_still = s_bmove == 0;
   // the lane: no REMOVE'd member (REMOVE needs the per-cell rule), base
@@ -790,16 +804,12 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       // the age words are read once (no peer reads them): they stream past
       // the caches the plane lines live in; the own plane words are a line
       // the row's receivers gather too
-      awu[u] = nib_load<W, true>(a4o_t + ow);
-      qwu[u] = nib_load<W, false>(plo_t + ow);
+      awu[u] = nib_load<W, true>(a4o_t, ow);
+      qwu[u] = nib_load<W, false>(plo_t, ow);
       const int4 sv4 = *reinterpret_cast<const int4*>(&s_inb[rs * KB]);
       const int sv[4] = {sv4.x, sv4.y, sv4.z, sv4.w};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        // unused slots read the own row's codes (a no-op under the merge)
-        const uint32_t sq = q < cntv ? (uint32_t)sv[q] : islot;
-        pwu[u][q] = nib_load<W, false>(plo_t + (sq * (TW / 2) + lbp));
-      }
+      for (int q = 0; q < 4; ++q) pwu[u][q] = nib_load<W, false>(plo_t, (uint32_t)sv[q] + lbp);
     }
 #pragma unroll
     for (int u = 0; u < RS; ++u) {
@@ -867,8 +877,8 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       const bool seg_okb = (__ballot(al && !okb) & gmask) == 0;
       int dpres = 0;
       if (al && seg_okb) {
-        nib_store<W, NT>(pln_t + owu[u], QO);
-        nib_store<W, NT>(a4n_t + owu[u], AO);
+        nib_store<W, NT>(pln_t, owu[u], QO);
+        nib_store<W, NT>(a4n_t, owu[u], AO);
         n_mrg += (uint32_t)mrg;
         dpres = gain;
       } else if (al && lc == 0) {
