@@ -153,10 +153,10 @@
 #define GH_WG_ROWS_WIDE 256      // round kernel: rows per workgroup at TW >= 128
 #endif
 #ifndef GH_NIB_CPL
-#define GH_NIB_CPL 8            // nibble path: cells per lane (8, 16, 32: 4-, 8-, 16-B lane accesses)
+#define GH_NIB_CPL 16           // nibble path: cells per lane (8, 16, 32: 4-, 8-, 16-B lane accesses; 16 measured best)
 #endif
 #ifndef GH_NIB_RS
-#define GH_NIB_RS 0             // nibble path: row steps per iteration (0: 2 for CPL <= 16, else 1)
+#define GH_NIB_RS 1             // nibble path: row steps per iteration (1 measured best at CPL 8 and 16)
 #endif
 #ifndef GH_NIB_WAVES
 #define GH_NIB_WAVES 1          // nibble path: min waves per SIMD it is compiled for (1: the compiler picks)
@@ -736,6 +736,9 @@ struct GhRound {
 // round.hip
 void launch_active_pre(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_active_post(const GhDev& d, const GhRound& p, hipStream_t s);
+// one engine (world 1): launch_base + the guard of every row, decided in
+// place (no count exchange, no launch_active_post)
+void launch_prologue(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 // row layout: draw validity at the senders' owners (pvf, then SUM over
 // shards), then every receiver's inbox

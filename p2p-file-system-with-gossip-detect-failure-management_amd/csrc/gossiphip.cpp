@@ -993,7 +993,9 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
       break;
     if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
         (rc = dalloc(e, &d.det_any, e->n, 0)) || (rc = dalloc(e, &d.und, e->n, 0)) ||
-        (rc = dalloc(e, &d.cntl, e->n + 8, 0)) || (rc = dalloc(e, &d.cntg, e->n + 8, 0)) ||
+        (rc = dalloc(e, &d.cntl, e->n + 8, 0)) ||
+        // one engine: the global counts ARE the local ones (no copy per round)
+        (e->world == 1 ? (d.cntg = d.cntl, 0) : (rc = dalloc(e, &d.cntg, e->n + 8, 0))) ||
         (rc = dalloc(e, &d.post, e->n, 0)))
       break;
     if ((rc = dalloc(e, &d.det_cnt[0], e->ld, 0)) || (rc = dalloc(e, &d.det_cnt[1], e->ld, 0)) ||
@@ -1079,6 +1081,11 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
 int decide_active(Engine* e, const GhRound& p) {
   GhDev& d = e->d;
   int rc;
+  if (e->world == 1) {  // with k_base in one launch (gh_step skips launch_base)
+    launch_prologue(d, e->cur, e->dcur, p, e->stream);
+    HIPCHK(e, hipGetLastError());
+    return GH_OK;
+  }
   if ((rc = allreduce_i32(e, d.cntl, d.cntg, (size_t)e->n + 3))) return rc;
   launch_active_pre(d, e->cur, e->dcur, p, e->stream);
   HIPCHK(e, hipGetLastError());
@@ -1554,7 +1561,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       e->sforce = false;
     }
     const GhRound p = round_params(e, r);
-    launch_base(e->d, e->cur, e->dcur, p, e->stream);
+    if (e->world > 1) launch_base(e->d, e->cur, e->dcur, p, e->stream);  // world 1: in decide_active
     if (e->rowlay && e->world > 1)  // each column's base from its owner row's shard
       COMMCHK(e, e->comm->allreduce(e->d.base[e->cur ^ 1], e->d.base[e->cur ^ 1], e->ld, GH_DT_I32, GH_OP_MAX,
                                     e->stream));

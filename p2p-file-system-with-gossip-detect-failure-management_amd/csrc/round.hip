@@ -40,10 +40,51 @@ __device__ __forceinline__ bool dbit(const uint32_t* bits, int64_t c) {
 // (slave/slave.go:344-346: a detector does not message itself).
 __device__ __forceinline__ bool removes_at(int dc, int dm, int j) { return !(dc == 1 && dm == j); }
 
-// Decides rows from the global count cntg and global |D| = cntg[n]; an
-// undecided row (|D| could push it under the threshold) gets its exact local
-// post-REMOVE count in post[] (und = 1), or is left to k_active_exact's full
-// recount in failure storms (und = 2).
+// Decides row i from its global count c = cntg[i] and the global |D| = ndg;
+// an undecided row (|D| could push it under the threshold) gets its exact
+// local post-REMOVE count in post (u = 1), or is left to k_active_exact's
+// full recount in failure storms (u = 2).
+__device__ __forceinline__ void active_row(const GhDev& d, int cur, int dcur, const GhRound& p, int i, int ndg,
+                                           bool& a, uint8_t& u, int32_t& post) {
+  a = false;
+  u = 0;
+  post = 0;
+  if (!d.alive[i]) return;
+  const int c = d.cntg[i];
+  if (c < p.min_members) {
+    a = false;
+  } else if (c - ndg >= p.min_members) {
+    a = true;
+  } else if (d.nd[dcur] > GH_DLIST_MAX) {
+    u = 2;
+  } else if (!gh_owned(d, i)) {
+    u = 1;  // row layout: the owner counts it, this shard adds 0
+  } else {
+    u = 1;
+    const int32_t* dc = d.det_cnt[dcur];
+    const int32_t* dm = d.det_min[dcur];
+    int rem = 0;
+    const int nd = d.nd[dcur];
+    for (int q = 0; q < nd; ++q) {
+      const int col = d.dlist[(int64_t)dcur * p.ld + q];
+      rem += (gh_get(d, cur, i, col, p.r).x >= 0) && removes_at(dc[col], dm[col], i);
+    }
+    post = d.cntl[i] - rem;
+  }
+}
+
+// ST_ACTIVE_ROWS += the block's active rows: one atomic per workgroup (per
+// wave they serialise on one address: 15 us at N = 65,536)
+__device__ __forceinline__ void count_active(const GhDev& d, bool a) {
+  __shared__ int s_act;
+  if (threadIdx.x == 0) s_act = 0;
+  __syncthreads();
+  const unsigned long long m = __ballot(a);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_act, __popcll(m));
+  __syncthreads();
+  if (d.rank == 0 && threadIdx.x == 0 && s_act) atomicAdd(&d.stats[ST_ACTIVE_ROWS], (unsigned long long)s_act);
+}
+
 __global__ __launch_bounds__(256) void k_active_pre(GhDev d, int cur, int dcur, GhRound p) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (threadIdx.x == 0 && blockIdx.x == 0) {
@@ -52,61 +93,49 @@ __global__ __launch_bounds__(256) void k_active_pre(GhDev d, int cur, int dcur, 
   }
   if (i >= p.n) return;
   d.det_any[i] = 0;
-  bool a = false;
-  uint8_t u = 0;
-  int32_t post = 0;
-  if (d.alive[i]) {
-    const int c = d.cntg[i];
-    const int ndg = d.cntg[p.n];
-    if (c < p.min_members) {
-      a = false;
-    } else if (c - ndg >= p.min_members) {
-      a = true;
-    } else if (d.nd[dcur] > GH_DLIST_MAX) {
-      u = 2;
-    } else if (!gh_owned(d, i)) {
-      u = 1;  // row layout: the owner counts it, this shard adds 0
-    } else {
-      u = 1;
-      const int32_t* dc = d.det_cnt[dcur];
-      const int32_t* dm = d.det_min[dcur];
-      int rem = 0;
-      const int nd = d.nd[dcur];
-      for (int q = 0; q < nd; ++q) {
-        const int col = d.dlist[(int64_t)dcur * p.ld + q];
-        rem += (gh_get(d, cur, i, col, p.r).x >= 0) && removes_at(dc[col], dm[col], i);
-      }
-      post = d.cntl[i] - rem;
-    }
-  }
+  bool a;
+  uint8_t u;
+  int32_t post;
+  active_row(d, cur, dcur, p, i, d.cntg[p.n], a, u, post);
   d.active[i] = a;
   d.und[i] = u;
   d.post[i] = post;
 }
 
 // Failure storms (local |D| > GH_DLIST_MAX): one wave recounts each
-// undecided row over the local columns with REMOVE applied.
-__global__ __launch_bounds__(256) void k_active_exact(GhDev d, int cur, int dcur, GhRound p) {
+// undecided row over the local columns with REMOVE applied. One engine
+// (fin): the recount is global, so the row is decided here (k_active_post's
+// work for it).
+__global__ __launch_bounds__(256) void k_active_exact(GhDev d, int cur, int dcur, GhRound p, int fin) {
   if (d.nd[dcur] <= GH_DLIST_MAX) return;
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (i >= p.n || d.und[i] != 2) return;
-  if (!gh_owned(d, i)) {  // row layout: the owner counts it, this shard adds 0
-    if (lane == 0) d.post[i] = 0;
-    return;
-  }
   const int32_t* dc = d.det_cnt[dcur];
   const int32_t* dm = d.det_min[dcur];
-  int cnt = 0;
-  for (int64_t c = lane * 8; c < p.ld; c += 512) {
-    const uint32_t pf = gh_pf8(d, cur, i, c);
-    const uint32_t b8 = (d.dbits[c >> 5] >> (c & 31)) & 0xFFu;
+  for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < p.n; i += gridDim.x * 4) {
+    if (d.und[i] != 2) continue;
+    if (!gh_owned(d, i)) {  // row layout: the owner counts it, this shard adds 0
+      if (lane == 0) d.post[i] = 0;
+      continue;
+    }
+    int cnt = 0;
+    for (int64_t c = lane * 8; c < p.ld; c += 512) {
+      const uint32_t pf = gh_pf8(d, cur, i, c);
+      const uint32_t b8 = (d.dbits[c >> 5] >> (c & 31)) & 0xFFu;
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      cnt += ((pf >> j) & 1u) && !(((b8 >> j) & 1u) && removes_at(dc[c + j], dm[c + j], i));
+      for (int j = 0; j < 8; ++j)
+        cnt += ((pf >> j) & 1u) && !(((b8 >> j) & 1u) && removes_at(dc[c + j], dm[c + j], i));
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if (lane == 0) {
+      d.post[i] = cnt;
+      if (fin) {
+        const bool a = cnt >= p.min_members;
+        d.active[i] = a;
+        d.stab[(p.r + 1) & 1][i] = !a;  // an undecided row is alive
+        if (a && d.rank == 0) atomicAdd(&d.stats[ST_ACTIVE_ROWS], 1ull);
+      }
+    }
   }
-  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-  if (lane == 0) d.post[i] = cnt;
 }
 
 // post[] now holds the global post-REMOVE counts of the undecided rows.
@@ -121,15 +150,7 @@ __global__ __launch_bounds__(256) void k_active_post(GhDev d, GhRound p) {
     }
     d.stab[(p.r + 1) & 1][i] = d.alive[i] && !a;  // quiet candidates for the next round
   }
-  // one atomic per workgroup (per wave they serialise on one address: 15 us
-  // at N = 65,536)
-  __shared__ int s_act;
-  if (threadIdx.x == 0) s_act = 0;
-  __syncthreads();
-  const unsigned long long m = __ballot(a);
-  if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_act, __popcll(m));
-  __syncthreads();
-  if (d.rank == 0 && threadIdx.x == 0 && s_act) atomicAdd(&d.stats[ST_ACTIVE_ROWS], (unsigned long long)s_act);
+  count_active(d, a);
 }
 
 // Receivers are this shard's member columns (their column holds the senders'
@@ -536,8 +557,7 @@ __device__ __forceinline__ void stn(uint16_t* p, v4u v) {
 // base[cur ^ 1]: member c's own heartbeat in buffer cur - GH_BASE_LAG, so the
 // round's output (its views of c lag the counter) is narrow; kept when the
 // member is not present in its own row.
-__global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRound p) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void base_col(const GhDev& d, int cur, int dcur, const GhRound& p, int64_t c) {
   if (c == 0) {
     // k_round variant of this round: the storm one when more than 1/32 of
     // the segments of the last round went to the slow list or hold cells
@@ -578,6 +598,37 @@ __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRoun
     b = INT_MIN;  // the owner of row cg decides; the host takes the max over shards
   }
   d.base[cur ^ 1][c] = b;
+}
+__global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRound p) {
+  base_col(d, cur, dcur, p, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// One engine (world 1): k_base and the <4 guard of every row in one launch.
+// No exchange is needed (cntg is cntl, and |D_{r-1}| is nd[dcur], which
+// base_col copies to cntl[n] in this same launch), and every row the guard
+// decides here is final (k_active_post's work); rows left to the full
+// recount (und 2) are finished by k_active_exact.
+__global__ __launch_bounds__(256) void k_prologue(GhDev d, int cur, int dcur, GhRound p) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  base_col(d, cur, dcur, p, t);
+  if (t == 0) {
+    d.nd[dcur ^ 1] = 0;
+    d.nd[2 + (dcur ^ 1)] = 0;
+  }
+  bool a = false;
+  if (t < p.n) {
+    const int i = (int)t;
+    d.det_any[i] = 0;
+    uint8_t u;
+    int32_t post;
+    active_row(d, cur, dcur, p, i, d.nd[dcur], a, u, post);
+    if (u == 1) a = post >= p.min_members;
+    d.active[i] = a;
+    d.und[i] = u;
+    d.post[i] = post;
+    if (u != 2) d.stab[(p.r + 1) & 1][i] = d.alive[i] && !a;  // quiet candidates for the next round
+  }
+  count_active(d, a);
 }
 
 // The round, fast part. Workgroup tile = RB rows x TW members of one table
@@ -1941,9 +1992,17 @@ void launch_quirk_apply(const GhDev& d, int cur, int dcur, const GhRound& p, hip
   GH_TW_DISPATCH(quirk_apply, d, cur, dcur, p, s)
 }
 
+// k_active_exact idles in all but failure storms: a grid-stride loop over
+// rows on a small grid keeps its idle dispatch short
+static unsigned exact_grid(const GhRound& p) { return (unsigned)std::min<int64_t>(1024, ((int64_t)p.n + 3) / 4); }
 void launch_active_pre(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_active_pre, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
-  hipLaunchKernelGGL(k_active_exact, dim3((p.n + 3) / 4), dim3(256), 0, s, d, cur, dcur, p);
+  hipLaunchKernelGGL(k_active_exact, dim3(exact_grid(p)), dim3(256), 0, s, d, cur, dcur, p, 0);
+}
+void launch_prologue(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  const int64_t nt = std::max<int64_t>(p.ld, p.n);
+  hipLaunchKernelGGL(k_prologue, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s, d, cur, dcur, p);
+  hipLaunchKernelGGL(k_active_exact, dim3(exact_grid(p)), dim3(256), 0, s, d, cur, dcur, p, 1);
 }
 
 void launch_active_post(const GhDev& d, const GhRound& p, hipStream_t s) {
@@ -1993,6 +2052,8 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
   if (nblk == 0) return;
   const bool tiered = d.a4[0] != nullptr;
   const bool few = variant == 1 || variant == 2 || (variant == 0 && tiered);
+  // (a resident-sized grid for the persistent variants, 1,280 workgroups for
+  // the storm one, measured slower: storm 5.3 -> 6.0 ms)
   const dim3 grid((unsigned)(few ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
 #define GH_ROUND_LAUNCH(NT, ST, IN) \
   hipLaunchKernelGGL((k_round<KB, TW, TPW, NT, ST, IN>), grid, blk, 0, s, d, cur, dcur, p)

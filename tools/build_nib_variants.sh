@@ -21,6 +21,8 @@ for v in "$@"; do
     cpl16_rs1) build $v -DGH_NIB_CPL=16 -DGH_NIB_RS=1 & ;;
     cpl16_rs2) build $v -DGH_NIB_CPL=16 -DGH_NIB_RS=2 & ;;
     cpl32_rs1) build $v -DGH_NIB_CPL=32 -DGH_NIB_RS=1 & ;;
+    cpl16_rs1_w8) build $v -DGH_NIB_CPL=16 -DGH_NIB_RS=1 -DGH_NIB_WAVES=8 & ;;
+    cpl8_rs1_w8) build $v -DGH_NIB_CPL=8 -DGH_NIB_RS=1 -DGH_NIB_WAVES=8 & ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
 done
