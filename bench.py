@@ -272,8 +272,10 @@ def crash_leg(gs, n, rounds=40):
     healthy rounds, the crashed members' views ageing past T_fail, the
     detection round, the REMOVE wave and the tombstones' release. Reports
     rounds/s over all of them and, per k_round variant (gh_tier_info: 3 the
-    nibble path, 1 storm, 2 / 0 lean 16-bit rule), its round count and mean
-    k_round time (HIP events)."""
+    nibble path, 1 storm, 2 / 0 lean 16-bit rule), its round count, mean
+    k_round time (HIP events) and mean whole-round wall time (the gh_step
+    call: every kernel of the round, the lane jobs included), plus a per-round
+    trace (variant, lane jobs of the nibble path, wall ms)."""
     from gossipsim.scenario import crash_ids
     crashed = crash_ids(n, 0.01, 0x5EED0003)
     eng = gs.Engine(gs.default_config(n, fanout=4, seed=0x5EED0003, t_fail=16, t_cleanup=16))
@@ -286,15 +288,22 @@ def crash_leg(gs, n, rounds=40):
     eng.sync()
     t0 = time.perf_counter()
     ms_prev = 0.0
+    trace = []
     for r in range(1, rounds + 1):
         if r == 8:
             eng.apply_events([(gs.GH_EV_CRASH, int(c)) for c in crashed])
+        t1 = time.perf_counter()
         st = eng.step(1)
-        ms, _ = eng.read_timing()
+        ms, _ = eng.read_timing()  # (synchronises)
+        wall = (time.perf_counter() - t1) * 1e3
         v = names.get(eng.tier_info(full=True)[3], "?")
-        e = per.setdefault(v, {"rounds": 0, "k_round_ms_sum": 0.0})
+        jobs, redo = eng.job_info()
+        e = per.setdefault(v, {"rounds": 0, "k_round_ms_sum": 0.0, "round_wall_ms_sum": 0.0, "lane_jobs": 0})
         e["rounds"] += 1
         e["k_round_ms_sum"] += ms - ms_prev
+        e["round_wall_ms_sum"] += wall
+        e["lane_jobs"] += jobs if v == "nibble_path" else 0
+        trace.append([r, v, jobs if v == "nibble_path" else 0, round(wall, 3)])
         ms_prev = ms
         for key in tot:
             tot[key] += st[key]
@@ -305,10 +314,12 @@ def crash_leg(gs, n, rounds=40):
     eng.close()
     for e in per.values():
         e["k_round_ms"] = e.pop("k_round_ms_sum") / max(e["rounds"], 1)
+        e["round_wall_ms"] = e.pop("round_wall_ms_sum") / max(e["rounds"], 1)
     return {"workload": f"N={n}, k=4 pull, T_fail=T_cleanup=16, full start, 655 members (1%, Philox seed "
                         f"0x5eed0003) crash at r=8, rounds 1..{rounds} timed one gh_step call per round "
                         "(host round trips included)",
-            "rounds_per_s": rounds / el, "first_detection_round": first_det, "variants": per, **tot}
+            "rounds_per_s": rounds / el, "first_detection_round": first_det, "variants": per, **tot,
+            "trace": trace, "trace_fields": ["round", "variant", "lane_jobs", "round_wall_ms"]}
 
 
 def placement_leg(gs, eng, n, files, t_fail):

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GH_ABI_VERSION 5
+#define GH_ABI_VERSION 6
 
 /* ---- error codes ---------------------------------------------------- */
 #define GH_OK 0
@@ -298,6 +298,14 @@ int gh_plane_info(void* h, int32_t* enabled, int32_t* valid, int64_t* fallback_w
  * 2 lean on a tier input widened to 16 bits, 3 the nibble path). Any output
  * may be NULL. No reference counterpart. */
 int gh_tier_info(void* h, int32_t* enabled, int32_t* current_8bit, int64_t* escaped_chunks, int32_t* last_variant);
+/* Lane jobs of the nibble path (diagnostic; DESIGN.md "Lane jobs"): in the
+ * last round, the lanes (16 cells of a row) whose cells left the 4-bit tier
+ * or needed the per-cell rule -- crashed members' aging, flagged and
+ * tombstoned cells, REMOVE -- and were done by k_round_jobs instead of
+ * sending their whole 256-cell segments to the slow list, and how many of
+ * them needed a wide segment (k_round_redo). Any output may be NULL. No
+ * reference counterpart. (ABI 6) */
+int gh_job_info(void* h, int64_t* lane_jobs, int64_t* redo_lanes);
 /* Row layout (GH_LAYOUT_ROWS): the last ghost-row exchange of this shard --
  * the sender rows it received, and the bytes it sent and received by
  * alltoallv (narrow codes, plane words, wide segments). Zero in the column

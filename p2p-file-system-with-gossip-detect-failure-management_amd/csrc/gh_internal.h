@@ -165,6 +165,8 @@
 #define GH_STORM_WAVES 5         // storm variant: waves per SIMD it is compiled for (96 VGPRs, SGPR spills only)
 #endif
 #define GH_MAXK 8                // max pull fanout
+#define GH_JOB_CAP 256           // nibble path: lane jobs per wave (a quarter of its lanes); beyond: whole segments to the slow list
+#define GH_REDO_CAP 65536        // lane jobs per round whose segment must go wide (beyond: the engine state is lost, GH_ENOMEM)
 #define GH_DLIST_MAX 1024        // local |D| above which undecided rows are recounted in full
 #define GH_TW_DEFAULT 64         // default tile width (members per tile)
 #define GH_TW_PLANE 256          // default tile width with the sender plane (pull, 3 <= k <= 4)
@@ -265,6 +267,20 @@ struct GhDev {
   int32_t *colq;    // [ld] scratch: per local column event index / merged value
   int64_t *slow;    // [ntiles * n] round: segments for k_round_slow, tile << 32 | row
   int32_t *slow_n;  // their count
+  // nibble path LANE JOBS (tiered engines): a lane of an active row whose
+  // cells leave the tier (escaped input, flag, tombstone, age or code out of
+  // the window), hold a REMOVE'd member, a base move outside 0..15, an
+  // unknown or old sender code, or the row's own member needing the per-cell
+  // rule goes to k_round_jobs instead of sending its whole segment to the
+  // slow list. Wave w of nibble workgroup b writes its jobs to
+  // jobs[(4 b + w) * GH_JOB_CAP ..] (uint4: row, tile << 8 | lane, the
+  // senders' minimum plane words) and their count to jobn[4 b + w], with no
+  // atomics. Results that need the wide arena go to redo (k_round_redo).
+  uint4 *jobs;
+  int32_t *jobn;    // [4 * nibble workgroups]
+  int32_t *njobs;   // [0] jobs of the last round (k_base's variant choice), [1] redo entries, [2] jobs of the round before
+  uint4 *redo;      // [GH_REDO_CAP] lane jobs whose cells need a wide segment
+  int64_t jobw;     // nibble workgroups (jobn entries / 4)
   int32_t *mode;    // k_round variant of the round: 0 lean, 1 storm (k_base)
   int32_t *nstorm;  // storm variant: segments holding flagged or tombstoned cells
   int32_t *nflag;   // [2]: segments written into buffer b holding flagged cells (quirk pre-pass gate)
@@ -754,6 +770,10 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
 // engines); all are launched every round and only the one k_base, the
 // input's tier and the plane select runs
 void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant);
+// the nibble path's lane jobs (tiered engines; after launch_round, before
+// launch_round_slow): k_round_jobs, then the wide redo of the rare lanes
+// whose cells leave the 16-bit window
+void launch_round_jobs(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 // the segments k_round listed, by the per-cell rule (after launch_round)
 void launch_round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);

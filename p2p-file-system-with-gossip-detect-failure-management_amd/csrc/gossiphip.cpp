@@ -991,6 +991,15 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
     if ((rc = dalloc(e, &d.m8, 8, 0))) break;
     if (e->c8 && ((rc = dalloc(e, &d.a4[0], cells / 8, 0)) || (rc = dalloc(e, &d.a4[1], cells / 8, 0))))
       break;
+    // the nibble path's lane jobs: one region of GH_JOB_CAP per wave of its
+    // grid (GH_WG_ROWS_WIDE rows x one tile per workgroup, 4 waves)
+    if (e->c8) {
+      d.jobw = ((d.nrows + GH_WG_ROWS_WIDE - 1) / GH_WG_ROWS_WIDE) * d.ntiles;
+      if ((rc = dalloc(e, &d.jobs, (size_t)d.jobw * 4 * GH_JOB_CAP, 0)) ||
+          (rc = dalloc(e, &d.jobn, (size_t)d.jobw * 4, 0)) || (rc = dalloc(e, &d.njobs, 4, 0)) ||
+          (rc = dalloc(e, &d.redo, GH_REDO_CAP, 0)))
+        break;
+    }
     if ((rc = dalloc(e, &d.alive, e->n, 0)) || (rc = dalloc(e, &d.active, e->n, 0)) ||
         (rc = dalloc(e, &d.det_any, e->n, 0)) || (rc = dalloc(e, &d.und, e->n, 0)) ||
         (rc = dalloc(e, &d.cntl, e->n + 8, 0)) ||
@@ -1369,6 +1378,20 @@ int gh_tier_info(void* h, int32_t* enabled, int32_t* current_8bit, int64_t* esca
   return GH_OK;
 }
 
+int gh_job_info(void* h, int64_t* lane_jobs, int64_t* redo_lanes) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  int32_t nj[2] = {0, 0};
+  if (e->d.njobs) {
+    HIPCHK(e, hipMemcpyAsync(nj, e->d.njobs, sizeof nj, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  if (lane_jobs) *lane_jobs = nj[0];
+  if (redo_lanes) *redo_lanes = std::min<int64_t>(nj[1], GH_REDO_CAP);
+  return GH_OK;
+}
+
 int gh_exchange_info(void* h, int64_t* ghost_rows, int64_t* bytes_out, int64_t* bytes_in) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
@@ -1586,6 +1609,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v);
     }
     if (e->timing) HIPCHK(e, hipEventRecord(e->evs[5 * q + nvar], e->stream));
+    launch_round_jobs(e->d, e->cur, e->dcur, pr, e->stream);
     if ((rc = ghost_codes_if_slow(e))) return rc;
     launch_round_slow(e->d, e->cur, e->dcur, pr, e->stream);
     if (e->rowlay && e->world > 1) {

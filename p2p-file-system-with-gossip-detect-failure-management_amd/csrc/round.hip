@@ -565,7 +565,16 @@ __device__ __forceinline__ void base_col(const GhDev& d, int cur, int dcur, cons
     // guard rows); flags are set one round ahead, so a detection wave is
     // seen the round before it happens
     const int64_t measure = (int64_t)*d.nstorm + *d.slow_n;
-    *d.mode = p.force_storm || measure * 32 > d.ntiles * (int64_t)d.n;
+    // ... or when the last round's lane jobs (k_round_jobs) were more than a
+    // quarter of the lanes: beyond that the packed storm rule is cheaper than
+    // the per-cell one
+    const int64_t jobs = d.njobs ? (int64_t)d.njobs[0] : 0;
+    *d.mode = p.force_storm || measure * 32 > d.ntiles * (int64_t)d.n ||
+              jobs * 4 * GH_NIB_CPL > (int64_t)d.nrows * p.ld;
+    if (d.njobs) {
+      d.njobs[0] = 0;
+      d.njobs[1] = 0;
+    }
     if (d.a4[0]) {
       // the lean variant writes the next buffer in the 4-bit tier, the storm
       // one in 16 bits; a buffer that changes tier is written whole (no
@@ -732,6 +741,23 @@ __device__ __forceinline__ void nib_store(__amdgpu_buffer_rsrc_t r, uint32_t off
   }
 }
 
+// Tile and row block of nibble workgroup bid (the XCD-aware map: XCD x =
+// bid % 8 sweeps tiles x, x + 8, ...); k_round_jobs walks the same regions.
+template <int TW>
+__device__ __forceinline__ void nib_region(const GhDev& d, const GhRound& p, int bid, int& tile, int& rb) {
+  constexpr int RB = round_rb<TW>();
+  const int nrb = (int)((d.nrows + RB - 1) / RB);
+  const int ngroups = (int)(p.ld / TW);
+  if (p.xmap && ngroups % 8 == 0) {
+    const int x = bid & 7, j = bid >> 3;
+    tile = x + 8 * (j / nrb);
+    rb = j - (j / nrb) * nrb;
+  } else {
+    tile = bid / nrb;
+    rb = bid - tile * nrb;
+  }
+}
+
 template <int TW, bool NT, int CPL>
 __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, const GhRound& p, const int bid) {
   constexpr int W = CPL / 8;         // dwords per lane and plane
@@ -742,6 +768,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   constexpr int KB = 4;
   constexpr int RS = GH_NIB_RS > 0 ? GH_NIB_RS : (CPL <= 16 ? 2 : 1);  // row steps per iteration
   static_assert(SEG >= 2 && SEG <= 64 && RB % (RSTEP * RS) == 0, "nibble path: whole row steps");
+  static_assert(W <= 2, "nibble path: a lane job carries at most two minimum plane words");
   __shared__ unsigned long long s_merged;
   __shared__ int s_quiet, s_nslow, s_slowbase, s_bmove;
   __shared__ unsigned long long s_d8bad;  // bit l: lane l's columns hold a base move outside 0..15
@@ -752,18 +779,9 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   __shared__ int s_meta[RB];
   __shared__ __attribute__((aligned(16))) int s_inb[RB * KB];
 
-  const int nrb = (int)((d.nrows + RB - 1) / RB);
-  const int ngroups = (int)(p.ld / TW);
   const int rowend = (int)(d.row0 + d.nrows);
   int tile, rb;
-  if (p.xmap && ngroups % 8 == 0) {  // XCD-aware: XCD x = bid % 8 sweeps tiles x, x + 8, ...
-    const int x = bid & 7, j = bid >> 3;
-    tile = x + 8 * (j / nrb);
-    rb = j - (j / nrb) * nrb;
-  } else {
-    tile = bid / nrb;
-    rb = bid - tile * nrb;
-  }
+  nib_region<TW>(d, p, bid, tile, rb);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = uni(tid >> 6);
@@ -816,13 +834,16 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const auto a4n_t = nib_rsrc(reinterpret_cast<const char*>(d.a4[cur ^ 1]) + tcell / 2, tbytes);
   const uint32_t lbp = (uint32_t)lc * (CPL / 2);  // the lane's byte offset in a plane row segment
   const bool tile_still = s_bmove == 0;
-  // the lane: no REMOVE'd member (REMOVE needs the per-cell rule), base
-  // moves of its columns in 0..15
+  // the lane needs the per-cell rule (a lane job) in every row when it holds
+  // a REMOVE'd member or a base move outside 0..15
   uint32_t rm = 0;
 #pragma unroll
   for (int w = 0; w < (CPL + 31) / 32; ++w) rm |= d.dbits[(l0 >> 5) + w];
   if constexpr (CPL < 32) rm = (rm >> (l0 & 31)) & ((1u << CPL) - 1u);
-  const bool lane_ok = !p.force_slow && rm == 0u && ((s_d8bad >> lc) & 1ull) == 0;
+  const bool lane_job = rm != 0u || ((s_d8bad >> lc) & 1ull) != 0;
+  // this wave's lane-job region (no atomics: the wave owns it)
+  uint4* __restrict__ jreg = d.jobs + ((int64_t)bid * 4 + wave) * GH_JOB_CAP;
+  int wjobs = 0;
   uint32_t D8[2 * W];  // [2w + h]: the base moves of dword w's even / odd nibbles
 #pragma unroll
   for (int x = 0; x < 2 * W; ++x) D8[x] = s_d8[lc * 2 * W + x];
@@ -866,7 +887,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
     for (int u = 0; u < RS; ++u) {
       const int i = iu[u];
       const bool al = alu[u];
-      uint32_t QO[W], AO[W], Bm = 0, Lz = 0;
+      uint32_t QO[W], AO[W], LW[W], Bm = 0, Lz = 0;
       int mrg = 0, gain = 0;
       bool esc = false;
 #pragma unroll
@@ -881,6 +902,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
                            pk_min_u16(pwu[u][2].v[w] & M, pwu[u][3].v[w] & M));
         }
         Lz |= nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu);  // a sender code unknown (0) or old (14)
+        LW[w] = Lw;
         const uint32_t QQ[2] = {qw & 0x0F0F0F0Fu, (qw >> 4) & 0x0F0F0F0Fu};
         const uint32_t GG[2] = {aw & 0x0F0F0F0Fu, (aw >> 4) & 0x0F0F0F0Fu};
         const uint32_t UU[2] = {Lw & 0x0F0F0F0Fu, (Lw >> 4) & 0x0F0F0F0Fu};
@@ -924,15 +946,35 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
             AO[x] = (AO[x] & ~(0xFu << sh)) | (1u << sh);
           }
       }
-      const bool okb = lane_ok && oku[u] && !esc && !ob && Bm == 0 && Lz == 0;
-      const bool seg_okb = (__ballot(al && !okb) & gmask) == 0;
+      // a row under the <4 guard, with more than KB senders (or every row,
+      // GH_FORCE_SLOW) sends its whole segment to the slow list; in any other
+      // row a lane whose cells leave the tier or need the per-cell rule is a
+      // lane job (k_round_jobs), and the segment's other lanes are written here
+      const bool rowok = oku[u] && !p.force_slow;
+      const bool jb = al && rowok && (lane_job || esc || ob || Bm != 0 || Lz != 0);
+      const unsigned long long jm = __ballot(jb);
+      bool jslow = false;
+      if (jm) {
+        const int nj = __popcll(jm);
+        if (wjobs + nj <= GH_JOB_CAP) {
+          if (jb) {
+            const int pos = wjobs + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(jm >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)jm, 0u));
+            jreg[pos] = uint4{(uint32_t)i, ((uint32_t)tile << 8) | (uint32_t)lc, LW[0], W > 1 ? LW[W - 1] : 0u};
+          }
+          wjobs += nj;
+        } else {
+          jslow = (jm & gmask) != 0;  // the wave's region is full: segments with jobs go slow, whole
+        }
+      }
+      const bool seg_slow = jslow || (__ballot(al && !rowok) & gmask) != 0;
       int dpres = 0;
-      if (al && seg_okb) {
+      if (al && !seg_slow && !jb) {
         nib_store<W, NT>(pln_t, owu[u], QO);
         nib_store<W, NT>(a4n_t, owu[u], AO);
         n_mrg += (uint32_t)mrg;
         dpres = gain;
-      } else if (al && lc == 0) {
+      } else if (al && seg_slow && lc == 0) {
         s_slow[atomicAdd(&s_nslow, 1)] = i;
       }
       if (__ballot(dpres != 0) != 0) {  // absent cells merged: the row's count moves
@@ -943,6 +985,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
     }
   }
 
+  if (lane == 0) d.jobn[(int64_t)bid * 4 + wave] = wjobs;
   if (n_mrg) atomicAdd(&s_merged, (unsigned long long)n_mrg);
   __syncthreads();
   if (tid == 0) {
@@ -1775,6 +1818,273 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
   if (n_merged) atomicAdd(&d.stats[ST_MERGED], (unsigned long long)n_merged);
 }
 
+// ---- lane jobs of the nibble path (gh_internal.h: jobs) ------------------
+// Per-lane tallies of a job's cells.
+struct JobAcc {
+  int unknown, tomb, det, rel, merged, dpres, esc;
+  bool flag, any_det;
+};
+// The reference's rule cell by cell (SPEC §2 steps 1, 3-6 of an active row;
+// slave/slave.go:276-286, 414-497) for the 8 cells (i, l0 .. l0 + 7) of a
+// lane job: the same per-cell code as k_round_slow, but each cell's merge
+// candidate comes from the senders' minimum plane code u (nibble gh_nib(j)
+// of uw) the nibble path already gathered: the freshest sender entry is
+// base + GH_P_REF + 1 - u (exact for u in 1..13; 15 = no entry). A cell of
+// a REMOVE'd column (only a sole detector keeps it, :344-346) or with an
+// unknown (0) or old (14) code gathers its senders' exact cells instead.
+// Detections are returned as a cell mask (detm, bit j) for the caller to
+// count once the chunk is written. Returns the cells for buffer cur ^ 1 in
+// o and their narrow codes in nx; fit = all have one.
+__device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, const GhRound& p, int i, int64_t l0,
+                                          uint32_t uw, bool pull, GhCell o[8], uint4& nx, JobAcc& a, uint32_t& detm) {
+  const int32_t r = p.r;
+  const int nxt = cur ^ 1;
+  const int64_t c0 = d.col0 + l0;
+  const int cnt = gh_in_cnt(d, pull, p.k, i);
+  const int64_t beg = gh_in_beg(d, pull, p.k, i);
+  const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
+  const int32_t* dc = d.det_cnt[dcur];
+  const int32_t* dm = d.det_min[dcur];
+  GhCell A[8];
+  gh_dec8(d, cur, i, l0, r, gh_ld16(d, cur, i, l0), A);
+  detm = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t c = c0 + j;
+    const bool rmj = (my8 >> j) & 1u;
+    const uint32_t u = (uw >> gh_nib(j)) & 0xFu;
+    int64_t m = -1;
+    if (!rmj && u != GH_P_UNK && u != GH_P_OLD) {
+      if (u != GH_P_NONE) m = (int64_t)d.base[cur][l0 + j] + (GH_P_REF + 1 - (int)u);
+    } else {
+      for (int q = 0; q < cnt; ++q) {
+        const int s = d.inbox[beg + q];
+        if (rmj && removes_at(dc[l0 + j], dm[l0 + j], s)) continue;  // s REMOVEs it before sending
+        const GhCell X = gh_get(d, cur, s, l0 + j, r);
+        if (X.x >= 0 && !X.f) m = max(m, (int64_t)X.x + (c == s));
+      }
+    }
+    const GhCell v = A[j];
+    int64_t x = v.x;
+    bool now = false;  // ts := r in this round
+    if (rmj && removes_at(dc[l0 + j], dm[l0 + j], i)) {  // step 1: REMOVE delivery (:236-240, 276-286)
+      if (x >= 0) {
+        x = GH_TOMBSTONE;
+        a.tomb++;
+      } else if (x == GH_ABSENT) {
+        a.unknown++;
+      }
+    }
+    if (c == i) {
+      if (x >= 0) {  // step 3 own heartbeat (:443-448); INT32_MAX is refused before the round
+        if (x == INT32_MAX) atomicExch(d.err, GH_ERANGE);
+        else x += 1;
+        now = true;
+      }
+    } else if (x >= 0 && v.f) {  // step 4 detect (:468-473), decided at the last write
+      x = GH_TOMBSTONE;
+      a.det++;
+      a.any_det = true;
+      detm |= 1u << j;
+    }
+    if (x == GH_TOMBSTONE && (int64_t)v.ts < (int64_t)r - p.t_cleanup) {  // step 5 clean (:490-492)
+      x = GH_ABSENT;
+      a.rel++;
+    }
+    if (x >= GH_ABSENT && m > x) {  // step 6 merge (:424-426, :435-437)
+      x = m;
+      now = true;
+      a.merged++;
+    }
+    GhCell out = gh_absent();
+    if (x != GH_ABSENT) {
+      const int32_t t2 = now ? r : v.ts;
+      out = GhCell{(int32_t)x, t2, x >= 0 && gh_flag_for((int32_t)x, t2, c, i, r + 1, p.t_fail)};
+      a.flag |= out.f;
+    }
+    o[j] = out;
+    a.dpres += (out.x >= 0) - (v.x >= 0);
+  }
+  bool fit = true;
+  nx = gh_enc8(d, nxt, l0, r + 1, o, fit);
+  return fit;
+}
+
+// The lane jobs the nibble path wrote this round (only when it ran: m8[4] =
+// 3), one workgroup per nibble workgroup's region at a time (one tile, one
+// block of rows): detections aggregate per column and row-count deltas per
+// row in LDS. A job whose cells all have narrow codes is written here (tier
+// chunks where they fit, else escaped 16-bit chunks, with their plane
+// words); one that needs the wide arena goes to the redo list.
+template <int TW, int CPL>
+__global__ __launch_bounds__(256) void k_round_jobs(GhDev d, int cur, int dcur, GhRound p) {
+  if (d.m8[4] != 3) return;
+  constexpr int W = CPL / 8;
+  constexpr int RB = round_rb<TW>();
+  __shared__ int s_dcnt[TW], s_dmin[TW], s_drow[RB];
+  __shared__ unsigned long long s_st[6];  // unknown, tomb, det, rel, merged, escaped chunks
+  __shared__ int s_jobs, s_flag;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool pull = p.peer_mode == GH_PEER_PULL;
+  const int nxt = cur ^ 1;
+  if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_jobs = s_flag = 0;
+  JobAcc tot{};
+  for (int64_t b = blockIdx.x; b < d.jobw; b += gridDim.x) {
+    const int nj = d.jobn[b * 4 + wave];
+    if (!__syncthreads_or(nj > 0)) continue;  // (uniform over the block)
+    int tile, rb;
+    nib_region<TW>(d, p, (int)b, tile, rb);
+    const int64_t cbase = (int64_t)tile * TW;
+    const int64_t rbase = d.row0 + (int64_t)rb * RB;
+    for (int t = threadIdx.x; t < TW; t += 256) {
+      s_dcnt[t] = 0;
+      s_dmin[t] = INT_MAX;
+    }
+    for (int t = threadIdx.x; t < RB; t += 256) s_drow[t] = 0;
+    __syncthreads();
+    const uint4* jreg = d.jobs + (b * 4 + wave) * GH_JOB_CAP;
+    for (int e = lane; e < nj; e += 64) {
+      const uint4 jb = jreg[e];
+      const int i = (int)jb.x;
+      const int64_t l0 = (int64_t)(jb.y >> 8) * TW + (int64_t)(jb.y & 255u) * CPL;
+      const uint32_t uw[2] = {jb.z, jb.w};
+      GhCell o[W][8];
+      uint4 nx[W];
+      uint32_t detm[W];
+      JobAcc a{};
+      bool fit = true;
+#pragma unroll
+      for (int w = 0; w < W; ++w) fit &= job_chunk(d, cur, dcur, p, i, l0 + 8 * w, uw[w], pull, o[w], nx[w], a, detm[w]);
+      if (!fit) {
+        // the segment goes wide: k_round_redo recomputes and counts this lane
+        const int pos = atomicAdd(&d.njobs[1], 1);
+        if (pos < GH_REDO_CAP) d.redo[pos] = jb;
+        else atomicExch(d.err, GH_ENOMEM);
+        continue;
+      }
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        uint32_t a4w;
+        a.esc += !c4_enc(v4u{nx[w].x, nx[w].y, nx[w].z, nx[w].w}, gh_jd(d, i, l0 + 8 * w), a4w);
+        gh_put8(d, nxt, i, l0 + 8 * w, true, nx[w], 0, o[w]);
+        for (uint32_t m = detm[w]; m; m &= m - 1) {
+          const int64_t t = l0 + 8 * w + __builtin_ctz(m) - cbase;
+          atomicAdd(&s_dcnt[t], 1);
+          atomicMin(&s_dmin[t], i);
+        }
+      }
+      if (a.dpres) atomicAdd(&s_drow[i - rbase], a.dpres);
+      if (a.any_det) d.det_any[i] = 1;
+      tot.unknown += a.unknown;
+      tot.tomb += a.tomb;
+      tot.det += a.det;
+      tot.rel += a.rel;
+      tot.merged += a.merged;
+      tot.esc += a.esc;
+      tot.flag |= a.flag;
+    }
+    if (lane == 0 && nj) atomicAdd(&s_jobs, nj);
+    __syncthreads();
+    for (int t = threadIdx.x; t < TW; t += 256)
+      if (s_dcnt[t]) {
+        atomicAdd(&d.det_cnt[dcur ^ 1][cbase + t], s_dcnt[t]);
+        atomicMin(&d.det_min[dcur ^ 1][cbase + t], s_dmin[t]);
+      }
+    for (int t = threadIdx.x; t < RB; t += 256)
+      if (s_drow[t]) atomicAdd(&d.cntl[rbase + t], s_drow[t]);
+  }
+  if (tot.unknown) atomicAdd(&s_st[0], (unsigned long long)tot.unknown);
+  if (tot.tomb) atomicAdd(&s_st[1], (unsigned long long)tot.tomb);
+  if (tot.det) atomicAdd(&s_st[2], (unsigned long long)tot.det);
+  if (tot.rel) atomicAdd(&s_st[3], (unsigned long long)tot.rel);
+  if (tot.merged) atomicAdd(&s_st[4], (unsigned long long)tot.merged);
+  if (tot.esc) atomicAdd(&s_st[5], (unsigned long long)tot.esc);
+  if (tot.flag) s_flag = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_st[0]) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], s_st[0]);
+    if (s_st[1]) atomicAdd(&d.stats[ST_TOMBSTONED], s_st[1]);
+    if (s_st[2]) atomicAdd(&d.stats[ST_DETECTIONS], s_st[2]);
+    if (s_st[3]) atomicAdd(&d.stats[ST_RELEASED], s_st[3]);
+    if (s_st[4]) atomicAdd(&d.stats[ST_MERGED], s_st[4]);
+    if (s_st[5]) atomicAdd(&d.m8[3], (int)s_st[5]);
+    if (s_jobs) atomicAdd(&d.njobs[0], s_jobs);
+    if (s_flag) atomicAdd(&d.nflag[nxt], 1);  // the quirk gate: written segments may hold flags
+  }
+}
+
+// Lane jobs whose cells need the wide arena (k_round_jobs' redo list), by
+// one thread: each listed segment becomes wide in buffer cur ^ 1 (a fresh
+// arena slot holding every chunk as the nibble path and the jobs wrote it),
+// then every listed lane of that segment writes its exact cells into the
+// slot. Rare (imports far from the counters, views older than the 16-bit
+// window), so the search for a segment's other entries is a plain scan.
+template <int TW, int CPL>
+__device__ __forceinline__ void redo_lane(const GhDev& d, int cur, int dcur, const GhRound& p, const uint4& jb,
+                                          int64_t slot, JobAcc& tot) {
+  constexpr int W = CPL / 8;
+  const bool pull = p.peer_mode == GH_PEER_PULL;
+  const int i = (int)jb.x;
+  const int64_t l0 = (int64_t)(jb.y >> 8) * TW + (int64_t)(jb.y & 255u) * CPL;
+  const uint32_t uw[2] = {jb.z, jb.w};
+  JobAcc a{};
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    GhCell o[8];
+    uint4 nx;
+    uint32_t detm;
+    job_chunk(d, cur, dcur, p, i, l0 + 8 * w, uw[w], pull, o, nx, a, detm);
+    gh_put8(d, cur ^ 1, i, l0 + 8 * w, false, nx, slot, o);
+    for (uint32_t m = detm; m; m &= m - 1) {
+      const int64_t c = l0 + 8 * w + __builtin_ctz(m);
+      atomicAdd(&d.det_cnt[dcur ^ 1][c], 1);
+      atomicMin(&d.det_min[dcur ^ 1][c], i);
+    }
+  }
+  if (a.dpres) atomicAdd(&d.cntl[i], a.dpres);
+  if (a.any_det) d.det_any[i] = 1;
+  tot.unknown += a.unknown;
+  tot.tomb += a.tomb;
+  tot.det += a.det;
+  tot.rel += a.rel;
+  tot.merged += a.merged;
+}
+template <int TW, int CPL>
+__global__ __launch_bounds__(64) void k_round_redo(GhDev d, int cur, int dcur, GhRound p) {
+  if (d.m8[4] != 3 || threadIdx.x != 0) return;
+  const int nr = min(d.njobs[1], GH_REDO_CAP);
+  const int nxt = cur ^ 1;
+  JobAcc tot{};
+  for (int e = 0; e < nr; ++e) {
+    const uint4 jb = d.redo[e];
+    if (jb.x == 0xFFFFFFFFu) continue;  // done with an earlier entry of its segment
+    const int i = (int)jb.x;
+    const int64_t t0 = (int64_t)(jb.y >> 8) * TW;
+    const int64_t slot = gh_wide_alloc(d, nxt);
+    if (slot < 0) return;  // the arena is full: err = GH_ENOMEM, the state is lost
+    for (int64_t c = t0; c < t0 + TW; c += 8) {  // the segment as written so far, into the slot
+      GhCell v[8];
+      gh_get8(d, nxt, i, c, p.r + 1, v);
+      gh_put8(d, nxt, i, c, false, uint4{0u, 0u, 0u, 0u}, slot, v);
+    }
+    redo_lane<TW, CPL>(d, cur, dcur, p, jb, slot, tot);
+    for (int e2 = e + 1; e2 < nr; ++e2) {
+      const uint4 j2 = d.redo[e2];
+      if (j2.x == jb.x && (j2.y >> 8) == (jb.y >> 8)) {
+        redo_lane<TW, CPL>(d, cur, dcur, p, j2, slot, tot);
+        d.redo[e2].x = 0xFFFFFFFFu;
+      }
+    }
+  }
+  if (nr) atomicAdd(&d.nflag[nxt], 1);
+  if (tot.unknown) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], (unsigned long long)tot.unknown);
+  if (tot.tomb) atomicAdd(&d.stats[ST_TOMBSTONED], (unsigned long long)tot.tomb);
+  if (tot.det) atomicAdd(&d.stats[ST_DETECTIONS], (unsigned long long)tot.det);
+  if (tot.rel) atomicAdd(&d.stats[ST_RELEASED], (unsigned long long)tot.rel);
+  if (tot.merged) atomicAdd(&d.stats[ST_MERGED], (unsigned long long)tot.merged);
+}
+
 // Columns: bitmap + list of D_r, and reset the consumed D_{r-1}
 // accumulators for reuse in round r+1 (the rows' counts are kept current by
 // the round kernels).
@@ -2124,6 +2434,19 @@ void launch_base(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_
 
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_finish, dim3((unsigned)((p.ld + 255) / 256)), dim3(256), 0, s, d, dcur, p);
+}
+
+template <int TW>
+static void round_jobs(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  if constexpr (TW >= 64) {
+    const unsigned g = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, d.jobw));
+    hipLaunchKernelGGL((k_round_jobs<TW, GH_NIB_CPL>), dim3(g), dim3(256), 0, s, d, cur, dcur, p);
+    hipLaunchKernelGGL((k_round_redo<TW, GH_NIB_CPL>), dim3(1), dim3(64), 0, s, d, cur, dcur, p);
+  }
+}
+void launch_round_jobs(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  if (!d.jobs) return;
+  GH_TW_DISPATCH(round_jobs, d, cur, dcur, p, s)
 }
 
 void launch_round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {

@@ -128,13 +128,20 @@ class Engine:
         return en.value, va.value, fb.value
 
     def tier_info(self, full=False):
-        """(8-bit tier kept, current table held in it, chunks the last round's
-        packed 16-bit path wrote escaped) -- gh_tier_info, diagnostic;
-        full=True adds the last round's kernel variant (0 lean on a 16-bit
-        input, 1 storm, 2 lean on an 8-bit input widened, 3 the byte path)."""
+        """(4-bit tier kept, current table held in it, chunks the last round
+        wrote escaped) -- gh_tier_info, diagnostic; full=True adds the last
+        round's kernel variant (0 lean on a 16-bit input, 1 storm, 2 lean on
+        a tier input widened, 3 the nibble path)."""
         en, cu, esc, var = C.c_int32(), C.c_int32(), C.c_int64(), C.c_int32()
         self._chk(self.lib.gh_tier_info(self.h, C.byref(en), C.byref(cu), C.byref(esc), C.byref(var)))
         return (en.value, cu.value, esc.value, var.value) if full else (en.value, cu.value, esc.value)
+
+    def job_info(self):
+        """(lane jobs, of them redone wide) of the last round's nibble path
+        (gh_job_info, diagnostic)."""
+        nj, nr = C.c_int64(), C.c_int64()
+        self._chk(self.lib.gh_job_info(self.h, C.byref(nj), C.byref(nr)))
+        return nj.value, nr.value
 
     def exchange_info(self):
         """dict(ghost_rows, bytes_out, bytes_in) of this shard's last ghost-row

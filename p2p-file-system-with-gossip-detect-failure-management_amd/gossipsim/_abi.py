@@ -99,6 +99,7 @@ SYMBOLS = [
     ("gh_plane_info", C.c_int, [_vp, _P(_i32), _P(_i32), _P(_i64)]),
     ("gh_tier_info", C.c_int, [_vp, _P(_i32), _P(_i32), _P(_i64), _P(_i32)]),
     ("gh_exchange_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i64)]),
+    ("gh_job_info", C.c_int, [_vp, _P(_i64), _P(_i64)]),
     ("gh_memory_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i64), _P(_i64)]),
     ("gh_footprint", C.c_int, [_P(Config), _i32, _i32, _i32, _P(_i64), _P(_i64)]),
 ]

@@ -46,7 +46,7 @@ def test_struct_layouts(abi):
 
 def test_abi_version_and_defaults(abi):
     lib = abi.load()
-    assert lib.gh_abi_version() == 5
+    assert lib.gh_abi_version() == 6
     cfg = abi.Config()
     lib.gh_config_default(C.byref(cfg))
     # reference constants: PERIOD/COOLDOWN 5 s at 1 s rounds, 4 replicas, literal 4
