@@ -161,11 +161,14 @@
 #ifndef GH_NIB_WAVES
 #define GH_NIB_WAVES 1          // nibble path: min waves per SIMD it is compiled for (1: the compiler picks)
 #endif
+#ifndef GH_JOB_WAVES
+#define GH_JOB_WAVES 4          // lane-job kernel: min waves per SIMD it is compiled for (A/B: 4 beats 3 and 5)
+#endif
 #ifndef GH_STORM_WAVES
 #define GH_STORM_WAVES 5         // storm variant: waves per SIMD it is compiled for (96 VGPRs, SGPR spills only)
 #endif
 #define GH_MAXK 8                // max pull fanout
-#define GH_JOB_CAP 256           // nibble path: lane jobs per wave (a quarter of its lanes); beyond: whole segments to the slow list
+#define GH_JOB_CAP 512           // nibble path: lane jobs per wave (half of its lanes at 16 cells per lane); beyond: whole segments to the slow list
 #define GH_REDO_CAP 65536        // lane jobs per round whose segment must go wide (beyond: the engine state is lost, GH_ENOMEM)
 #define GH_DLIST_MAX 1024        // local |D| above which undecided rows are recounted in full
 #define GH_TW_DEFAULT 64         // default tile width (members per tile)

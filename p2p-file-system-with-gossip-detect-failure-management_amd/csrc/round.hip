@@ -1826,44 +1826,60 @@ struct JobAcc {
 };
 // The reference's rule cell by cell (SPEC §2 steps 1, 3-6 of an active row;
 // slave/slave.go:276-286, 414-497) for the 8 cells (i, l0 .. l0 + 7) of a
-// lane job: the same per-cell code as k_round_slow, but each cell's merge
-// candidate comes from the senders' minimum plane code u (nibble gh_nib(j)
-// of uw) the nibble path already gathered: the freshest sender entry is
-// base + GH_P_REF + 1 - u (exact for u in 1..13; 15 = no entry). A cell of
-// a REMOVE'd column (only a sole detector keeps it, :344-346) or with an
-// unknown (0) or old (14) code gathers its senders' exact cells instead.
-// Detections are returned as a cell mask (detm, bit j) for the caller to
-// count once the chunk is written. Returns the cells for buffer cur ^ 1 in
-// o and their narrow codes in nx; fit = all have one.
-__device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, const GhRound& p, int i, int64_t l0,
-                                          uint32_t uw, bool pull, GhCell o[8], uint4& nx, JobAcc& a, uint32_t& detm) {
+// lane job, given as A (exact cells of buffer cur): the same per-cell code
+// as k_round_slow, but each cell's merge candidate comes from the senders'
+// minimum plane code u (nibble gh_nib(j) of uw) the nibble path already
+// gathered: the freshest sender entry is bo[j] + GH_P_REF + 1 - u (exact for
+// u in 1..13; 15 = no entry). A cell of a REMOVE'd column (only a sole
+// detector keeps it, :344-346) or with an unknown (0) or old (14) code
+// gathers its senders' exact cells instead. Detections come back as a cell
+// mask (detm) for the caller to count once the chunk is written. Returns the
+// cells for buffer cur ^ 1 in o.
+__device__ __forceinline__ void job_rule(const GhDev& d, int cur, int dcur, const GhRound& p, int i, int64_t l0,
+                                         uint32_t uw, const GhCell A[8], const int32_t bo[8], GhCell o[8], JobAcc& a,
+                                         uint32_t& detm) {
   const int32_t r = p.r;
-  const int nxt = cur ^ 1;
   const int64_t c0 = d.col0 + l0;
-  const int cnt = gh_in_cnt(d, pull, p.k, i);
-  const int64_t beg = gh_in_beg(d, pull, p.k, i);
   const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
   const int32_t* dc = d.det_cnt[dcur];
   const int32_t* dm = d.det_min[dcur];
-  GhCell A[8];
-  gh_dec8(d, cur, i, l0, r, gh_ld16(d, cur, i, l0), A);
   detm = 0;
+  // merge candidates: from the plane codes, then (a rolled loop: the code
+  // stays small) the cells that gather their senders' exact cells
+  int64_t mm[8];
+  uint32_t ex = 0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int64_t c = c0 + j;
-    const bool rmj = (my8 >> j) & 1u;
     const uint32_t u = (uw >> gh_nib(j)) & 0xFu;
-    int64_t m = -1;
-    if (!rmj && u != GH_P_UNK && u != GH_P_OLD) {
-      if (u != GH_P_NONE) m = (int64_t)d.base[cur][l0 + j] + (GH_P_REF + 1 - (int)u);
-    } else {
+    mm[j] = u == GH_P_NONE ? -1 : (int64_t)bo[j] + (GH_P_REF + 1 - (int)u);
+    if (((my8 >> j) & 1u) || u == GH_P_UNK || u == GH_P_OLD) ex |= 1u << j;
+  }
+  if (ex) {
+    const bool pull = p.peer_mode == GH_PEER_PULL;
+    const int cnt = gh_in_cnt(d, pull, p.k, i);
+    const int64_t beg = gh_in_beg(d, pull, p.k, i);
+#pragma unroll 1
+    for (; ex; ex &= ex - 1) {
+      const int j = __builtin_ctz(ex);
+      const bool rmj = (my8 >> j) & 1u;
+      int64_t m = -1;
+#pragma unroll 1
       for (int q = 0; q < cnt; ++q) {
         const int s = d.inbox[beg + q];
         if (rmj && removes_at(dc[l0 + j], dm[l0 + j], s)) continue;  // s REMOVEs it before sending
         const GhCell X = gh_get(d, cur, s, l0 + j, r);
-        if (X.x >= 0 && !X.f) m = max(m, (int64_t)X.x + (c == s));
+        if (X.x >= 0 && !X.f) m = max(m, (int64_t)X.x + ((c0 + j) == s));
       }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q == j) mm[q] = m;
     }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t c = c0 + j;
+    const bool rmj = (my8 >> j) & 1u;
+    const int64_t m = mm[j];
     const GhCell v = A[j];
     int64_t x = v.x;
     bool now = false;  // ts := r in this round
@@ -1905,9 +1921,166 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
     o[j] = out;
     a.dpres += (out.x >= 0) - (v.x >= 0);
   }
+}
+
+// One chunk (i, l0 .. l0 + 7) of a lane job, lean: its codes in buffer cur
+// (the tier's nibbles or, escaped, the 16-bit chunk: the three words are
+// loaded together), the rule of job_rule in 32-bit arithmetic on decoded
+// cells (every value an encodable cell can take fits: heartbeats <= INT32_MAX
+// with the INT32_MAX refusal before the round), and, when every result has a
+// narrow code, the write of buffer cur ^ 1 (tier chunk where it fits, else
+// escaped, with its plane word). Returns false, writing nothing, when the
+// input is a wide segment or a result needs the wide arena (k_round_redo).
+__device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, const GhRound& p, int i, int64_t l0,
+                                          uint32_t uw, JobAcc& acc, uint32_t& detm) {
+  const int nxt = cur ^ 1;
+  const int32_t r = p.r;
+  const int64_t cell = gh_cell(d, i, l0);
+  const int jd = gh_jd(d, i, l0);
+  const uint32_t a4w = d.a4[cur][cell >> 3];
+  const uint32_t plw = d.pl[cur][cell >> 3];
+  const uint4 hx = *reinterpret_cast<const uint4*>(d.hn[cur] + cell);
+  const int4 b0 = *reinterpret_cast<const int4*>(d.base[cur] + l0);
+  const int4 b1 = *reinterpret_cast<const int4*>(d.base[cur] + l0 + 4);
+  const int4 n0 = *reinterpret_cast<const int4*>(d.base[nxt] + l0);
+  const int4 n1 = *reinterpret_cast<const int4*>(d.base[nxt] + l0 + 4);
+  const int32_t bo[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+  const int32_t bn[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+  uint32_t xw[4] = {hx.x, hx.y, hx.z, hx.w};
+  if (!gh_t4_esc(a4w)) {
+    const v4u w = c4_dec(plw, a4w, jd);
+    xw[0] = w[0], xw[1] = w[1], xw[2] = w[2], xw[3] = w[3];
+  }
+  const uint32_t h0 = xw[0] & 0xFFFFu;
+  if (h0 == GH_N_WIDE || h0 == GH_N_FROZEN) return false;  // a wide input: k_round_redo
+  const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
+  const int32_t* dc = d.det_cnt[dcur];
+  const int32_t* dm = d.det_min[dcur];
+  // merge candidates: from the plane codes, then (a rolled loop) the cells
+  // that gather their senders' exact cells
+  int32_t mm[8];
+  uint32_t ex = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t u = (uw >> gh_nib(j)) & 0xFu;
+    mm[j] = u == GH_P_NONE ? -1 : bo[j] + (GH_P_REF + 1 - (int32_t)u);
+    if (((my8 >> j) & 1u) || u == GH_P_UNK || u == GH_P_OLD) ex |= 1u << j;
+  }
+  const int64_t c0 = d.col0 + l0;
+  if (ex) {
+    const bool pull = p.peer_mode == GH_PEER_PULL;
+    const int cnt = gh_in_cnt(d, pull, p.k, i);
+    const int64_t beg = gh_in_beg(d, pull, p.k, i);
+#pragma unroll 1
+    for (; ex; ex &= ex - 1) {
+      const int j = __builtin_ctz(ex);
+      const bool rmj = (my8 >> j) & 1u;
+      int32_t m = -1;
+      bool okg = true;
+#pragma unroll 1
+      for (int q = 0; q < cnt; ++q) {
+        const int s = d.inbox[beg + q];
+        if (rmj && removes_at(dc[l0 + j], dm[l0 + j], s)) continue;  // s REMOVEs it before sending
+        // the sender's cell from its narrow code (a tier nibble or an escaped
+        // code); a wide or stopped sender segment: k_round_redo
+        const int64_t sc = gh_cell(d, s, l0 + j);
+        const uint32_t sa = d.a4[cur][sc >> 3];
+        uint32_t h;
+        if (gh_t4_esc(sa)) {
+          h = d.hn[cur][sc];
+          const uint32_t h0 = d.hn[cur][sc & ~(int64_t)7];
+          okg &= h0 != GH_N_WIDE && h0 != GH_N_FROZEN;
+        } else {
+          const uint32_t u = (d.pl[cur][sc >> 3] >> gh_nib((int)(sc & 7))) & 0xFu;
+          // tier: visible with offset GH_P_REF + 1 - u (GH_P_REF - u on s's
+          // own member, its plane diagonal code), or absent (15)
+          h = u == GH_P_NONE ? GH_N_ABSENT : (uint32_t)(GH_P_REF + 1 - (int)u - (int)((c0 + j) == s)) << 5;
+        }
+        const int32_t off = (int32_t)((h >> 5) & 1023u);
+        if (h != GH_N_ABSENT && off != 1023 && (h >> 15) == 0)  // present and not flagged (detected by s)
+          m = max(m, d.base[cur][l0 + j] + off + (int32_t)((c0 + j) == s));
+      }
+      if (!okg) return false;
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (q == j) mm[q] = m;
+    }
+  }
+  uint32_t nw[4] = {0u, 0u, 0u, 0u};
   bool fit = true;
-  nx = gh_enc8(d, nxt, l0, r + 1, o, fit);
-  return fit;
+  detm = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t c = c0 + j;
+    // the cell (x, ts, flag) of buffer cur (SPEC §1)
+    const uint32_t h = (xw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+    const int32_t age = (int32_t)(h & 31u), off = (int32_t)((h >> 5) & 1023u);
+    const int32_t vx = h == GH_N_ABSENT ? GH_ABSENT : off == 1023 ? GH_TOMBSTONE : bo[j] + off;
+    const int32_t vts = r - age;
+    const bool vf = vx >= 0 && (h >> 15) != 0;
+    int32_t x = vx;
+    bool now = false;  // ts := r in this round
+    if (((my8 >> j) & 1u) && removes_at(dc[l0 + j], dm[l0 + j], i)) {  // step 1 REMOVE (:236-240, 276-286)
+      if (x >= 0) {
+        x = GH_TOMBSTONE;
+        acc.tomb++;
+      } else if (x == GH_ABSENT) {
+        acc.unknown++;
+      }
+    }
+    if (c == i) {
+      if (x >= 0) {  // step 3 own heartbeat (:443-448); INT32_MAX is refused before the round
+        if (x == INT32_MAX) atomicExch(d.err, GH_ERANGE);
+        else x += 1;
+        now = true;
+      }
+    } else if (x >= 0 && vf) {  // step 4 detect (:468-473), decided at the last write
+      x = GH_TOMBSTONE;
+      acc.det++;
+      acc.any_det = true;
+      detm |= 1u << j;
+    }
+    if (x == GH_TOMBSTONE && vts < r - p.t_cleanup) {  // step 5 clean (:490-492)
+      x = GH_ABSENT;
+      acc.rel++;
+    }
+    if (x >= GH_ABSENT && mm[j] > x) {  // step 6 merge (:424-426, :435-437)
+      x = mm[j];
+      now = true;
+      acc.merged++;
+    }
+    // the cell for round r + 1 in buffer cur ^ 1, narrow (gh_enc16)
+    uint32_t code = GH_N_ABSENT;
+    if (x != GH_ABSENT) {
+      const int32_t t2 = now ? r : vts;
+      int32_t a2 = r + 1 - t2;
+      if (x < 0) {
+        if (d.tsat && a2 > GH_N_TAGEMAX) a2 = GH_N_TAGEMAX;
+        fit &= a2 >= 0 && a2 <= GH_N_TAGEMAX;
+        code = GH_N_TOMB | ((uint32_t)a2 & 31u);
+      } else {
+        const bool fl = x > 1 && c != i && t2 < r + 1 - p.t_fail;  // gh_flag_for, round r + 1
+        const uint32_t o2 = (uint32_t)x - (uint32_t)bn[j];          // x - base, wrapped if below
+        fit &= o2 <= (uint32_t)GH_N_OFFMAX && a2 >= 0 && a2 <= GH_N_AGEMAX;
+        code = (fl ? 0x8000u : 0u) | ((o2 & 1023u) << 5) | ((uint32_t)a2 & 31u);
+        acc.flag |= fl;
+      }
+    }
+    nw[j >> 1] |= code << (16 * (j & 1));
+    acc.dpres += (x >= 0) - (vx >= 0);
+  }
+  if (!fit) return false;
+  const v4u nv = {nw[0], nw[1], nw[2], nw[3]};
+  d.pl[nxt][cell >> 3] = plane_word(nv, jd);
+  uint32_t a4n;
+  if (c4_enc(nv, jd, a4n)) {
+    d.a4[nxt][cell >> 3] = a4n;
+  } else {
+    d.a4[nxt][cell >> 3] = GH_T4_ESC;
+    *reinterpret_cast<uint4*>(d.hn[nxt] + cell) = uint4{nw[0], nw[1], nw[2], nw[3]};
+    acc.esc++;
+  }
+  return true;
 }
 
 // The lane jobs the nibble path wrote this round (only when it ran: m8[4] =
@@ -1917,7 +2090,7 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
 // chunks where they fit, else escaped 16-bit chunks, with their plane
 // words); one that needs the wide arena goes to the redo list.
 template <int TW, int CPL>
-__global__ __launch_bounds__(256) void k_round_jobs(GhDev d, int cur, int dcur, GhRound p) {
+__global__ __launch_bounds__(256, GH_JOB_WAVES) void k_round_jobs(GhDev d, int cur, int dcur, GhRound p) {
   if (d.m8[4] != 3) return;
   constexpr int W = CPL / 8;
   constexpr int RB = round_rb<TW>();
@@ -1925,7 +2098,6 @@ __global__ __launch_bounds__(256) void k_round_jobs(GhDev d, int cur, int dcur, 
   __shared__ unsigned long long s_st[6];  // unknown, tomb, det, rel, merged, escaped chunks
   __shared__ int s_jobs, s_flag;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool pull = p.peer_mode == GH_PEER_PULL;
   const int nxt = cur ^ 1;
   if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_jobs = s_flag = 0;
@@ -1948,31 +2120,29 @@ __global__ __launch_bounds__(256) void k_round_jobs(GhDev d, int cur, int dcur, 
       const uint4 jb = jreg[e];
       const int i = (int)jb.x;
       const int64_t l0 = (int64_t)(jb.y >> 8) * TW + (int64_t)(jb.y & 255u) * CPL;
-      const uint32_t uw[2] = {jb.z, jb.w};
-      GhCell o[W][8];
-      uint4 nx[W];
-      uint32_t detm[W];
+      uint32_t detl = 0;  // detections, bit 8 w + j
       JobAcc a{};
       bool fit = true;
-#pragma unroll
-      for (int w = 0; w < W; ++w) fit &= job_chunk(d, cur, dcur, p, i, l0 + 8 * w, uw[w], pull, o[w], nx[w], a, detm[w]);
+      // chunk by chunk (a rolled loop: the code stays small), each written as
+      // soon as it is known to fit; a chunk that needs the wide arena sends
+      // the lane to k_round_redo, which recomputes and counts it whole
+      // (overwriting any chunk written here)
+#pragma unroll 1
+      for (int w = 0; w < W && fit; ++w) {
+        uint32_t dm8 = 0;
+        fit = job_chunk(d, cur, dcur, p, i, l0 + 8 * w, w ? jb.w : jb.z, a, dm8);
+        detl |= dm8 << (8 * w);
+      }
       if (!fit) {
-        // the segment goes wide: k_round_redo recomputes and counts this lane
         const int pos = atomicAdd(&d.njobs[1], 1);
         if (pos < GH_REDO_CAP) d.redo[pos] = jb;
         else atomicExch(d.err, GH_ENOMEM);
         continue;
       }
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        uint32_t a4w;
-        a.esc += !c4_enc(v4u{nx[w].x, nx[w].y, nx[w].z, nx[w].w}, gh_jd(d, i, l0 + 8 * w), a4w);
-        gh_put8(d, nxt, i, l0 + 8 * w, true, nx[w], 0, o[w]);
-        for (uint32_t m = detm[w]; m; m &= m - 1) {
-          const int64_t t = l0 + 8 * w + __builtin_ctz(m) - cbase;
-          atomicAdd(&s_dcnt[t], 1);
-          atomicMin(&s_dmin[t], i);
-        }
+      for (uint32_t m = detl; m; m &= m - 1) {
+        const int64_t t = l0 + __builtin_ctz(m) - cbase;
+        atomicAdd(&s_dcnt[t], 1);
+        atomicMin(&s_dmin[t], i);
       }
       if (a.dpres) atomicAdd(&s_drow[i - rbase], a.dpres);
       if (a.any_det) d.det_any[i] = 1;
@@ -2024,22 +2194,27 @@ template <int TW, int CPL>
 __device__ __forceinline__ void redo_lane(const GhDev& d, int cur, int dcur, const GhRound& p, const uint4& jb,
                                           int64_t slot, JobAcc& tot) {
   constexpr int W = CPL / 8;
-  const bool pull = p.peer_mode == GH_PEER_PULL;
   const int i = (int)jb.x;
   const int64_t l0 = (int64_t)(jb.y >> 8) * TW + (int64_t)(jb.y & 255u) * CPL;
   const uint32_t uw[2] = {jb.z, jb.w};
   JobAcc a{};
 #pragma unroll
   for (int w = 0; w < W; ++w) {
-    GhCell o[8];
-    uint4 nx;
+    const int64_t c = l0 + 8 * w;
+    const int4 b0 = *reinterpret_cast<const int4*>(d.base[cur] + c);
+    const int4 b1 = *reinterpret_cast<const int4*>(d.base[cur] + c + 4);
+    const int32_t bo[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    GhCell A[8], o[8];
+    gh_get8(d, cur, i, c, p.r, A);
     uint32_t detm;
-    job_chunk(d, cur, dcur, p, i, l0 + 8 * w, uw[w], pull, o, nx, a, detm);
-    gh_put8(d, cur ^ 1, i, l0 + 8 * w, false, nx, slot, o);
+    job_rule(d, cur, dcur, p, i, c, uw[w], A, bo, o, a, detm);
+    bool fit = true;
+    const uint4 nx = gh_enc8(d, cur ^ 1, c, p.r + 1, o, fit);
+    gh_put8(d, cur ^ 1, i, c, false, nx, slot, o);
     for (uint32_t m = detm; m; m &= m - 1) {
-      const int64_t c = l0 + 8 * w + __builtin_ctz(m);
-      atomicAdd(&d.det_cnt[dcur ^ 1][c], 1);
-      atomicMin(&d.det_min[dcur ^ 1][c], i);
+      const int64_t cc = c + __builtin_ctz(m);
+      atomicAdd(&d.det_cnt[dcur ^ 1][cc], 1);
+      atomicMin(&d.det_min[dcur ^ 1][cc], i);
     }
   }
   if (a.dpres) atomicAdd(&d.cntl[i], a.dpres);

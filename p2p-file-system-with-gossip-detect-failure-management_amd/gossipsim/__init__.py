@@ -400,7 +400,8 @@ class ShardGroup:
 
 
 PutResult = namedtuple("PutResult", "file put_or_not replicas version status acks quorum_met")
-GetResult = namedtuple("GetResult", "file replicas version acks quorum_met source")
+GetResult = namedtuple("GetResult", "file replicas version acks quorum_met source source_version",
+                       defaults=(None,))
 
 
 class Cluster:
@@ -440,6 +441,17 @@ class Cluster:
         self.ids = {a: i for i, a in enumerate(self.addresses)}
         self.scheduled: dict[int, list[int]] = {}
         self.plans: list[tuple[int, int, tuple]] = []  # (round, observer, plan)
+        # each member's SDFSInfo.Local_files (sdfs_slave/sdfs_slave.go:20-41):
+        # file -> {member: (version, process epoch)}, written when a put or a
+        # repair copies the file to the member; a restarted process (join
+        # after a crash) starts with an empty map, so entries of an older
+        # epoch read as Go's zero value
+        self._local: dict[int, dict[int, tuple[int, int]]] = {}
+        self._epoch = np.zeros(n, np.int64)
+        # the process epoch in which a member last held the file metadata as
+        # master (SDFSMaster's maps live in the process, master/master.go:38):
+        # any other running member's metadata is empty
+        self._meta_epoch = {self.master: 0}
 
     # REPL vocabulary (slave/slave.go:546-613)
     def join(self, member):
@@ -450,6 +462,7 @@ class Cluster:
         member = int(member)
         self.engine.apply_events([(GH_EV_JOIN, member)])
         if member in self.dead:
+            self._epoch[member] += 1  # a fresh process: empty Local_files
             self.dead.discard(member)
             self.mview[member] = self._configured_master
             self.vote_on[member] = False
@@ -462,6 +475,17 @@ class Cluster:
     def crash(self, member):
         self.engine.apply_events([(GH_EV_CRASH, member)])
         self.dead.add(int(member))
+
+    def local_version(self, member, file):
+        """SDFSInfo.Get_file_version at `member` (sdfs_slave/sdfs_slave.go:39-41):
+        the version its process stored, 0 (Go's zero value) if it holds none."""
+        v = self._local.get(int(file), {}).get(int(member))
+        return v[0] if v is not None and v[1] == self._epoch[int(member)] else 0
+
+    def _store(self, file, members, version):
+        loc = self._local.setdefault(int(file), {})
+        for m in members:
+            loc[int(m)] = (int(version), int(self._epoch[int(m)]))
 
     def lsm(self, member):
         ids, hb, ts = self.engine.lsm(member)
@@ -519,6 +543,8 @@ class Cluster:
             for x, f in enumerate(go):
                 r = [int(a) for a in rep[x] if a >= 0]
                 placed[f] = (r, int(ver[x]), int(st[x]), sum(int(alive[a]) for a in r))
+                if int(st[x]) == GH_OK:  # Put_file at every live replica (slave/slave.go:724-760)
+                    self._store(f, [a for a in r if alive[a]], int(ver[x]))
         out = []
         for f in files:
             if f not in placed:
@@ -528,23 +554,38 @@ class Cluster:
             out.append(PutResult(f, True, r, v, st, acks, st == GH_OK and acks >= self.quorum(len(r))))
         return out
 
+    @staticmethod
+    def get_source(responses, version):
+        """Get's copy source (slave/slave.go:857-878) over the replicas'
+        responses [(member, local_version), ...] in arrival order: the first
+        whose local version is <= the master's `version`, or the only
+        response; None when no response qualifies (nothing is copied). A
+        replica without the file answers Go's zero value 0, which qualifies:
+        the reference can copy from a replica that holds no file."""
+        for m, lv in responses:
+            if lv <= version or len(responses) == 1:
+                return m, lv
+        return None
+
     def get(self, files):
         """get (slave/slave.go:815-890): the master's replica list and
-        version (-1: "No File Found"), and whether a read quorum of replicas
-        is alive to answer."""
+        version (-1: "No File Found"), whether a read quorum of replicas is
+        alive to answer, and the copy source: every live replica answers
+        Get_file_data with its local version (:799-810; arrival order is
+        taken as replica order) and get_source picks among the answers."""
         rep, ver = self.engine.get_files(files)
         alive = self._running()
         out = []
         for x, f in enumerate(files):
             r = [int(a) for a in rep[x] if a >= 0]
             acks = sum(int(alive[a]) for a in r)
-            # Get's copy source (slave/slave.go:857-878): the first response
-            # whose local version is <= the master's, or the only one. Under
-            # the store model (SPEC §9) every live replica holds the file at
-            # the master's version, so responses arrive in replica order and
-            # the first live replica is the source.
-            src = next((a for a in r if alive[a]), -1)
-            out.append(GetResult(int(f), r, int(ver[x]), acks, int(ver[x]) >= 0 and acks >= self.quorum(len(r)), src))
+            src, sv = -1, None
+            if int(ver[x]) >= 0:
+                pick = self.get_source([(a, self.local_version(a, f)) for a in r if alive[a]], int(ver[x]))
+                if pick is not None:
+                    src, sv = pick
+            out.append(GetResult(int(f), r, int(ver[x]), acks, int(ver[x]) >= 0 and acks >= self.quorum(len(r)),
+                                 src, sv))
         return out
 
     def _running(self):
@@ -588,10 +629,23 @@ class Cluster:
                     if self.mview[obs] in self.dead:  # Fail_recover dials a dead master (:1125-1127)
                         self._fatal(r, obs, "Fail_recover: master unreachable")
                         continue
-                    if self.mview[obs] != self.master:
-                        continue  # a stale but running master: its own (empty) metadata, not modelled
+                    m = int(self.mview[obs])
+                    if m != self.master:
+                        # a stale but running master answers from its own
+                        # SDFSMaster: empty unless this very process was the
+                        # master (a member demoted while running keeps its old
+                        # maps, which are not modelled). An empty plan:
+                        # Fail_recover returns at once (slave/slave.go:1139-1142)
+                        if self._meta_epoch.get(m) != self._epoch[m]:
+                            self.plans.append((r, obs, ()))
+                        continue
                 if self.engine.cfg.max_files > 0:
-                    self.plans.append((r, obs, tuple(self.engine.repair(obs))))
+                    plan = tuple(self.engine.repair(obs))
+                    self.plans.append((r, obs, plan))
+                    alive = self._running()
+                    for f, node1, v, st, new in plan:  # Re_put / Remote_reput copy the file (:1148-1170)
+                        if node1 >= 0:
+                            self._store(f, [a for a in new if alive[a]], v)
         return total
 
     # ---- master re-election (SPEC §9) -----------------------------------
@@ -622,6 +676,7 @@ class Cluster:
             if self.engine.cfg.max_files > 0:
                 f0, _ = self.engine.rebuild_meta(m)
             self.master = m
+            self._meta_epoch[m] = int(self._epoch[m])
             self.mview[f0] = m  # Assign_New_Master (:1045-1048)
             self.vote_on[f0] = False
             self.vote_on[m] = False  # :1039-1040

@@ -238,3 +238,36 @@ def test_crash_join_then_master_crash(gs):
     assert all(not (m == 5 and why.startswith("revote")) for _, m, why in cl.fatal)
     g = cl.get([0, 1])
     assert all(x.source == next((a for a in x.replicas if a not in cl.dead), -1) for x in g)
+
+
+@pytest.mark.gpu
+def test_repair_at_stale_running_master(gs):
+    """Fail_recover (slave/slave.go:1122-1142) dials the observer's own idea
+    of the master. Master 0 crashes, 1 is elected and rebuilds; 0 restarts as
+    a fresh process (Join, :288-308), believing the configured master -- itself
+    -- is the master. A repair it runs goes to its own SDFSMaster, which a
+    fresh process holds empty (master/master.go:38): Update_metadata returns
+    nothing and Fail_recover returns at once (:1139-1142). The same repair
+    from a member that follows the new master gets the master's plan."""
+    n, F = 32, 400
+    cl = gs.Cluster(n, elect=True, max_files=F, seed=0x5EED0F34, t_fail=8, t_cleanup=8, peer_mode=gs.GH_PEER_PULL)
+    cl.engine.import_state(*sc.full_state(n), 0)
+    cl.tick(2)
+    cl.put(range(F))
+    cl.crash(0)
+    for _ in range(40):
+        cl.tick(1)
+        if cl.master != 0:
+            break
+    assert cl.master == 1
+    cl.join(0)
+    cl.tick(1)
+    assert cl.mview[0] == 0 and 0 not in cl.dead
+    alive = cl.engine.alive()
+    obs = next(i for i in range(1, n) if alive[i] and i not in cl.dead and cl.mview[i] == cl.master)
+    r = cl.engine.round
+    cl.scheduled[r + 1] = [0, obs]
+    cl.tick(1)
+    got = {o: plan for rr, o, plan in cl.plans if rr == r + 1}
+    assert got[0] == () and obs in got
+    cl.engine.close()

@@ -306,11 +306,23 @@ def test_put_conflicts_and_cluster_ops(gs, oracle_mod):
     assert all(p.put_or_not and p.version == 1 and p.quorum_met for p in res)
     again = cl.put([0, 1], confirm=[1])  # file 0 clashes (0 rounds ago), 1 is confirmed
     assert (again[0].put_or_not, again[1].put_or_not, again[1].version) == (False, True, 2)
-    for a in res[1].replicas[:3]:
+    # Get's copy source (slave/slave.go:857-878): every live replica holds
+    # version 2 of file 1, so the first one in arrival (= replica) order
+    g = cl.get([1])[0]
+    assert (g.source, g.source_version) == (again[1].replicas[0], 2)
+    for a in again[1].replicas[:3]:
         cl.crash(a)
     cl.tick()
     g = cl.get([1, 5])[0]
     assert g.acks == 1 and g.quorum_met is False and cl.get([5])[0].version == -1
+    assert g.source == again[1].replicas[3] and g.source_version == 2  # the only live replica
+    # a crashed replica that restarts is a fresh process: no Local_files, so
+    # it answers version 0, which is <= 2, and is picked when it answers first
+    first = again[1].replicas[0]
+    cl.join(first)
+    cl.tick()
+    g = cl.get([1])[0]
+    assert cl.local_version(first, 1) == 0 and (g.source, g.source_version) == (first, 0)
 
 
 def c5_run(eng, orc, n, F, rounds=32):

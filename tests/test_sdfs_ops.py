@@ -32,3 +32,17 @@ def test_write_window_oracle(oracle_mod):
     o.put([0])  # Update_timestamp refreshes the window (:231-238)
     assert list(o.put_conflicts([0])) == [1]
     assert list(o.put_conflicts([0], window=0)) == [0]
+
+
+def test_get_source_kats():
+    """Get's copy source, hand-derived from slave/slave.go:857-878: the first
+    response (arrival order) whose local version is <= the master's, or the
+    only response; a replica without the file answers Go's zero value 0."""
+    from gossipsim import Cluster
+    src = Cluster.get_source
+    assert src([(4, 3), (7, 2)], 2) == (7, 2)   # 3 > 2 is skipped
+    assert src([(4, 2), (7, 2)], 2) == (4, 2)   # the first qualifying response
+    assert src([(4, 7)], 5) == (4, 7)           # the only response, even if newer
+    assert src([(4, 7), (7, 9)], 5) is None     # nothing qualifies: no copy
+    assert src([(4, 0), (7, 5)], 5) == (4, 0)   # an empty replica is picked first
+    assert src([], 5) is None
