@@ -161,6 +161,9 @@
 #ifndef GH_NIB_WAVES
 #define GH_NIB_WAVES 1          // nibble path: min waves per SIMD it is compiled for (1: the compiler picks)
 #endif
+#ifndef GH_NIB_WORD
+#define GH_NIB_WORD 1           // nibble path: the rule on whole nibble words with carry checks (1; A/B 2.09-2.18 vs 2.26-2.33 ms) or on split bytes (0)
+#endif
 #ifndef GH_JOB_WAVES
 #define GH_JOB_WAVES 4          // lane-job kernel: min waves per SIMD it is compiled for (A/B: 4 beats 3 and 5)
 #endif
@@ -276,9 +279,10 @@ struct GhDev {
   // unknown or old sender code, or the row's own member needing the per-cell
   // rule goes to k_round_jobs instead of sending its whole segment to the
   // slow list. Wave w of nibble workgroup b writes its jobs to
-  // jobs[(4 b + w) * GH_JOB_CAP ..] (uint4: row, tile << 8 | lane, the
-  // senders' minimum plane words) and their count to jobn[4 b + w], with no
-  // atomics. Results that need the wide arena go to redo (k_round_redo).
+  // jobs[2 (4 b + w) * GH_JOB_CAP ..], two uint4 each (row, tile << 8 |
+  // lane, the minimum plane words; the lane's own lag words and age words)
+  // and their count to jobn[4 b + w], with no atomics. Results that need the
+  // wide arena go to redo (k_round_redo, the first uint4).
   uint4 *jobs;
   int32_t *jobn;    // [4 * nibble workgroups]
   int32_t *njobs;   // [0] jobs of the last round (k_base's variant choice), [1] redo entries, [2] jobs of the round before

@@ -995,7 +995,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
     // grid (GH_WG_ROWS_WIDE rows x one tile per workgroup, 4 waves)
     if (e->c8) {
       d.jobw = ((d.nrows + GH_WG_ROWS_WIDE - 1) / GH_WG_ROWS_WIDE) * d.ntiles;
-      if ((rc = dalloc(e, &d.jobs, (size_t)d.jobw * 4 * GH_JOB_CAP, 0)) ||
+      if ((rc = dalloc(e, &d.jobs, (size_t)d.jobw * 4 * GH_JOB_CAP * 2, 0)) ||
           (rc = dalloc(e, &d.jobn, (size_t)d.jobw * 4, 0)) || (rc = dalloc(e, &d.njobs, 4, 0)) ||
           (rc = dalloc(e, &d.redo, GH_REDO_CAP, 0)))
         break;

@@ -775,6 +775,9 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   // per column the base move, one byte each, a lane's CPL bytes in its dword
   // order, even nibbles (cells 0,4,1,5) then odd ones (2,6,3,7) per dword
   __shared__ __attribute__((aligned(16))) uint32_t s_d8[TW / 4];
+  // GH_NIB_WORD: per chunk the base moves as one nibble word in the plane's
+  // nibble order (cell j at gh_nib(j))
+  __shared__ __attribute__((aligned(16))) uint32_t s_dn[TW / 8];
   __shared__ int s_slow[RB];
   __shared__ int s_meta[RB];
   __shared__ __attribute__((aligned(16))) int s_inb[RB * KB];
@@ -822,6 +825,17 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
     if (delta < 0 || delta > 15) atomicOr(&s_d8bad, 1ull << (cc / CPL));
     if (delta) s_bmove = 1;
   }
+  if constexpr (GH_NIB_WORD) {
+    for (int w = tid; w < TW / 8; w += 256) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t c = (int64_t)tile * TW + 8 * w + j;
+        x |= (uint32_t)((bn[c] - bo[c]) & 0xF) << gh_nib(j);
+      }
+      s_dn[w] = x;
+    }
+  }
   __syncthreads();
 
   const int64_t l0 = (int64_t)tile * TW + lc * CPL;  // local column of this lane's first cell
@@ -842,12 +856,16 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   if constexpr (CPL < 32) rm = (rm >> (l0 & 31)) & ((1u << CPL) - 1u);
   const bool lane_job = rm != 0u || ((s_d8bad >> lc) & 1ull) != 0;
   // this wave's lane-job region (no atomics: the wave owns it)
-  uint4* __restrict__ jreg = d.jobs + ((int64_t)bid * 4 + wave) * GH_JOB_CAP;
+  uint4* __restrict__ jreg = d.jobs + ((int64_t)bid * 4 + wave) * GH_JOB_CAP * 2;
   int wjobs = 0;
   uint32_t D8[2 * W];  // [2w + h]: the base moves of dword w's even / odd nibbles
+  uint32_t DN[W];      // (GH_NIB_WORD) the base moves of dword w, nibble order
 #pragma unroll
-  for (int x = 0; x < 2 * W; ++x) D8[x] = s_d8[lc * 2 * W + x];
+  for (int x = 0; x < 2 * W; ++x) D8[x] = GH_NIB_WORD ? 0u : s_d8[lc * 2 * W + x];
+#pragma unroll
+  for (int x = 0; x < W; ++x) DN[x] = GH_NIB_WORD ? s_dn[lc * W + x] : 0u;
   const uint32_t tfb = (uint32_t)(0x7F - min(p.t_fail, 15)) * 0x01010101u;  // age + tfb: bit 7 iff age > T_fail
+  const uint32_t tfk = (uint32_t)(15 - min(max(p.t_fail, 0), 15)) * 0x11111111u;  // (GH_NIB_WORD) age + tfk carries iff age > T_fail
   uint32_t n_mrg = 0;
 
 #pragma unroll 1
@@ -894,6 +912,55 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       for (int w = 0; w < W; ++w) {
         const uint32_t qw = qwu[u].v[w], aw = awu[u].v[w];
         esc |= gh_t4_esc(aw);
+        if constexpr (GH_NIB_WORD) {
+          // whole-word nibble rule: L = min(own, senders) per nibble is the
+          // next code before the rebase (merged iff it differs from the own
+          // code); a nibble add or compare that carries marks the lane out
+          // of the tier (a lane job), so no guard bits are needed
+          constexpr uint32_t N1 = 0x11111111u;
+          uint32_t Lw = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t M = 0x000F000Fu << (4 * j);
+            Lw |= pk_min_u16(pk_min_u16(pk_min_u16(qw & M, pwu[u][0].v[w] & M), pk_min_u16(pwu[u][1].v[w] & M,
+                                                                                         pwu[u][2].v[w] & M)),
+                             pwu[u][3].v[w] & M);
+          }
+          // a sender code unknown (0) or old (14) that the own code does not beat
+          Lz |= nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu);
+          LW[w] = Lw;
+          const uint32_t D = Lw ^ qw;
+          uint32_t t = D | (D >> 2);
+          t |= t >> 1;
+          const uint32_t m1 = t & N1;  // merged (bit 0 of the nibble)
+          const uint32_t E = ~qw;
+          uint32_t t2 = E | (E >> 2);
+          t2 |= t2 >> 1;
+          const uint32_t a1 = ~t2 & N1;     // own absent (code 15)
+          const uint32_t an1 = a1 & ~m1;    // absent, not merged: stays (15, 15)
+          const uint32_t ANm = an1 * 15u;
+          const uint32_t MM = m1 * 15u;
+          const uint32_t ddx = DN[w] & ~ANm;
+          const uint32_t S = Lw + ddx;  // next code, rebased
+          uint32_t bad = ((Lw ^ ddx ^ S) & (N1 - 1u)) | (S < Lw ? 1u : 0u);  // a code past 15 (carry into the next nibble)
+          const uint32_t s1 = S >> 1, s2 = S >> 2, s3 = S >> 3;
+          bad |= ((s1 & s2 & s3) | ~(s1 | s2 | s3)) & N1 & ~an1;         // a code of 14, 15 or below 2
+          const uint32_t ag = aw & ~(MM | ANm);                           // ages that grow by one
+          const uint32_t inc = N1 & ~(m1 | an1);
+          const uint32_t T = ag + inc;
+          bad |= ((ag ^ inc ^ T) & (N1 - 1u)) | (T < ag ? 1u : 0u);       // an age past 15
+          const uint32_t AN = T | m1 | ANm;                               // merged: age 1; absent: 15
+          const uint32_t X = AN & ~ANm;                                   // ages above min(T_fail, 15)
+          const uint32_t K = tfk & ~ANm;
+          const uint32_t V = X + K;
+          bad |= ((X ^ K ^ V) & (N1 - 1u)) | (V < X ? 1u : 0u);
+          Bm |= bad;
+          QO[w] = S;
+          AO[w] = AN;
+          mrg += __builtin_popcount(m1);
+          gain += __builtin_popcount(m1 & a1);
+          continue;
+        }
         uint32_t Lw = 0;  // per nibble the min over senders (fields at their bit position)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -960,7 +1027,10 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
           if (jb) {
             const int pos = wjobs + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(jm >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)jm, 0u));
-            jreg[pos] = uint4{(uint32_t)i, ((uint32_t)tile << 8) | (uint32_t)lc, LW[0], W > 1 ? LW[W - 1] : 0u};
+            // the job: row, tile and lane, the minimum plane words; then the
+            // lane's own lag and age words (the job kernel needs not re-read them)
+            jreg[2 * pos] = uint4{(uint32_t)i, ((uint32_t)tile << 8) | (uint32_t)lc, LW[0], W > 1 ? LW[W - 1] : 0u};
+            jreg[2 * pos + 1] = uint4{qwu[u].v[0], W > 1 ? qwu[u].v[W - 1] : 0u, awu[u].v[0], W > 1 ? awu[u].v[W - 1] : 0u};
           }
           wjobs += nj;
         } else {
@@ -1932,24 +2002,24 @@ __device__ __forceinline__ void job_rule(const GhDev& d, int cur, int dcur, cons
 // escaped, with its plane word). Returns false, writing nothing, when the
 // input is a wide segment or a result needs the wide arena (k_round_redo).
 __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, const GhRound& p, int i, int64_t l0,
-                                          uint32_t uw, JobAcc& acc, uint32_t& detm) {
+                                          uint32_t uw, uint32_t plw, uint32_t a4w, JobAcc& acc, uint32_t& detm) {
   const int nxt = cur ^ 1;
   const int32_t r = p.r;
   const int64_t cell = gh_cell(d, i, l0);
   const int jd = gh_jd(d, i, l0);
-  const uint32_t a4w = d.a4[cur][cell >> 3];
-  const uint32_t plw = d.pl[cur][cell >> 3];
-  const uint4 hx = *reinterpret_cast<const uint4*>(d.hn[cur] + cell);
   const int4 b0 = *reinterpret_cast<const int4*>(d.base[cur] + l0);
   const int4 b1 = *reinterpret_cast<const int4*>(d.base[cur] + l0 + 4);
   const int4 n0 = *reinterpret_cast<const int4*>(d.base[nxt] + l0);
   const int4 n1 = *reinterpret_cast<const int4*>(d.base[nxt] + l0 + 4);
   const int32_t bo[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
   const int32_t bn[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
-  uint32_t xw[4] = {hx.x, hx.y, hx.z, hx.w};
+  uint32_t xw[4];
   if (!gh_t4_esc(a4w)) {
     const v4u w = c4_dec(plw, a4w, jd);
     xw[0] = w[0], xw[1] = w[1], xw[2] = w[2], xw[3] = w[3];
+  } else {  // an escaped chunk: its 16-bit codes
+    const uint4 hx = *reinterpret_cast<const uint4*>(d.hn[cur] + cell);
+    xw[0] = hx.x, xw[1] = hx.y, xw[2] = hx.z, xw[3] = hx.w;
   }
   const uint32_t h0 = xw[0] & 0xFFFFu;
   if (h0 == GH_N_WIDE || h0 == GH_N_FROZEN) return false;  // a wide input: k_round_redo
@@ -2115,9 +2185,10 @@ __global__ __launch_bounds__(256, GH_JOB_WAVES) void k_round_jobs(GhDev d, int c
     }
     for (int t = threadIdx.x; t < RB; t += 256) s_drow[t] = 0;
     __syncthreads();
-    const uint4* jreg = d.jobs + (b * 4 + wave) * GH_JOB_CAP;
+    const uint4* jreg = d.jobs + (b * 4 + wave) * GH_JOB_CAP * 2;
     for (int e = lane; e < nj; e += 64) {
-      const uint4 jb = jreg[e];
+      const uint4 jb = jreg[2 * e];
+      const uint4 jo = jreg[2 * e + 1];  // the lane's own lag words, age words
       const int i = (int)jb.x;
       const int64_t l0 = (int64_t)(jb.y >> 8) * TW + (int64_t)(jb.y & 255u) * CPL;
       uint32_t detl = 0;  // detections, bit 8 w + j
@@ -2130,7 +2201,7 @@ __global__ __launch_bounds__(256, GH_JOB_WAVES) void k_round_jobs(GhDev d, int c
 #pragma unroll 1
       for (int w = 0; w < W && fit; ++w) {
         uint32_t dm8 = 0;
-        fit = job_chunk(d, cur, dcur, p, i, l0 + 8 * w, w ? jb.w : jb.z, a, dm8);
+        fit = job_chunk(d, cur, dcur, p, i, l0 + 8 * w, w ? jb.w : jb.z, w ? jo.y : jo.x, w ? jo.w : jo.z, a, dm8);
         detl |= dm8 << (8 * w);
       }
       if (!fit) {

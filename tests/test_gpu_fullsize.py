@@ -18,8 +18,10 @@ Two regimes:
 Counters, the failed set and the detectors are compared every round; the
 whole hb and ts tables (65,536 x 65,536 each) row block by row block at the
 rounds listed. The steady-state test also asserts, from round 8 on, that the
-round ran the byte path (gh_tier_info variant 3) with no escaped chunk: the
-path the bench times is the path checked here."""
+round ran the nibble path (gh_tier_info variant 3) with at most one in a
+million lanes handed to the lane-job kernel: the path the bench times is the
+path checked here. The crash case runs on the nibble path and its lane jobs
+throughout (no storm round)."""
 import os
 import time
 
@@ -99,20 +101,26 @@ def run(gs, om, t_fail, rounds, full_at, expect, sched=None, per_round=None):
 
 
 def byte_path_from(r0):
-    """per-round check: from round r0 on, the round ran the byte path (tier
-    variant 3) and wrote no escaped chunk"""
+    """per-round check: from round r0 on, the round ran the nibble path (tier
+    variant 3), and the lanes it handed to the lane-job kernel and the chunks
+    written escaped stay below one in a million (stragglers: a view not
+    refreshed for 16 rounds leaves the tier's 15-round age window; the job
+    kernel writes it escaped, bit-exact)"""
     def check(eng, r, st):
         if r >= r0:
             kept, current, escaped, variant = eng.tier_info(full=True)
+            jobs, redo = eng.job_info()
             assert (kept, current, variant) == (1, 1, 3), f"round {r}: tier_info {kept, current, escaped, variant}"
-            assert escaped == 0, f"round {r}: {escaped} escaped chunks"
+            n = eng.cfg.n_members
+            assert escaped * 10**6 <= n * n // 8 and jobs * 10**6 <= n * n // 16 and redo == 0, \
+                f"round {r}: {escaped} escaped chunks, {jobs} lane jobs, {redo} redos"
     return check
 
 
 def test_c3_fullsize_steady_state(gs, oracle_mod):
     """The bench's workload (T_fail = 16) through the rounds the bench times
     (the driver's --warmup 5 --steps 20 covers rounds 6-25): no detections,
-    full tables equal at r = 6, 12 and 25, the byte path from round 8 on."""
+    full tables equal at r = 6, 12 and 25, the nibble path from round 8 on."""
     run(gs, oracle_mod, 16, 25, {6, 12, 25}, lambda s: s["detections"] == 0 or pytest.fail("unexpected detections"),
         per_round=byte_path_from(8))
 
