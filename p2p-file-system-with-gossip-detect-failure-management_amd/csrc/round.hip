@@ -687,11 +687,17 @@ constexpr int round_rb() {
 // A lane owns CPL consecutive cells: W = CPL / 8 dwords of the plane and of
 // the age plane, and the same W dwords of each of its k senders' plane rows;
 // a row segment of 256 members is 256 / CPL lanes (one 128-B line per plane
-// row segment). Per dword (8 cells) the rule is SWAR on bytes after splitting
-// the even and odd nibbles. RS row steps per iteration: all their loads are
-// issued before any is computed. A row segment whose every lane stays in the
-// tier (codes 2..13, age <= min(T_fail, 15): no flag, no REMOVE, no guard
-// row, no escape, sender codes exact) is written here; any other goes to the
+// row segment). Per dword (8 cells) the rule runs on whole nibble words
+// (GH_NIB_WORD): L = the min of the own and the senders' codes per nibble
+// (masked fields, v_pk_min_u16) is the merged code; merged nibbles are those
+// where L differs from the own code; the rebase and the ageing are plain
+// 32-bit adds whose nibble carries mark the lane out of the tier (the older
+// form splits even and odd nibbles into bytes with guard bits). RS row steps
+// per iteration: all their loads are issued before any is computed. A lane
+// whose every cell stays in the tier (codes 2..13, age <= min(T_fail, 15):
+// no flag, no REMOVE, no escape, sender codes exact) is written here; any
+// other lane of an active row is a lane job (k_round_jobs), and only rows
+// under the <4 guard or with more than KB senders send whole segments to the
 // slow list (k_round_slow, the per-cell rule).
 template <int W>
 struct NibWords {
