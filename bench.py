@@ -100,8 +100,14 @@ def pmc_traffic(n, k, world, warmup, plane, tw, encoding):
     the same configuration, layout (sender plane, tile width), table encoding
     and warm-up (tools/pmc.sh -> profiles/*k_round_pmc*.json); a profile taken
     at another warm-up is refused (its timed rounds are another regime)."""
+    import re
+
+    def order(f):  # the latest round and session win: r03_s12 after r03_s6
+        m = re.match(r"r(\d+)(?:_s(\d+))?", f.name)
+        return (int(m.group(1)), int(m.group(2) or 0), f.name) if m else (0, 0, f.name)
+
     best = None
-    for f in sorted((REPO / "profiles").glob("*k_round_pmc*.json")):
+    for f in sorted((REPO / "profiles").glob("*k_round_pmc*.json"), key=order):
         try:
             d = json.loads(f.read_text())
         except (OSError, ValueError):
