@@ -99,6 +99,8 @@
 //                                   offset, 1..12: the plane's diagonal code)
 //                                   with age 1..15
 //                    absent cells   u = 15, age nibble 15
+//                    tombstones     u = 15, age nibble s = 1..14: age toff + s
+//                                   (GH_TIER_TOMB; toff = gh_tier_toff(T_cleanup))
 //                  so the plane word a round writes for its senders is the
 //                  row's own lag code as well: the steady state streams one
 //                  nibble of lag and one of age per cell each way, and the
@@ -161,11 +163,14 @@
 #ifndef GH_NIB_WAVES
 #define GH_NIB_WAVES 1          // nibble path: min waves per SIMD it is compiled for (1: the compiler picks)
 #endif
-#ifndef GH_NIB_WORD
-#define GH_NIB_WORD 1           // nibble path: the rule on whole nibble words with carry checks (1; A/B 2.09-2.18 vs 2.26-2.33 ms) or on split bytes (0)
-#endif
 #ifndef GH_JOB_WAVES
 #define GH_JOB_WAVES 4          // lane-job kernel: min waves per SIMD it is compiled for (A/B: 4 beats 3 and 5)
+#endif
+#ifndef GH_TIER_TOMB
+#define GH_TIER_TOMB 1          // 4-bit tier: tombstones in their last 14 ages before release are tier cells
+#endif
+#ifndef GH_TIER_TOMB_GATE
+#define GH_TIER_TOMB_GATE 1     // nibble path: the tombstone rule only in waves whose own cells include code 15
 #endif
 #ifndef GH_STORM_WAVES
 #define GH_STORM_WAVES 5         // storm variant: waves per SIMD it is compiled for (96 VGPRs, SGPR spills only)
@@ -270,6 +275,7 @@ struct GhDev {
   // frozen store of stopped rows: [fzcap][ld] exact x / ts; frow[i] = slot or -1
   int32_t *frow, *fzh, *fzt;
   int32_t tsat;     // T_cleanup < GH_TSAT_T: tombstone ages saturate at 30
+  int32_t toff;     // 4-bit tier: a tombstone of age toff + s is the tier cell (15, s), s = 1..14 (gh_tier_toff)
   int32_t *colq;    // [ld] scratch: per local column event index / merged value
   int64_t *slow;    // [ntiles * n] round: segments for k_round_slow, tile << 32 | row
   int32_t *slow_n;  // their count
@@ -423,45 +429,64 @@ __device__ __forceinline__ uint32_t plane_word(const v4u& o, int jd) {
 __host__ __device__ __forceinline__ int gh_nib(int j) { return 4 * (j >> 1) + 16 * (j & 1); }
 // the escape test of a tier chunk's age word
 __host__ __device__ __forceinline__ bool gh_t4_esc(uint32_t age) { return (age & 0xFu) == 0u; }
+// Tombstone age offset of the 4-bit tier for T_cleanup tc: the tier holds a
+// tombstone's last 14 ages before its release, tc - 12 .. tc + 1, as age
+// nibbles 1..14, so the age the release reads (tc + 1) is always nibble 14;
+// GH_TOFF_NONE (no tombstone in the tier) when tc + 1 passes the 16-bit
+// tombstone's 30 (GH_N_TAGEMAX)
+#define GH_TOFF_NONE (-128)
+__host__ __device__ __forceinline__ int gh_tier_toff(int tc) {
+  return !GH_TIER_TOMB || tc < 0 || tc + 1 > 30 ? GH_TOFF_NONE : tc - 13;
+}
 // The 16-bit codes of a tier chunk (not escaped): lag plane word u, age word
 // a; jd = the row's own member in the chunk (0..7, its code is the plane's
-// diagonal code) or -1.
-__device__ __forceinline__ v4u c4_dec(uint32_t u, uint32_t a, int jd) {
+// diagonal code) or -1; toff = GhDev::toff.
+__device__ __forceinline__ v4u c4_dec(uint32_t u, uint32_t a, int jd, int toff) {
   v4u o;
+  const uint32_t TO = (uint32_t)(toff & 0xFFFF) * 0x00010001u;  // (modulo 2^16 per half)
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const uint32_t U = (u >> (4 * m)) & 0x000F000Fu, A = (a >> (4 * m)) & 0x000F000Fu;
     // offset = GH_P_REF + 1 - u; no borrow crosses the halves (u <= 15)
     const uint32_t code = ((uint32_t)((GH_P_REF + 1) << 5) * 0x10001u - (U << 5)) | A;
-    const uint32_t ab = ((U + 0x00010001u) >> 4) & 0x00010001u;  // 1 per absent half (u = 15)
-    o[m] = code | pk_sub_u16(0u, ab);
+    const uint32_t nv = pk_sub_u16(0u, ((U + 0x00010001u) >> 4) & 0x00010001u);  // 0xFFFF per half with u = 15
+    // u = 15: absent (age nibble 15: 0xFFFF) or a tombstone of age toff + A
+    const uint32_t ab = pk_zero_mask(A ^ 0x000F000Fu);
+    const uint32_t tb = 0xFFE0FFE0u | (pk_add_u16(A, TO) & ~ab) | (0x001F001Fu & ab);
+    o[m] = (code & ~nv) | (tb & nv);
   }
   if (jd >= 0) {  // the diagonal's code is one offset lower: offset = GH_P_REF - u
     const int m = jd >> 1, sh = 16 * (jd & 1);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      if (q == m && ((o[q] >> sh) & 0xFFFFu) != 0xFFFFu) o[q] -= 0x20u << sh;
+      if (q == m && ((o[q] >> sh) & 0x8000u) == 0u) o[q] -= 0x20u << sh;
   }
   return o;
 }
 // The age word of 16-bit codes o whose plane word is u = plane_word(o, jd),
-// when the chunk has a tier encoding (every cell absent, or visible with an
-// exact plane code in the window and age 1..15); else false.
-__device__ __forceinline__ bool c4_enc(const v4u& o, int jd, uint32_t& age) {
+// when the chunk has a tier encoding (every cell absent, visible with an
+// exact plane code in the window and age 1..15, or a tombstone of age
+// toff + 1..14); else false.
+__device__ __forceinline__ bool c4_enc(const v4u& o, int jd, uint32_t& age, int toff) {
   uint32_t a = 0, bad = 0;
+  const uint32_t TO = (uint32_t)(toff & 0xFFFF) * 0x00010001u;  // (modulo 2^16 per half)
+  const uint32_t tno = toff == GH_TOFF_NONE ? 0x80008000u : 0u;  // no tombstone in the tier
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const uint32_t y = o[m];
     const uint32_t ab = pk_zero_mask(pk_add_u16(y, 0x00010001u));  // absent halves
+    const uint32_t ta = pk_zero_mask(pk_lshr16(pk_add_u16(y, 0x00200020u), 5));  // tombstone or absent
     // raw plane code GH_P_REF + 1 - offset in 2..13 (the diagonal's 1..12 is
     // the same range before its - 1); flagged, tombstone and marker codes
     // have bit 15 or an offset far above the window
     const uint32_t ur = pk_sub_u16((uint32_t)(GH_P_REF + 1) * 0x10001u, pk_lshr16(y, 5));
-    const uint32_t ag = y & 0x001F001Fu;
-    // per half: bit 15 of (y), (ur - 2), (13 - ur), (ag - 1), (15 - ag)
+    const uint32_t ag = pk_sub_u16(y & 0x001F001Fu, TO & ta & ~ab);  // a tombstone's age - toff
+    // visible halves: bit 15 of (y), (ur - 2), (13 - ur), (ag - 1), (15 - ag);
+    // tombstones: (ag - 1), (14 - ag) (15 is the absent code)
     const uint32_t b = y | pk_sub_u16(ur, 0x00020002u) | pk_sub_u16(0x000D000Du, ur) | pk_sub_u16(ag, 0x00010001u) |
                        pk_sub_u16(0x000F000Fu, ag);
-    bad |= b & ~ab & 0x80008000u;
+    const uint32_t bt = pk_sub_u16(ag, 0x00010001u) | pk_sub_u16(0x000E000Eu, ag) | tno;
+    bad |= ((b & ~ta) | (bt & ta & ~ab)) & 0x80008000u;
     a |= ((ag | ab) & 0x000F000Fu) << (4 * m);  // absent: age nibble 15
   }
   (void)jd;
@@ -487,7 +512,7 @@ __device__ __forceinline__ uint4 gh_ld16s(const GhDev& d, int buf, int64_t s, in
   if (gh_m8(d, buf)) {
     const uint32_t a = d.a4[buf][cell >> 3];
     if (!gh_t4_esc(a)) {
-      const v4u w = c4_dec(d.pl[buf][cell >> 3], a, jd);
+      const v4u w = c4_dec(d.pl[buf][cell >> 3], a, jd, d.toff);
       return uint4{w[0], w[1], w[2], w[3]};
     }
   }
@@ -505,7 +530,7 @@ __device__ __forceinline__ void gh_st16(const GhDev& d, int buf, int64_t i, int6
   const int64_t cell = gh_cell(d, i, c);
   if (gh_m8(d, buf)) {
     uint32_t a = 0;
-    if (t4 && c4_enc(v4u{x.x, x.y, x.z, x.w}, gh_jd(d, i, c), a)) {
+    if (t4 && c4_enc(v4u{x.x, x.y, x.z, x.w}, gh_jd(d, i, c), a, d.toff)) {
       d.a4[buf][cell >> 3] = a;
       return;
     }

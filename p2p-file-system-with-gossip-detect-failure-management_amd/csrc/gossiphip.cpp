@@ -954,6 +954,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   d.rank = rank;
   d.world = world;
   d.tsat = cfg->t_cleanup < GH_TSAT_T;
+  d.toff = gh_tier_toff(cfg->t_cleanup);
   // every shard sizes (and grows) its arena from the same segment count, the
   // largest over the shards, so the grow and lose decisions are collective
   // (ghost rows' wide segments take arena slots of the current buffer too)
@@ -2050,7 +2051,9 @@ int gh_debug_raw(void* h, int32_t row, int64_t c0, int64_t n, uint16_t* codes, i
       const int sh = gh_nib((int)(c & 7));
       const uint32_t u = (u4 >> sh) & 15u, a = (a4 >> sh) & 15u;
       const int diag = e->d.col0 + c == row;  // the plane's diagonal code
-      codes[c - c0] = u == 15u ? (uint16_t)GH_N_ABSENT : (uint16_t)(((GH_P_REF + 1 - diag - (int)u) << 5) | a);
+      // u = 15: absent (age nibble 15) or a tombstone of age toff + a
+      codes[c - c0] = u == 15u ? (uint16_t)(a == 15u ? GH_N_ABSENT : (GH_N_TOMB | (uint32_t)(e->d.toff + (int)a)))
+                               : (uint16_t)(((GH_P_REF + 1 - diag - (int)u) << 5) | a);
     } else {
       HIPCHK(e, hipMemcpy(codes + (c - c0), e->d.hn[e->cur] + cell, 2, hipMemcpyDeviceToHost));
     }

@@ -534,7 +534,6 @@ __device__ __forceinline__ uint32_t pair_bits(uint32_t m, int j) {
 
 // ---- sender snapshot plane (gh_internal.h: pl) ---------------------------
 // 0xFF in each byte of m that has bit 7 set (m: 0x80 / 0x00 bytes), no multiply
-__device__ __forceinline__ uint32_t bmask(uint32_t m) { return m | (m - (m >> 7)); }
 // nonzero iff a nibble of a is zero (exact when no nibble is zero; a
 // borrow can only add bits above a zero nibble)
 __device__ __forceinline__ uint32_t nib_haszero(uint32_t a) { return (a - 0x11111111u) & ~a & 0x88888888u; }
@@ -687,12 +686,12 @@ constexpr int round_rb() {
 // A lane owns CPL consecutive cells: W = CPL / 8 dwords of the plane and of
 // the age plane, and the same W dwords of each of its k senders' plane rows;
 // a row segment of 256 members is 256 / CPL lanes (one 128-B line per plane
-// row segment). Per dword (8 cells) the rule runs on whole nibble words
-// (GH_NIB_WORD): L = the min of the own and the senders' codes per nibble
-// (masked fields, v_pk_min_u16) is the merged code; merged nibbles are those
-// where L differs from the own code; the rebase and the ageing are plain
-// 32-bit adds whose nibble carries mark the lane out of the tier (the older
-// form splits even and odd nibbles into bytes with guard bits). RS row steps
+// row segment). Per dword (8 cells) the rule runs on whole nibble words:
+// L = the min of the own and the senders' codes per nibble (masked fields,
+// v_pk_min_u16) is the merged code; merged nibbles are those where L differs
+// from the own code; the rebase and the ageing are plain 32-bit adds whose
+// nibble carries mark the lane out of the tier (round 3's first form split
+// even and odd nibbles into bytes with guard bits: 7% slower). RS row steps
 // per iteration: all their loads are issued before any is computed. A lane
 // whose every cell stays in the tier (codes 2..13, age <= min(T_fail, 15):
 // no flag, no REMOVE, no escape, sender codes exact) is written here; any
@@ -764,6 +763,78 @@ __device__ __forceinline__ void nib_region(const GhDev& d, const GhRound& p, int
   }
 }
 
+// Per nibble of x: 1 (bit 0) where the nibble is 15.
+__device__ __forceinline__ uint32_t nib_is15(uint32_t x) {
+  const uint32_t e = ~x;
+  uint32_t t = e | (e >> 2);
+  t |= t >> 1;
+  return ~t & 0x11111111u;
+}
+// The nibble path's rule on one dword (8 cells) of a lane: own lag word qw,
+// age word aw, the senders' lag words p0..p3, a1 = nib_is15(qw), dn = the
+// base moves. L = min(own, senders) per nibble is the next code before the
+// rebase (merged iff it differs from the own code); a nibble add or compare
+// that carries marks the lane out of the tier (a lane job), so no guard bits
+// are needed. tt (wave-uniform): the wave holds own code-15 cells, which may be tier
+// tombstones (code 15, age nibble 1..14): age nibble 14 is older than
+// T_cleanup and released (step 5, :490-492: absent, and merges like one),
+// the others keep code 15 and age by one, never merged. Without tt no own
+// cell has code 15.
+__device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint32_t p0, uint32_t p1, uint32_t p2,
+                                         uint32_t p3, uint32_t a1, uint32_t dn, uint32_t tfk, uint32_t& QO,
+                                         uint32_t& AO, uint32_t& LWo, uint32_t& Bm, uint32_t& Lz, int& mrg, int& gain,
+                                         int& rel) {
+  constexpr uint32_t N1 = 0x11111111u;
+  uint32_t Lw = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t M = 0x000F000Fu << (4 * j);
+    Lw |= pk_min_u16(pk_min_u16(pk_min_u16(qw & M, p0 & M), pk_min_u16(p1 & M, p2 & M)), p3 & M);
+  }
+  uint32_t kp1 = 0, KM = 0;
+  if (tt) {
+    // a code-15 cell with age nibble s: absent (15), a tombstone released
+    // this round (14: its age is T_cleanup + 1, gh_tier_toff), or a kept
+    // tombstone (1..13); an escaped chunk's age word is 0 (the lane is a
+    // job, whose merge candidates are the plain minimum)
+    const uint32_t h3 = (aw >> 1) & (aw >> 2) & (aw >> 3) & N1;  // s >= 14
+    kp1 = gh_t4_esc(aw) ? 0u : a1 & ~h3;
+    KM = kp1 * 15u;
+    Lw |= KM;  // a kept tombstone takes no entry
+    rel += __builtin_popcount(a1 & h3 & ~aw);
+  }
+  // a sender code unknown (0) or old (14) that the own code does not beat
+  Lz |= nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu);
+  LWo = Lw;
+  const uint32_t D = Lw ^ qw;
+  uint32_t t = D | (D >> 2);
+  t |= t >> 1;
+  const uint32_t m1 = t & N1;            // merged (bit 0 of the nibble)
+  const uint32_t an1 = a1 & ~m1 & ~kp1;  // absent (or released), not merged: stays (15, 15)
+  const uint32_t ANm = an1 * 15u;
+  const uint32_t MM = m1 * 15u;
+  const uint32_t ST = ANm | KM;          // cells whose code stays 15
+  const uint32_t ddx = dn & ~ST;
+  const uint32_t S = Lw + ddx;  // next code, rebased
+  uint32_t bad = ((Lw ^ ddx ^ S) & (N1 - 1u)) | (S < Lw ? 1u : 0u);  // a code past 15 (carry into the next nibble)
+  const uint32_t s1 = S >> 1, s2 = S >> 2, s3 = S >> 3;
+  bad |= ((s1 & s2 & s3) | ~(s1 | s2 | s3)) & N1 & ~(an1 | kp1);  // a code of 14, 15 or below 2
+  const uint32_t ag = aw & ~(MM | ANm);                           // ages that grow by one (kept tombstones to 14 at most)
+  const uint32_t inc = N1 & ~(m1 | an1);
+  const uint32_t T = ag + inc;
+  bad |= ((ag ^ inc ^ T) & (N1 - 1u)) | (T < ag ? 1u : 0u);  // an age past 15
+  const uint32_t AN = T | m1 | ANm;  // merged: age 1; absent: 15
+  const uint32_t X = AN & ~ST;       // ages above min(T_fail, 15)
+  const uint32_t K = tfk & ~ST;
+  const uint32_t V = X + K;
+  bad |= ((X ^ K ^ V) & (N1 - 1u)) | (V < X ? 1u : 0u);
+  Bm |= bad;
+  QO = S;
+  AO = AN;
+  mrg += __builtin_popcount(m1);
+  gain += __builtin_popcount(m1 & a1);
+}
+
 template <int TW, bool NT, int CPL>
 __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, const GhRound& p, const int bid) {
   constexpr int W = CPL / 8;         // dwords per lane and plane
@@ -775,14 +846,11 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   constexpr int RS = GH_NIB_RS > 0 ? GH_NIB_RS : (CPL <= 16 ? 2 : 1);  // row steps per iteration
   static_assert(SEG >= 2 && SEG <= 64 && RB % (RSTEP * RS) == 0, "nibble path: whole row steps");
   static_assert(W <= 2, "nibble path: a lane job carries at most two minimum plane words");
-  __shared__ unsigned long long s_merged;
+  __shared__ unsigned long long s_merged, s_rel;
   __shared__ int s_quiet, s_nslow, s_slowbase, s_bmove;
   __shared__ unsigned long long s_d8bad;  // bit l: lane l's columns hold a base move outside 0..15
-  // per column the base move, one byte each, a lane's CPL bytes in its dword
-  // order, even nibbles (cells 0,4,1,5) then odd ones (2,6,3,7) per dword
-  __shared__ __attribute__((aligned(16))) uint32_t s_d8[TW / 4];
-  // GH_NIB_WORD: per chunk the base moves as one nibble word in the plane's
-  // nibble order (cell j at gh_nib(j))
+  // per chunk the base moves as one nibble word in the plane's nibble order
+  // (cell j at gh_nib(j))
   __shared__ __attribute__((aligned(16))) uint32_t s_dn[TW / 8];
   __shared__ int s_slow[RB];
   __shared__ int s_meta[RB];
@@ -797,7 +865,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const int sub = lane / SEG, lc = lane % SEG;
   const unsigned long long gmask = (SEG == 64 ? ~0ull : ((1ull << SEG) - 1)) << (sub * SEG);
   if (tid == 0) {
-    s_merged = 0;
+    s_merged = s_rel = 0;
     s_quiet = s_nslow = s_bmove = 0;
     s_d8bad = 0ull;
   }
@@ -826,21 +894,17 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   for (int cc = tid; cc < TW; cc += 256) {
     const int64_t c = (int64_t)tile * TW + cc;
     const int64_t delta = (int64_t)bn[c] - bo[c];
-    const int j = cc & 7;
-    reinterpret_cast<uint8_t*>(s_d8)[(cc & ~7) + (j >> 2) + 2 * (j & 1) + 4 * ((j >> 1) & 1)] = (uint8_t)(delta & 0xFF);
     if (delta < 0 || delta > 15) atomicOr(&s_d8bad, 1ull << (cc / CPL));
     if (delta) s_bmove = 1;
   }
-  if constexpr (GH_NIB_WORD) {
-    for (int w = tid; w < TW / 8; w += 256) {
-      uint32_t x = 0;
+  for (int w = tid; w < TW / 8; w += 256) {
+    uint32_t x = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int64_t c = (int64_t)tile * TW + 8 * w + j;
-        x |= (uint32_t)((bn[c] - bo[c]) & 0xF) << gh_nib(j);
-      }
-      s_dn[w] = x;
+    for (int j = 0; j < 8; ++j) {
+      const int64_t c = (int64_t)tile * TW + 8 * w + j;
+      x |= (uint32_t)((bn[c] - bo[c]) & 0xF) << gh_nib(j);
     }
+    s_dn[w] = x;
   }
   __syncthreads();
 
@@ -864,15 +928,11 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   // this wave's lane-job region (no atomics: the wave owns it)
   uint4* __restrict__ jreg = d.jobs + ((int64_t)bid * 4 + wave) * GH_JOB_CAP * 2;
   int wjobs = 0;
-  uint32_t D8[2 * W];  // [2w + h]: the base moves of dword w's even / odd nibbles
-  uint32_t DN[W];      // (GH_NIB_WORD) the base moves of dword w, nibble order
+  uint32_t DN[W];  // the base moves of dword w, nibble order
 #pragma unroll
-  for (int x = 0; x < 2 * W; ++x) D8[x] = GH_NIB_WORD ? 0u : s_d8[lc * 2 * W + x];
-#pragma unroll
-  for (int x = 0; x < W; ++x) DN[x] = GH_NIB_WORD ? s_dn[lc * W + x] : 0u;
-  const uint32_t tfb = (uint32_t)(0x7F - min(p.t_fail, 15)) * 0x01010101u;  // age + tfb: bit 7 iff age > T_fail
-  const uint32_t tfk = (uint32_t)(15 - min(max(p.t_fail, 0), 15)) * 0x11111111u;  // (GH_NIB_WORD) age + tfk carries iff age > T_fail
-  uint32_t n_mrg = 0;
+  for (int x = 0; x < W; ++x) DN[x] = s_dn[lc * W + x];
+  const uint32_t tfk = (uint32_t)(15 - min(max(p.t_fail, 0), 15)) * 0x11111111u;  // age + tfk carries iff age > T_fail
+  uint32_t n_mrg = 0, n_rel = 0;
 
 #pragma unroll 1
   for (int it = 0; it < RB / RSTEP; it += RS) {
@@ -911,95 +971,23 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
     for (int u = 0; u < RS; ++u) {
       const int i = iu[u];
       const bool al = alu[u];
-      uint32_t QO[W], AO[W], LW[W], Bm = 0, Lz = 0;
-      int mrg = 0, gain = 0;
+      uint32_t QO[W], AO[W], LW[W], A1[W], Bm = 0, Lz = 0;
+      int mrg = 0, gain = 0, rel = 0;
       bool esc = false;
+      uint32_t a1any = 0;
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        const uint32_t qw = qwu[u].v[w], aw = awu[u].v[w];
-        esc |= gh_t4_esc(aw);
-        if constexpr (GH_NIB_WORD) {
-          // whole-word nibble rule: L = min(own, senders) per nibble is the
-          // next code before the rebase (merged iff it differs from the own
-          // code); a nibble add or compare that carries marks the lane out
-          // of the tier (a lane job), so no guard bits are needed
-          constexpr uint32_t N1 = 0x11111111u;
-          uint32_t Lw = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t M = 0x000F000Fu << (4 * j);
-            Lw |= pk_min_u16(pk_min_u16(pk_min_u16(qw & M, pwu[u][0].v[w] & M), pk_min_u16(pwu[u][1].v[w] & M,
-                                                                                         pwu[u][2].v[w] & M)),
-                             pwu[u][3].v[w] & M);
-          }
-          // a sender code unknown (0) or old (14) that the own code does not beat
-          Lz |= nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu);
-          LW[w] = Lw;
-          const uint32_t D = Lw ^ qw;
-          uint32_t t = D | (D >> 2);
-          t |= t >> 1;
-          const uint32_t m1 = t & N1;  // merged (bit 0 of the nibble)
-          const uint32_t E = ~qw;
-          uint32_t t2 = E | (E >> 2);
-          t2 |= t2 >> 1;
-          const uint32_t a1 = ~t2 & N1;     // own absent (code 15)
-          const uint32_t an1 = a1 & ~m1;    // absent, not merged: stays (15, 15)
-          const uint32_t ANm = an1 * 15u;
-          const uint32_t MM = m1 * 15u;
-          const uint32_t ddx = DN[w] & ~ANm;
-          const uint32_t S = Lw + ddx;  // next code, rebased
-          uint32_t bad = ((Lw ^ ddx ^ S) & (N1 - 1u)) | (S < Lw ? 1u : 0u);  // a code past 15 (carry into the next nibble)
-          const uint32_t s1 = S >> 1, s2 = S >> 2, s3 = S >> 3;
-          bad |= ((s1 & s2 & s3) | ~(s1 | s2 | s3)) & N1 & ~an1;         // a code of 14, 15 or below 2
-          const uint32_t ag = aw & ~(MM | ANm);                           // ages that grow by one
-          const uint32_t inc = N1 & ~(m1 | an1);
-          const uint32_t T = ag + inc;
-          bad |= ((ag ^ inc ^ T) & (N1 - 1u)) | (T < ag ? 1u : 0u);       // an age past 15
-          const uint32_t AN = T | m1 | ANm;                               // merged: age 1; absent: 15
-          const uint32_t X = AN & ~ANm;                                   // ages above min(T_fail, 15)
-          const uint32_t K = tfk & ~ANm;
-          const uint32_t V = X + K;
-          bad |= ((X ^ K ^ V) & (N1 - 1u)) | (V < X ? 1u : 0u);
-          Bm |= bad;
-          QO[w] = S;
-          AO[w] = AN;
-          mrg += __builtin_popcount(m1);
-          gain += __builtin_popcount(m1 & a1);
-          continue;
-        }
-        uint32_t Lw = 0;  // per nibble the min over senders (fields at their bit position)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t M = 0x000F000Fu << (4 * j);
-          Lw |= pk_min_u16(pk_min_u16(pwu[u][0].v[w] & M, pwu[u][1].v[w] & M),
-                           pk_min_u16(pwu[u][2].v[w] & M, pwu[u][3].v[w] & M));
-        }
-        Lz |= nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu);  // a sender code unknown (0) or old (14)
-        LW[w] = Lw;
-        const uint32_t QQ[2] = {qw & 0x0F0F0F0Fu, (qw >> 4) & 0x0F0F0F0Fu};
-        const uint32_t GG[2] = {aw & 0x0F0F0F0Fu, (aw >> 4) & 0x0F0F0F0Fu};
-        const uint32_t UU[2] = {Lw & 0x0F0F0F0Fu, (Lw >> 4) & 0x0F0F0F0Fu};
-        uint32_t qo[2], ao[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const uint32_t Q = QQ[h], G = GG[h], U = UU[h], dd = D8[2 * w + h];
-          const uint32_t A = (Q + 0x01010101u) & 0x10101010u;                 // own absent (0x10)
-          const uint32_t Mg = ((Q + 0x7F7F7F7Fu) - U) & 0x80808080u;          // merged: u < q (0x80)
-          const uint32_t MM = bmask(Mg);
-          const uint32_t qn = ((U & MM) | (Q & ~MM)) + dd;                     // next code, rebased
-          const uint32_t ANm = bmask((A & ~(Mg >> 3)) << 3);                  // absent next
-          const uint32_t an = (0x01010101u & MM) | ((G + 0x01010101u) & ~MM);  // next age
-          // a running cell outside the tier: code above 13 or below 2, age
-          // above min(T_fail, 15)
-          Bm |= ((qn + 0x72727272u) | ~(qn + 0x7E7E7E7Eu) | (an + tfb)) & ~ANm & 0x80808080u;
-          qo[h] = (qn | ANm) & 0x0F0F0F0Fu;  // absent: 15
-          ao[h] = (an | ANm) & 0x0F0F0F0Fu;  // absent: age nibble 15
-          mrg += __builtin_popcount(Mg);
-          gain += __builtin_popcount(Mg & (A << 3));
-        }
-        QO[w] = qo[0] | (qo[1] << 4);
-        AO[w] = ao[0] | (ao[1] << 4);
+        esc |= gh_t4_esc(awu[u].v[w]);
+        A1[w] = nib_is15(qwu[u].v[w]);
+        a1any |= A1[w];
       }
+      // (wave-uniform) the wave's own cells include code 15 (absent or a tier
+      // tombstone): the rule ages and releases tombstones
+      const bool tt = GH_TIER_TOMB && (!GH_TIER_TOMB_GATE || __ballot(a1any != 0) != 0);
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        nib_word(tt, qwu[u].v[w], awu[u].v[w], pwu[u][0].v[w], pwu[u][1].v[w], pwu[u][2].v[w], pwu[u][3].v[w], A1[w],
+                 DN[w], tfk, QO[w], AO[w], LW[w], Bm, Lz, mrg, gain, rel);
       bool ob = false;
       const int jd = i - c0;
       // (a wave-uniform branch: 1 wave in TW / CPL... holds an own member)
@@ -1049,6 +1037,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
         nib_store<W, NT>(pln_t, owu[u], QO);
         nib_store<W, NT>(a4n_t, owu[u], AO);
         n_mrg += (uint32_t)mrg;
+        n_rel += (uint32_t)rel;
         dpres = gain;
       } else if (al && seg_slow && lc == 0) {
         s_slow[atomicAdd(&s_nslow, 1)] = i;
@@ -1063,10 +1052,12 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
 
   if (lane == 0) d.jobn[(int64_t)bid * 4 + wave] = wjobs;
   if (n_mrg) atomicAdd(&s_merged, (unsigned long long)n_mrg);
+  if (n_rel) atomicAdd(&s_rel, (unsigned long long)n_rel);
   __syncthreads();
   if (tid == 0) {
     if (s_nslow) s_slowbase = atomicAdd(d.slow_n, s_nslow);
     if (s_merged) atomicAdd(&d.stats[ST_MERGED], s_merged);
+    if (s_rel) atomicAdd(&d.stats[ST_RELEASED], s_rel);
     if (s_quiet) atomicAdd(d.nquiet, s_quiet);
   }
   __syncthreads();
@@ -1372,7 +1363,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       if (gh_t4_esc(a4w))
         w = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + ob));
       else
-        w = c4_dec(q4w, a4w, own_in ? jd : -1);
+        w = c4_dec(q4w, a4w, own_in ? jd : -1, d.toff);
     }
     bad |= (w[0] & 0xFFFFu) == GH_N_WIDE;  // own segment wide
     // The row's own member in the lane (step 3, :443-448): hb + 1 with a
@@ -1459,7 +1450,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
             if (gh_t4_esc(sa[u]))
               pv = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + (psl[g + u] * (TW * 2) + lb)));
             else
-              pv = c4_dec(su[u], sa[u], (unsigned)js < 8u ? js : -1);
+              pv = c4_dec(su[u], sa[u], (unsigned)js < 8u ? js : -1, d.toff);
             fold(pv, g + u);
           }
         } else {
@@ -1623,7 +1614,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         if (m8n) {
           // the tier: the age word, the plane word below is the lag
           uint32_t age = 0;
-          const bool t4 = c4_enc(o, own_in ? jd : -1, age);
+          const bool t4 = c4_enc(o, own_in ? jd : -1, age, d.toff);
           uint32_t* ap = reinterpret_cast<uint32_t*>(a4n_t + obp);
           if constexpr (NT)
             __builtin_nontemporal_store(t4 ? age : GH_T4_ESC, ap);
@@ -2021,7 +2012,7 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
   const int32_t bn[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
   uint32_t xw[4];
   if (!gh_t4_esc(a4w)) {
-    const v4u w = c4_dec(plw, a4w, jd);
+    const v4u w = c4_dec(plw, a4w, jd, d.toff);
     xw[0] = w[0], xw[1] = w[1], xw[2] = w[2], xw[3] = w[3];
   } else {  // an escaped chunk: its 16-bit codes
     const uint4 hx = *reinterpret_cast<const uint4*>(d.hn[cur] + cell);
@@ -2149,7 +2140,7 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
   const v4u nv = {nw[0], nw[1], nw[2], nw[3]};
   d.pl[nxt][cell >> 3] = plane_word(nv, jd);
   uint32_t a4n;
-  if (c4_enc(nv, jd, a4n)) {
+  if (c4_enc(nv, jd, a4n, d.toff)) {
     d.a4[nxt][cell >> 3] = a4n;
   } else {
     d.a4[nxt][cell >> 3] = GH_T4_ESC;

@@ -24,7 +24,8 @@ for v in "$@"; do
     cpl16_rs1_w8) build $v -DGH_NIB_CPL=16 -DGH_NIB_RS=1 -DGH_NIB_WAVES=8 & ;;
     cpl8_rs1_w8) build $v -DGH_NIB_CPL=8 -DGH_NIB_RS=1 -DGH_NIB_WAVES=8 & ;;
     jobw4) build $v -DGH_JOB_WAVES=4 & ;;
-    word) build $v -DGH_NIB_WORD=1 & ;;
+    notomb) build $v -DGH_TIER_TOMB=0 & ;;
+    tombng) build $v -DGH_TIER_TOMB_GATE=0 & ;;
     jobw5) build $v -DGH_JOB_WAVES=5 & ;;
     *) echo "unknown variant $v"; exit 1 ;;
   esac
