@@ -261,3 +261,34 @@ def test_tier_wide_segments(gs, oracle_mod, case):
         tn.test_stale_outliers(gs, oracle_mod, 257, 5)
     else:
         tn.test_base_jump_by_merge(gs, oracle_mod)
+
+
+@pytest.mark.parametrize("t_cleanup", [3, 13, 16, 29, 30])
+def test_tier_tombstones(gs, oracle_mod, t_cleanup):
+    """Tombstones in the 4-bit tier (GH_TIER_TOMB, gh_internal.h gh_tier_toff):
+    a tombstone's last 14 ages before release are tier cells (age nibble 1..14
+    with the offset T_cleanup - 13, nibble 14 = released this round). Crashes,
+    a LEAVE and a rejoin at N=2,048 with T_cleanup from below the offset's
+    zero (3) to past the tier's range (30: no tombstone in the tier), so the
+    offset is negative, zero, positive and absent; bit-exact every round."""
+    n = 2048
+    cfg = dict(fanout=4, seed=0x5EED0B10, t_fail=12, t_cleanup=t_cleanup)
+    sched = {3: [(sc.CRASH, 17), (sc.CRASH, 900), (sc.CRASH, 1500)], 14: [(sc.LEAVE, 40)],
+             30: [(sc.JOIN, 17)]}
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    hb, ts, alive = sc.full_state(n)
+    eng.import_state(hb, ts, alive, 0)
+    orc.import_state(hb, ts, alive, 0)
+    rel = 0
+    for r in range(1, 34 + t_cleanup // 2):
+        ev = sched.get(r, [])
+        if ev:
+            eng.apply_events(ev)
+            orc.apply_events(ev)
+        s1, s2 = eng.step(1), orc.step(1)
+        assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
+        rel += s1["released"]
+        compare(eng, orc, r)
+    assert rel > 0
+    assert eng.tier_info()[0] == 1
