@@ -163,6 +163,21 @@
 #ifndef GH_NIB_WAVES
 #define GH_NIB_WAVES 1          // nibble path: min waves per SIMD it is compiled for (1: the compiler picks)
 #endif
+// nibble path cache policies (gfx950 buffer aux bits: 1 sc0, 2 nt, 16 sc1):
+// the own age words (read once), the own lag words (also gathered by the
+// tile's receivers), the sender gathers, and the stores of both planes
+#ifndef GH_NIB_AGE_AUX
+#define GH_NIB_AGE_AUX 2
+#endif
+#ifndef GH_NIB_OWN_AUX
+#define GH_NIB_OWN_AUX 0
+#endif
+#ifndef GH_NIB_GAT_AUX
+#define GH_NIB_GAT_AUX 0
+#endif
+#ifndef GH_NIB_ST_AUX
+#define GH_NIB_ST_AUX 2
+#endif
 #ifndef GH_JOB_WAVES
 #define GH_JOB_WAVES 4          // lane-job kernel: min waves per SIMD it is compiled for (A/B: 4 beats 3 and 5)
 #endif
@@ -291,7 +306,9 @@ struct GhDev {
   // wide arena go to redo (k_round_redo, the first uint4).
   uint4 *jobs;
   int32_t *jobn;    // [4 * nibble workgroups]
-  int32_t *njobs;   // [0] jobs of the last round (k_base's variant choice), [1] redo entries, [2] jobs of the round before
+  int32_t *njobs;   // [0] jobs of the last round (k_base's variant choice), [1] redo entries, [2] jobs of the round before,
+                    // [3] nibble workgroups listed in jlist this round
+  int32_t *jlist;   // [jobw] the nibble workgroups that wrote lane jobs this round (k_round_jobs walks only these)
   uint4 *redo;      // [GH_REDO_CAP] lane jobs whose cells need a wide segment
   int64_t jobw;     // nibble workgroups (jobn entries / 4)
   int32_t *mode;    // k_round variant of the round: 0 lean, 1 storm (k_base)

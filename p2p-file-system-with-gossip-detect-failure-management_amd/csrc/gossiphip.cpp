@@ -38,6 +38,12 @@ struct Engine {
   int rank = 0, world = 1;
   std::unique_ptr<GhComm> comm;
   hipStream_t stream = nullptr;
+  // a tiered engine launches the round variants the nibble path does not need
+  // on a side stream (forked after the round's inputs, joined before the lane
+  // jobs): one of the four runs, the three idle ones return at once while the
+  // nibble path runs, off the round's critical path
+  hipStream_t vstream = nullptr;
+  hipEvent_t vfork = nullptr, vjoin = nullptr;
   GhDev d{};
   int cur = 0, dcur = 0;
   int32_t round = 0;
@@ -932,7 +938,10 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   e->lorder = cfg->list_order == GH_ORDER_APPEND;
   const int64_t pad = std::max<int64_t>(GH_PAD, 8 * (int64_t)tw);
   e->ld = (ncs + pad - 1) / pad * pad;
-  if (!dry && hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (!dry && (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+               hipStreamCreateWithFlags(&e->vstream, hipStreamNonBlocking) != hipSuccess ||
+               hipEventCreateWithFlags(&e->vfork, hipEventDisableTiming) != hipSuccess ||
+               hipEventCreateWithFlags(&e->vjoin, hipEventDisableTiming) != hipSuccess)) {
     delete e;
     return GH_EHIP;
   }
@@ -997,7 +1006,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
     if (e->c8) {
       d.jobw = ((d.nrows + GH_WG_ROWS_WIDE - 1) / GH_WG_ROWS_WIDE) * d.ntiles;
       if ((rc = dalloc(e, &d.jobs, (size_t)d.jobw * 4 * GH_JOB_CAP * 2, 0)) ||
-          (rc = dalloc(e, &d.jobn, (size_t)d.jobw * 4, 0)) || (rc = dalloc(e, &d.njobs, 4, 0)) ||
+          (rc = dalloc(e, &d.jobn, (size_t)d.jobw * 4, 0)) || (rc = dalloc(e, &d.njobs, 8, 0)) ||
+          (rc = dalloc(e, &d.jlist, (size_t)d.jobw, 0)) ||
           (rc = dalloc(e, &d.redo, GH_REDO_CAP, 0)))
         break;
     }
@@ -1281,6 +1291,9 @@ void gh_destroy(void* h) {
   for (auto ev : e->evs) (void)hipEventDestroy(ev);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
+  if (e->vstream) (void)hipStreamDestroy(e->vstream);
+  if (e->vfork) (void)hipEventDestroy(e->vfork);
+  if (e->vjoin) (void)hipEventDestroy(e->vjoin);
   delete e;
 }
 
@@ -1537,8 +1550,8 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   bool busy = false;
   if ((rc0 = check_lost(e)) || (rc0 = maybe_grow(e, &busy))) return rc0;
   HIPCHK(e, hipMemsetAsync(e->d.stats, 0, sizeof(unsigned long long) * ST_COUNT, e->stream));
-  if (e->timing && (int64_t)e->evs.size() < 5 * (int64_t)rounds) {
-    while ((int64_t)e->evs.size() < 5 * (int64_t)rounds) {
+  if (e->timing && (int64_t)e->evs.size() < 6 * (int64_t)rounds) {
+    while ((int64_t)e->evs.size() < 6 * (int64_t)rounds) {
       hipEvent_t ev;
       HIPCHK(e, hipEventCreate(&ev));
       e->evs.push_back(ev);
@@ -1604,12 +1617,29 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     GhRound pr = p;
     pr.gpo = e->gpo;  // row layout: the ghosts carry only their plane so far
     // the variants of k_round; the ones not selected return at once
-    const int nvar = e->c8 ? 4 : 2;  // lean 16-bit input, storm, lean tier input (16-bit rule, nibble path)
-    for (int v = 0; v < nvar; ++v) {
-      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[5 * q + v], e->stream));
-      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v);
+    // (events 6q + 0..3 bracket variants 0..2, 6q + 4..5 the last one)
+    if (e->c8) {
+      // lean 16-bit input, storm, lean tier input by the 16-bit rule on the
+      // side stream, beside the nibble path
+      HIPCHK(e, hipEventRecord(e->vfork, e->stream));
+      HIPCHK(e, hipStreamWaitEvent(e->vstream, e->vfork, 0));
+      for (int v = 0; v < 3; ++v) {
+        if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + v], e->vstream));
+        launch_round(e->d, e->cur, e->dcur, pr, e->vstream, e->nt, v);
+      }
+      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 3], e->vstream));
+      HIPCHK(e, hipEventRecord(e->vjoin, e->vstream));
+      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 4], e->stream));
+      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, 3);
+      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 5], e->stream));
+      HIPCHK(e, hipStreamWaitEvent(e->stream, e->vjoin, 0));
+    } else {  // lean 16-bit input, storm
+      for (int v = 0; v < 2; ++v) {
+        if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + v], e->stream));
+        launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v);
+      }
+      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 2], e->stream));
     }
-    if (e->timing) HIPCHK(e, hipEventRecord(e->evs[5 * q + nvar], e->stream));
     launch_round_jobs(e->d, e->cur, e->dcur, pr, e->stream);
     if ((rc = ghost_codes_if_slow(e))) return rc;
     launch_round_slow(e->d, e->cur, e->dcur, pr, e->stream);
@@ -1665,7 +1695,8 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       float ms = 0.f;  // the variant that ran
       for (int v = 0; v < (e->c8 ? 4 : 2); ++v) {
         float mv = 0.f;
-        HIPCHK(e, hipEventElapsedTime(&mv, e->evs[5 * q + v], e->evs[5 * q + v + 1]));
+        const int b = 6 * q + (v == 3 ? 4 : v);
+        HIPCHK(e, hipEventElapsedTime(&mv, e->evs[b], e->evs[b + 1]));
         ms = std::max(ms, mv);
       }
       e->timed_ms += ms;

@@ -573,6 +573,7 @@ __device__ __forceinline__ void base_col(const GhDev& d, int cur, int dcur, cons
     if (d.njobs) {
       d.njobs[0] = 0;
       d.njobs[1] = 0;
+      d.njobs[3] = 0;
     }
     if (d.a4[0]) {
       // the lean variant writes the next buffer in the 4-bit tier, the storm
@@ -716,9 +717,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t nib_rsrc(const void* p, int64_
                                            uni((int)min(bytes, (int64_t)INT_MAX)), 0x00020000);
 }
 // cache policy of a buffer access on gfx950: 2 = nt (streamed once)
-template <int W, bool NTL>
+template <int W, int aux>
 __device__ __forceinline__ NibWords<W> nib_load(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  constexpr int aux = NTL ? 2 : 0;
   NibWords<W> o;
   if constexpr (W == 1) {
     o.v[0] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, aux);
@@ -733,9 +733,8 @@ __device__ __forceinline__ NibWords<W> nib_load(__amdgpu_buffer_rsrc_t r, uint32
   }
   return o;
 }
-template <int W, bool NTS>
+template <int W, int aux>
 __device__ __forceinline__ void nib_store(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint32_t* v) {
-  constexpr int aux = NTS ? 2 : 0;
   if constexpr (W == 1) {
     __builtin_amdgcn_raw_buffer_store_b32(v[0], r, (int)off, 0, aux);
   } else if constexpr (W == 2) {
@@ -847,7 +846,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   static_assert(SEG >= 2 && SEG <= 64 && RB % (RSTEP * RS) == 0, "nibble path: whole row steps");
   static_assert(W <= 2, "nibble path: a lane job carries at most two minimum plane words");
   __shared__ unsigned long long s_merged, s_rel;
-  __shared__ int s_quiet, s_nslow, s_slowbase, s_bmove;
+  __shared__ int s_quiet, s_nslow, s_slowbase, s_bmove, s_hasjob;
   __shared__ unsigned long long s_d8bad;  // bit l: lane l's columns hold a base move outside 0..15
   // per chunk the base moves as one nibble word in the plane's nibble order
   // (cell j at gh_nib(j))
@@ -866,7 +865,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const unsigned long long gmask = (SEG == 64 ? ~0ull : ((1ull << SEG) - 1)) << (sub * SEG);
   if (tid == 0) {
     s_merged = s_rel = 0;
-    s_quiet = s_nslow = s_bmove = 0;
+    s_quiet = s_nslow = s_bmove = s_hasjob = 0;
     s_d8bad = 0ull;
   }
   const bool pull = p.peer_mode == GH_PEER_PULL;
@@ -960,12 +959,12 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       // the age words are read once (no peer reads them): they stream past
       // the caches the plane lines live in; the own plane words are a line
       // the row's receivers gather too
-      awu[u] = nib_load<W, true>(a4o_t, ow);
-      qwu[u] = nib_load<W, false>(plo_t, ow);
+      awu[u] = nib_load<W, GH_NIB_AGE_AUX>(a4o_t, ow);
+      qwu[u] = nib_load<W, GH_NIB_OWN_AUX>(plo_t, ow);
       const int4 sv4 = *reinterpret_cast<const int4*>(&s_inb[rs * KB]);
       const int sv[4] = {sv4.x, sv4.y, sv4.z, sv4.w};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) pwu[u][q] = nib_load<W, false>(plo_t, (uint32_t)sv[q] + lbp);
+      for (int q = 0; q < 4; ++q) pwu[u][q] = nib_load<W, GH_NIB_GAT_AUX>(plo_t, (uint32_t)sv[q] + lbp);
     }
 #pragma unroll
     for (int u = 0; u < RS; ++u) {
@@ -1034,8 +1033,8 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       const bool seg_slow = jslow || (__ballot(al && !rowok) & gmask) != 0;
       int dpres = 0;
       if (al && !seg_slow && !jb) {
-        nib_store<W, NT>(pln_t, owu[u], QO);
-        nib_store<W, NT>(a4n_t, owu[u], AO);
+        nib_store<W, NT ? GH_NIB_ST_AUX : 0>(pln_t, owu[u], QO);
+        nib_store<W, NT ? GH_NIB_ST_AUX : 0>(a4n_t, owu[u], AO);
         n_mrg += (uint32_t)mrg;
         n_rel += (uint32_t)rel;
         dpres = gain;
@@ -1050,7 +1049,10 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
     }
   }
 
-  if (lane == 0) d.jobn[(int64_t)bid * 4 + wave] = wjobs;
+  if (lane == 0) {
+    d.jobn[(int64_t)bid * 4 + wave] = wjobs;
+    if (wjobs) s_hasjob = 1;
+  }
   if (n_mrg) atomicAdd(&s_merged, (unsigned long long)n_mrg);
   if (n_rel) atomicAdd(&s_rel, (unsigned long long)n_rel);
   __syncthreads();
@@ -1059,6 +1061,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
     if (s_merged) atomicAdd(&d.stats[ST_MERGED], s_merged);
     if (s_rel) atomicAdd(&d.stats[ST_RELEASED], s_rel);
     if (s_quiet) atomicAdd(d.nquiet, s_quiet);
+    if (s_hasjob) d.jlist[atomicAdd(&d.njobs[3], 1)] = bid;  // k_round_jobs walks the listed workgroups only
   }
   __syncthreads();
   for (int t = tid; t < s_nslow; t += 256) d.slow[s_slowbase + t] = ((int64_t)tile << 32) | (uint32_t)s_slow[t];
@@ -2159,6 +2162,8 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
 template <int TW, int CPL>
 __global__ __launch_bounds__(256, GH_JOB_WAVES) void k_round_jobs(GhDev d, int cur, int dcur, GhRound p) {
   if (d.m8[4] != 3) return;
+  const int nlist = d.njobs[3];  // the nibble workgroups with jobs (none in a quiet steady-state round)
+  if (nlist == 0) return;
   constexpr int W = CPL / 8;
   constexpr int RB = round_rb<TW>();
   __shared__ int s_dcnt[TW], s_dmin[TW], s_drow[RB];
@@ -2169,9 +2174,9 @@ __global__ __launch_bounds__(256, GH_JOB_WAVES) void k_round_jobs(GhDev d, int c
   if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
   if (threadIdx.x == 0) s_jobs = s_flag = 0;
   JobAcc tot{};
-  for (int64_t b = blockIdx.x; b < d.jobw; b += gridDim.x) {
+  for (int x = blockIdx.x; x < nlist; x += gridDim.x) {
+    const int64_t b = d.jlist[x];
     const int nj = d.jobn[b * 4 + wave];
-    if (!__syncthreads_or(nj > 0)) continue;  // (uniform over the block)
     int tile, rb;
     nib_region<TW>(d, p, (int)b, tile, rb);
     const int64_t cbase = (int64_t)tile * TW;

@@ -1,0 +1,17 @@
+#!/bin/bash
+# A/B builds of round.hip under extra defines (tools only; the product is the
+# default build): lib/variants/libgossiphip_<name>.so, every other object from
+# build/. Run `make` first. Usage: build_variants.sh 'name=-DX=1 -DY=2' ...
+# Select one at run time with GOSSIPHIP_LIB=<path>.
+set -e
+cd "$(dirname "$0")/../../p2p-file-system-with-gossip-detect-failure-management_amd"
+mkdir -p lib/variants build/variants
+FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result"
+OBJS="build/events.o build/place.o build/elect.o build/comm.o build/rows.o build/order.o build/gossiphip.o"
+for spec in "$@"; do
+  name=${spec%%=*}; defs=${spec#*=}
+  ( /opt/rocm/bin/hipcc $FLAGS $defs -c -o build/variants/round_$name.o csrc/round.hip &&
+    /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o lib/variants/libgossiphip_$name.so \
+      build/variants/round_$name.o $OBJS -ldl ) &
+done
+wait
