@@ -508,7 +508,10 @@ def main():
         b_plane = 1.0 * nrows_r * ncols if plane else 0.0
     b_compulsory = b_table + b_plane
     b_prev_model = 3.0 * nrows_r * ncols  # round 2's 8-bit tier: 1-B cells in + out, the plane out + in
-    b_gather = 2.0 * nrows_r * ncols * k       # the k sender segments per cell (L2 / Infinity Cache / HBM)
+    # the k sender segments per cell (L2 / Infinity Cache / HBM): 4-bit plane
+    # codes (the tier's lag nibbles, or the plane beside a 16-bit table), else
+    # the senders' 16-bit codes
+    b_gather = (0.5 if (tier4 or plane) else 2.0) * nrows_r * ncols * k
     b_survey = 4.0 * nrows_r * ncols * (k + 4)  # SURVEY.md §8d (int32 hb + ts streams)
     encoding = "t4" if tier4 else "u16"
     traffic = pmc_traffic(n, k, world, args.warmup, plane, tile_w, encoding)

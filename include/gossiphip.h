@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GH_ABI_VERSION 6
+#define GH_ABI_VERSION 7
 
 /* ---- error codes ---------------------------------------------------- */
 #define GH_OK 0
@@ -64,6 +64,16 @@ extern "C" {
  * bytes (double-buffered [N][N] int32 lists). */
 #define GH_ORDER_ID 0
 #define GH_ORDER_APPEND 1
+/* Who receives a detector's REMOVE (SPEC D4). GH_REMOVE_LIST is the
+ * reference: Remove (slave/slave.go:338-363) runs right after removeMember
+ * inside the detection sweep (:472-473) and messages every member of the
+ * detector's list as it stands then (the member itself and the members the
+ * sweep removed before it are gone, the later ones still listed), itself
+ * excluded (:344-346). GH_REMOVE_ALL delivers it to every alive row but a sole
+ * detector (equal whenever the detectors' lists agree, as in a healthy
+ * cluster; the victim of a false positive then removes itself too). */
+#define GH_REMOVE_ALL 0
+#define GH_REMOVE_LIST 1
 
 /* ---- events (SPEC.md §5) ---------------------------------------------- */
 #define GH_EV_JOIN 1       /* slave/slave.go:288 Join + :250 addNewMember     */
@@ -92,7 +102,9 @@ typedef struct gh_config {
   int32_t shard_layout;  /* sharded engines (gh_create_sharded):
                             GH_LAYOUT_COLUMNS (0, default) or GH_LAYOUT_ROWS */
   int32_t list_order;    /* GH_ORDER_ID (0, default) or GH_ORDER_APPEND      */
-  int32_t reserved[4];
+  int32_t remove_mode;   /* REMOVE recipients: GH_REMOVE_ALL (0, default) or
+                            GH_REMOVE_LIST (the reference's, slave.go:344)  */
+  int32_t reserved[3];
 } gh_config;
 
 typedef struct gh_event {

@@ -51,6 +51,7 @@ class Node:
     def __init__(self, addr, order="id"):
         self.addr = addr
         self.alive = False
+        self.sent: dict[int, set[int]] = {}   # the last sweep's REMOVE recipients per member
         self.members: list[Member] = []      # MemberList
         self.recent_fail: list[Member] = []  # RecentFailList
         self.order = order
@@ -113,9 +114,16 @@ class Node:
         self.clean_fail_list(now)
         return detected  # revote_master (:452-457) is out of scope
 
+    def _remove_msg(self, c, live):
+        # Remove (slave/slave.go:338-363): REMOVE c to every member of the
+        # list as it stands when the call is made (after removeMember(c) and
+        # the removals before it in the sweep), self excluded (:344-346)
+        self.sent.setdefault(c, set()).update(m.addr for m in live if m.addr != self.addr)
+
     def detect_failure(self, now, quirk):  # slave/slave.go:460-482
         current = now
         detected = []
+        self.sent = {}  # c -> recipients of this sweep's REMOVE(c) messages
         if not quirk:
             # canonical: every candidate of the list is detected
             cands = [m for m in self.members
@@ -123,6 +131,7 @@ class Node:
             for m in cands:
                 self.remove_member(m.addr)
                 detected.append(m.addr)
+                self._remove_msg(m.addr, self.members)
             return detected
         # literal Go: `for _, member := range self.MemberList` captures the
         # header (array, len); removeMember shifts the same array in place.
@@ -139,9 +148,11 @@ class Node:
                 live = backing[:length]
                 ri = get_index(member.addr, live)
                 ti = get_index(member.addr, self.recent_fail)
+                panicked = False
                 if ti == -1:
                     if ri == -1:
                         self.stats["remove_unknown"] += 1
+                        panicked = True  # :280 panics before Remove is reached
                     else:
                         self.recent_fail.append(live[ri])
                 if ri != -1:
@@ -149,7 +160,9 @@ class Node:
                         backing[q] = backing[q + 1]
                     length -= 1  # backing[length] keeps the stale last entry
                     detected.append(member.addr)
-                # self.Remove(member.Address) is sent again on a stale re-read
+                # self.Remove(member.Address), sent again on a stale re-read
+                if not panicked:
+                    self._remove_msg(member.addr, backing[:length])
         self.members = backing[:length]
         return detected
 
@@ -173,7 +186,7 @@ class ListSim:
     """N nodes run in synchronous rounds (SPEC.md §2) with reference logic."""
 
     def __init__(self, n, seed=0x5EED0001, peer_mode="ring", fanout=3, quirk=False,
-                 order="id", introducer=0, master=0, replicas=4, population=None):
+                 order="id", introducer=0, master=0, replicas=4, population=None, remove="all"):
         self.n = n
         self.nodes = [Node(a, order) for a in range(n)]
         self.seed = seed
@@ -183,8 +196,14 @@ class ListSim:
         self.introducer = introducer
         self.master = master
         self.R = replicas
+        # REMOVE recipients: "list" = the reference's (every member of the
+        # detector's list when Remove runs, slave/slave.go:344, 472-473);
+        # "all" = SPEC D4 (every alive row but a sole detector)
+        assert remove in ("all", "list")
+        self.remove = remove
         self.round = 0
         self.pending_remove: dict[int, list[int]] = {}  # c -> detectors (D_{r-1})
+        self.pending_recv: dict[int, set[int]] = {}     # c -> recipients of REMOVE(c) ("list")
         self.events: list[tuple[int, int]] = []
         self.files: dict[int, dict] = {}  # File_matadata (master/master.go:23)
         self.draws: dict[int, int] = {}
@@ -263,12 +282,16 @@ class ListSim:
             for j, nd in enumerate(nodes):
                 if not nd.alive:
                     continue
-                if dets == [j]:
+                if self.remove == "list":
+                    if j not in self.pending_recv.get(c, ()):
+                        continue  # no detector had j in its list (:344)
+                elif dets == [j]:
                     continue  # the sole detector does not message itself (:344-346)
                 self._remove_at(j, c)
         # steps 2-5 per node (HeartBeat, slave/slave.go:499-511)
         active = [False] * self.n
         detected_by: dict[int, list[int]] = {}
+        recv: dict[int, set[int]] = {}
         self.last_detectors = []
         for i, nd in enumerate(nodes):
             if not nd.alive:
@@ -283,6 +306,8 @@ class ListSim:
             self.stats["detections"] += len(det)
             for c in det:
                 detected_by.setdefault(c, []).append(i)
+            for c, to in nd.sent.items():
+                recv.setdefault(c, set()).update(to)
             if det:
                 self.last_detectors.append(i)
         snaps = {i: nodes[i].snapshot() for i in range(self.n) if active[i]}
@@ -314,6 +339,7 @@ class ListSim:
                 changed |= nodes[i].merge(snaps[s], r)
             self.stats["merged_cells"] += len(changed)
         self.pending_remove = detected_by
+        self.pending_recv = recv
         self.last_failed = sorted(detected_by)
         self.stats["failed_members"] += len(detected_by)
         self.round = r

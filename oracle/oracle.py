@@ -23,6 +23,7 @@ GH_EPLACEMENT_STARVED = -5
 GH_ERANGE = -6
 GH_PEER_PULL, GH_PEER_RING = 0, 1
 GH_DETECT_CANONICAL, GH_DETECT_QUIRK = 0, 1
+GH_REMOVE_ALL, GH_REMOVE_LIST = 0, 1
 GH_EV_JOIN, GH_EV_LEAVE, GH_EV_CRASH = 1, 2, 3
 
 
@@ -33,7 +34,8 @@ class Config(C.Structure):
         ("min_members", C.c_int32), ("replicas", C.c_int32), ("introducer", C.c_int32),
         ("master", C.c_int32), ("device", C.c_int32), ("tile_width", C.c_int32),
         ("seed", C.c_uint64), ("max_files", C.c_int64), ("wide_segments", C.c_int64),
-        ("reserved", C.c_int32 * 6),
+        ("shard_layout", C.c_int32), ("list_order", C.c_int32), ("remove_mode", C.c_int32),
+        ("reserved", C.c_int32 * 3),
     ]
 
 

@@ -53,6 +53,13 @@ typedef struct ors {
   int32_t *det_cnt, *det_min;   /* pending REMOVE set D_{r-1} (per column) */
   int32_t *ndet_cnt, *ndet_min; /* detections of the current round         */
   int32_t *targets;             /* ring mode: rows x 3                     */
+  /* GH_REMOVE_LIST (the reference's REMOVE recipients, slave/slave.go:344):
+   * per row the members listed before the detection sweep (self excluded)
+   * and the members the sweep detected, W = ceil(n / 64) words each; per
+   * column the rows REMOVE(c) reaches: recv (D_{r-1}, delivered in step 1)
+   * and nrecv (D_r, built after phase A) */
+  int64_t W;
+  uint64_t *lbase, *ldet, *recv, *nrecv;
   gh_event *ev;
   int64_t nev, evcap;
   int64_t fcap;
@@ -90,6 +97,19 @@ int or_create(const gh_config *cfg, int64_t rows, void **out) {
   s->ndet_cnt = (int32_t *)calloc(s->n, 4);
   s->ndet_min = (int32_t *)malloc((size_t)s->n * 4);
   s->targets = (int32_t *)malloc((size_t)rows * 3 * 4);
+  s->W = (s->n + 63) / 64;
+  if (cfg->remove_mode == GH_REMOVE_LIST) {
+    s->lbase = (uint64_t *)calloc((size_t)rows * s->W, 8);
+    s->ldet = (uint64_t *)calloc((size_t)rows * s->W, 8);
+    s->recv = (uint64_t *)calloc((size_t)s->n * s->W, 8);
+    s->nrecv = (uint64_t *)calloc((size_t)s->n * s->W, 8);
+  } else if (cfg->remove_mode != GH_REMOVE_ALL) {
+    free(s->hb);
+    free(s->ts);
+    free(s->snap);
+    free(s);
+    return GH_EINVAL;
+  }
   if (!s->hb || !s->ts || !s->snap) {
     free(s->hb);
     free(s->ts);
@@ -128,6 +148,10 @@ void or_destroy(void *h) {
   free(s->det_any);
   free(s->det_cnt);
   free(s->det_min);
+  free(s->lbase);
+  free(s->ldet);
+  free(s->recv);
+  free(s->nrecv);
   free(s->ndet_cnt);
   free(s->ndet_min);
   free(s->targets);
@@ -330,9 +354,16 @@ static int phase_a(ors *s, int64_t i, int32_t r, gh_round_stats *st, int32_t *ld
   int32_t *row = s->hb + i * n;
   int32_t *trow = s->ts + i * n;
   /* step 1: REMOVE delivery */
+  const int literal = s->cfg.remove_mode == GH_REMOVE_LIST;
   for (int32_t c = 0; c < n; ++c) {
     int32_t dc = s->det_cnt[c];
-    if (dc == 0 || (dc == 1 && s->det_min[c] == i)) continue;
+    if (dc == 0) continue;
+    if (literal) {
+      /* no detector of c had row i in its list when it sent REMOVE(c) */
+      if (!((s->recv[(int64_t)c * s->W + (i >> 6)] >> (i & 63)) & 1u)) continue;
+    } else if (dc == 1 && s->det_min[c] == i) {
+      continue; /* the sole detector does not message itself (:344-346) */
+    }
     or_remove_member(s, i, c, st);
   }
   /* step 2: guard */
@@ -362,6 +393,14 @@ static int phase_a(ors *s, int64_t i, int32_t r, gh_round_stats *st, int32_t *ld
   int prev_cand = 0;
   int64_t off = 0;
   int found = 0;
+  uint64_t *lb = literal ? s->lbase + i * s->W : NULL;
+  uint64_t *ld = literal ? s->ldet + i * s->W : NULL;
+  if (literal) { /* the list the sweep starts from, self excluded (:344-346) */
+    memset(lb, 0, (size_t)s->W * 8);
+    memset(ld, 0, (size_t)s->W * 8);
+    for (int32_t c = 0; c < n; ++c)
+      if (row[c] >= 0 && c != i) lb[c >> 6] |= 1ull << (c & 63);
+  }
   for (int32_t c = 0; c < n; ++c) {
     int32_t v = row[c];
     if (v < 0) continue; /* not in the list */
@@ -378,6 +417,7 @@ static int phase_a(ors *s, int64_t i, int32_t r, gh_round_stats *st, int32_t *ld
     prev_cand = 1;
     if (!det) continue;
     row[c] = GH_TOMBSTONE; /* removeMember keeps the stale ts (:280) */
+    if (literal) ld[c >> 6] |= 1ull << (c & 63);
     st->detections++;
     found = 1;
     ldc[c] += 1; /* this thread's D_r counts; rows ascend within a thread */
@@ -453,6 +493,32 @@ static int one_round(ors *s, gh_round_stats *acc) {
     }
     free(ldc);
     free(ldm);
+  }
+  if (s->cfg.remove_mode == GH_REMOVE_LIST) {
+    /* REMOVE(c) from detector i reaches i's list as it stands right after
+     * removeMember(c) in the sweep (:472-473): the listed members but the
+     * ones the sweep removed up to c (ID order), c itself included */
+    const int64_t W = s->W;
+#pragma omp parallel for num_threads(s->threads) schedule(dynamic, 16)
+    for (int32_t c = 0; c < n; ++c) {
+      uint64_t *rc = s->nrecv + (int64_t)c * W;
+      memset(rc, 0, (size_t)W * 8);
+      if (s->ndet_cnt[c] == 0) continue;
+      const int64_t cw = c >> 6;
+      const uint64_t upto = (c & 63) == 63 ? ~0ull : ((1ull << ((c & 63) + 1)) - 1);
+      for (int64_t i = 0; i < rows; ++i) {
+        const uint64_t *ld = s->ldet + i * W;
+        if (!s->active[i] || !((ld[cw] >> (c & 63)) & 1u)) continue;
+        const uint64_t *lb = s->lbase + i * W;
+        for (int64_t w = 0; w < W; ++w) {
+          const uint64_t gone = w < cw ? ld[w] : w == cw ? (ld[w] & upto) : 0;
+          rc[w] |= lb[w] & ~gone;
+        }
+      }
+    }
+    uint64_t *t = s->recv;
+    s->recv = s->nrecv;
+    s->nrecv = t;
   }
   /* snapshot of every active alive row after steps 1-5 (what it sends) */
 #pragma omp parallel for num_threads(s->threads) schedule(static)

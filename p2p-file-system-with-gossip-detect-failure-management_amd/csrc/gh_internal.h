@@ -157,6 +157,7 @@
 #ifndef GH_NIB_CPL
 #define GH_NIB_CPL 16           // nibble path: cells per lane (8, 16, 32: 4-, 8-, 16-B lane accesses; 16 measured best)
 #endif
+#define GH_JOB_CPL 16           // a lane job covers 16 cells (a 32-cell lane of the nibble path writes two)
 #ifndef GH_NIB_RS
 #define GH_NIB_RS 1             // nibble path: row steps per iteration (1 measured best at CPL 8 and 16)
 #endif
@@ -319,6 +320,18 @@ struct GhDev {
   int32_t *post;         // [n]: post-REMOVE present counts of undecided rows (allreduced)
   int32_t *det_cnt[2], *det_min[2];
   uint32_t *dbits;
+  // GH_REMOVE_LIST (the reference's REMOVE recipients, slave/slave.go:344;
+  // one engine, member-ID list order): rcv[b] holds, per column c of the
+  // REMOVE set of parity b, bit j of word c * nw + j / 32 = row j receives
+  // REMOVE(c). Built after each detection round (remove.hip) from column
+  // bitmaps over the rows that ran the sweep: cdet (the row detected the
+  // member), csurv (listed and not detected), clst (listed; self excluded)
+  // and their counts ccnt [0, ld) survivors, [ld, 2 ld) listed, [2 ld] rows
+  int32_t rlist;
+  int64_t nw;       // words of a column bitmap over the rows, ceil(n / 32)
+  uint32_t *rcv[2];
+  uint32_t *cdet, *csurv, *clst;
+  int32_t *ccnt;
   int32_t *dlist;
   int32_t *nd;      // [0..1] local |D| per parity, [2..3] dlist fill, [4] join adds, [5] list merges
   int32_t *inbox_beg, *inbox_cnt, *inbox, *inbox_fill, *targets;
@@ -799,6 +812,14 @@ struct GhRound {
 
 // ---- launchers (kernels in round.hip / events.hip / place.hip) ----------
 // round.hip
+// Row j receives REMOVE(c) of the REMOVE set of parity dcur (c in that set):
+// the reference's recipients under GH_REMOVE_LIST, else every row but a sole
+// detector (SPEC D4; the detector does not message itself, :344-346).
+__device__ __forceinline__ bool gh_rm_at(const GhDev& d, int dcur, int64_t c, int64_t j) {
+  if (d.rlist) return (d.rcv[dcur][c * d.nw + (j >> 5)] >> (j & 31)) & 1u;
+  return !(d.det_cnt[dcur][c] == 1 && d.det_min[dcur][c] == j);
+}
+
 void launch_active_pre(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_active_post(const GhDev& d, const GhRound& p, hipStream_t s);
 // one engine (world 1): launch_base + the guard of every row, decided in
@@ -826,6 +847,10 @@ void launch_round_jobs(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
 // the segments k_round listed, by the per-cell rule (after launch_round)
 void launch_round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s);
+// GH_REMOVE_LIST: the column bitmaps of the round's sweep (before
+// launch_finish) and the recipients of D_r (after it); remove.hip
+void launch_rm_cols(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
+void launch_rm_recv(const GhDev& d, int dnew, const GhRound& p, hipStream_t s);
 // base[cur ^ 1] from buffer cur (member c's own heartbeat - GH_BASE_LAG),
 // |D_{r-1}| next to the local counts, empty slow list
 void launch_base(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);

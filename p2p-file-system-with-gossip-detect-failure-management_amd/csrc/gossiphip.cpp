@@ -849,6 +849,10 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (world < 1 || rank < 0 || rank >= world) return GH_EINVAL;
   // the list order of a row spans every member column: one engine holds it
   if (cfg->list_order == GH_ORDER_APPEND && world > 1) return GH_EINVAL;
+  // the reference's REMOVE recipients: one engine (a recipient set spans
+  // every row and column), member-ID list order (remove.hip)
+  if (cfg->remove_mode != GH_REMOVE_ALL && cfg->remove_mode != GH_REMOVE_LIST) return GH_EINVAL;
+  if (cfg->remove_mode == GH_REMOVE_LIST && (world > 1 || cfg->list_order != GH_ORDER_ID)) return GH_EINVAL;
   if (world > 1 && !comm_id && !dry) return GH_EINVAL;
   if (transport != GH_COMM_RCCL && transport != GH_COMM_LOCAL) return GH_EINVAL;
   if (!dry) {
@@ -964,6 +968,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   d.world = world;
   d.tsat = cfg->t_cleanup < GH_TSAT_T;
   d.toff = gh_tier_toff(cfg->t_cleanup);
+  d.rlist = cfg->remove_mode == GH_REMOVE_LIST;
   // every shard sizes (and grows) its arena from the same segment count, the
   // largest over the shards, so the grow and lose decisions are collective
   // (ghost rows' wide segments take arena slots of the current buffer too)
@@ -1023,6 +1028,16 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.dbits, e->ld / 32 + 2, 0)) || (rc = dalloc(e, &d.dlist, 2 * e->ld, 0)) ||
         (rc = dalloc(e, &d.nd, 8, 0)))
       break;
+    // GH_REMOVE_LIST: the recipients of two REMOVE sets and the column
+    // bitmaps of a sweep, [ld][ceil(n / 32)] words each (remove.hip)
+    if (d.rlist) {
+      d.nw = ((int64_t)e->n + 31) / 32;
+      const size_t words = (size_t)e->ld * d.nw;
+      if ((rc = dalloc(e, &d.rcv[0], words, 0)) || (rc = dalloc(e, &d.rcv[1], words, 0)) ||
+          (rc = dalloc(e, &d.cdet, words, 0)) || (rc = dalloc(e, &d.csurv, words, 0)) ||
+          (rc = dalloc(e, &d.clst, words, 0)) || (rc = dalloc(e, &d.ccnt, 2 * e->ld + 2, 0)))
+        break;
+    }
     if ((rc = dalloc(e, &d.inbox_beg, e->n, 0)) ||
         (rc = dalloc(e, &d.inbox_cnt, slots, 0)) || (rc = dalloc(e, &d.inbox_fill, e->n, 0)) ||
         (rc = dalloc(e, &d.inbox, inbox, 0)) || (rc = dalloc(e, &d.targets, 3 * (int64_t)e->n, 0xFF)) ||
@@ -1658,7 +1673,11 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       launch_list_round(e->d, e->cur, e->dcur, p, e->lcur, e->stream);
       e->lcur ^= 1;
     }
+    // the reference's REMOVE recipients of D_r: the sweep's column bitmaps
+    // (needs D_{r-1}, before k_finish replaces it), then per member of D_r
+    if (e->d.rlist) launch_rm_cols(e->d, e->cur, e->dcur, p, e->stream);
     launch_finish(e->d, e->dcur, p, e->stream);
+    if (e->d.rlist) launch_rm_recv(e->d, e->dcur ^ 1, p, e->stream);
     HIPCHK(e, hipGetLastError());
     e->cur ^= 1;
     e->dcur ^= 1;

@@ -39,7 +39,7 @@ constexpr int kMaxSenders = 128;  // distinct senders of one receiver per batch 
 // detector does not message itself, slave/slave.go:344-346)
 __device__ __forceinline__ bool removed_at(const GhDev& d, int dcur, int64_t c, int64_t j) {
   if (!((d.dbits[c >> 5] >> (c & 31)) & 1u)) return false;
-  return !(d.det_cnt[dcur][c] == 1 && d.det_min[dcur][c] == j);
+  return gh_rm_at(d, dcur, c, j);
 }
 
 __device__ __forceinline__ bool bit(const uint32_t* b, int64_t c) { return (b[c >> 5] >> (c & 31)) & 1u; }

@@ -36,9 +36,9 @@ __device__ __forceinline__ bool dbit(const uint32_t* bits, int64_t c) {
   return (bits[c >> 5] >> (c & 31)) & 1u;
 }
 
-// Step 1 applies REMOVE(c) at row j unless j is c's only detector
-// (slave/slave.go:344-346: a detector does not message itself).
-__device__ __forceinline__ bool removes_at(int dc, int dm, int j) { return !(dc == 1 && dm == j); }
+// Step 1 applies REMOVE(c) at row j when gh_rm_at(d, dcur, c, j)
+// (gh_internal.h: every row but a sole detector, or the reference's
+// recipients under GH_REMOVE_LIST).
 
 // Decides row i from its global count c = cntg[i] and the global |D| = ndg;
 // an undecided row (|D| could push it under the threshold) gets its exact
@@ -61,13 +61,11 @@ __device__ __forceinline__ void active_row(const GhDev& d, int cur, int dcur, co
     u = 1;  // row layout: the owner counts it, this shard adds 0
   } else {
     u = 1;
-    const int32_t* dc = d.det_cnt[dcur];
-    const int32_t* dm = d.det_min[dcur];
     int rem = 0;
     const int nd = d.nd[dcur];
     for (int q = 0; q < nd; ++q) {
       const int col = d.dlist[(int64_t)dcur * p.ld + q];
-      rem += (gh_get(d, cur, i, col, p.r).x >= 0) && removes_at(dc[col], dm[col], i);
+      rem += (gh_get(d, cur, i, col, p.r).x >= 0) && gh_rm_at(d, dcur, col, i);
     }
     post = d.cntl[i] - rem;
   }
@@ -109,8 +107,6 @@ __global__ __launch_bounds__(256) void k_active_pre(GhDev d, int cur, int dcur, 
 __global__ __launch_bounds__(256) void k_active_exact(GhDev d, int cur, int dcur, GhRound p, int fin) {
   if (d.nd[dcur] <= GH_DLIST_MAX) return;
   const int lane = threadIdx.x & 63;
-  const int32_t* dc = d.det_cnt[dcur];
-  const int32_t* dm = d.det_min[dcur];
   for (int i = blockIdx.x * 4 + (threadIdx.x >> 6); i < p.n; i += gridDim.x * 4) {
     if (d.und[i] != 2) continue;
     if (!gh_owned(d, i)) {  // row layout: the owner counts it, this shard adds 0
@@ -123,7 +119,7 @@ __global__ __launch_bounds__(256) void k_active_exact(GhDev d, int cur, int dcur
       const uint32_t b8 = (d.dbits[c >> 5] >> (c & 31)) & 0xFFu;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        cnt += ((pf >> j) & 1u) && !(((b8 >> j) & 1u) && removes_at(dc[c + j], dm[c + j], i));
+        cnt += ((pf >> j) & 1u) && !(((b8 >> j) & 1u) && gh_rm_at(d, dcur, c + j, i));
     }
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
     if (lane == 0) {
@@ -175,7 +171,7 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
       // i must be in s's snapshot list: present, not detected by s this
       // round and not REMOVE'd at s in step 1.
       ok = v.x >= 0 && !v.f;
-      if (ok && dbit(d.dbits, t) && removes_at(d.det_cnt[dcur][t], d.det_min[dcur][t], s)) ok = false;
+      if (ok && dbit(d.dbits, t) && gh_rm_at(d, dcur, t, s)) ok = false;
     }
   }
   const unsigned long long m = __ballot(ok);
@@ -192,8 +188,6 @@ __global__ __launch_bounds__(256) void k_peers_rows(GhDev d, int cur, int dcur, 
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n) return;
   const bool ib = dbit(d.dbits, i);
-  const int dci = ib ? d.det_cnt[dcur][i] : 0;
-  const int dmi = ib ? d.det_min[dcur][i] : 0;
   for (int q = 0; q < p.k; ++q) {
     int v = 0;
     if (d.alive[i] && p.n >= 2) {
@@ -202,7 +196,7 @@ __global__ __launch_bounds__(256) void k_peers_rows(GhDev d, int cur, int dcur, 
       const int s = (int)w + ((int64_t)w >= i);
       if (gh_owned(d, s) && d.alive[s] && d.active[s]) {
         const GhCell c = gh_get(d, cur, s, i, p.r);
-        v = c.x >= 0 && !c.f && !(ib && removes_at(dci, dmi, s));
+        v = c.x >= 0 && !c.f && !(ib && gh_rm_at(d, dcur, i, s));
       }
     }
     d.pvf[i * p.k + q] = v;
@@ -266,7 +260,7 @@ __device__ __forceinline__ uint32_t removed8(const GhDev& d, int dcur, int64_t l
   uint32_t m = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
   uint32_t out = 0;
   for (int j = 0; j < 8; ++j)
-    if (((m >> j) & 1u) && removes_at(d.det_cnt[dcur][l0 + j], d.det_min[dcur][l0 + j], i)) out |= 1u << j;
+    if (((m >> j) & 1u) && gh_rm_at(d, dcur, l0 + j, i)) out |= 1u << j;
   return out;
 }
 
@@ -366,7 +360,7 @@ __device__ __forceinline__ int64_t ring_find(const GhDev& d, int cur, int dcur, 
     const int64_t c = t * d.tw + j;
     const GhCell v = gh_get(d, cur, s, c, 0);
     if (v.x < 0 || v.f) continue;
-    if (dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], s)) continue;
+    if (dbit(d.dbits, c) && gh_rm_at(d, dcur, c, s)) continue;
     if (want-- == 0) return c;
   }
   return -1;
@@ -393,13 +387,13 @@ __global__ __launch_bounds__(256) void k_ring_count(GhDev d, int cur, int dcur, 
     if (t == own_t) {
       const GhCell v = gh_get(d, cur, sdr, ls, 0);
       const bool in = v.x >= 0 && !v.f &&
-                      !(dbit(d.dbits, ls) && removes_at(d.det_cnt[dcur][ls], d.det_min[dcur][ls], sdr));
+                      !(dbit(d.dbits, ls) && gh_rm_at(d, dcur, ls, sdr));
       if (in) {
         pos = total;
         for (int64_t c = t * d.tw; c < ls; ++c) {
           const GhCell x = gh_get(d, cur, sdr, c, 0);
           pos += x.x >= 0 && !x.f &&
-                 !(dbit(d.dbits, c) && removes_at(d.det_cnt[dcur][c], d.det_min[dcur][c], sdr));
+                 !(dbit(d.dbits, c) && gh_rm_at(d, dcur, c, sdr));
         }
       }
     }
@@ -569,7 +563,7 @@ __device__ __forceinline__ void base_col(const GhDev& d, int cur, int dcur, cons
     // the per-cell one
     const int64_t jobs = d.njobs ? (int64_t)d.njobs[0] : 0;
     *d.mode = p.force_storm || measure * 32 > d.ntiles * (int64_t)d.n ||
-              jobs * 4 * GH_NIB_CPL > (int64_t)d.nrows * p.ld;
+              jobs * 4 * GH_JOB_CPL > (int64_t)d.nrows * p.ld;
     if (d.njobs) {
       d.njobs[0] = 0;
       d.njobs[1] = 0;
@@ -844,7 +838,8 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   constexpr int KB = 4;
   constexpr int RS = GH_NIB_RS > 0 ? GH_NIB_RS : (CPL <= 16 ? 2 : 1);  // row steps per iteration
   static_assert(SEG >= 2 && SEG <= 64 && RB % (RSTEP * RS) == 0, "nibble path: whole row steps");
-  static_assert(W <= 2, "nibble path: a lane job carries at most two minimum plane words");
+  static_assert(W == 2 || W == 4, "nibble path: 16 or 32 cells per lane (one or two lane jobs of 16 cells)");
+  constexpr int H = W / 2;  // lane jobs of GH_JOB_CPL cells per job lane
   __shared__ unsigned long long s_merged, s_rel;
   __shared__ int s_quiet, s_nslow, s_slowbase, s_bmove, s_hasjob;
   __shared__ unsigned long long s_d8bad;  // bit l: lane l's columns hold a base move outside 0..15
@@ -1016,16 +1011,21 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       bool jslow = false;
       if (jm) {
         const int nj = __popcll(jm);
-        if (wjobs + nj <= GH_JOB_CAP) {
+        if (wjobs + H * nj <= GH_JOB_CAP) {
           if (jb) {
-            const int pos = wjobs + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(jm >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)jm, 0u));
-            // the job: row, tile and lane, the minimum plane words; then the
-            // lane's own lag and age words (the job kernel needs not re-read them)
-            jreg[2 * pos] = uint4{(uint32_t)i, ((uint32_t)tile << 8) | (uint32_t)lc, LW[0], W > 1 ? LW[W - 1] : 0u};
-            jreg[2 * pos + 1] = uint4{qwu[u].v[0], W > 1 ? qwu[u].v[W - 1] : 0u, awu[u].v[0], W > 1 ? awu[u].v[W - 1] : 0u};
+            const int pos = wjobs + H * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(jm >> 32),
+                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)jm, 0u));
+            // per 16 cells a job: row, tile and 16-cell lane, the minimum
+            // plane words; then the lane's own lag and age words (the job
+            // kernel needs not re-read them)
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+              jreg[2 * (pos + h)] = uint4{(uint32_t)i, ((uint32_t)tile << 8) | (uint32_t)(lc * H + h), LW[2 * h],
+                                          LW[2 * h + 1]};
+              jreg[2 * (pos + h) + 1] = uint4{qwu[u].v[2 * h], qwu[u].v[2 * h + 1], awu[u].v[2 * h], awu[u].v[2 * h + 1]};
+            }
           }
-          wjobs += nj;
+          wjobs += H * nj;
         } else {
           jslow = (jm & gmask) != 0;  // the wave's region is full: segments with jobs go slow, whole
         }
@@ -1239,7 +1239,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     for (int h = 0; h < 2; ++h) {
       const int64_t c = (int64_t)tile * TW + 2 * pp + h;
       if (dbit(d.dbits, c)) {
-        if (d.det_cnt[dcur][c] == 1)
+        if (d.det_cnt[dcur][c] == 1 || d.rlist)  // a recipient set the packed path does not hold
           rm1 = 1;
         else
           rmm |= 0xFFFFu << (16 * h);
@@ -1800,7 +1800,7 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
           // sender snapshot: present and not detected by s, +1 on s's
           // diagonal (its heartbeat of this round), not REMOVE'd at s
           int64_t val = (X[j].x < 0 || X[j].f) ? -1 : (int64_t)X[j].x + ((c0 + j) == s);
-          if (((my8 >> j) & 1u) && removes_at(d.det_cnt[dcur][l0 + j], d.det_min[dcur][l0 + j], s)) val = -1;
+          if (((my8 >> j) & 1u) && gh_rm_at(d, dcur, l0 + j, s)) val = -1;
           m[j] = max(m[j], val);
         }
       }
@@ -1811,7 +1811,7 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
         int64_t x = v.x;
         bool now = false;  // ts := r in this round
         // step 1: REMOVE delivery (slave/slave.go:236-240, 276-286)
-        if (((my8 >> j) & 1u) && removes_at(d.det_cnt[dcur][l0 + j], d.det_min[dcur][l0 + j], i)) {
+        if (((my8 >> j) & 1u) && gh_rm_at(d, dcur, l0 + j, i)) {
           if (x >= 0) {
             x = GH_TOMBSTONE;
             n_tomb++;
@@ -1911,8 +1911,6 @@ __device__ __forceinline__ void job_rule(const GhDev& d, int cur, int dcur, cons
   const int32_t r = p.r;
   const int64_t c0 = d.col0 + l0;
   const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
-  const int32_t* dc = d.det_cnt[dcur];
-  const int32_t* dm = d.det_min[dcur];
   detm = 0;
   // merge candidates: from the plane codes, then (a rolled loop: the code
   // stays small) the cells that gather their senders' exact cells
@@ -1936,7 +1934,7 @@ __device__ __forceinline__ void job_rule(const GhDev& d, int cur, int dcur, cons
 #pragma unroll 1
       for (int q = 0; q < cnt; ++q) {
         const int s = d.inbox[beg + q];
-        if (rmj && removes_at(dc[l0 + j], dm[l0 + j], s)) continue;  // s REMOVEs it before sending
+        if (rmj && gh_rm_at(d, dcur, l0 + j, s)) continue;  // s REMOVEs it before sending
         const GhCell X = gh_get(d, cur, s, l0 + j, r);
         if (X.x >= 0 && !X.f) m = max(m, (int64_t)X.x + ((c0 + j) == s));
       }
@@ -1953,7 +1951,7 @@ __device__ __forceinline__ void job_rule(const GhDev& d, int cur, int dcur, cons
     const GhCell v = A[j];
     int64_t x = v.x;
     bool now = false;  // ts := r in this round
-    if (rmj && removes_at(dc[l0 + j], dm[l0 + j], i)) {  // step 1: REMOVE delivery (:236-240, 276-286)
+    if (rmj && gh_rm_at(d, dcur, l0 + j, i)) {  // step 1: REMOVE delivery (:236-240, 276-286)
       if (x >= 0) {
         x = GH_TOMBSTONE;
         a.tomb++;
@@ -2024,8 +2022,6 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
   const uint32_t h0 = xw[0] & 0xFFFFu;
   if (h0 == GH_N_WIDE || h0 == GH_N_FROZEN) return false;  // a wide input: k_round_redo
   const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
-  const int32_t* dc = d.det_cnt[dcur];
-  const int32_t* dm = d.det_min[dcur];
   // merge candidates: from the plane codes, then (a rolled loop) the cells
   // that gather their senders' exact cells
   int32_t mm[8];
@@ -2050,7 +2046,7 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
 #pragma unroll 1
       for (int q = 0; q < cnt; ++q) {
         const int s = d.inbox[beg + q];
-        if (rmj && removes_at(dc[l0 + j], dm[l0 + j], s)) continue;  // s REMOVEs it before sending
+        if (rmj && gh_rm_at(d, dcur, l0 + j, s)) continue;  // s REMOVEs it before sending
         // the sender's cell from its narrow code (a tier nibble or an escaped
         // code); a wide or stopped sender segment: k_round_redo
         const int64_t sc = gh_cell(d, s, l0 + j);
@@ -2090,7 +2086,7 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
     const bool vf = vx >= 0 && (h >> 15) != 0;
     int32_t x = vx;
     bool now = false;  // ts := r in this round
-    if (((my8 >> j) & 1u) && removes_at(dc[l0 + j], dm[l0 + j], i)) {  // step 1 REMOVE (:236-240, 276-286)
+    if (((my8 >> j) & 1u) && gh_rm_at(d, dcur, l0 + j, i)) {  // step 1 REMOVE (:236-240, 276-286)
       if (x >= 0) {
         x = GH_TOMBSTONE;
         acc.tomb++;
@@ -2688,8 +2684,8 @@ template <int TW>
 static void round_jobs(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
   if constexpr (TW >= 64) {
     const unsigned g = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, d.jobw));
-    hipLaunchKernelGGL((k_round_jobs<TW, GH_NIB_CPL>), dim3(g), dim3(256), 0, s, d, cur, dcur, p);
-    hipLaunchKernelGGL((k_round_redo<TW, GH_NIB_CPL>), dim3(1), dim3(64), 0, s, d, cur, dcur, p);
+    hipLaunchKernelGGL((k_round_jobs<TW, GH_JOB_CPL>), dim3(g), dim3(256), 0, s, d, cur, dcur, p);
+    hipLaunchKernelGGL((k_round_redo<TW, GH_JOB_CPL>), dim3(1), dim3(64), 0, s, d, cur, dcur, p);
   }
 }
 void launch_round_jobs(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {

@@ -27,7 +27,7 @@ import numpy as np
 
 from . import _abi, codec
 from ._abi import (GH_COMM_LOCAL, GH_COMM_RCCL, GH_DETECT_CANONICAL, GH_DETECT_QUIRK,  # noqa: F401
-                   GH_LAYOUT_COLUMNS, GH_LAYOUT_ROWS, GH_ORDER_APPEND, GH_ORDER_ID,
+                   GH_LAYOUT_COLUMNS, GH_LAYOUT_ROWS, GH_ORDER_APPEND, GH_ORDER_ID, GH_REMOVE_ALL, GH_REMOVE_LIST,
                    GH_EPLACEMENT_STARVED, GH_EV_CRASH, GH_EV_JOIN, GH_EV_LEAVE, GH_OK, GH_PEER_PULL,
                    GH_PEER_RING, Config, PlanEntry)
 

@@ -31,6 +31,7 @@ GH_COMM_RCCL, GH_COMM_LOCAL = 0, 1
 GH_COMM_ID_BYTES = 128
 GH_LAYOUT_COLUMNS, GH_LAYOUT_ROWS = 0, 1
 GH_ORDER_ID, GH_ORDER_APPEND = 0, 1
+GH_REMOVE_ALL, GH_REMOVE_LIST = 0, 1
 
 
 class Config(C.Structure):
@@ -40,7 +41,8 @@ class Config(C.Structure):
         ("min_members", C.c_int32), ("replicas", C.c_int32), ("introducer", C.c_int32),
         ("master", C.c_int32), ("device", C.c_int32), ("tile_width", C.c_int32),
         ("seed", C.c_uint64), ("max_files", C.c_int64), ("wide_segments", C.c_int64),
-        ("shard_layout", C.c_int32), ("list_order", C.c_int32), ("reserved", C.c_int32 * 4),
+        ("shard_layout", C.c_int32), ("list_order", C.c_int32), ("remove_mode", C.c_int32),
+        ("reserved", C.c_int32 * 3),
     ]
 
 

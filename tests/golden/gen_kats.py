@@ -249,6 +249,56 @@ kats.append(dict(
     expect_failed=[], expect_detectors=[],
     expect_stats=dict(remove_unknown=1, tombstoned=2, detections=1, failed_members=1)))
 
+# KAT-14L: KAT-14 with the reference's REMOVE recipients (GH_REMOVE_LIST,
+# slave/slave.go:344, 472-473). Row 1's list is [1, 3, 5, 6, 7]; Remove(3)
+# runs right after removeMember(3), so it messages 5, 6 and 7 (not itself,
+# :344-346) - all crashed. Rows 0 and 2 are outside row 1's list: they keep
+# member 3 (hb 6, ts 19: fresh, nobody gossips a higher count), row 4 gets no
+# REMOVE of a member it never knew.
+hb, ts, alive = blank(8)
+for i in (0, 1, 2, 4):
+    alive[i] = 1
+    for c in (i, 5, 6, 7):
+        hb[i][c] = 5
+        ts[i][c] = 19
+hb[0][3], ts[0][3] = 6, 19
+hb[1][3], ts[1][3] = 6, 10
+hb[2][3], ts[2][3] = 6, 19
+kats.append(dict(
+    name="kat14L_remove_outside_list", n=8, round=19, detect_mode=0, peer_mode=0, fanout=3, seed=1, t_fail=5,
+    t_cleanup=5, remove_mode=1, hb=hb, ts=ts, alive=alive, events=[], rounds=2, expect_row=1,
+    expect_hb=[A, 7, A, A, A, 5, 5, 5], expect_ts=[0, 21, 0, 0, 0, 19, 19, 19],
+    expect_more=[dict(row=2, hb=[A, A, 7, 6, A, 5, 5, 5], ts=[0, 0, 21, 19, 0, 19, 19, 19]),
+                 dict(row=0, hb=[7, A, A, 6, A, 5, 5, 5], ts=[21, 0, 0, 19, 0, 19, 19, 19])],
+    expect_failed=[], expect_detectors=[],
+    expect_stats=dict(remove_unknown=0, tombstoned=0, detections=1, failed_members=1)))
+
+# KAT-15 a false positive's victim (slave/slave.go:338-363 with :443-448).
+# Five alive members know each other (hb 5, ts 19); only row 1 holds member 2
+# stale (ts 10). Round 20: row 1 alone detects 2 (and releases it at once);
+# member 2 is alive and counts to 6. Round 21, the REMOVE(2) delivery:
+#  * reference recipients (remove_mode 1): Remove(2) runs after
+#    removeMember(2), so row 1 messages 0, 3 and 4 only. They tombstone 2;
+#    the victim never hears of it and counts on: its own cell is 7 at 21.
+#  * SPEC D4 (remove_mode 0): every alive row but the sole detector, the
+#    victim included: row 2 tombstones itself (ts 20 kept) and stops counting.
+# Rows 0, 3 and 4 hold member 2 as a tombstone either way (its ts depends on
+# the round-20 merges, not checked).
+hb, ts, alive = blank(5)
+for i in range(5):
+    alive[i] = 1
+    for c in range(5):
+        hb[i][c], ts[i][c] = 5, 19
+ts[1][2] = 10
+for mode, own, own_ts, tomb in ((1, 7, 21, 3), (0, T, 20, 4)):
+    kats.append(dict(
+        name=f"kat15_victim_{'list' if mode else 'all'}", n=5, round=19, detect_mode=0, peer_mode=0, fanout=3,
+        seed=5, t_fail=5, t_cleanup=5, remove_mode=mode, hb=hb, ts=ts, alive=alive, events=[], rounds=2,
+        expect_row=2, expect_hb=[None, None, own, None, None], expect_ts=[None, None, own_ts, None, None],
+        expect_tomb=[[0, 2], [3, 2], [4, 2]],
+        expect_failed=[], expect_detectors=[],
+        expect_stats=dict(tombstoned=tomb, detections=1, failed_members=1, remove_unknown=0)))
+
 
 def row_matches(name, hb, ts, i, exp_hb, exp_ts):
     """hb of row i equals exp_hb (None = any), ts where present"""
@@ -265,7 +315,7 @@ def check_with_listsim(k):
     L.T_FAIL, L.T_CLEANUP = k["t_fail"], k["t_cleanup"]
     sim = ListSim.from_dense(k["hb"], k["ts"], k["alive"], k["round"], seed=k["seed"],
                              peer_mode="ring" if k["peer_mode"] else "pull", fanout=k["fanout"],
-                             quirk=bool(k["detect_mode"]))
+                             quirk=bool(k["detect_mode"]), remove="list" if k.get("remove_mode") else "all")
     if k["events"]:
         sim.apply_events([tuple(e) for e in k["events"]])
     st = sim.step(k.get("rounds", 1))
@@ -274,6 +324,8 @@ def check_with_listsim(k):
         row_matches(k["name"], hb, ts, k["expect_row"], k["expect_hb"], k["expect_ts"])
     for m in k.get("expect_more", []):
         row_matches(k["name"], hb, ts, m["row"], m["hb"], m["ts"])
+    for i, c in k.get("expect_tomb", []):
+        assert hb[i][c] == T, (k["name"], i, c, list(hb[i]))
     for key, v in k["expect_stats"].items():
         assert st[key] == v, (k["name"], key, st[key], v)
     if k.get("rounds", 1) == 1:

@@ -11,7 +11,7 @@ KATS = json.loads((pathlib.Path(__file__).parent / "golden" / "kats.json").read_
 def kat_config(mod, k):
     return mod.default_config(k["n"], peer_mode=k["peer_mode"], fanout=k["fanout"],
                               detect_mode=k["detect_mode"], seed=k["seed"], t_fail=k["t_fail"],
-                              t_cleanup=k["t_cleanup"])
+                              t_cleanup=k["t_cleanup"], remove_mode=k.get("remove_mode", 0))
 
 
 def check_row(k, hb, ts, i, exp_hb, exp_ts):
@@ -35,6 +35,8 @@ def run_kat(engine, k):
         check_row(k, hb, ts, k["expect_row"], k["expect_hb"], k["expect_ts"])
     for m in k.get("expect_more", []):
         check_row(k, hb, ts, m["row"], m["hb"], m["ts"])
+    for i, c in k.get("expect_tomb", []):
+        assert hb[i][c] == -2, (k["name"], i, c, list(hb[i]))
     for key, v in k["expect_stats"].items():
         assert st[key] == v, (k["name"], key, st[key], v)
     if k.get("rounds", 1) == 1:

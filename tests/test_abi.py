@@ -46,11 +46,29 @@ def test_struct_layouts(abi):
 
 def test_abi_version_and_defaults(abi):
     lib = abi.load()
-    assert lib.gh_abi_version() == 6
+    assert lib.gh_abi_version() == 7
     cfg = abi.Config()
     lib.gh_config_default(C.byref(cfg))
     # reference constants: PERIOD/COOLDOWN 5 s at 1 s rounds, 4 replicas, literal 4
     assert (cfg.t_fail, cfg.t_cleanup, cfg.min_members, cfg.replicas) == (5, 5, 4, 4)
+    assert cfg.remove_mode == abi.GH_REMOVE_ALL
+
+
+def test_remove_list_validation(abi):
+    """GH_REMOVE_LIST is a one-engine, ID-order mode: gh_create and
+    gh_footprint refuse it sharded, in append order, or an unknown mode,
+    before looking for a device; a valid one plans its recipient bitmaps."""
+    from gossipsim import default_config, footprint, GossipError, GH_ORDER_APPEND
+    lib = abi.load()
+    h = C.c_void_p()
+    for kw in (dict(remove_mode=2), dict(remove_mode=1, list_order=GH_ORDER_APPEND)):
+        cfg = default_config(64, **kw)
+        assert lib.gh_create(C.byref(cfg), C.byref(h)) == abi.GH_EINVAL
+    with pytest.raises(GossipError):
+        footprint(default_config(64, remove_mode=1), rank=0, world=2)
+    base = footprint(default_config(4096))["create_bytes"]
+    lit = footprint(default_config(4096, remove_mode=1))["create_bytes"]
+    assert lit - base >= 5 * 4096 * 4096 // 8  # two recipient sets + three column bitmaps of N x N bits
 
 
 def test_no_cpu_fallback(abi):

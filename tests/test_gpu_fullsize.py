@@ -60,8 +60,8 @@ def compare_blocks(eng, orc, r):
     print(f"  r={r}: full tables equal ({time.perf_counter() - t0:.1f} s)", flush=True)
 
 
-def run(gs, om, t_fail, rounds, full_at, expect, sched=None, per_round=None):
-    cfg = dict(fanout=4, seed=0x5EED0003, t_fail=t_fail, t_cleanup=t_fail)
+def run(gs, om, t_fail, rounds, full_at, expect, sched=None, per_round=None, remove_mode=0):
+    cfg = dict(fanout=4, seed=0x5EED0003, t_fail=t_fail, t_cleanup=t_fail, remove_mode=remove_mode)
     eng = gs.Engine(gs.default_config(N, **cfg))
     orc = om.Oracle(om.default_config(N, **cfg), threads=THREADS)
     try:
@@ -139,6 +139,22 @@ def test_c3_fullsize_crash_1pct(gs, oracle_mod):
         assert s["detections"] > 0 and s["first_detection"] is not None, s
 
     run(gs, oracle_mod, 16, 32, {12, 32}, expect, sched=sched)
+
+
+def test_c3_fullsize_crash_1pct_remove_list(gs, oracle_mod):
+    """The 1% crash with the reference's REMOVE recipients (GH_REMOVE_LIST:
+    each detector's list right after removeMember, slave/slave.go:344,
+    472-473): the recipient sets of all 655 crashed members are decided at
+    full size (remove.hip) and the REMOVE wave matches tablesim's literal
+    per-detector restatement."""
+    from scenarios import crash_ids
+    crashed = crash_ids(N, 0.01, 0x5EED0003)
+    sched = {8: [(gs.GH_EV_CRASH, int(c)) for c in crashed]}
+
+    def expect(s):
+        assert s["detections"] > 0 and s["first_detection"] is not None, s
+
+    run(gs, oracle_mod, 16, 28, {28}, expect, sched=sched, remove_mode=1)
 
 
 def test_c3_fullsize_reference_timeouts(gs, oracle_mod):

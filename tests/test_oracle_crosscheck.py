@@ -10,18 +10,19 @@ import scenarios as sc
 
 
 def run_pair(om, n, rounds, sched, peer_mode, fanout=3, quirk=False, seed=0x5EED0001,
-             init_full=False, t_fail=5, t_cleanup=5):
+             init_full=False, t_fail=5, t_cleanup=5, remove="all"):
     cfg = om.default_config(n, peer_mode=om.GH_PEER_RING if peer_mode == "ring" else om.GH_PEER_PULL,
                             fanout=fanout, detect_mode=int(quirk), seed=seed, t_fail=t_fail,
-                            t_cleanup=t_cleanup)
+                            t_cleanup=t_cleanup,
+                            remove_mode=om.GH_REMOVE_LIST if remove == "list" else om.GH_REMOVE_ALL)
     orc = om.Oracle(cfg)
     if init_full:
         hb, ts, alive = sc.full_state(n)
         orc.import_state(hb, ts, alive, 0)
         ls = ListSim.from_dense(hb, ts, alive, 0, seed=seed, peer_mode=peer_mode, fanout=fanout,
-                                quirk=quirk)
+                                quirk=quirk, remove=remove)
     else:
-        ls = ListSim(n, seed=seed, peer_mode=peer_mode, fanout=fanout, quirk=quirk)
+        ls = ListSim(n, seed=seed, peer_mode=peer_mode, fanout=fanout, quirk=quirk, remove=remove)
     import oracle.listsim as L
     L.T_FAIL, L.T_CLEANUP = t_fail, t_cleanup
     try:
@@ -79,3 +80,35 @@ def test_fast_fail_short_cooldown(oracle_mod):
     n = 12
     sched = sc.random_churn(n, 40, 9, p_crash=0.1)
     run_pair(oracle_mod, n, 40, sched, "pull", fanout=3, init_full=True, t_fail=3, t_cleanup=6)
+
+
+# ---- the reference's REMOVE recipients (GH_REMOVE_LIST, slave/slave.go:344) ----
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+@pytest.mark.parametrize("peer_mode", ["ring", "pull"])
+@pytest.mark.parametrize("quirk", [False, True])
+def test_random_churn_remove_list(oracle_mod, seed, peer_mode, quirk):
+    """listsim's literal Remove (recipients = the detector's list right after
+    removeMember in the sweep) against tablesim's column-wise form."""
+    n = 16
+    sched = sc.random_churn(n, 50, seed, p_crash=0.06)
+    run_pair(oracle_mod, n, 50, sched, peer_mode, fanout=2, init_full=True, quirk=quirk,
+             seed=0x3000 + seed, remove="list")
+
+
+@pytest.mark.parametrize("quirk", [False, True])
+def test_collapse_remove_list(oracle_mod, quirk):
+    """The reference's constants at a size where dissemination outruns them
+    not: the round-6 detection storm and the collapse, literal recipients."""
+    n = 48
+    run_pair(oracle_mod, n, 14, {}, "pull", fanout=3, init_full=True, quirk=quirk, seed=0x5EED0002,
+             remove="list")
+
+
+@pytest.mark.parametrize("seed", [7, 8])
+def test_bootstrap_churn_remove_list(oracle_mod, seed):
+    n = 12
+    sched = sc.bootstrap_schedule(n)
+    for r, ev in sc.random_churn(n, 50, seed, p_crash=0.05).items():
+        sched.setdefault(r + n, []).extend(ev)
+    run_pair(oracle_mod, n, 60, sched, "ring", init_full=False, seed=0x4000 + seed, remove="list")

@@ -3,7 +3,7 @@
 # bench per library, AB_PASSES passes in alternating order.
 #   tools/r04/ab.sh name... (default = the in-tree build)
 set -o pipefail
-mkdir -p gpurun_out/ab
+mkdir -p gpurun_out/ab gpurun_out/r04
 for pass in ${AB_PASSES:-1 2}; do
   for v in "$@"; do
     if [ "$v" = default ]; then lib=p2p-file-system-with-gossip-detect-failure-management_amd/lib/libgossiphip.so

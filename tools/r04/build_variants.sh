@@ -7,7 +7,7 @@ set -e
 cd "$(dirname "$0")/../../p2p-file-system-with-gossip-detect-failure-management_amd"
 mkdir -p lib/variants build/variants
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result"
-OBJS="build/events.o build/place.o build/elect.o build/comm.o build/rows.o build/order.o build/gossiphip.o"
+OBJS="build/remove.o build/events.o build/place.o build/elect.o build/comm.o build/rows.o build/order.o build/gossiphip.o"
 for spec in "$@"; do
   name=${spec%%=*}; defs=${spec#*=}
   ( /opt/rocm/bin/hipcc $FLAGS $defs -c -o build/variants/round_$name.o csrc/round.hip &&

@@ -1,7 +1,7 @@
 """Per-dispatch means of PMC counters over the nibble-path launches (the
 k_round variant IN = 2 that did work) in rocprofv3 csv directories.
 usage: pmc_parse.py <dir-glob>..."""
-import csv, glob, sys, collections, json
+import csv, glob, sys, collections, json, re
 
 out = {}
 for pat in sys.argv[1:]:
@@ -11,7 +11,7 @@ for pat in sys.argv[1:]:
         for f in files:
             for row in csv.DictReader(open(f)):
                 k = row.get("Kernel_Name", "")
-                if "k_round<" not in k or not k.rstrip(")").split("(")[0].endswith("false, 2>"):
+                if not re.search(r"k_round<\d+, \d+, \d+, \w+, false, 2>", k):
                     continue
                 per[row["Dispatch_Id"]][row["Counter_Name"]] += float(row["Counter_Value"])
         # drop idle dispatches (the nibble path's early-return launches)
