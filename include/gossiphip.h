@@ -155,9 +155,9 @@ int gh_abi_version(void);
  * >= -2 (GH_ABSENT, GH_TOMBSTONE, heartbeats up to INT32_MAX; below -2 is
  * GH_ERANGE); ts: any int32. Pending REMOVEs are cleared on import. Export:
  * the ts of an absent cell is 0 (the reference keeps no entry for it), and
- * with T_cleanup < 30 a tombstone older than 30 rounds exports ts =
- * round + 1 - 30 (its age is only ever compared with COOLDOWN,
- * slave/slave.go:490; SPEC.md §1). */
+ * with T_cleanup < 30 a tombstone older than T_cleanup + 1 rounds exports
+ * ts = round + 1 - (T_cleanup + 1) (its age is only ever compared with
+ * COOLDOWN, slave/slave.go:490; SPEC.md §1). */
 int gh_import_state(void* h, const int32_t* hb, const int32_t* ts,
                     const uint8_t* alive, int64_t row0, int64_t n_rows,
                     int32_t round);

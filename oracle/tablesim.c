@@ -191,14 +191,15 @@ int or_import_state(void *h, const int32_t *hb, const int32_t *ts, const uint8_t
 }
 
 /* Exported ts (SPEC.md §1): 0 for an absent member (the reference keeps no
- * entry for it); with COOLDOWN < 30 rounds, a tombstone older than 30 rounds
- * as exactly 30 rounds old -- its UpdateTime is only ever compared with
- * now - COOLDOWN (cleanFailList, slave/slave.go:490), so every older value
- * decides the same. */
+ * entry for it); with COOLDOWN < 30 rounds, a tombstone older than
+ * COOLDOWN + 1 rounds as exactly COOLDOWN + 1 rounds old -- its UpdateTime is
+ * only ever compared with now - COOLDOWN (cleanFailList,
+ * slave/slave.go:490), so every older value decides the same. */
 static int32_t export_ts(const ors *s, int32_t hb, int32_t ts) {
   if (hb == GH_ABSENT) return 0;
   int32_t now = s->round + 1;
-  if (hb == GH_TOMBSTONE && s->cfg.t_cleanup < 30 && (int64_t)now - ts > 30) return now - 30;
+  const int32_t tsa = s->cfg.t_cleanup + 1;
+  if (hb == GH_TOMBSTONE && s->cfg.t_cleanup < 30 && (int64_t)now - ts > tsa) return now - tsa;
   return ts;
 }
 

@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void k_unpack(GhDev d, int cur, int32_t* dst, 
     gh_get8(d, cur, i, c, p.r, v);
     int32_t* o = dst + (i - row0) * d.ncs + c;
     const int lim = (int)min<int64_t>(8, d.ncs - c);
-    for (int j = 0; j < lim; ++j) o[j] = what == 0 ? v[j].x : gh_export_ts(v[j], p.r, d.tsat != 0);
+    for (int j = 0; j < lim; ++j) o[j] = what == 0 ? v[j].x : gh_export_ts(v[j], p.r, d.tsa);
   }
 }
 

@@ -38,8 +38,9 @@
 //                  buffer b is "for" round r (its ages count to r):
 //                    present    H<<15 | off<<5 | age   off = x - base 0..1022,
 //                                                      age = r - ts 0..31 exact
-//                    tombstone  0xFFE0 | age           age 0..30 (tsat: 30 =
-//                                                      "30 or more")
+//                    tombstone  0xFFE0 | age           age 0..30 (tsa =
+//                                                      T_cleanup + 1: "tsa or
+//                                                      more")
 //                    absent     0xFFFF
 //                  Visible (present, unflagged) cells are the non-negative
 //                  int16 values and compare like their heartbeats, so a
@@ -113,11 +114,13 @@
 //                  lean variants write tier chunks); every other reader and
 //                  writer goes through gh_ld16 / gh_put8 / gh_st16, which
 //                  follow m8.
-//   tsat = T_cleanup < 30: a tombstone's age is only ever compared with
-//            T_cleanup (cleanFailList, slave/slave.go:490), so every age
-//            past 30 decides the same; narrow tombstones saturate at 30 and
-//            the exported ts of an older tombstone is round + 1 - 30 (SPEC
-//            §1; the oracle exports the same).
+//   tsa = T_cleanup + 1 when T_cleanup < 30: a tombstone's age is only ever
+//            compared with T_cleanup (cleanFailList, slave/slave.go:490), so
+//            every age past T_cleanup decides the same; tombstones saturate
+//            at tsa and the exported ts of an older tombstone is round + 1 -
+//            tsa (SPEC §1; the oracle exports the same). A row under the <4
+//            guard (:504-509) never cleans, so its tombstones age without
+//            bound: saturated, they stop changing and the row goes quiet.
 //   Local columns are padded to ld (multiple of 8*TW and 256); padding cells
 //   stay absent.
 //   per row (global): alive, active, und (u8), cntl / cntg (local / global
@@ -139,7 +142,7 @@
 #define GH_N_FROZEN 0x7FFEu                // every cell of a stopped row (frozen store)
 #define GH_N_OFFMAX 1022                   // largest narrow heartbeat offset
 #define GH_N_AGEMAX 31                     // largest narrow age of a present cell
-#define GH_N_TAGEMAX 30                    // largest narrow age of a tombstone (saturates when tsat)
+#define GH_N_TAGEMAX 30                    // largest narrow age of a tombstone (saturates at GhDev.tsa)
 #define GH_TSAT_T 30                       // tsat = T_cleanup < GH_TSAT_T
 #define GH_BASE_LAG 1000                   // base = own heartbeat - GH_BASE_LAG
 #define GH_P_REF (GH_BASE_LAG + 2)         // plane: an active member's own snapshot offset
@@ -290,7 +293,7 @@ struct GhDev {
   int32_t *err;     // device-side error (GH_ENOMEM: arena full; GH_ERANGE), 0 = none
   // frozen store of stopped rows: [fzcap][ld] exact x / ts; frow[i] = slot or -1
   int32_t *frow, *fzh, *fzt;
-  int32_t tsat;     // T_cleanup < GH_TSAT_T: tombstone ages saturate at 30
+  int32_t tsa;      // tombstone ages saturate here: T_cleanup + 1 when T_cleanup < GH_TSAT_T, else 0 (none; SPEC §1)
   int32_t toff;     // 4-bit tier: a tombstone of age toff + s is the tier cell (15, s), s = 1..14 (gh_tier_toff)
   int32_t *colq;    // [ld] scratch: per local column event index / merged value
   int64_t *slow;    // [ntiles * n] round: segments for k_round_slow, tile << 32 | row
@@ -579,12 +582,12 @@ __host__ __device__ __forceinline__ GhCell gh_dec16(uint32_t h, int32_t b, int32
   return GhCell{b + off, r - a, (h >> 15) != 0};
 }
 // Narrow code of cell v in a buffer for round r with column base b; fit &= it
-// has one. tsat: tombstone ages past 30 saturate (SPEC §1).
-__host__ __device__ __forceinline__ uint32_t gh_enc16(const GhCell& v, int32_t b, int32_t r, bool tsat, bool& fit) {
+// has one. tsa: tombstone ages past tsa saturate (SPEC §1; 0: none).
+__host__ __device__ __forceinline__ uint32_t gh_enc16(const GhCell& v, int32_t b, int32_t r, int32_t tsa, bool& fit) {
   if (v.x == GH_ABSENT) return GH_N_ABSENT;
   int64_t a = (int64_t)r - v.ts;
   if (v.x < 0) {
-    if (tsat && a > GH_N_TAGEMAX) a = GH_N_TAGEMAX;
+    if (tsa && a > tsa) a = tsa;
     fit &= a >= 0 && a <= GH_N_TAGEMAX;
     return GH_N_TOMB | (uint32_t)(a & 31);
   }
@@ -750,7 +753,7 @@ __device__ __forceinline__ uint4 gh_enc8(const GhDev& d, int buf, int64_t c, int
   const int32_t* bp = d.base[buf] + c;
   uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int j = 0; j < 8; ++j) w[j >> 1] |= gh_enc16(v[j], bp[j], r, d.tsat != 0, fit) << (16 * (j & 1));
+  for (int j = 0; j < 8; ++j) w[j >> 1] |= gh_enc16(v[j], bp[j], r, d.tsa, fit) << (16 * (j & 1));
   return uint4{w[0], w[1], w[2], w[3]};
 }
 // A fresh arena slot of buffer buf (one lane per segment calls it); on
@@ -765,10 +768,11 @@ __device__ __forceinline__ int64_t gh_wide_alloc(const GhDev& d, int buf) {
 }
 
 // The exported ts of a cell (SPEC §1): 0 for absent; a tombstone older than
-// 30 rounds (tsat) as 30 rounds old (r = the round the buffer is for).
-__host__ __device__ __forceinline__ int32_t gh_export_ts(const GhCell& v, int32_t r, bool tsat) {
+// tsa = T_cleanup + 1 rounds (T_cleanup < 30) as tsa rounds old (r = the
+// round the buffer is for).
+__host__ __device__ __forceinline__ int32_t gh_export_ts(const GhCell& v, int32_t r, int32_t tsa) {
   if (v.x == GH_ABSENT) return 0;
-  if (v.x == GH_TOMBSTONE && tsat && (int64_t)r - v.ts > GH_N_TAGEMAX) return r - GH_N_TAGEMAX;
+  if (v.x == GH_TOMBSTONE && tsa && (int64_t)r - v.ts > tsa) return r - tsa;
   return v.ts;
 }
 
@@ -902,6 +906,21 @@ void launch_join_reset(const GhDev& d, int cur, const int32_t* rows, int32_t nr,
 // fresh arena slots of buffer cur, the ghost rows' markers rewritten
 #define GH_GX_PLANE 1
 #define GH_GX_CODES 2
+// the slices of one exchange chunk (k_gx_idx): destination r's rows are
+// wlist[r][src[r] .. src[r] + out[r + 1] - out[r]), at out[r] in the chunk
+constexpr int GH_GX_MAXG = 16;
+struct GxSlices {
+  int32_t g;
+  int64_t total;
+  int64_t src[GH_GX_MAXG];
+  int64_t out[GH_GX_MAXG + 1];
+};
+// want lists of every shard from the replicated inboxes (rows.hip): wbits
+// [G][ceil(n/32)], wsum [G][blocks], wlist [G][n], mcnt [G][G] + [G] totals
+void launch_want_lists(const GhDev& d, const GhRound& p, int64_t nrs, int G, uint32_t* wbits, int32_t* wsum,
+                       int32_t* wlist, int32_t* mcnt, hipStream_t s);
+void launch_ghost_slots(const GhDev& d, const int32_t* mine, const int32_t* cnt, hipStream_t s);
+void launch_gx_idx(const int32_t* wlist, int64_t n, const GxSlices& sl, int32_t* rows, int32_t* dest, hipStream_t s);
 int64_t ghost_part_bytes(const GhDev& d, int part);
 int64_t ghost_wide_record_bytes(const GhDev& d);
 void launch_ghost_pack(const GhDev& d, int cur, const int32_t* rows, const int32_t* dest, int64_t ns, int part,

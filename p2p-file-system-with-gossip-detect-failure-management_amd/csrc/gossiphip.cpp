@@ -80,6 +80,13 @@ struct Engine {
   std::vector<std::vector<int32_t>> gx_send;  // rows this shard sends each rank this round
   std::vector<int64_t> gx_rcnt, gx_rbeg;      // ghosts from each owner: count, first ghost index
   int64_t gx_maxsend = 0;                     // the most rows any shard sends (the chunk count)
+  // device want lists (round_ghosts): the set-up ghosts are want[me] in
+  // wlist, this shard's send list to r is wlist[r][gx_soff[r], + gx_sn[r])
+  bool gx_dev = false;
+  uint32_t* wbits = nullptr;
+  int32_t *wsum = nullptr, *wlist = nullptr, *mcnt = nullptr;
+  std::vector<int32_t> gx_m;            // host copy of mcnt: [G][G] counts, [G] totals
+  std::vector<int64_t> gx_sn, gx_soff;  // rows this shard sends each rank, their offset in want[r]
   bool gpo = false;                           // this round's ghosts carry only their plane (GhRound.gpo)
   bool plane_valid = false;                   // the current buffer's plane was written by a round
   int32_t* gwcnt = nullptr;  // [2 * world] wide counts / cursors per destination
@@ -425,13 +432,10 @@ constexpr int64_t kGhostChunk = (int64_t)1 << 30;
 // (ascending, so grouped by owner); the rows it owns that other ranks want
 // are its send lists. The previous ghosts are dropped; nothing moves yet
 // (ghost_move).
-int ghost_setup(Engine* e, const std::vector<std::vector<int32_t>>& want) {
+// The ghost table holds at least nr rows (its rows are rewritten every round).
+int ghost_reserve(Engine* e, int64_t nr) {
   GhDev& d = e->d;
-  const int G = e->world, me = e->rank;
-  for (int32_t s : e->ghosts) e->rslot_h[s] = -1;
-  e->ghosts = want[me];
-  const int64_t nr = (int64_t)e->ghosts.size();
-  if (nr > d.gcap) {  // the ghost table grows (its rows are rewritten every round)
+  if (nr > d.gcap) {
     const int64_t cap = std::max<int64_t>(nr, d.gcap + d.gcap / 4);
     dfree(e, d.gcodes);
     dfree(e, d.gplane);
@@ -443,6 +447,18 @@ int ghost_setup(Engine* e, const std::vector<std::vector<int32_t>>& want) {
     if (e->plane && (rc = dalloc(e, &d.gplane, (size_t)cap * e->ld / 8, 0xFF))) return rc;
     d.gcap = cap;
   }
+  return GH_OK;
+}
+
+int ghost_setup(Engine* e, const std::vector<std::vector<int32_t>>& want) {
+  GhDev& d = e->d;
+  const int G = e->world, me = e->rank;
+  for (int32_t s : e->ghosts) e->rslot_h[s] = -1;
+  e->ghosts = want[me];
+  e->gx_dev = false;
+  const int64_t nr = (int64_t)e->ghosts.size();
+  int rc;
+  if ((rc = ghost_reserve(e, nr))) return rc;
   e->gx_rcnt.assign(G, 0);
   e->gx_rbeg.assign(G, 0);
   for (int64_t j = 0; j < nr; ++j) {
@@ -451,6 +467,8 @@ int ghost_setup(Engine* e, const std::vector<std::vector<int32_t>>& want) {
   }
   for (int r = 1; r < G; ++r) e->gx_rbeg[r] = e->gx_rbeg[r - 1] + e->gx_rcnt[r - 1];
   e->gx_send.assign(G, {});
+  e->gx_sn.assign(G, 0);
+  e->gx_soff.assign(G, 0);
   std::vector<int64_t> sends(G, 0);  // every shard's send rows (replicated wants: the same everywhere)
   for (int r = 0; r < G; ++r)
     for (int32_t s : want[r]) {
@@ -458,6 +476,7 @@ int ghost_setup(Engine* e, const std::vector<std::vector<int32_t>>& want) {
       sends[o]++;
       if (o == me) e->gx_send[r].push_back(s);
     }
+  for (int r = 0; r < G; ++r) e->gx_sn[r] = (int64_t)e->gx_send[r].size();
   e->gx_maxsend = *std::max_element(sends.begin(), sends.end());
   e->gx_rows = nr;
   e->gx_out = e->gx_in = 0;
@@ -489,6 +508,43 @@ int upload_rows(Engine* e, const std::vector<int32_t>& rows, const std::vector<i
 // their owners straight into the ghost table, by alltoallv with receive
 // displacements, in C chunks (the same C on every shard): chunk c carries
 // rows [c*n/C, (c+1)*n/C) of every (source, destination) list.
+// The rows (and destinations) of slice [lo_r, hi_r) of every send list into
+// gidx: uploaded from the host lists, or gathered on the device from the
+// want lists (gx_dev). Returns the row count.
+int send_rows(Engine* e, const std::vector<int64_t>& lo, const std::vector<int64_t>& hi, int64_t* ns) {
+  const int G = e->world;
+  if (!e->gx_dev) {
+    std::vector<int32_t> rows, dst;
+    for (int r = 0; r < G; ++r)
+      for (int64_t x = lo[r]; x < hi[r]; ++x) {
+        rows.push_back(e->gx_send[r][x]);
+        dst.push_back(r);
+      }
+    *ns = (int64_t)rows.size();
+    return upload_rows(e, rows, dst);
+  }
+  GxSlices sl{};
+  sl.g = G;
+  sl.out[0] = 0;
+  for (int r = 0; r < G; ++r) {
+    sl.src[r] = e->gx_soff[r] + lo[r];
+    sl.out[r + 1] = sl.out[r] + (hi[r] - lo[r]);
+  }
+  sl.total = sl.out[G];
+  *ns = sl.total;
+  if (sl.total > e->gidx_cap) {
+    dfree(e, e->gidx);
+    e->gidx = nullptr;
+    e->gidx_cap = 0;
+    int rc;
+    if ((rc = dalloc(e, &e->gidx, 2 * std::max<int64_t>(sl.total, 1024), 0))) return rc;
+    e->gidx_cap = std::max<int64_t>(sl.total, 1024);
+  }
+  launch_gx_idx(e->wlist, e->n, sl, e->gidx, e->gidx + e->gidx_cap, e->stream);
+  HIPCHK(e, hipGetLastError());
+  return GH_OK;
+}
+
 int ghost_move(Engine* e, int part) {
   GhDev& d = e->d;
   const int G = e->world;
@@ -498,22 +554,21 @@ int ghost_move(Engine* e, int part) {
   int rc;
   if (part == GH_GX_CODES) HIPCHK(e, hipMemsetAsync(e->gwcnt, 0, sizeof(int32_t) * G, e->stream));
   std::vector<size_t> sb(G), rb(G), rd(G);
+  std::vector<int64_t> lo(G), hi(G);
   for (int64_t c = 0; c < C; ++c) {
-    std::vector<int32_t> rows, dst;
     for (int r = 0; r < G; ++r) {
-      const int64_t m = (int64_t)e->gx_send[r].size(), lo = c * m / C, hi = (c + 1) * m / C;
-      for (int64_t x = lo; x < hi; ++x) {
-        rows.push_back(e->gx_send[r][x]);
-        dst.push_back(r);
-      }
-      sb[r] = (size_t)(hi - lo) * B;
+      const int64_t m = e->gx_sn[r];
+      lo[r] = c * m / C;
+      hi[r] = (c + 1) * m / C;
+      sb[r] = (size_t)(hi[r] - lo[r]) * B;
       const int64_t q = e->gx_rcnt[r], qlo = c * q / C, qhi = (c + 1) * q / C;
       rb[r] = (size_t)(qhi - qlo) * B;
       rd[r] = (size_t)(e->gx_rbeg[r] + qlo) * B;
     }
-    if ((rc = upload_rows(e, rows, dst)) || (rc = gbuf_reserve(e, 0, (size_t)std::max<size_t>(rows.size(), 1) * B)))
+    int64_t ns = 0;
+    if ((rc = send_rows(e, lo, hi, &ns)) || (rc = gbuf_reserve(e, 0, (size_t)std::max<int64_t>(ns, 1) * B)))
       return rc;
-    launch_ghost_pack(d, e->cur, e->gidx, e->gidx + e->gidx_cap, (int64_t)rows.size(), part,
+    launch_ghost_pack(d, e->cur, e->gidx, e->gidx + e->gidx_cap, ns, part,
                       static_cast<char*>(e->gbuf[0]), e->gwcnt, e->stream);
     HIPCHK(e, hipGetLastError());
     COMMCHK(e, e->comm->alltoallv(e->gbuf[0], sb.data(), region, rb.data(), e->stream, rd.data()));
@@ -534,7 +589,7 @@ int ghost_move(Engine* e, int part) {
   for (int32_t v : m) any += v;
   if (any == 0) return GH_OK;
   const int64_t REC = ghost_wide_record_bytes(d);
-  std::vector<int32_t> cur0(G), rows, dst;
+  std::vector<int32_t> cur0(G);
   int64_t ws = 0, wr = 0;
   for (int r = 0; r < G; ++r) {
     cur0[r] = (int32_t)ws;
@@ -542,16 +597,15 @@ int ghost_move(Engine* e, int part) {
     wr += m[(size_t)r * G + me];  // r's records to me
     sb[r] = (size_t)m[(size_t)me * G + r] * REC;
     rb[r] = (size_t)m[(size_t)r * G + me] * REC;
-    for (int32_t s : e->gx_send[r]) {
-      rows.push_back(s);
-      dst.push_back(r);
-    }
+    lo[r] = 0;
+    hi[r] = e->gx_sn[r];
   }
-  if ((rc = upload_rows(e, rows, dst)) || (rc = gbuf_reserve(e, 2, (size_t)std::max<int64_t>(ws, 1) * REC)) ||
+  int64_t ns = 0;
+  if ((rc = send_rows(e, lo, hi, &ns)) || (rc = gbuf_reserve(e, 2, (size_t)std::max<int64_t>(ws, 1) * REC)) ||
       (rc = gbuf_reserve(e, 3, (size_t)std::max<int64_t>(wr, 1) * REC)))
     return rc;
   HIPCHK(e, hipMemcpyAsync(e->gwcnt + G, cur0.data(), sizeof(int32_t) * G, hipMemcpyHostToDevice, e->stream));
-  launch_ghost_wide(d, e->cur, e->gidx, e->gidx + e->gidx_cap, (int64_t)rows.size(), e->gwcnt + G,
+  launch_ghost_wide(d, e->cur, e->gidx, e->gidx + e->gidx_cap, ns, e->gwcnt + G,
                     static_cast<char*>(e->gbuf[2]), e->stream);
   HIPCHK(e, hipGetLastError());
   COMMCHK(e, e->comm->alltoallv(e->gbuf[2], sb.data(), e->gbuf[3], rb.data(), e->stream));
@@ -590,8 +644,50 @@ int64_t exchange_footprint(const Engine* e) {
 // in the storm variant, the plane valid) moves only their sender planes
 // (e->gpo; the codes follow after k_round if a segment needs the per-cell
 // rule), any other round the whole rows.
-int round_ghosts(Engine* e) {
-  const int G = e->world;
+int round_ghosts(Engine* e, const GhRound& p) {
+  const int G = e->world, me = e->rank;
+  if (G <= GH_GX_MAXG) {
+    // the want lists on the device: the host reads back G x G counts only
+    GhDev& d = e->d;
+    launch_want_lists(d, p, e->nrs, G, e->wbits, e->wsum, e->wlist, e->mcnt, e->stream);
+    HIPCHK(e, hipGetLastError());
+    int32_t storm = 0;  // shards in the storm variant (summed by decide_active)
+    e->gx_m.resize((size_t)G * G + G);
+    HIPCHK(e, hipMemcpyAsync(e->gx_m.data(), e->mcnt, sizeof(int32_t) * e->gx_m.size(), hipMemcpyDeviceToHost,
+                             e->stream));
+    HIPCHK(e, hipMemcpyAsync(&storm, d.cntg + e->n + 2, sizeof storm, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    const int32_t* M = e->gx_m.data();
+    int rc;
+    if ((rc = ghost_reserve(e, M[G * G + me]))) return rc;
+    for (int32_t s : e->ghosts) e->rslot_h[s] = -1;  // host-set ghosts (a join broadcast) are gone
+    e->ghosts.clear();
+    e->gx_dev = true;
+    e->gx_rcnt.assign(G, 0);
+    e->gx_rbeg.assign(G, 0);
+    e->gx_sn.assign(G, 0);
+    e->gx_soff.assign(G, 0);
+    std::vector<int64_t> sends(G, 0);
+    for (int r = 0; r < G; ++r)
+      for (int o = 0; o < G; ++o) {
+        const int64_t c = M[r * G + o];
+        sends[o] += c;
+        if (o < me) e->gx_soff[r] += c;
+      }
+    for (int r = 0; r < G; ++r) {
+      e->gx_rcnt[r] = M[me * G + r];
+      e->gx_sn[r] = M[r * G + me];
+      if (r) e->gx_rbeg[r] = e->gx_rbeg[r - 1] + e->gx_rcnt[r - 1];
+    }
+    e->gx_maxsend = *std::max_element(sends.begin(), sends.end());
+    e->gx_rows = M[G * G + me];
+    e->gx_out = e->gx_in = 0;
+    launch_ghost_slots(d, e->wlist + (size_t)me * e->n, e->mcnt + G * G + me, e->stream);
+    HIPCHK(e, hipGetLastError());
+    e->gpo = e->plane && e->plane_valid && storm == 0;
+    if (e->plane && (rc = ghost_move(e, GH_GX_PLANE))) return rc;
+    return e->gpo ? GH_OK : ghost_move(e, GH_GX_CODES);
+  }
   const int k = e->cfg.fanout;
   const bool pull = e->cfg.peer_mode == GH_PEER_PULL;
   // pull: [n][k + 1] (count, senders); ring: CSR (beg, cnt) into <= 3N senders
@@ -966,7 +1062,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   d.ncsw = (int32_t)(ncs / 32);
   d.rank = rank;
   d.world = world;
-  d.tsat = cfg->t_cleanup < GH_TSAT_T;
+  d.tsa = cfg->t_cleanup < GH_TSAT_T ? cfg->t_cleanup + 1 : 0;
   d.toff = gh_tier_toff(cfg->t_cleanup);
   d.rlist = cfg->remove_mode == GH_REMOVE_LIST;
   // every shard sizes (and grows) its arena from the same segment count, the
@@ -1073,6 +1169,14 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
                        (e->plane && (rc = dalloc(e, &d.gplane, (size_t)gcap * e->ld / 8, 0xFF)))))
         break;
       d.gcap = gcap;
+      // the device want lists of every shard (round_ghosts)
+      if (world > 1 && world <= GH_GX_MAXG) {
+        const int64_t nw = ((int64_t)e->n + 31) / 32, nb = (nw + 255) / 256;
+        if ((rc = dalloc(e, &e->wbits, (size_t)world * nw, 0)) || (rc = dalloc(e, &e->wsum, (size_t)world * nb, 0)) ||
+            (rc = dalloc(e, &e->wlist, (size_t)world * e->n, 0)) ||
+            (rc = dalloc(e, &e->mcnt, (size_t)world * world + world, 0)))
+          break;
+      }
       if (!dry && hipMemcpyAsync(d.rslot, e->rslot_h.data(), sizeof(int32_t) * e->n, hipMemcpyHostToDevice,
                                  e->stream) != hipSuccess) {
         rc = GH_EHIP;
@@ -1178,7 +1282,7 @@ int build_inboxes(Engine* e, const GhRound& p) {
       launch_inbox(d, p, e->stream);
     }
     HIPCHK(e, hipGetLastError());
-    return e->world > 1 ? round_ghosts(e) : GH_OK;
+    return e->world > 1 ? round_ghosts(e, p) : GH_OK;
   }
   if (e->cfg.peer_mode == GH_PEER_PULL) {
     launch_peers_pull(d, e->cur, e->dcur, p, e->stream);

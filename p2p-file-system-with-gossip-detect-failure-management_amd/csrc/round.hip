@@ -1258,6 +1258,8 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     s_rm1[pp] = rm1;
   }
   const uint32_t tfp = (uint32_t)min(p.t_fail, 31) * 0x10001u;
+  // tombstone age + tsk carries into bit 5 iff age >= the saturation age
+  const uint32_t tsk = (uint32_t)(32 - (d.tsa ? d.tsa : GH_N_TAGEMAX)) * 0x10001u;
   const uint32_t tcp = (uint32_t)min(p.t_cleanup, 31) * 0x10001u;
   __syncthreads();
   const bool tile_still = s_bmove == 0;
@@ -1541,7 +1543,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         const uint32_t z = pk_add_u16(x | 0x001F001Fu, 0x00010001u);
         const uint32_t ta0 = pk_zero_mask(z);                  // tombstone or absent
         const uint32_t ab = pk_zero_mask(pk_add_u16(x, 0x00010001u));  // absent
-        acc |= ((x & 0x001F001Fu) + 0x00020002u) & ~ab & ta0 & 0x00200020u;  // tombstone age >= 30
+        acc |= ((x & 0x001F001Fu) + tsk) & ~ab & ta0 & 0x00200020u;  // tombstone age >= tsa (saturation)
         mm = 0u;
         y0 = (((x & 0x7FE07FE0u) | 0x00010001u) & ~ta0) | (pk_adds_u16(x, 0x00010001u) & ta0);
         npre = ta0;
@@ -1567,7 +1569,8 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         // when T_cleanup reaches the age field and st says "fresh")
         const uint32_t keep = ((ta & ~ab) | fl) & ~st;
         const uint32_t nowm = ~ta & ~actm;                     // guard rows: present cells stamped now
-        acc |= (ag + 0x00020002u) & ~ab & ~nowm & 0x00200020u; // age >= 30 (saturation) or wide marker
+        // age >= 30 or wide marker; a guard row's tombstone at its saturation age
+        acc |= (((ag + 0x00020002u) & ~ab & ~nowm) | ((ag + tsk) & ta & ~ab & ~actm)) & 0x00200020u;
         const uint32_t key = ((xr & ~(nowm & 0x80008000u)) | 0x001F001Fu) | rel;  // heartbeat key (absent: -1)
         mm = pk_sra15(pk_subs_i16(key, m)) & ~keep;            // merged (step 6)
         // not merged: age + 1 (a detected cell becomes a tombstone of its
@@ -2121,7 +2124,7 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
       const int32_t t2 = now ? r : vts;
       int32_t a2 = r + 1 - t2;
       if (x < 0) {
-        if (d.tsat && a2 > GH_N_TAGEMAX) a2 = GH_N_TAGEMAX;
+        if (d.tsa && a2 > d.tsa) a2 = d.tsa;
         fit &= a2 >= 0 && a2 <= GH_N_TAGEMAX;
         code = GH_N_TOMB | ((uint32_t)a2 & 31u);
       } else {

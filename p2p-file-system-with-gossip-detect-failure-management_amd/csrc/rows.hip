@@ -90,6 +90,105 @@ __global__ __launch_bounds__(256) void k_ghost_unwide(GhDev d, int cur, const ch
   for (int j = 0; j < d.tw; j += 8) *reinterpret_cast<uint4*>(d.gcodes + g * d.ld + t * d.tw + j) = m;
 }
 
+// ---- the round's want lists on the device --------------------------------
+// Every shard holds every receiver's inbox (replicated), so every shard
+// computes every shard's wants alike: want[r] = the senders, owned by
+// another shard, of the receivers shard r owns, ascending. wbits: [G][nw]
+// bitmaps; wlist: [G][n] the compacted lists; mcnt: [G][G] counts, M[r][o] =
+// the rows of owner o in want[r] (the exchange's send and receive sizes).
+__global__ __launch_bounds__(256) void k_want_mark(GhDev d, GhRound p, int64_t nrs, uint32_t* wbits, int64_t nw) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const bool pull = p.peer_mode == GH_PEER_PULL;
+  const int64_t r = i / nrs;
+  const int cnt = gh_in_cnt(d, pull, p.k, i);
+  const int64_t beg = gh_in_beg(d, pull, p.k, i);
+  for (int q = 0; q < cnt; ++q) {
+    const int64_t s = d.inbox[beg + q];
+    if (s / nrs != r) atomicOr(&wbits[r * nw + (s >> 5)], 1u << (s & 31));
+  }
+}
+
+// per (rank, 256-word block): the block's set bits (wsum[r][b])
+__global__ __launch_bounds__(256) void k_want_sum(const uint32_t* wbits, int64_t nw, int32_t* wsum, int64_t nb) {
+  const int64_t r = blockIdx.y, b = blockIdx.x;
+  const int64_t w = b * 256 + threadIdx.x;
+  int tot = w < nw ? __popc(wbits[r * nw + w]) : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+  __shared__ int s_w[4];
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = tot;
+  __syncthreads();
+  if (threadIdx.x == 0) wsum[r * nb + b] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
+// per rank: exclusive prefix of its block sums (one thread per rank; nb is small)
+__global__ void k_want_scan(int32_t* wsum, int64_t nb, int G, int32_t* wtot) {
+  const int r = threadIdx.x;
+  if (r >= G) return;
+  int acc = 0;
+  for (int64_t b = 0; b < nb; ++b) {
+    const int v = wsum[r * nb + b];
+    wsum[r * nb + b] = acc;
+    acc += v;
+  }
+  wtot[r] = acc;
+}
+
+// compaction: the set bits of each block in ascending order at the block's
+// offset; M[r][owner] counted per block in LDS
+__global__ __launch_bounds__(256) void k_want_fill(const uint32_t* wbits, int64_t nw, const int32_t* wsum, int64_t nb,
+                                                   int64_t n, int64_t nrs, int G, int32_t* wlist, int32_t* mcnt) {
+  const int64_t r = blockIdx.y, b = blockIdx.x;
+  const int64_t w = b * 256 + threadIdx.x;
+  const uint32_t x = w < nw ? wbits[r * nw + w] : 0u;
+  __shared__ int s_w[4], s_m[64];
+  const int c = __popc(x);
+  // exclusive prefix of c over the block
+  int incl = c;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) s_w[threadIdx.x >> 6] = incl;
+  if (threadIdx.x < 64) s_m[threadIdx.x] = 0;
+  __syncthreads();
+  int base = wsum[r * nb + b] + incl - c;
+  for (int q = 0; q < (int)(threadIdx.x >> 6); ++q) base += s_w[q];
+  for (uint32_t m = x; m; m &= m - 1) {
+    const int64_t s = w * 32 + __builtin_ctz(m);
+    wlist[r * n + base++] = (int32_t)s;
+    atomicAdd(&s_m[s / nrs], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x < G && s_m[threadIdx.x]) atomicAdd(&mcnt[r * G + threadIdx.x], s_m[threadIdx.x]);
+}
+
+// this shard's ghost slots: every row it does not own unmapped, ghost j
+// (want[me][j]) at slot nrows + j
+__global__ __launch_bounds__(256) void k_ghost_slots(GhDev d) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x < d.n && !gh_owned(d, x)) d.rslot[x] = -1;
+}
+__global__ __launch_bounds__(256) void k_ghost_slots_set(GhDev d, const int32_t* mine, const int32_t* cnt) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < *cnt) d.rslot[mine[j]] = (int32_t)(d.nrows + j);
+}
+
+// rows (and destinations) of one exchange chunk: for each destination r the
+// slice [lo_r, hi_r) of this shard's send list to r, back to back
+__global__ __launch_bounds__(256) void k_gx_idx(const int32_t* wlist, int64_t n, GxSlices sl, int32_t* rows,
+                                                int32_t* dest) {
+  const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= sl.total) return;
+  int r = 0;
+  while (r + 1 < sl.g && sl.out[r + 1] <= x) ++r;
+  rows[x] = wlist[(int64_t)r * n + sl.src[r] + (x - sl.out[r])];
+  dest[x] = r;
+}
+
 unsigned ghost_grid(int64_t work) {
   return (unsigned)std::max<int64_t>(1, std::min<int64_t>((work + 255) / 256, 65536));
 }
@@ -111,6 +210,28 @@ void launch_ghost_wide(const GhDev& d, int cur, const int32_t* rows, const int32
   if (ns == 0) return;
   hipLaunchKernelGGL(k_ghost_wide, dim3(ghost_grid(ns * d.ntiles)), dim3(256), 0, s, d, cur, rows, dest, ns, wcur,
                      out);
+}
+
+void launch_want_lists(const GhDev& d, const GhRound& p, int64_t nrs, int G, uint32_t* wbits, int32_t* wsum,
+                       int32_t* wlist, int32_t* mcnt, hipStream_t s) {
+  const int64_t nw = ((int64_t)p.n + 31) / 32, nb = (nw + 255) / 256;
+  (void)hipMemsetAsync(wbits, 0, sizeof(uint32_t) * G * nw, s);
+  (void)hipMemsetAsync(mcnt, 0, sizeof(int32_t) * (G * G + G), s);
+  hipLaunchKernelGGL(k_want_mark, dim3((unsigned)((p.n + 255) / 256)), dim3(256), 0, s, d, p, nrs, wbits, nw);
+  hipLaunchKernelGGL(k_want_sum, dim3((unsigned)nb, (unsigned)G), dim3(256), 0, s, wbits, nw, wsum, nb);
+  hipLaunchKernelGGL(k_want_scan, dim3(1), dim3(64), 0, s, wsum, nb, G, mcnt + G * G);
+  hipLaunchKernelGGL(k_want_fill, dim3((unsigned)nb, (unsigned)G), dim3(256), 0, s, wbits, nw, wsum, nb, (int64_t)p.n,
+                     nrs, G, wlist, mcnt);
+}
+
+void launch_ghost_slots(const GhDev& d, const int32_t* mine, const int32_t* cnt, hipStream_t s) {
+  hipLaunchKernelGGL(k_ghost_slots, dim3((unsigned)((d.n + 255) / 256)), dim3(256), 0, s, d);
+  hipLaunchKernelGGL(k_ghost_slots_set, dim3((unsigned)((d.n + 255) / 256)), dim3(256), 0, s, d, mine, cnt);
+}
+
+void launch_gx_idx(const int32_t* wlist, int64_t n, const GxSlices& sl, int32_t* rows, int32_t* dest, hipStream_t s) {
+  if (sl.total == 0) return;
+  hipLaunchKernelGGL(k_gx_idx, dim3((unsigned)((sl.total + 255) / 256)), dim3(256), 0, s, wlist, n, sl, rows, dest);
 }
 
 void launch_ghost_unwide(const GhDev& d, int cur, const char* in, int64_t nrec, hipStream_t s) {

@@ -64,11 +64,12 @@ def masked(hb, ts):
 def export_view(hb, ts, round_, t_cleanup):
     """A dense (hb, ts) state as gh_export_state / or_export_state present it
     (SPEC.md §1): ts 0 for absent cells, and with T_cleanup < 30 a tombstone
-    older than 30 rounds at exactly 30 rounds (round_ = last completed)."""
+    older than T_cleanup + 1 rounds at exactly T_cleanup + 1 rounds (round_ =
+    last completed)."""
     t = ts.astype(np.int64).copy()
     t[hb == -1] = 0
     if t_cleanup < 30:
         now = round_ + 1
-        old = (hb == -2) & (now - t > 30)
-        t[old] = now - 30
+        old = (hb == -2) & (now - t > t_cleanup + 1)
+        t[old] = now - (t_cleanup + 1)
     return hb, t.astype(np.int32)

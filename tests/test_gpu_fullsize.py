@@ -60,9 +60,13 @@ def compare_blocks(eng, orc, r):
     print(f"  r={r}: full tables equal ({time.perf_counter() - t0:.1f} s)", flush=True)
 
 
-def run(gs, om, t_fail, rounds, full_at, expect, sched=None, per_round=None, remove_mode=0):
-    cfg = dict(fanout=4, seed=0x5EED0003, t_fail=t_fail, t_cleanup=t_fail, remove_mode=remove_mode)
-    eng = gs.Engine(gs.default_config(N, **cfg))
+def run(gs, om, t_fail, rounds, full_at, expect, sched=None, per_round=None, remove_mode=0, world=1, layout=0,
+        extra=None, after_round=None):
+    cfg = dict(fanout=4, seed=0x5EED0003, t_fail=t_fail, t_cleanup=t_fail, remove_mode=remove_mode, **(extra or {}))
+    if world > 1:  # G in-process shards of one cluster on this GPU (GH_COMM_LOCAL)
+        eng = gs.ShardGroup(gs.default_config(N, shard_layout=layout, **cfg), world)
+    else:
+        eng = gs.Engine(gs.default_config(N, **cfg))
     orc = om.Oracle(om.default_config(N, **cfg), threads=THREADS)
     try:
         eng.init_full(2, 0, 0)
@@ -83,9 +87,12 @@ def run(gs, om, t_fail, rounds, full_at, expect, sched=None, per_round=None, rem
             np.testing.assert_array_equal(eng.read_failed(), orc.read_failed(), err_msg=f"failed r={r}")
             np.testing.assert_array_equal(eng.read_detectors(), orc.read_detectors(), err_msg=f"detectors r={r}")
             seen["detections"] += s1["detections"]
-            seen["storm"] |= eng.encoding_info(full=True)[2] == 1
-            var = eng.tier_info(full=True)[3]
-            seen["variants"][var] = seen["variants"].get(var, 0) + 1
+            if world == 1:  # (per-shard diagnostics differ between shards)
+                seen["storm"] |= eng.encoding_info(full=True)[2] == 1
+                var = eng.tier_info(full=True)[3]
+                seen["variants"][var] = seen["variants"].get(var, 0) + 1
+            if after_round:
+                after_round(eng, orc, r)
             if per_round:
                 per_round(eng, r, s1)
             if s1["detections"] and seen["first_detection"] is None:
@@ -163,3 +170,75 @@ def test_c3_fullsize_reference_timeouts(gs, oracle_mod):
     def expect(s):
         assert s["detections"] > 0 and s["storm"]
     run(gs, oracle_mod, 5, 9, {6, 7, 9}, expect)
+
+
+def crash_sched(gs):
+    from scenarios import crash_ids
+    crashed = crash_ids(N, 0.01, 0x5EED0003)
+    return {8: [(gs.GH_EV_CRASH, int(c)) for c in crashed]}
+
+
+def expect_detection(s):
+    assert s["detections"] > 0 and s["first_detection"] is not None, s
+
+
+def test_c3_fullsize_rows_g8(gs, oracle_mod):
+    """North_star's layout at the largest size one MI355X holds: 8 row shards
+    (each owns 8,192 observer rows; the senders' plane rows of other shards
+    arrive by alltoallv into its ghost table, the want lists built on the
+    device), N=65,536, k=4, T_fail=16, the 1% crash at r=8, 25 rounds: full
+    tables at r=6, 25, the detection round and the one after."""
+    run(gs, oracle_mod, 16, 25, {6, 25}, expect_detection, sched=crash_sched(gs), world=8, layout=1)
+
+
+def test_c3_fullsize_columns_g8(gs, oracle_mod):
+    """The default multi-GPU layout at full size: 8 column shards (each holds
+    every row of 8,192 member columns, O(N) exchanges), the same workload
+    against tablesim (not against one engine)."""
+    run(gs, oracle_mod, 16, 25, {6, 25}, expect_detection, sched=crash_sched(gs), world=8, layout=0)
+
+
+def test_c3_fullsize_crash_1pct_quirk(gs, oracle_mod):
+    """Quirk-mode detection (Go's range over the slice removeMember shifts,
+    slave/slave.go:464-477) through the 1% crash at N=65,536: the crashed
+    members' runs of candidates in every row, the skipped ones detected a
+    round later."""
+    run(gs, oracle_mod, 16, 28, {28}, expect_detection, sched=crash_sched(gs), extra=dict(detect_mode=1))
+
+
+def test_c5_fullsize_files(gs, oracle_mod):
+    """SURVEY C5's shape at N=65,536 with 2^20 files (master/master.go:74-175):
+    every file put at r=3 (Init_replica over the master's list), a 1% crash
+    wave at r=4, 1% leaves at r=8, the r=4 crashed members rejoining at r=12,
+    re-replication from the first detectors' views at detection + 8
+    (Fail_recover, slave/slave.go:1122-1133), then Get_file_replica_list /
+    Get_file_version of every file."""
+    from scenarios import crash_ids
+    F = 1 << 20
+    crashed = crash_ids(N, 0.01, 0x5EED0005)
+    leavers = [c for c in crash_ids(N, 0.02, 0x5EED0006) if c not in set(crashed)][: N // 100]
+    sched = {4: [(gs.GH_EV_CRASH, int(c)) for c in crashed],
+             8: [(gs.GH_EV_LEAVE, int(c)) for c in leavers],
+             12: [(gs.GH_EV_JOIN, int(c)) for c in crashed]}
+    files = np.arange(F, dtype=np.int32)
+    repair_at = {}
+
+    def after_round(eng, orc, r):
+        if r == 3:
+            a, b = eng.put(files), orc.put(files)
+            for x, y in zip(a, b):
+                np.testing.assert_array_equal(x, y)
+        dets = orc.read_detectors()
+        if len(dets) and r + 8 not in repair_at:
+            repair_at[r + 8] = [int(x) for x in dets[:2]]
+        for obs in repair_at.get(r, []):
+            pa, pb = eng.repair(obs), orc.repair(obs)
+            assert pa == pb, f"repair at r={r} from {obs}: {len(pa)} vs {len(pb)} plan entries"
+            print(f"  r={r}: repair from {obs}: {len(pa)} plan entries equal", flush=True)
+        if r == 40:
+            for x, y in zip(eng.get_files(files), orc.get_files(files)):
+                np.testing.assert_array_equal(x, y)
+            print("  r=40: get_files of 2^20 files equal", flush=True)
+
+    run(gs, oracle_mod, 16, 40, {40}, expect_detection, sched=sched, extra=dict(max_files=F),
+        after_round=after_round)

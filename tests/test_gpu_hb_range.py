@@ -170,8 +170,8 @@ def test_arena_overflow_in_a_round_loses_state_loudly(gs, oracle_mod):
 def test_long_collapse_stays_narrow(gs, oracle_mod):
     """The reference's 5-round timeouts at N=2,048: the round-6 storm, the
     collapse under the <4 guard, then 40 more rounds in which every guard
-    row's tombstones age past the narrow field (tsat: saturated at 30,
-    exported as 30 rounds old by both)."""
+    row's tombstones age past T_cleanup (saturated at T_cleanup + 1 = 6,
+    exported as 6 rounds old by both; the rows then stop changing)."""
     n = 2048
     eng, orc = pair(gs, oracle_mod, n, fanout=3, seed=0xA501)
     eng.init_full(2, 0, 0)
