@@ -261,6 +261,8 @@ struct GhDev {
   uint32_t *gplane; // ... their sender plane words [gcap][ld / 8] (null without the plane)
   int64_t gcap;     // ghost rows the ghost table holds
   int32_t *pvf;     // row layout: [n][k] validity of each receiver's draws (summed over shards)
+  uint8_t *pvb;     // column layout, G > 1, pull: [G * ncs] per receiver the validity bits of its k draws
+                    // (its column's owner decides them; allgathered, then every shard rebuilds every inbox)
   uint16_t *hn[2];  // narrow double buffer
   uint32_t *a4[2];  // 4-bit tier: age plane per buffer (null: tier off); with pl[b] it holds buffer b
   int32_t *m8;      // [0..1] buffer b is in the 4-bit tier; [2] this round switches the next buffer's tier;
@@ -307,7 +309,7 @@ struct GhDev {
   // jobs[2 (4 b + w) * GH_JOB_CAP ..], two uint4 each (row, tile << 8 |
   // lane, the minimum plane words; the lane's own lag words and age words)
   // and their count to jobn[4 b + w], with no atomics. Results that need the
-  // wide arena go to redo (k_round_redo, the first uint4).
+  // wide arena go to redo (the redo pass redo_all in k_round_slow, the first uint4).
   uint4 *jobs;
   int32_t *jobn;    // [4 * nibble workgroups]
   int32_t *njobs;   // [0] jobs of the last round (k_base's variant choice), [1] redo entries, [2] jobs of the round before,
@@ -833,6 +835,7 @@ void launch_peers_pull(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
 // row layout: draw validity at the senders' owners (pvf, then SUM over
 // shards), then every receiver's inbox
 void launch_peers_rows(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
+void launch_inbox_bits(const GhDev& d, const GhRound& p, hipStream_t s);
 void launch_inbox_rows(const GhDev& d, const GhRound& p, hipStream_t s);
 void launch_negate(int32_t* x, int64_t n, hipStream_t s);
 void launch_ring_count(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);

@@ -726,13 +726,19 @@ int round_ghosts(Engine* e, const GhRound& p) {
 // shard's k_round listed segments for k_round_slow (one collective decision).
 int ghost_codes_if_slow(Engine* e) {
   if (!e->rowlay || e->world < 2 || !e->gpo) return GH_OK;
+  // segments for k_round_slow, or (4-bit tier) lane jobs that gather their
+  // senders' codes (a REMOVE'd member, an unknown or old minimum)
   int32_t* flag = e->d.wn + 4;
   HIPCHK(e, hipMemcpyAsync(flag, e->d.slow_n, sizeof(int32_t), hipMemcpyDeviceToDevice, e->stream));
-  COMMCHK(e, e->comm->allreduce(flag, flag, 1, GH_DT_I32, GH_OP_MAX, e->stream));
-  int32_t any = 0;
-  HIPCHK(e, hipMemcpyAsync(&any, flag, sizeof any, hipMemcpyDeviceToHost, e->stream));
+  if (e->c8)
+    HIPCHK(e, hipMemcpyAsync(flag + 1, e->d.m8 + 5, sizeof(int32_t), hipMemcpyDeviceToDevice, e->stream));
+  else
+    HIPCHK(e, hipMemsetAsync(flag + 1, 0, sizeof(int32_t), e->stream));
+  COMMCHK(e, e->comm->allreduce(flag, flag, 2, GH_DT_I32, GH_OP_MAX, e->stream));
+  int32_t any[2] = {0, 0};
+  HIPCHK(e, hipMemcpyAsync(any, flag, sizeof any, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  return any > 0 ? ghost_move(e, GH_GX_CODES) : GH_OK;
+  return any[0] > 0 || any[1] > 0 ? ghost_move(e, GH_GX_CODES) : GH_OK;
 }
 
 int allreduce_i32(Engine* e, int32_t* send, int32_t* recv, size_t count) {
@@ -994,7 +1000,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   // the 4-bit tier streams the steady state the plane serves at 1 B per cell,
   // half of it the plane itself (its window is the plane's: lags of healthy
   // pull dissemination); the row layout ships 16-bit ghost rows
-  e->c8 = e->plane && cfg->shard_layout == GH_LAYOUT_COLUMNS && e->tpw == 1 && tw >= 64;
+  e->c8 = e->plane && e->tpw == 1 && tw >= 64;
   if (const char* v = std::getenv("GH_C8")) e->c8 = e->c8 && std::atoi(v) != 0;
   if (cfg->shard_layout != GH_LAYOUT_COLUMNS && cfg->shard_layout != GH_LAYOUT_ROWS) {
     delete e;
@@ -1159,6 +1165,9 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
           (rc = dalloc(e, &d.lsel[0], e->n, 0)) || (rc = dalloc(e, &d.lsel[1], e->n, 0)))
         break;
     }
+    if (!rowlay && world > 1 && cfg->peer_mode == GH_PEER_PULL &&
+        (rc = dalloc(e, &d.pvb, (size_t)world * ncs + 64, 0)))
+      break;
     if (rowlay) {
       e->rslot_h.assign(e->n, -1);
       for (int64_t i = row0; i < row0 + nrows; ++i) e->rslot_h[i] = (int32_t)(i - row0);
@@ -1288,9 +1297,11 @@ int build_inboxes(Engine* e, const GhRound& p) {
     launch_peers_pull(d, e->cur, e->dcur, p, e->stream);
     HIPCHK(e, hipGetLastError());
     if (e->world > 1) {
-      const size_t row = (size_t)e->cfg.fanout + 1;  // count + senders per receiver
-      COMMCHK(e, e->comm->allgather(d.inbox + (size_t)e->rank * d.ncs * row, d.inbox,
-                                    sizeof(int32_t) * d.ncs * row, e->stream));
+      // one validity byte per receiver (k <= 8 draws) instead of its
+      // (k + 1)-int inbox row: every shard redraws the peers and rebuilds
+      COMMCHK(e, e->comm->allgather(d.pvb + (size_t)e->rank * d.ncs, d.pvb, (size_t)d.ncs, e->stream));
+      launch_inbox_bits(d, p, e->stream);
+      HIPCHK(e, hipGetLastError());
     }
     return GH_OK;
   }
@@ -1759,8 +1770,9 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       }
       if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 2], e->stream));
     }
-    launch_round_jobs(e->d, e->cur, e->dcur, pr, e->stream);
+    // (row layout: the ghosts' codes before the kernels that may read them)
     if ((rc = ghost_codes_if_slow(e))) return rc;
+    launch_round_jobs(e->d, e->cur, e->dcur, pr, e->stream);
     launch_round_slow(e->d, e->cur, e->dcur, pr, e->stream);
     if (e->rowlay && e->world > 1) {
       // every shard detected in its own rows: D_r's counts and first

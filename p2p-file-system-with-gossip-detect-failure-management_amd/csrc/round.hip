@@ -167,10 +167,23 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
     const uint32_t w = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
     s = (int)w + ((int64_t)w >= i);
     if (d.alive[s] && d.active[s]) {
-      const GhCell v = gh_get(d, cur, s, t, p.r);
       // i must be in s's snapshot list: present, not detected by s this
-      // round and not REMOVE'd at s in step 1.
-      ok = v.x >= 0 && !v.f;
+      // round and not REMOVE'd at s in step 1. A tier chunk answers from its
+      // two words, loaded together (code 15: absent or a tombstone; a tier
+      // cell is never flagged)
+      if (gh_m8(d, cur)) {
+        const int64_t cell = gh_cell(d, s, t & ~(int64_t)7);
+        const uint32_t aw = d.a4[cur][cell >> 3], lw = d.pl[cur][cell >> 3];
+        if (!gh_t4_esc(aw)) {
+          ok = ((lw >> gh_nib((int)(t & 7))) & 0xFu) != 15u;
+        } else {
+          const GhCell v = gh_get(d, cur, s, t, p.r);
+          ok = v.x >= 0 && !v.f;
+        }
+      } else {
+        const GhCell v = gh_get(d, cur, s, t, p.r);
+        ok = v.x >= 0 && !v.f;
+      }
       if (ok && dbit(d.dbits, t) && gh_rm_at(d, dcur, t, s)) ok = false;
     }
   }
@@ -178,7 +191,27 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
   const int lane = threadIdx.x & 63;
   const uint32_t grp = (uint32_t)(m >> (lane & ~7)) & 0xFFu;  // this receiver's valid draws
   if (ok) d.inbox[beg + __builtin_popcount(grp & ((1u << q) - 1u))] = s;
-  if (inr && q == 0) d.inbox[beg - 1] = __builtin_popcount(grp);
+  if (inr && q == 0) {
+    d.inbox[beg - 1] = __builtin_popcount(grp);
+    if (d.pvb) d.pvb[i] = (uint8_t)grp;  // G > 1: the bits travel, not the inbox (k_inbox_bits)
+  }
+}
+
+// Column layout, G > 1: every receiver's inbox from the allgathered validity
+// bits of its draws (the same draws as k_peers_pull, in draw order).
+__global__ __launch_bounds__(256) void k_inbox_bits(GhDev d, GhRound p) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const uint32_t b = d.pvb[i];
+  const int64_t beg = i * (p.k + 1) + 1;
+  int nv = 0;
+  for (int q = 0; q < p.k; ++q) {
+    if (!((b >> q) & 1u)) continue;
+    const uint32_t u = gh_philox_word(p.seed, (uint32_t)i, (uint32_t)p.r, GH_TAG_PEER, (uint32_t)(q >> 2), q & 3);
+    const uint32_t w = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
+    d.inbox[beg + nv++] = (int)w + ((int64_t)w >= i);
+  }
+  d.inbox[beg - 1] = nv;
 }
 
 // Row layout: sender s's owner checks receiver i's draws against s's row
@@ -577,6 +610,7 @@ __device__ __forceinline__ void base_col(const GhDev& d, int cur, int dcur, cons
       d.m8[2] = w8 != d.m8[cur ^ 1];
       d.m8[cur ^ 1] = w8;
       d.m8[3] = 0;  // escaped chunks the round writes
+      d.m8[5] = 0;  // row layout: a lane job needs its ghost senders' codes
     }
     *d.slow_n = 0;
     *d.nstorm = 0;
@@ -828,7 +862,11 @@ __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint
   gain += __builtin_popcount(m1 & a1);
 }
 
-template <int TW, bool NT, int CPL>
+// ROWS (row layout, IN = 4): a sender is an owned row of this shard (its
+// plane segment in the tile slice, as with columns) or a ghost row whose
+// plane words the round's exchange put in the ghost table (row-major,
+// gplane); the gathers then take per-sender 64-bit addresses staged in LDS.
+template <int TW, bool NT, int CPL, bool ROWS>
 __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, const GhRound& p, const int bid) {
   constexpr int W = CPL / 8;         // dwords per lane and plane
   constexpr int SEG = TW / CPL;      // lanes per row segment
@@ -848,7 +886,9 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   __shared__ __attribute__((aligned(16))) uint32_t s_dn[TW / 8];
   __shared__ int s_slow[RB];
   __shared__ int s_meta[RB];
-  __shared__ __attribute__((aligned(16))) int s_inb[RB * KB];
+  __shared__ __attribute__((aligned(16))) int s_inb[ROWS ? 4 : RB * KB];
+  __shared__ __attribute__((aligned(16))) unsigned long long s_inb64[ROWS ? RB * KB : 2];
+  __shared__ int s_need;  // ROWS: a lane job gathers its senders' 16-bit codes (ghosts' codes must travel)
 
   const int rowend = (int)(d.row0 + d.nrows);
   int tile, rb;
@@ -860,7 +900,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const unsigned long long gmask = (SEG == 64 ? ~0ull : ((1ull << SEG) - 1)) << (sub * SEG);
   if (tid == 0) {
     s_merged = s_rel = 0;
-    s_quiet = s_nslow = s_bmove = s_hasjob = 0;
+    s_quiet = s_nslow = s_bmove = s_hasjob = s_need = 0;
     s_d8bad = 0ull;
   }
   const bool pull = p.peer_mode == GH_PEER_PULL;
@@ -878,10 +918,20 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       meta = al | (act << 1) | (cnt << 2) | ((quiet && al && !act && cnt == 0 && stab_cur[i]) ? 1 << 30 : 0);
       // the sender's plane row segment as a byte offset in the tile slice;
       // unused slots read the own row's (a no-op under the merge)
-      sv = (q < cnt ? d.inbox[gh_in_beg(d, pull, p.k, i) + q] : (int)(i - d.row0)) * (TW / 2);
+      if constexpr (ROWS) {
+        const int64_t sslot = q < cnt ? d.rslot[d.inbox[gh_in_beg(d, pull, p.k, i) + q]] : i - d.row0;
+        const char* a = sslot < d.nrows
+                            ? reinterpret_cast<const char*>(d.pl[cur]) + ((int64_t)tile * d.tstride + sslot * TW) / 2
+                            : reinterpret_cast<const char*>(d.gplane) + (sslot - d.nrows) * (d.ld / 2) + tile * (TW / 2);
+        s_inb64[t] = reinterpret_cast<unsigned long long>(a);
+      } else {
+        sv = (q < cnt ? d.inbox[gh_in_beg(d, pull, p.k, i) + q] : (int)(i - d.row0)) * (TW / 2);
+      }
+    } else if constexpr (ROWS) {
+      s_inb64[t] = reinterpret_cast<unsigned long long>(d.pl[cur]);  // (never read: the row is idle)
     }
     if (q == 0) s_meta[row] = meta;
-    s_inb[t] = sv;
+    if constexpr (!ROWS) s_inb[t] = sv;
   }
   const int32_t* __restrict__ bo = d.base[cur];
   const int32_t* __restrict__ bn = d.base[cur ^ 1];
@@ -956,10 +1006,21 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       // the row's receivers gather too
       awu[u] = nib_load<W, GH_NIB_AGE_AUX>(a4o_t, ow);
       qwu[u] = nib_load<W, GH_NIB_OWN_AUX>(plo_t, ow);
-      const int4 sv4 = *reinterpret_cast<const int4*>(&s_inb[rs * KB]);
-      const int sv[4] = {sv4.x, sv4.y, sv4.z, sv4.w};
+      if constexpr (ROWS) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) pwu[u][q] = nib_load<W, GH_NIB_GAT_AUX>(plo_t, (uint32_t)sv[q] + lbp);
+        for (int q = 0; q < 4; ++q) {
+          typedef uint32_t gw __attribute__((ext_vector_type(W)));
+          typedef const __attribute__((address_space(1))) gw ggw;
+          const gw x = *reinterpret_cast<ggw*>(s_inb64[rs * KB + q] + lbp);
+#pragma unroll
+          for (int w = 0; w < W; ++w) pwu[u][q].v[w] = x[w];
+        }
+      } else {
+        const int4 sv4 = *reinterpret_cast<const int4*>(&s_inb[rs * KB]);
+        const int sv[4] = {sv4.x, sv4.y, sv4.z, sv4.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pwu[u][q] = nib_load<W, GH_NIB_GAT_AUX>(plo_t, (uint32_t)sv[q] + lbp);
+      }
     }
 #pragma unroll
     for (int u = 0; u < RS; ++u) {
@@ -1008,6 +1069,11 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       const bool rowok = oku[u] && !p.force_slow;
       const bool jb = al && rowok && (lane_job || esc || ob || Bm != 0 || Lz != 0);
       const unsigned long long jm = __ballot(jb);
+      // a job whose rule gathers its senders' 16-bit codes (a REMOVE'd member,
+      // an unknown or old minimum): with ghost senders, their codes travel
+      if constexpr (ROWS) {
+        if (__ballot(jb && (rm != 0u || Lz != 0)) != 0 && lane == 0) s_need = 1;
+      }
       bool jslow = false;
       if (jm) {
         const int nj = __popcll(jm);
@@ -1062,6 +1128,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
     if (s_rel) atomicAdd(&d.stats[ST_RELEASED], s_rel);
     if (s_quiet) atomicAdd(d.nquiet, s_quiet);
     if (s_hasjob) d.jlist[atomicAdd(&d.njobs[3], 1)] = bid;  // k_round_jobs walks the listed workgroups only
+    if (ROWS && s_need) d.m8[5] = 1;
   }
   __syncthreads();
   for (int t = tid; t < s_nslow; t += 256) d.slow[s_slowbase + t] = ((int64_t)tile << 32) | (uint32_t)s_slow[t];
@@ -1724,15 +1791,15 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 // of the workgroups, each taking blocks a multiple of 8 apart (same XCD), so
 // idle they are a small dispatch.
 template <int KB, int TW, int TPW, bool NT, bool STORM, int IN>
-__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : IN == 2 ? GH_NIB_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
+__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : (IN == 2 || IN == 4) ? GH_NIB_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
   if (*d.mode != (int)STORM) return;
   if constexpr (!STORM) {
     int want = 0;
     if (d.a4[0])
-      want = !gh_m8(d, cur) ? 3 : (KB == 4 && p.plane && d.pvalid[cur] && gh_m8(d, cur ^ 1)) ? 2 : 1;
+      want = !gh_m8(d, cur) ? 3 : (KB == 4 && p.plane && d.pvalid[cur] && gh_m8(d, cur ^ 1)) ? (d.rowlay ? 4 : 2) : 1;
     if (want != IN) return;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) d.m8[4] = STORM ? 1 : IN == 2 ? 3 : IN == 1 ? 2 : 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.m8[4] = STORM ? 1 : (IN == 2 || IN == 4) ? 3 : IN == 1 ? 2 : 0;
   if constexpr (STORM || IN == 1 || IN == 3) {
     constexpr int RB = round_rb<TW>();
     const int nblk = (int)((d.nrows + RB - 1) / RB) * ((int)(p.ld / TW) / TPW);
@@ -1740,8 +1807,8 @@ __global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM 
       round_block<KB, TW, TPW, NT, STORM, IN>(d, cur, dcur, p, b);
       __syncthreads();  // LDS of this block before the next
     }
-  } else if constexpr (IN == 2) {
-    round_block_nib<TW, NT, GH_NIB_CPL>(d, cur, p, blockIdx.x);  // one block per workgroup
+  } else if constexpr (IN == 2 || IN == 4) {
+    round_block_nib<TW, NT, GH_NIB_CPL, IN == 4>(d, cur, p, blockIdx.x);  // one block per workgroup
   } else {
     // one block per workgroup (a loop here costs the lean variants 20+ VGPRs)
     round_block<KB, TW, TPW, NT, STORM, IN>(d, cur, dcur, p, blockIdx.x);
@@ -1755,8 +1822,17 @@ __global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM 
 // listed segments of cur ^ 1, narrow where every cell of a segment has a
 // narrow code, else into a fresh slot of the next buffer's wide arena. In
 // failure storms most segments come here.
+template <int TW, int CPL>
+__device__ void redo_all(const GhDev& d, int cur, int dcur, const GhRound& p);
+
 template <int TW>
 __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, GhRound p) {
+  // the lane jobs whose segment must go wide (k_round_jobs' redo list; one
+  // thread, disjoint from the listed segments: the slow list never holds a
+  // segment with lane jobs)
+  if constexpr (TW >= 64) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && d.jobs) redo_all<TW, GH_JOB_CPL>(d, cur, dcur, p);
+  }
   constexpr int CPL = 8;
   constexpr int SEG = TW / CPL;
   constexpr int RPW = 64 / SEG;
@@ -2001,7 +2077,7 @@ __device__ __forceinline__ void job_rule(const GhDev& d, int cur, int dcur, cons
 // with the INT32_MAX refusal before the round), and, when every result has a
 // narrow code, the write of buffer cur ^ 1 (tier chunk where it fits, else
 // escaped, with its plane word). Returns false, writing nothing, when the
-// input is a wide segment or a result needs the wide arena (k_round_redo).
+// input is a wide segment or a result needs the wide arena (the redo pass, redo_all).
 __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, const GhRound& p, int i, int64_t l0,
                                           uint32_t uw, uint32_t plw, uint32_t a4w, JobAcc& acc, uint32_t& detm) {
   const int nxt = cur ^ 1;
@@ -2023,7 +2099,7 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
     xw[0] = hx.x, xw[1] = hx.y, xw[2] = hx.z, xw[3] = hx.w;
   }
   const uint32_t h0 = xw[0] & 0xFFFFu;
-  if (h0 == GH_N_WIDE || h0 == GH_N_FROZEN) return false;  // a wide input: k_round_redo
+  if (h0 == GH_N_WIDE || h0 == GH_N_FROZEN) return false;  // a wide input: the redo pass (redo_all)
   const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
   // merge candidates: from the plane codes, then (a rolled loop) the cells
   // that gather their senders' exact cells
@@ -2051,7 +2127,7 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
         const int s = d.inbox[beg + q];
         if (rmj && gh_rm_at(d, dcur, l0 + j, s)) continue;  // s REMOVEs it before sending
         // the sender's cell from its narrow code (a tier nibble or an escaped
-        // code); a wide or stopped sender segment: k_round_redo
+        // code); a wide or stopped sender segment: the redo pass (redo_all)
         const int64_t sc = gh_cell(d, s, l0 + j);
         const uint32_t sa = d.a4[cur][sc >> 3];
         uint32_t h;
@@ -2197,7 +2273,7 @@ __global__ __launch_bounds__(256, GH_JOB_WAVES) void k_round_jobs(GhDev d, int c
       bool fit = true;
       // chunk by chunk (a rolled loop: the code stays small), each written as
       // soon as it is known to fit; a chunk that needs the wide arena sends
-      // the lane to k_round_redo, which recomputes and counts it whole
+      // the lane to the redo pass (redo_all, in k_round_slow), which recomputes and counts it whole
       // (overwriting any chunk written here)
 #pragma unroll 1
       for (int w = 0; w < W && fit; ++w) {
@@ -2298,8 +2374,8 @@ __device__ __forceinline__ void redo_lane(const GhDev& d, int cur, int dcur, con
   tot.merged += a.merged;
 }
 template <int TW, int CPL>
-__global__ __launch_bounds__(64) void k_round_redo(GhDev d, int cur, int dcur, GhRound p) {
-  if (d.m8[4] != 3 || threadIdx.x != 0) return;
+__device__ void redo_all(const GhDev& d, int cur, int dcur, const GhRound& p) {
+  if (d.m8[4] != 3) return;
   const int nr = min(d.njobs[1], GH_REDO_CAP);
   const int nxt = cur ^ 1;
   JobAcc tot{};
@@ -2574,6 +2650,10 @@ void launch_peers_rows(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
   hipLaunchKernelGGL(k_peers_rows, dim3((p.n + 255) / 256), dim3(256), 0, s, d, cur, dcur, p);
 }
 
+void launch_inbox_bits(const GhDev& d, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_inbox_bits, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
+}
+
 void launch_inbox_rows(const GhDev& d, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_inbox_rows, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
 }
@@ -2626,7 +2706,12 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
       switch (variant) {
         case 0: GH_ROUND_NT(false, 3); return;
         case 2: GH_ROUND_NT(false, 1); return;
-        case 3: GH_ROUND_NT(false, 2); return;
+        case 3:
+          if (d.rowlay)
+            GH_ROUND_NT(false, 4);  // row layout: ghost senders
+          else
+            GH_ROUND_NT(false, 2);
+          return;
         default: break;
       }
     }
@@ -2688,7 +2773,7 @@ static void round_jobs(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
   if constexpr (TW >= 64) {
     const unsigned g = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, d.jobw));
     hipLaunchKernelGGL((k_round_jobs<TW, GH_JOB_CPL>), dim3(g), dim3(256), 0, s, d, cur, dcur, p);
-    hipLaunchKernelGGL((k_round_redo<TW, GH_JOB_CPL>), dim3(1), dim3(64), 0, s, d, cur, dcur, p);
+    // (its redo list: k_round_slow's first thread, launched after it)
   }
 }
 void launch_round_jobs(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void k_ghost_pack(GhDev d, int cur, const int3
     if (part == GH_GX_PLANE) {
       reinterpret_cast<uint32_t*>(out)[e * cpr + k] = d.pl[cur][cell >> 3];
     } else {
-      const uint4 x = *reinterpret_cast<const uint4*>(d.hn[cur] + cell);
+      const uint4 x = gh_ld16(d, cur, rows[e], c);  // (a tier chunk's codes decoded)
       *reinterpret_cast<uint4*>(out + (e * d.ld + c) * 2) = x;
       if ((c & (d.tw - 1)) == 0 && (x.x & 0xFFFFu) == GH_N_WIDE) atomicAdd(&wcnt[dest[e]], 1);
     }
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void k_ghost_wide(GhDev d, int cur, const int3
        idx += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = idx / d.ntiles, t = idx - e * d.ntiles;
     const int32_t s = rows[e];
-    const uint2 h = *reinterpret_cast<const uint2*>(d.hn[cur] + gh_cell(d, s, t * d.tw));
+    const uint4 h = gh_ld16(d, cur, s, t * d.tw);  // (a tier chunk is never wide)
     if ((h.x & 0xFFFFu) != GH_N_WIDE) continue;
     const int64_t slot = gh_wide_slot(h.x, h.y);
     char* o = out + (int64_t)atomicAdd(&wcur[dest[e]], 1) * rec;

@@ -12,7 +12,7 @@ the same collectives:
   join                      all_reduce(sum) of the introducer adds
   guard                     all_reduce(sum) of local present counts + |D|,
                             then of the post-REMOVE counts of undecided rows
-  pull                      all_gather of the inboxes of the local receivers
+  pull                      all_gather of the local receivers' draw-validity bytes
   ring                      all_gather of (local list length, sender position),
                             all_reduce(max) of the targets
   read-outs                 all_gather of the D bitmap, all_reduce(max) of
@@ -220,22 +220,23 @@ class ShardModel:
 
     def _inbox_pull(self, snap, active, r):
         """Receivers in the local columns draw and validate their peers
-        (k_peers_pull); the inbox rows are all_gathered."""
-        loc = np.full((self.ncs, self.k), -1, np.int64)
+        (k_peers_pull); one byte per receiver, the validity bits of its k
+        draws, is all_gathered, and every shard redraws the peers of every
+        receiver and keeps the valid ones in draw order (k_inbox_bits)."""
+        loc = np.zeros(self.ncs, np.uint8)
         for t in range(self.ncol):
             i = self.col0 + t
             if not self.alive[i] or self.n < 2:
                 continue
-            nv = 0
             for q in range(self.k):
                 s = philox.peer(self.seed, i, r, q, self.n)
                 if self.alive[s] and active[s] and snap[s, t] >= 0:
-                    loc[t, nv] = s
-                    nv += 1
-        parts = [torch.zeros((self.ncs, self.k), dtype=torch.int64) for _ in range(self.world)]
+                    loc[t] |= 1 << q
+        parts = [torch.zeros(self.ncs, dtype=torch.uint8) for _ in range(self.world)]
         dist.all_gather(parts, torch.from_numpy(loc))
-        full = torch.cat(parts).numpy()[: self.n]
-        return [[int(s) for s in row if s >= 0] for row in full]
+        bits = torch.cat(parts).numpy()[: self.n]
+        return [[philox.peer(self.seed, i, r, q, self.n) for q in range(self.k) if (int(bits[i]) >> q) & 1]
+                for i in range(self.n)]
 
     def _inbox_ring(self, snap, active, st):
         """k_ring_count / all_gather / k_ring_select / all_reduce(max)."""

@@ -230,3 +230,31 @@ def test_plane_only_ghosts(gs, oracle_mod, monkeypatch):
     finally:
         grp.close()
         orc.close()
+
+
+@pytest.mark.parametrize("world,peer_mode", [(2, 0), (4, 0), (3, 1)])
+def test_tier_rows(gs, oracle_mod, monkeypatch, world, peer_mode):
+    """The 4-bit tier on row shards: the nibble path runs on every shard
+    (tier_info variant 3) with its ghost senders' lag nibbles gathered from
+    the ghost table; lane jobs that gather their senders' codes pull the
+    ghosts' 16-bit codes first. A 1% crash through detection and REMOVE,
+    bit-exact against the oracle every round."""
+    monkeypatch.setenv("GH_PLANE", "1")
+    n = 2048
+    sched = {4: [(sc.CRASH, c) for c in sc.crash_ids(n, 0.01, 0x5EED0880 + world)]}
+    seen = {}
+
+    def check(grp, r):
+        info = grp.run("tier_info", full=True)
+        if r >= 3:
+            for g, (kept, current, escaped, variant) in enumerate(info):
+                assert kept == 1, (r, g, info)
+                seen.setdefault(variant, set()).add(r)
+
+    if peer_mode == 0:
+        run_group(gs, oracle_mod, world, rows_cfg(fanout=4, seed=0x5EED0880 + world, t_fail=8, t_cleanup=8), n, 24,
+                  sched, init=sc.full_state(n), per_round=check)
+        assert seen.get(3) and len(seen[3]) >= 18, seen  # the nibble path ran on the row shards
+    else:  # ring mode has no sender plane: the tier is off, the ghosts carry 16-bit codes
+        run_group(gs, oracle_mod, world, rows_cfg(peer_mode=1, seed=0x5EED0890, t_fail=8, t_cleanup=8), n, 16,
+                  sched, init=sc.full_state(n))

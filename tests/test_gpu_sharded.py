@@ -31,7 +31,7 @@ def compare(eng, orc, r):
     np.testing.assert_array_equal(eng.read_detectors(), orc.read_detectors(), err_msg=f"detectors r={r}")
 
 
-def run_group(gs, om, world, cfg_kw, n, rounds, sched, init=None, every=1, files=None):
+def run_group(gs, om, world, cfg_kw, n, rounds, sched, init=None, every=1, files=None, per_round=None):
     grp = gs.ShardGroup(gs.default_config(n, **cfg_kw), world)
     orc = om.Oracle(om.default_config(n, **cfg_kw), threads=8)
     try:
@@ -53,6 +53,8 @@ def run_group(gs, om, world, cfg_kw, n, rounds, sched, init=None, every=1, files
                     assert grp.repair(int(obs)) == orc.repair(int(obs))
             if r % every == 0 or r == rounds or ev:
                 compare(grp, orc, r)
+            if per_round:
+                per_round(grp, r)
     finally:
         grp.close()
 
