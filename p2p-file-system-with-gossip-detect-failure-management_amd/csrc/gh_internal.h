@@ -475,7 +475,10 @@ __host__ __device__ __forceinline__ int gh_tier_toff(int tc) {
 }
 // The 16-bit codes of a tier chunk (not escaped): lag plane word u, age word
 // a; jd = the row's own member in the chunk (0..7, its code is the plane's
-// diagonal code) or -1; toff = GhDev::toff.
+// diagonal code) or -1; toff = GhDev::toff. Invariant: a code-15 cell with an
+// age nibble 1..14 (a tier tombstone) is written only when toff !=
+// GH_TOFF_NONE, and then toff + nibble lies in 0..30 (gh_tier_toff); the
+// decode relies on it, gh_debug_raw reports a cell that breaks it.
 __device__ __forceinline__ v4u c4_dec(uint32_t u, uint32_t a, int jd, int toff) {
   v4u o;
   const uint32_t TO = (uint32_t)(toff & 0xFFFF) * 0x00010001u;  // (modulo 2^16 per half)
@@ -843,9 +846,10 @@ void launch_ring_select(const GhDev& d, int cur, int dcur, const GhRound& p, hip
 void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
 // nt = non-temporal hints on the once-touched streams of k_round
 // variant: 0 the lean one on a 16-bit input, 1 the storm one, 2 the lean one
-// on an 8-bit input by the 16-bit rule, 3 by the byte path (2 and 3: tiered
-// engines); all are launched every round and only the one k_base, the
-// input's tier and the plane select runs
+// on a 4-bit-tier input by the 16-bit rule, 3 the nibble path (2 and 3:
+// tiered engines; the nibble path's row-layout form is k_round IN = 4); all
+// are launched every round (0-2 on the side stream) and only the one k_base,
+// the input's tier and the plane select runs
 void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant);
 // the nibble path's lane jobs (tiered engines; after launch_round, before
 // launch_round_slow): k_round_jobs, then the wide redo of the rare lanes

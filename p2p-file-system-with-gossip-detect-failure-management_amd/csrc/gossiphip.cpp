@@ -2217,13 +2217,45 @@ int gh_debug_raw(void* h, int32_t row, int64_t c0, int64_t n, uint16_t* codes, i
       const int sh = gh_nib((int)(c & 7));
       const uint32_t u = (u4 >> sh) & 15u, a = (a4 >> sh) & 15u;
       const int diag = e->d.col0 + c == row;  // the plane's diagonal code
-      // u = 15: absent (age nibble 15) or a tombstone of age toff + a
+      // u = 15: absent (age nibble 15) or a tombstone of age toff + a (a
+      // tier tombstone exists only with an offset, and its age lies in
+      // 0..30: anything else is a corrupt cell, reported as an error)
+      if (u == 15u && a != 15u && (e->d.toff == GH_TOFF_NONE || e->d.toff + (int)a < 0 || e->d.toff + (int)a > 30))
+        return set_err(e, GH_EINVAL, "a tier tombstone outside the tombstone window");
       codes[c - c0] = u == 15u ? (uint16_t)(a == 15u ? GH_N_ABSENT : (GH_N_TOMB | (uint32_t)(e->d.toff + (int)a)))
                                : (uint16_t)(((GH_P_REF + 1 - diag - (int)u) << 5) | a);
     } else {
       HIPCHK(e, hipMemcpy(codes + (c - c0), e->d.hn[e->cur] + cell, 2, hipMemcpyDeviceToHost));
     }
     HIPCHK(e, hipMemcpy(bases + (c - c0), e->d.base[e->cur] + c, 4, hipMemcpyDeviceToHost));
+  }
+  return GH_OK;
+}
+
+// Debug hook (not part of the ABI header): the 4-bit tier nibbles of row
+// `row`, local columns [c0, c0 + n) of the current buffer: (lag code << 4) |
+// age nibble per cell, or 0xFF where the chunk is escaped or the buffer is
+// not in the tier.
+int gh_debug_tier(void* h, int32_t row, int64_t c0, int64_t n, uint8_t* out) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || !out || row < 0 || row >= e->n || c0 < 0 || c0 + n > e->ld) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  int32_t m8 = 0;
+  if (e->c8) HIPCHK(e, hipMemcpy(&m8, e->d.m8 + e->cur, 4, hipMemcpyDeviceToHost));
+  const int64_t slot = e->rowlay ? e->rslot_h[row] : row;
+  if (slot < 0 || slot >= e->d.nrows) return set_err(e, GH_EINVAL, "row not owned by this shard");
+  for (int64_t c = c0; c < c0 + n; ++c) {
+    out[c - c0] = 0xFF;
+    if (!m8) continue;
+    const int64_t cell = gh_cell_slot(e->d, slot, c);
+    uint32_t a4 = 0, u4 = 0, a40 = 0;
+    HIPCHK(e, hipMemcpy(&a4, e->d.a4[e->cur] + (cell >> 3), 4, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(&u4, e->d.pl[e->cur] + (cell >> 3), 4, hipMemcpyDeviceToHost));
+    a40 = a4;
+    if (gh_t4_esc(a40)) continue;
+    const int sh = gh_nib((int)(c & 7));
+    out[c - c0] = (uint8_t)((((u4 >> sh) & 15u) << 4) | ((a4 >> sh) & 15u));
   }
   return GH_OK;
 }

@@ -1784,9 +1784,9 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 }
 
 // The variants are launched every round (lean on a 16-bit input; in a
-// tiered engine also lean on an 8-bit input by the byte path and by the
-// 16-bit rule; storm); the ones k_base, the input's tier and the plane did
-// not select return at once. The byte path runs one block per workgroup; the
+// tiered engine also the nibble path on a 4-bit-tier input and the lean one
+// on it by the 16-bit rule; storm); the ones k_base, the input's tier and the
+// plane did not select return at once. The nibble path runs one block per workgroup; the
 // storm variant and the rarely selected lean ones of a tiered engine run 1/8
 // of the workgroups, each taking blocks a multiple of 8 apart (same XCD), so
 // idle they are a small dispatch.
@@ -2679,8 +2679,8 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_inbox_fill, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
 }
 
-// variant: 0 lean on a 16-bit input, 1 storm, 2 lean on an 8-bit input by
-// the 16-bit rule, 3 lean on an 8-bit input by the byte path
+// variant: 0 lean on a 16-bit input, 1 storm, 2 lean on a 4-bit-tier input
+// by the 16-bit rule, 3 the nibble path (IN 2, or IN 4 on row shards)
 template <int KB, int TW, int TPW>
 static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant) {
   constexpr int RB = round_rb<TW>();

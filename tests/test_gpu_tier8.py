@@ -1,8 +1,9 @@
-"""8-bit tier (csrc/gh_internal.h `h8`, DESIGN.md "8-bit tier"): in plane
-mode the lean round variant streams each 8-cell chunk as 8 one-byte codes
-(lag behind the member's own counter, age) and keeps the chunks no byte code
-holds -- flags, tombstones, wide and frozen markers, lags past 14, ages past
-15 -- in the 16-bit table, escaped. These tests pin that the tier is in use
+"""4-bit tier (csrc/gh_internal.h `c4_dec` / `c4_enc`, DESIGN.md "Cell
+encoding"): in plane mode every cell of a healthy chunk is a 4-bit lag code
+(which is also the sender plane) and a 4-bit age, run by the nibble path
+(k_round IN 2 / 4) and its lane jobs; chunks the tier cannot hold -- flags,
+young tombstones, wide and frozen markers, lags past the window, ages past
+min(T_fail, 15) -- are escaped to 16-bit codes. These tests pin that the tier is in use
 where it should be, that escapes happen and stay bit-exact against the
 oracle, that events, imports, quirk flag clears, list merges, storms and
 quiet rows cross it, and that it changes no result against the 16-bit table
@@ -280,7 +281,10 @@ def test_tier_tombstones(gs, oracle_mod, t_cleanup):
     hb, ts, alive = sc.full_state(n)
     eng.import_state(hb, ts, alive, 0)
     orc.import_state(hb, ts, alive, 0)
-    rel = 0
+    import ctypes as C
+    eng.lib.gh_debug_tier.argtypes = [C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p]
+    nib = np.zeros(8, np.uint8)
+    rel, tier_tombs, rel_variants, rel_jobs = 0, 0, set(), []
     for r in range(1, 34 + t_cleanup // 2):
         ev = sched.get(r, [])
         if ev:
@@ -290,5 +294,23 @@ def test_tier_tombstones(gs, oracle_mod, t_cleanup):
         assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
         rel += s1["released"]
         compare(eng, orc, r)
+        if s1["released"] and r > 3:
+            rel_variants.add(eng.tier_info(full=True)[3])
+            rel_jobs.append(eng.job_info()[0])
+        # the crashed members' columns in a few rows: a tier tombstone is
+        # lag code 15 with an age nibble 1..14 (gh_debug_tier)
+        for row in (0, 511, 1023, 2047):
+            for col in (17, 900, 1500):
+                assert eng.lib.gh_debug_tier(eng.h, row, col & ~7, 8, nib.ctypes.data_as(C.c_void_p)) == 0
+                v = int(nib[col & 7])
+                tier_tombs += v != 0xFF and (v >> 4) == 15 and 1 <= (v & 15) <= 14
     assert rel > 0
     assert eng.tier_info()[0] == 1
+    # rounds that released tombstones ran the nibble path, with few lane jobs
+    # (the tombstones age and release inside it, not as jobs)
+    assert rel_variants == {3}, rel_variants
+    assert max(rel_jobs) * 100 <= n * n // 16, rel_jobs
+    if t_cleanup < 30:  # the tier holds tombstones (gh_tier_toff)
+        assert tier_tombs > 0
+    else:
+        assert tier_tombs == 0
