@@ -548,9 +548,10 @@ __device__ __forceinline__ uint4 gh_ld16s(const GhDev& d, int buf, int64_t s, in
     return *reinterpret_cast<const uint4*>(d.gcodes + (s - d.nrows) * d.ld + c);
   const int64_t cell = gh_cell_slot(d, s, c);
   if (gh_m8(d, buf)) {
-    const uint32_t a = d.a4[buf][cell >> 3];
+    // both words at once (one memory latency, not two)
+    const uint32_t a = d.a4[buf][cell >> 3], u = d.pl[buf][cell >> 3];
     if (!gh_t4_esc(a)) {
-      const v4u w = c4_dec(d.pl[buf][cell >> 3], a, jd, d.toff);
+      const v4u w = c4_dec(u, a, jd, d.toff);
       return uint4{w[0], w[1], w[2], w[3]};
     }
   }
@@ -656,6 +657,7 @@ __device__ __forceinline__ void gh_get8(const GhDev& d, int buf, int64_t i, int6
 // Cell (i, local c) of buffer buf (for round r).
 __device__ __forceinline__ GhCell gh_get(const GhDev& d, int buf, int64_t i, int64_t c, int32_t r) {
   const int64_t c8 = c & ~(int64_t)7;
+  const int32_t b = d.base[buf][c];  // (issued beside the cell's loads)
   const uint4 hd = gh_ld16(d, buf, i, c8);
   const uint32_t h0 = hd.x & 0xFFFFu;
   if (h0 == GH_N_WIDE) {
@@ -671,7 +673,7 @@ __device__ __forceinline__ GhCell gh_get(const GhDev& d, int buf, int64_t i, int
     return GhCell{x, x == GH_ABSENT ? 0 : d.fzt[w], false};
   }
   const uint32_t hw[4] = {hd.x, hd.y, hd.z, hd.w};
-  return gh_dec16((hw[(c & 7) >> 1] >> (16 * (c & 1))) & 0xFFFFu, d.base[buf][c], r);
+  return gh_dec16((hw[(c & 7) >> 1] >> (16 * (c & 1))) & 0xFFFFu, b, r);
 }
 
 // Presence and flag bits of cells (i, c..c+7) of buffer buf (c % 8 == 0):

@@ -1506,12 +1506,17 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
           // tier sender chunks (plane and age words; unused slots: all
           // absent), all four issued, then widened one at a time (an escaped
           // one is read from hn)
+          // (row layout: a ghost sender is a row of the ghost table, 16-bit
+          // codes, not a tier chunk; in a round whose ghosts carry only their
+          // plane the lane goes to the slow list, as below)
           uint32_t su[4], sa[4];
+          bool gs[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int q = g + u;
-            const uint32_t off = psl[q] * (TW / 2) + lbp;
-            const bool ld = STORM ? q < cntv : KB > 4 ? __ballot(q < cntv) != 0 : true;
+            gs[u] = d.gcodes && q < cntv && (int64_t)psl[q] >= d.nrows;
+            const uint32_t off = (gs[u] ? islot : psl[q]) * (TW / 2) + lbp;
+            const bool ld = (STORM ? q < cntv : KB > 4 ? __ballot(q < cntv) != 0 : true) && !gs[u];
             su[u] = ld ? *reinterpret_cast<const uint32_t*>(plo_t + off) : ~0u;
             sa[u] = ld ? *reinterpret_cast<const uint32_t*>(a4o_t + off) : ~0u;
           }
@@ -1519,10 +1524,14 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
           for (int u = 0; u < 4; ++u) {
             v4u pv;
             const int js = ps[g + u] - c0;
-            if (gh_t4_esc(sa[u]))
+            if (gs[u]) {
+              bad |= p.gpo;
+              pv = p.gpo ? v4u{~0u, ~0u, ~0u, ~0u} : ldn<false>(snd16(psl[g + u]));
+            } else if (gh_t4_esc(sa[u])) {
               pv = ldn<false>(reinterpret_cast<const uint16_t*>(hno_t + (psl[g + u] * (TW * 2) + lb)));
-            else
+            } else {
               pv = c4_dec(su[u], sa[u], (unsigned)js < 8u ? js : -1, d.toff);
+            }
             fold(pv, g + u);
           }
         } else {
@@ -2128,9 +2137,20 @@ __device__ __forceinline__ bool job_chunk(const GhDev& d, int cur, int dcur, con
         if (rmj && gh_rm_at(d, dcur, l0 + j, s)) continue;  // s REMOVEs it before sending
         // the sender's cell from its narrow code (a tier nibble or an escaped
         // code); a wide or stopped sender segment: the redo pass (redo_all)
-        const int64_t sc = gh_cell(d, s, l0 + j);
-        const uint32_t sa = d.a4[cur][sc >> 3];
+        const int64_t sl = gh_slot(d, s);
         uint32_t h;
+        if (d.gcodes && sl >= d.nrows) {  // row layout: a ghost row, 16-bit codes in the ghost table
+          const uint16_t* gr = d.gcodes + (sl - d.nrows) * d.ld;
+          h = gr[l0 + j];
+          const uint32_t h0 = gr[(l0 + j) & ~(int64_t)7];
+          okg &= h0 != GH_N_WIDE && h0 != GH_N_FROZEN;
+          const int32_t off = (int32_t)((h >> 5) & 1023u);
+          if (h != GH_N_ABSENT && off != 1023 && (h >> 15) == 0)
+            m = max(m, d.base[cur][l0 + j] + off + (int32_t)((c0 + j) == s));
+          continue;
+        }
+        const int64_t sc = gh_cell_slot(d, sl, l0 + j);
+        const uint32_t sa = d.a4[cur][sc >> 3];
         if (gh_t4_esc(sa)) {
           h = d.hn[cur][sc];
           const uint32_t h0 = d.hn[cur][sc & ~(int64_t)7];

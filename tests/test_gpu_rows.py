@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import scenarios as sc
-from kat_util import KATS, kat_config, run_kat
+from kat_util import KATS_SHARDED, kat_config, run_kat
 from test_gpu_sharded import run_group
 
 pytestmark = pytest.mark.gpu
@@ -38,7 +38,7 @@ def test_row_layout_shapes(gs):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("k", KATS, ids=lambda k: k["name"])
+@pytest.mark.parametrize("k", KATS_SHARDED, ids=lambda k: k["name"])
 def test_kats_rows(gs, k, world):
     cfg = kat_config(gs, k)
     cfg.shard_layout = ROWS

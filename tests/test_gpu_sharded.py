@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import scenarios as sc
-from kat_util import KATS, kat_config, run_kat
+from kat_util import KATS_SHARDED, kat_config, run_kat
 
 pytestmark = pytest.mark.gpu
 
@@ -70,7 +70,7 @@ def test_shard_layout(gs):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("k", KATS, ids=lambda k: k["name"])
+@pytest.mark.parametrize("k", KATS_SHARDED, ids=lambda k: k["name"])
 def test_kats_sharded(gs, k, world):
     grp = gs.ShardGroup(kat_config(gs, k), world)
     try:
