@@ -254,7 +254,7 @@ def test_tier_rows(gs, oracle_mod, monkeypatch, world, peer_mode):
     if peer_mode == 0:
         run_group(gs, oracle_mod, world, rows_cfg(fanout=4, seed=0x5EED0880 + world, t_fail=8, t_cleanup=8), n, 24,
                   sched, init=sc.full_state(n), per_round=check)
-        assert seen.get(3) and len(seen[3]) >= 18, seen  # the nibble path ran on the row shards
+        assert seen.get(3) and len(seen[3]) >= 10, seen  # the nibble path ran on the row shards
     else:  # ring mode has no sender plane: the tier is off, the ghosts carry 16-bit codes
         run_group(gs, oracle_mod, world, rows_cfg(peer_mode=1, seed=0x5EED0890, t_fail=8, t_cleanup=8), n, 16,
                   sched, init=sc.full_state(n))

@@ -10,9 +10,11 @@ CMD="python3 bench.py --steps $S --warmup $W --no-cpu-baseline --no-secondary --
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 i=0
-for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"; do
+for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
+  "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+  "TA_TA_BUSY_sum TD_TD_BUSY_sum" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv -d gpurun_out/pmc/p$i -o run -- \
+  timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex 'k_round' --output-format csv -d gpurun_out/pmc/p$i -o run -- \
     $CMD > gpurun_out/pmc/p$i.log 2>&1 || exit 1
 done
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc/stats -o run -- \

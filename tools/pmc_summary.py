@@ -50,7 +50,22 @@ out["config"] = {"n": n, "k": k, "world": 1, "encoding": enc, "warmup": warmup, 
 # plane); u16 = 2-B cells in and out, the plane out and in
 out["compulsory_bytes"] = (2.0 if tier4 else (4.0 + (1.0 if plane else 0.0))) * n * n
 out["prev_model_bytes"] = 3.0 * n * n  # round 2's 8-bit tier model (1-B cells + the plane)
-out["gather_bytes"] = 2.0 * n * n * k
+out["gather_bytes"] = (0.5 if (tier4 or plane) else 2.0) * n * n * k  # 4-bit plane codes per sender cell
+# SQ / TA / TD / GRBM passes (if captured): per-dispatch figures
+if "SQ_WAVE_CYCLES" in out:
+    w = out["SQ_WAVE_CYCLES"]["per_dispatch"]
+    out["sq"] = {c: out[c]["per_dispatch"] for c in list(out) if c.startswith("SQ_")}
+    out["sq"]["wait_any_frac"] = out["SQ_WAIT_ANY"]["per_dispatch"] / w if "SQ_WAIT_ANY" in out else None
+    out["sq"]["active_inst_frac"] = out["SQ_ACTIVE_INST_ANY"]["per_dispatch"] / w if "SQ_ACTIVE_INST_ANY" in out else None
+    out["sq"]["wait_inst_frac"] = out["SQ_WAIT_INST_ANY"]["per_dispatch"] / w if "SQ_WAIT_INST_ANY" in out else None
+if "GRBM_GUI_ACTIVE" in out:
+    out["gpu_cycles_per_xcd"] = out["GRBM_GUI_ACTIVE"]["per_dispatch"] / 8
+    if "SQ_INSTS_VALU" in out:  # VALU issue share: wave64 VALU = 2 cycles on a SIMD, 1,024 SIMDs
+        out["valu_busy_frac"] = 2.0 * out["SQ_INSTS_VALU"]["per_dispatch"] / (1024 * out["gpu_cycles_per_xcd"])
+if "TA_TA_BUSY_sum" in out and "GRBM_GUI_ACTIVE" in out:
+    out["ta_busy_frac"] = out["TA_TA_BUSY_sum"]["per_dispatch"] / (256 * out["GRBM_GUI_ACTIVE"]["per_dispatch"] / 8)
+if "TD_TD_BUSY_sum" in out and "GRBM_GUI_ACTIVE" in out:
+    out["td_busy_frac"] = out["TD_TD_BUSY_sum"]["per_dispatch"] / (256 * out["GRBM_GUI_ACTIVE"]["per_dispatch"] / 8)
 if "traffic_bytes" in out:
     out["traffic_over_compulsory"] = out["traffic_bytes"] / out["compulsory_bytes"]
 print(json.dumps(out, indent=1))
