@@ -14,11 +14,16 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 G = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 out = {"n": n, "world": G, "k": 4, "transport": "LOCAL (one GPU)"}
-for layout, pm in (("columns", "pull"), ("rows", "pull"), ("rows", "ring")):
+only = os.environ.get("GH_EXCHANGE_ONLY")  # e.g. "rows_ring"
+# (single: one engine over the whole table, the reference point of each mode)
+for layout, pm in (("columns", "pull"), ("rows", "pull"), ("rows", "ring"), ("columns", "ring"),
+                   ("single", "pull"), ("single", "ring")):
+    if only and f"{layout}_{pm}" not in only.split(","):
+        continue
     cfg = gs.default_config(n, fanout=4, seed=0x5EED0003, t_fail=16, t_cleanup=16,
                             peer_mode=gs.GH_PEER_RING if pm == "ring" else gs.GH_PEER_PULL,
                             shard_layout=gs.GH_LAYOUT_ROWS if layout == "rows" else gs.GH_LAYOUT_COLUMNS)
-    grp = gs.ShardGroup(cfg, G)
+    grp = gs.ShardGroup(cfg, 1 if layout == "single" else G)
     try:
         grp.run("init_full", 2, 0, 0)
         grp.run("step", 12)
