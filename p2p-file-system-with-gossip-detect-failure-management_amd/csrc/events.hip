@@ -79,6 +79,9 @@ __global__ __launch_bounds__(256) void k_seg(GhDev d, int buf, SegSet set, const
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int64_t total = set.count();
+  // the ops' counters, summed per wave and added once (one global atomic
+  // per cell serialised a 1% LEAVE wave's 43 M tombstones: 0.5 s)
+  uint32_t tal[2] = {0u, 0u};
   for (int64_t s0 = wave * RPW; s0 < total; s0 += nw * RPW) {
     const int64_t sid = s0 + sub;
     const bool valid = sid < total;
@@ -93,7 +96,7 @@ __global__ __launch_bounds__(256) void k_seg(GhDev d, int buf, SegSet set, const
       gh_dec8(d, buf, i, c, p.r, x, v);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const GhCell y = op(i, c + j, v[j]);
+        const GhCell y = op(i, c + j, v[j], tal);
         changed |= !same(y, v[j]);
         v[j] = y;
       }
@@ -115,24 +118,34 @@ __global__ __launch_bounds__(256) void k_seg(GhDev d, int buf, SegSet set, const
     if (slot < 0) continue;  // arena full: the state is lost (d.err)
     gh_put8(d, buf, i, c, narrow, nx, slot, v);
   }
+  if constexpr (Op::kTally) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      tal[0] += __shfl_xor(tal[0], o);
+      tal[1] += __shfl_xor(tal[1], o);
+    }
+    if (lane == 0 && (tal[0] | tal[1])) op.flush(tal);
+  }
 }
 
 struct OpFill {
+  static constexpr bool kTally = false;
   GhDev d;
   int32_t hb0, ts0;
   GhRound p;
-  __device__ GhCell operator()(int64_t i, int64_t c, const GhCell&) const {
+  __device__ GhCell operator()(int64_t i, int64_t c, const GhCell&, uint32_t*) const {
     if (c >= d.ncol) return gh_absent();
     return external(hb0, ts0, d.col0 + c, i, p);
   }
 };
 
 struct OpPack {
+  static constexpr bool kTally = false;
   GhDev d;
   const int32_t *hb_rows, *ts_rows;
   int64_t row0;
   GhRound p;
-  __device__ GhCell operator()(int64_t i, int64_t c, const GhCell& v) const {
+  __device__ GhCell operator()(int64_t i, int64_t c, const GhCell& v, uint32_t*) const {
     if (c >= d.ncol) return v;
     const int64_t src = (i - row0) * d.n + d.col0 + c;
     return external(hb_rows[src], ts_rows[src], d.col0 + c, i, p);
@@ -141,37 +154,45 @@ struct OpPack {
 
 // Fresh joiner processes start with an empty MemberList (SPEC D7).
 struct OpReset {
-  __device__ GhCell operator()(int64_t, int64_t, const GhCell&) const { return gh_absent(); }
+  static constexpr bool kTally = false;
+  __device__ GhCell operator()(int64_t, int64_t, const GhCell&, uint32_t*) const { return gh_absent(); }
 };
 
 // LEAVE from each leaver c to every alive member j of c's list (j != c):
 // removeMember(c) at j. colq[c] = the leaver's index q in the gathered
 // bitmaps rbits [world][nl][ncsw] (-1: not a leaver).
 struct OpLeave {
+  static constexpr bool kTally = true;  // tombstoned, unknown
   GhDev d;
   int32_t nl;
-  __device__ GhCell operator()(int64_t j, int64_t c, const GhCell& v) const {
+  __device__ GhCell operator()(int64_t j, int64_t c, const GhCell& v, uint32_t* t) const {
     const int q = d.colq[c];
     if (q < 0 || !d.alive[j] || d.col0 + c == j || !gh_gbit(d, d.rbits, nl, q, j)) return v;
     if (v.x >= 0) {
-      atomicAdd(&d.stats[ST_TOMBSTONED], 1ull);
+      t[0]++;
       return GhCell{GH_TOMBSTONE, v.ts, false};  // keeps its ts (slave/slave.go:280)
     }
-    if (v.x == GH_ABSENT) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], 1ull);
+    if (v.x == GH_ABSENT) t[1]++;
     return v;
+  }
+  __device__ void flush(const uint32_t* t) const {
+    if (t[0]) atomicAdd(&d.stats[ST_TOMBSTONED], (unsigned long long)t[0]);
+    if (t[1]) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], (unsigned long long)t[1]);
   }
 };
 
 // addNewMember at the introducer (slave/slave.go:250-255) for the joiners
 // whose column is local (colq[c] >= 0). nd[4] counts this shard's adds.
 struct OpJoinAdd {
+  static constexpr bool kTally = true;  // adds
   GhDev d;
   GhRound p;
-  __device__ GhCell operator()(int64_t, int64_t c, const GhCell& v) const {
+  __device__ GhCell operator()(int64_t, int64_t c, const GhCell& v, uint32_t* t) const {
     if (d.colq[c] < 0 || v.x >= 0) return v;
-    atomicAdd(&d.nd[4], 1);
+    t[0]++;
     return GhCell{0, p.r, false};  // hb 0, ts = now
   }
+  __device__ void flush(const uint32_t* t) const { atomicAdd(&d.nd[4], (int)t[0]); }
 };
 
 // The introducer's full list to every alive member of it (:256-272), merged
@@ -182,12 +203,14 @@ struct OpJoinBcast {
   int cur;
   int32_t I;
   GhRound p;
-  __device__ GhCell operator()(int64_t j, int64_t c, const GhCell& v) const {
+  static constexpr bool kTally = true;  // merges
+  __device__ void flush(const uint32_t* t) const { atomicAdd(&d.stats[ST_MERGED], (unsigned long long)t[0]); }
+  __device__ GhCell operator()(int64_t j, int64_t c, const GhCell& v, uint32_t* t) const {
     if (c >= d.ncol || j == I || !d.alive[j] || !gh_gbit(d, d.rbits, 1, 0, j)) return v;
     const GhCell m = gh_get(d, cur, I, c, p.r);
     if (m.x < 0) return v;
     if (v.x >= GH_ABSENT && m.x > v.x) {
-      atomicAdd(&d.stats[ST_MERGED], 1ull);
+      t[0]++;
       return GhCell{m.x, p.r, gh_flag_for(m.x, p.r, d.col0 + c, j, p.r, p.t_fail)};  // ts = now
     }
     return v;
@@ -200,10 +223,12 @@ struct OpJoinBcast {
 struct OpMergeList {
   GhDev d;
   GhRound p;
-  __device__ GhCell operator()(int64_t obs, int64_t c, const GhCell& v) const {
+  static constexpr bool kTally = true;  // merges
+  __device__ void flush(const uint32_t* t) const { atomicAdd(&d.nd[5], (int)t[0]); }
+  __device__ GhCell operator()(int64_t obs, int64_t c, const GhCell& v, uint32_t* t) const {
     const int32_t m = d.colq[c];
     if (m < -2 || !(v.x >= GH_ABSENT && m > v.x)) return v;  // :424-426, :435-438; tombstones blocked (:432-434)
-    atomicAdd(&d.nd[5], 1);
+    t[0]++;
     return GhCell{m, p.r - 1, gh_flag_for(m, p.r - 1, d.col0 + c, obs, p.r, p.t_fail)};
   }
 };
