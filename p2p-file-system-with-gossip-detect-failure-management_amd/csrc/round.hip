@@ -590,7 +590,10 @@ __device__ __forceinline__ void base_col(const GhDev& d, int cur, int dcur, cons
     // that need the per-cell rule in the lean variant (flagged, tombstone,
     // guard rows); flags are set one round ahead, so a detection wave is
     // seen the round before it happens
-    const int64_t measure = (int64_t)*d.nstorm + *d.slow_n;
+    // (quiet segments count too: a collapsed cluster stays on the storm
+    // variant, whose quiet skip holds while the output tier does not change;
+    // on the nibble or 4-slot lean variant its guard rows would be listed)
+    const int64_t measure = (int64_t)*d.nstorm + *d.slow_n + *d.nquiet;
     // ... or when the last round's lane jobs (k_round_jobs) were more than a
     // quarter of the lanes: beyond that the packed storm rule is cheaper than
     // the per-cell one
@@ -1248,7 +1251,13 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
       if (d.rowlay) s_isl[t] = d.rslot[sv];
     }
   }
-  __syncthreads();
+  // every row of the workgroup quiet (a collapsed cluster): a tile whose
+  // bases stayed is skipped whole, its row segments counted as quiet
+  bool myq = true;
+  for (int row = tid; row < RB; row += 256)
+    if ((int)d.row0 + rb * RB + row < rowend) myq &= ((s_meta[row] >> 30) & 1) != 0;
+  const bool allq = __syncthreads_and(myq) != 0;
+  const int nvrows = min(RB, rowend - ((int)d.row0 + rb * RB));
 
   const uint16_t* __restrict__ hno = d.hn[cur];
   uint16_t* __restrict__ hnn = d.hn[cur ^ 1];
@@ -1327,6 +1336,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   const uint32_t tfp = (uint32_t)min(p.t_fail, 31) * 0x10001u;
   // tombstone age + tsk carries into bit 5 iff age >= the saturation age
   const uint32_t tsk = (uint32_t)(32 - (d.tsa ? d.tsa : GH_N_TAGEMAX)) * 0x10001u;
+  // ... and into bit 5 iff age > tsa with saturation (never written by the
+  // round: such a cell goes to the per-cell rule, which caps it), else as tsk
+  const uint32_t tsk1 = d.tsa ? (uint32_t)(31 - d.tsa) * 0x10001u : tsk;
+  const uint32_t tsm = d.tsa ? 0xFFFFFFFFu : 0u;  // tombstone ages saturate at tsa (SPEC §1)
   const uint32_t tcp = (uint32_t)min(p.t_cleanup, 31) * 0x10001u;
   __syncthreads();
   const bool tile_still = s_bmove == 0;
@@ -1341,8 +1354,10 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
   }
 
   constexpr int NIT = RB / RSTEP;
+  const bool tile_quiet = allq && tile_still;
+  if (tile_quiet && tid == 0) atomicAdd(&s_quiet, nvrows);
 #pragma unroll 1
-  for (int it = 0; it < NIT; ++it) {
+  for (int it = 0; it < (tile_quiet ? 0 : NIT); ++it) {
     const int rr = wave * RPW + it * RSTEP + sub;
     const int i_raw = (int)d.row0 + rb * RB + rr;
     const bool valid = i_raw < rowend;
@@ -1619,9 +1634,13 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         const uint32_t z = pk_add_u16(x | 0x001F001Fu, 0x00010001u);
         const uint32_t ta0 = pk_zero_mask(z);                  // tombstone or absent
         const uint32_t ab = pk_zero_mask(pk_add_u16(x, 0x00010001u));  // absent
-        acc |= ((x & 0x001F001Fu) + tsk) & ~ab & ta0 & 0x00200020u;  // tombstone age >= tsa (saturation)
+        // a tombstone at its saturation age keeps it (slave/slave.go:490 only
+        // compares it with now - COOLDOWN); beyond it (or at the 16-bit cap
+        // without saturation) the per-cell rule takes the segment
+        const uint32_t satb = ((((x & 0x001F001Fu) + tsk) & 0x00200020u) >> 5) & ~ab & ta0 & tsm;
+        acc |= ((x & 0x001F001Fu) + tsk1) & ~ab & ta0 & 0x00200020u;
         mm = 0u;
-        y0 = (((x & 0x7FE07FE0u) | 0x00010001u) & ~ta0) | (pk_adds_u16(x, 0x00010001u) & ta0);
+        y0 = (((x & 0x7FE07FE0u) | 0x00010001u) & ~ta0) | (pk_adds_u16(x, 0x00010001u & ~satb) & ta0);
         npre = ta0;
         stb = ~0u;  // a guard row: what the lean variant lists
       } else {
@@ -1645,14 +1664,16 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
         // when T_cleanup reaches the age field and st says "fresh")
         const uint32_t keep = ((ta & ~ab) | fl) & ~st;
         const uint32_t nowm = ~ta & ~actm;                     // guard rows: present cells stamped now
-        // age >= 30 or wide marker; a guard row's tombstone at its saturation age
-        acc |= (((ag + 0x00020002u) & ~ab & ~nowm) | ((ag + tsk) & ta & ~ab & ~actm)) & 0x00200020u;
+        // age >= 30 or wide marker; a guard row's tombstone beyond its
+        // saturation age (at it, it keeps its age: satb)
+        acc |= (((ag + 0x00020002u) & ~ab & ~nowm) | ((ag + tsk1) & ta & ~ab & ~actm)) & 0x00200020u;
+        const uint32_t satb = (((ag + tsk) & 0x00200020u) >> 5) & ta & ~ab & tsm;
         const uint32_t key = ((xr & ~(nowm & 0x80008000u)) | 0x001F001Fu) | rel;  // heartbeat key (absent: -1)
         mm = pk_sra15(pk_subs_i16(key, m)) & ~keep;            // merged (step 6)
         // not merged: age + 1 (a detected cell becomes a tombstone of its
         // age), released cells absent, absent stays absent; guard rows'
         // present cells age 1
-        const uint32_t yact = pk_adds_u16(xr | (fl & 0xFFE0FFE0u), 0x00010001u) | rel;
+        const uint32_t yact = pk_adds_u16(xr | (fl & 0xFFE0FFE0u), 0x00010001u & ~satb) | rel;
         y0 = (((xr & 0x7FE07FE0u) | 0x00010001u) & nowm) | (yact & ~nowm);
         npre = ta0;
         stb |= ((fl0 | ta) & ~ab) | (LEAN_GUARD ? 0u : ~actm);  // what the lean variant lists
