@@ -279,6 +279,11 @@ struct GhDev {
   // one round ago). A collapsed cluster stops rewriting its tables.
   uint8_t *stab[2];
   int32_t *nquiet;  // row segments the last round skipped as quiet
+  // one engine, column layout: aq[0] != 0 when a running row of this round
+  // is not a quiet candidate or a column base moved (k_peers_pull /
+  // k_inbox_fill, base_col; reset by k_finish); else k_round has nothing to
+  // read or write and every variant returns at once
+  int32_t *aq;
   // MemberList order (GH_ORDER_APPEND, order.hip; null under GH_ORDER_ID).
   // Generation g (the host's lcur) of row i: the list is lord[lsel[g][i]] +
   // i * ld (member at each position), llen[g][i] entries, the row's own

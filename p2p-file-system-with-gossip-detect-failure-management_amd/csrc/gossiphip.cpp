@@ -1099,7 +1099,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.nflag, 2, 0)) || (rc = dalloc(e, &d.pvalid, 2, 0)) ||
         (rc = dalloc(e, &d.pfb, 1, 0)) ||
         (rc = dalloc(e, &d.stab[0], e->n, 0)) || (rc = dalloc(e, &d.stab[1], e->n, 0)) ||
-        (rc = dalloc(e, &d.nquiet, 1, 0)))
+        (rc = dalloc(e, &d.nquiet, 1, 0)) || (rc = dalloc(e, &d.aq, 1, 0x01)))
       break;
     if (e->plane && ((rc = dalloc(e, &d.pl[0], cells / 8, 0xFF)) || (rc = dalloc(e, &d.pl[1], cells / 8, 0xFF))))
       break;

@@ -192,6 +192,7 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
   const uint32_t grp = (uint32_t)(m >> (lane & ~7)) & 0xFFu;  // this receiver's valid draws
   if (ok) d.inbox[beg + __builtin_popcount(grp & ((1u << q) - 1u))] = s;
   if (inr && q == 0) {
+    if (t < d.ncol && d.alive[i] && (d.active[i] || grp || !d.stab[p.r & 1][i])) d.aq[0] = 1;  // not quiet
     d.inbox[beg - 1] = __builtin_popcount(grp);
     if (d.pvb) d.pvb[i] = (uint8_t)grp;  // G > 1: the bits travel, not the inbox (k_inbox_bits)
   }
@@ -545,6 +546,7 @@ __global__ __launch_bounds__(1024) void k_inbox_scan(GhDev d, GhRound p) {
 __global__ __launch_bounds__(256) void k_inbox_fill(GhDev d, GhRound p) {
   const int s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= p.n) return;
+  if (d.alive[s] && (d.active[s] || d.inbox_cnt[s] || !d.stab[p.r & 1][s])) d.aq[0] = 1;  // row s is not quiet
   for (int q = 0; q < 3; ++q) {
     const int t = d.targets[(int64_t)s * 3 + q];
     if (t >= 0 && d.alive[t]) {
@@ -629,7 +631,8 @@ __device__ __forceinline__ void base_col(const GhDev& d, int cur, int dcur, cons
     *d.pfb = 0;
   }
   if (c >= p.ld) return;
-  int32_t b = d.base[cur][c];
+  const int32_t b0 = d.base[cur][c];
+  int32_t b = b0;
   const int64_t cg = d.col0 + c;
   if (c < d.ncol && cg < p.n && gh_owned(d, cg)) {
     const GhCell v = gh_get(d, cur, cg, c, p.r);
@@ -638,6 +641,7 @@ __device__ __forceinline__ void base_col(const GhDev& d, int cur, int dcur, cons
     b = INT_MIN;  // the owner of row cg decides; the host takes the max over shards
   }
   d.base[cur ^ 1][c] = b;
+  if (b != b0 && d.aq) d.aq[0] = 1;
 }
 __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRound p) {
   base_col(d, cur, dcur, p, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
@@ -1830,6 +1834,12 @@ __global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM 
     if (want != IN) return;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) d.m8[4] = STORM ? 1 : (IN == 2 || IN == 4) ? 3 : IN == 1 ? 2 : 0;
+  // every running row a quiet candidate and no base moved (one engine): the
+  // round reads and writes nothing (a collapsed cluster)
+  if (d.world == 1 && !d.rowlay && d.aq[0] == 0 && d.cntg[p.n] == 0 && !p.force_slow && !(d.a4[0] && d.m8[2])) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *d.nquiet = (int)min<int64_t>(d.ntiles * d.nrows, INT_MAX);
+    return;
+  }
   if constexpr (STORM || IN == 1 || IN == 3) {
     constexpr int RB = round_rb<TW>();
     const int nblk = (int)((d.nrows + RB - 1) / RB) * ((int)(p.ld / TW) / TPW);
@@ -2456,6 +2466,7 @@ __global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int dnew = dcur ^ 1;
   bool has = false;
+  if (x == 0) d.aq[0] = 0;  // the next round's writers of base_col / the inbox pass set it
   if (x < p.ld) {
     has = d.det_cnt[dnew][x] > 0;
     d.det_cnt[dcur][x] = 0;
