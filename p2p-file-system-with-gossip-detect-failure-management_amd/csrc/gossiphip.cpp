@@ -58,6 +58,7 @@ struct Engine {
   int force_storm = 0;   // storm variant every round (GH_FORCE_STORM, diagnostics)
   int force_slow = 0;    // every segment by the per-cell rule (GH_FORCE_SLOW, diagnostics)
   bool timing = false;
+  bool side = true;      // idle round variants on the side stream (GH_SIDE=0: in line)
   // the current table may hold flags no round kernel counted (import, fill,
   // events, list merges): the next quirk pre-pass runs ungated
   bool qforce = true;
@@ -1001,6 +1002,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   // half of it the plane itself (its window is the plane's: lags of healthy
   // pull dissemination); the row layout ships 16-bit ghost rows
   e->c8 = e->plane && e->tpw == 1 && tw >= 64;
+  if (const char* v = std::getenv("GH_SIDE")) e->side = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_C8")) e->c8 = e->c8 && std::atoi(v) != 0;
   if (cfg->shard_layout != GH_LAYOUT_COLUMNS && cfg->shard_layout != GH_LAYOUT_ROWS) {
     delete e;
@@ -1044,8 +1046,13 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   e->lorder = cfg->list_order == GH_ORDER_APPEND;
   const int64_t pad = std::max<int64_t>(GH_PAD, 8 * (int64_t)tw);
   e->ld = (ncs + pad - 1) / pad * pad;
+  // the idle round variants' side stream at the highest priority: their
+  // workgroups (which return at once) dispatch ahead of the nibble path's
+  // instead of queueing behind all of them
+  int prio_lo = 0, prio_hi = 0;
+  if (!dry) (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (!dry && (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-               hipStreamCreateWithFlags(&e->vstream, hipStreamNonBlocking) != hipSuccess ||
+               hipStreamCreateWithPriority(&e->vstream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
                hipEventCreateWithFlags(&e->vfork, hipEventDisableTiming) != hipSuccess ||
                hipEventCreateWithFlags(&e->vjoin, hipEventDisableTiming) != hipSuccess)) {
     delete e;
@@ -1748,7 +1755,18 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     pr.gpo = e->gpo;  // row layout: the ghosts carry only their plane so far
     // the variants of k_round; the ones not selected return at once
     // (events 6q + 0..3 bracket variants 0..2, 6q + 4..5 the last one)
-    if (e->c8) {
+    if (e->c8 && !e->side) {
+      // lean 16-bit input, storm, lean tier input by the 16-bit rule, then
+      // the nibble path, all on the round's stream
+      for (int v = 0; v < 3; ++v) {
+        if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + v], e->stream));
+        launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v);
+      }
+      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 3], e->stream));
+      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 4], e->stream));
+      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, 3);
+      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 5], e->stream));
+    } else if (e->c8) {
       // lean 16-bit input, storm, lean tier input by the 16-bit rule on the
       // side stream, beside the nibble path
       HIPCHK(e, hipEventRecord(e->vfork, e->stream));

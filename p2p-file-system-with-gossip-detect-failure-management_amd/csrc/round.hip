@@ -1865,14 +1865,17 @@ __global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM 
 template <int TW, int CPL>
 __device__ void redo_all(const GhDev& d, int cur, int dcur, const GhRound& p);
 
+// The lane jobs whose segment must go wide (k_round_jobs' redo list): one
+// thread, in a kernel of its own (a one-wave grid: its private arrays would
+// give every wave of a large grid a scratch allocation, 70 us of dispatch),
+// disjoint from the slow list's segments (which never hold lane jobs).
+template <int TW>
+__global__ __launch_bounds__(64) void k_round_redo(GhDev d, int cur, int dcur, GhRound p) {
+  if (threadIdx.x == 0) redo_all<TW, GH_JOB_CPL>(d, cur, dcur, p);
+}
+
 template <int TW>
 __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, GhRound p) {
-  // the lane jobs whose segment must go wide (k_round_jobs' redo list; one
-  // thread, disjoint from the listed segments: the slow list never holds a
-  // segment with lane jobs)
-  if constexpr (TW >= 64) {
-    if (blockIdx.x == 0 && threadIdx.x == 0 && d.jobs) redo_all<TW, GH_JOB_CPL>(d, cur, dcur, p);
-  }
   constexpr int CPL = 8;
   constexpr int SEG = TW / CPL;
   constexpr int RPW = 64 / SEG;
@@ -2324,7 +2327,7 @@ __global__ __launch_bounds__(256, GH_JOB_WAVES) void k_round_jobs(GhDev d, int c
       bool fit = true;
       // chunk by chunk (a rolled loop: the code stays small), each written as
       // soon as it is known to fit; a chunk that needs the wide arena sends
-      // the lane to the redo pass (redo_all, in k_round_slow), which recomputes and counts it whole
+      // the lane to the redo pass (redo_all, k_round_redo), which recomputes and counts it whole
       // (overwriting any chunk written here)
 #pragma unroll 1
       for (int w = 0; w < W && fit; ++w) {
@@ -2825,7 +2828,7 @@ static void round_jobs(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
   if constexpr (TW >= 64) {
     const unsigned g = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, d.jobw));
     hipLaunchKernelGGL((k_round_jobs<TW, GH_JOB_CPL>), dim3(g), dim3(256), 0, s, d, cur, dcur, p);
-    // (its redo list: k_round_slow's first thread, launched after it)
+    hipLaunchKernelGGL((k_round_redo<TW>), dim3(1), dim3(64), 0, s, d, cur, dcur, p);
   }
 }
 void launch_round_jobs(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
