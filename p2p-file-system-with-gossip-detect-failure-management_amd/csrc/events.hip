@@ -89,6 +89,7 @@ __global__ __launch_bounds__(256) void k_seg(GhDev d, int buf, SegSet set, const
     if (valid) set.at(sid, i, t);
     const int64_t c = t * TW + lc * 8;
     bool changed = force, fit = true;
+    int dpres = 0;  // present after - present before, this lane's cells
     GhCell v[8];
     uint4 x = {0u, 0u, 0u, 0u}, nx = {0u, 0u, 0u, 0u};
     if (valid) {
@@ -98,12 +99,20 @@ __global__ __launch_bounds__(256) void k_seg(GhDev d, int buf, SegSet set, const
       for (int j = 0; j < 8; ++j) {
         const GhCell y = op(i, c + j, v[j], tal);
         changed |= !same(y, v[j]);
+        dpres += (y.x >= 0) - (v[j].x >= 0);
         v[j] = y;
       }
       nx = gh_enc8(d, buf, c, p.r, v, fit);
     }
     const bool any = (__ballot(changed) & gmask) != 0;
     const bool narrow = (__ballot(valid && !fit) & gmask) == 0;
+    // the row's present count follows the segment (no full recount after
+    // events: k_count reads the whole table, 2.3 ms at N=65,536)
+    if (__ballot(dpres != 0) != 0) {
+#pragma unroll
+      for (int o = SEG / 2; o > 0; o >>= 1) dpres += __shfl_xor(dpres, o);
+      if (valid && lc == 0 && dpres != 0) atomicAdd(&d.cntl[i], dpres);
+    }
     if (!valid || !any) continue;
     int64_t slot = 0;
     if (!narrow) {

@@ -836,7 +836,7 @@ int process_events(Engine* e, int32_t r) {
     }
     launch_join_bcast(e->d, e->cur, I, p, e->stream);
   }
-  launch_count(e->d, e->cur, p, e->stream);
+  // (the row counts followed every segment the events rewrote: k_seg)
   HIPCHK(e, hipGetLastError());
   if (e->lorder) {
     // list order (order.hip): a fresh process starts from an empty list;
@@ -1984,7 +1984,6 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
     launch_merge_list(e->d, e->cur, observer, st.as<int32_t>(), st.as<int32_t>() + n, n, p, e->stream);
     HIPCHK(e, hipGetLastError());
     if ((rc = allreduce_i32(e, e->d.nd + 5, e->d.nd + 5, 1))) return rc;
-    launch_count(e->d, e->cur, p, e->stream);  // presence changed: refresh the row counts
     if (e->lorder) {  // added members in datagram order (:433-437), then the row back in place
       if ((rc = upload(e, e->rows_buf, {observer}))) return rc;
       launch_list_events(e->d, e->cur, e->lcur, e->rows_buf, 1, st.as<int32_t>(), (int32_t)n, -1, -1, e->stream);
