@@ -284,6 +284,12 @@ struct GhDev {
   // k_inbox_fill, base_col; reset by k_finish); else k_round has nothing to
   // read or write and every variant returns at once
   int32_t *aq;
+  // one tiered engine, column layout: each row's nibble-path record, written
+  // by k_peers_pull: nmeta[i] (alive | active << 1 | senders << 2 | quiet
+  // candidate << 30) and nsnd[4 i .. 4 i + 3] (the senders, unused slots the
+  // row itself), so a nibble workgroup stages its rows with two coalesced
+  // loads per row instead of five scattered ones per (row, slot)
+  int32_t *nmeta, *nsnd;
   // MemberList order (GH_ORDER_APPEND, order.hip; null under GH_ORDER_ID).
   // Generation g (the host's lcur) of row i: the list is lord[lsel[g][i]] +
   // i * ld (member at each position), llen[g][i] entries, the row's own

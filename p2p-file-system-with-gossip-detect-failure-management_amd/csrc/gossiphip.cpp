@@ -1108,6 +1108,10 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.stab[0], e->n, 0)) || (rc = dalloc(e, &d.stab[1], e->n, 0)) ||
         (rc = dalloc(e, &d.nquiet, 1, 0)) || (rc = dalloc(e, &d.aq, 1, 0x01)))
       break;
+    const char* nrec_env = std::getenv("GH_NREC");  // 0: stage the rows from the inboxes (A/B)
+    if (e->c8 && world == 1 && !rowlay && cfg->peer_mode == GH_PEER_PULL && !(nrec_env && std::atoi(nrec_env) == 0) &&
+        ((rc = dalloc(e, &d.nmeta, e->n, 0)) || (rc = dalloc(e, &d.nsnd, 4 * (size_t)e->n, 0))))
+      break;
     if (e->plane && ((rc = dalloc(e, &d.pl[0], cells / 8, 0xFF)) || (rc = dalloc(e, &d.pl[1], cells / 8, 0xFF))))
       break;
     // 4-bit tier: every chunk escaped (age word 0), both buffers 16-bit

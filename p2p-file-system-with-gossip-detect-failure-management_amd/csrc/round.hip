@@ -191,6 +191,29 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
   const int lane = threadIdx.x & 63;
   const uint32_t grp = (uint32_t)(m >> (lane & ~7)) & 0xFFu;  // this receiver's valid draws
   if (ok) d.inbox[beg + __builtin_popcount(grp & ((1u << q) - 1u))] = s;
+  if (d.nsnd) {  // the nibble path's row record (one engine: receivers are rows 0..n-1, k <= 4)
+    const int b8 = lane & ~7;
+    int sq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) sq[u] = __shfl(s, b8 + u);
+    if (inr && q == 0 && t < d.ncol) {
+      int rec[4], nv = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) rec[u] = (int)i;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if ((grp >> u) & 1u) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            if (v == nv) rec[v] = sq[u];
+          nv++;
+        }
+      const int al = d.alive[i], act = d.active[i];
+      const bool quiet = d.cntg[p.n] == 0 && !p.force_slow && !d.m8[2];
+      d.nmeta[i] = al | (act << 1) | (nv << 2) | ((quiet && al && !act && nv == 0 && d.stab[p.r & 1][i]) ? 1 << 30 : 0);
+      *reinterpret_cast<int4*>(d.nsnd + 4 * i) = int4{rec[0], rec[1], rec[2], rec[3]};
+    }
+  }
   if (inr && q == 0) {
     if (t < d.ncol && d.alive[i] && (d.active[i] || grp || !d.stab[p.r & 1][i])) d.aq[0] = 1;  // not quiet
     d.inbox[beg - 1] = __builtin_popcount(grp);
@@ -914,7 +937,20 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const bool quiet = d.cntg[p.n] == 0 && !p.force_slow && !d.m8[2];
   const uint8_t* __restrict__ stab_cur = d.stab[p.r & 1];
   __syncthreads();
-  for (int t = tid; t < RB * KB; t += 256) {
+  if (!ROWS && d.nsnd) {  // k_peers_pull's row records (one engine)
+    for (int row = tid; row < RB; row += 256) {
+      const int i = (int)d.row0 + rb * RB + row;
+      int meta = 0;
+      int4 sv = {0, 0, 0, 0};
+      if (i < rowend) {
+        meta = d.nmeta[i];
+        sv = *reinterpret_cast<const int4*>(d.nsnd + 4 * (int64_t)i);
+      }
+      s_meta[row] = meta;
+      *reinterpret_cast<int4*>(&s_inb[row * KB]) = int4{sv.x * (TW / 2), sv.y * (TW / 2), sv.z * (TW / 2), sv.w * (TW / 2)};
+    }
+  }
+  for (int t = tid; t < ((!ROWS && d.nsnd) ? 0 : RB * KB); t += 256) {
     const int row = t / KB, q = t - row * KB;
     const int i = (int)d.row0 + rb * RB + row;
     int meta = 0, sv = 0;
