@@ -290,6 +290,11 @@ struct GhDev {
   // row itself), so a nibble workgroup stages its rows with two coalesced
   // loads per row instead of five scattered ones per (row, slot)
   int32_t *nmeta, *nsnd;
+  // a tiered column-layout engine: this round's base move per 8-column
+  // chunk as one nibble word (dnw, the nibble path's order) and whether any
+  // of its columns moves outside 0..15 (dbad), written by base_col
+  uint32_t *dnw;
+  uint8_t *dbad;
   // MemberList order (GH_ORDER_APPEND, order.hip; null under GH_ORDER_ID).
   // Generation g (the host's lcur) of row i: the list is lord[lsel[g][i]] +
   // i * ld (member at each position), llen[g][i] entries, the row's own

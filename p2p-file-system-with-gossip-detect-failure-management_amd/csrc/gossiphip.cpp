@@ -1108,6 +1108,10 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
         (rc = dalloc(e, &d.stab[0], e->n, 0)) || (rc = dalloc(e, &d.stab[1], e->n, 0)) ||
         (rc = dalloc(e, &d.nquiet, 1, 0)) || (rc = dalloc(e, &d.aq, 1, 0x01)))
       break;
+    const char* dnw_env = std::getenv("GH_DNW");  // 0: the nibble path derives the moves from the bases (A/B)
+    if (e->c8 && !rowlay && !(dnw_env && std::atoi(dnw_env) == 0) &&
+        ((rc = dalloc(e, &d.dnw, e->ld / 8, 0)) || (rc = dalloc(e, &d.dbad, e->ld / 8, 0))))
+      break;
     const char* nrec_env = std::getenv("GH_NREC");  // 0: stage the rows from the inboxes (A/B)
     if (e->c8 && world == 1 && !rowlay && cfg->peer_mode == GH_PEER_PULL && !(nrec_env && std::atoi(nrec_env) == 0) &&
         ((rc = dalloc(e, &d.nmeta, e->n, 0)) || (rc = dalloc(e, &d.nsnd, 4 * (size_t)e->n, 0))))

@@ -665,6 +665,20 @@ __device__ __forceinline__ void base_col(const GhDev& d, int cur, int dcur, cons
   }
   d.base[cur ^ 1][c] = b;
   if (b != b0 && d.aq) d.aq[0] = 1;
+  if (d.dnw) {  // the chunk's move word for the nibble path (8 consecutive lanes, ld % 8 == 0)
+    const int64_t delta = (int64_t)b - b0;
+    uint32_t x = (uint32_t)(delta & 0xF) << gh_nib((int)(c & 7));
+    uint32_t bad = delta < 0 || delta > 15;
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1) {
+      x |= __shfl_xor(x, o);
+      bad |= __shfl_xor(bad, o);
+    }
+    if ((c & 7) == 0) {
+      d.dnw[c >> 3] = x;
+      d.dbad[c >> 3] = (uint8_t)bad;
+    }
+  }
 }
 __global__ __launch_bounds__(256) void k_base(GhDev d, int cur, int dcur, GhRound p) {
   base_col(d, cur, dcur, p, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
@@ -928,6 +942,12 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const int wave = uni(tid >> 6);
   const int sub = lane / SEG, lc = lane % SEG;
   const unsigned long long gmask = (SEG == 64 ? ~0ull : ((1ull << SEG) - 1)) << (sub * SEG);
+  const int64_t l0 = (int64_t)tile * TW + lc * CPL;  // local column of this lane's first cell
+  // the lane's REMOVE'd members (D_{r-1}), loaded beside the staging below
+  uint32_t rm = 0;
+#pragma unroll
+  for (int w = 0; w < (CPL + 31) / 32; ++w) rm |= d.dbits[(l0 >> 5) + w];
+  if constexpr (CPL < 32) rm = (rm >> (l0 & 31)) & ((1u << CPL) - 1u);
   if (tid == 0) {
     s_merged = s_rel = 0;
     s_quiet = s_nslow = s_bmove = s_hasjob = s_need = 0;
@@ -978,24 +998,34 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   }
   const int32_t* __restrict__ bo = d.base[cur];
   const int32_t* __restrict__ bn = d.base[cur ^ 1];
-  for (int cc = tid; cc < TW; cc += 256) {
-    const int64_t c = (int64_t)tile * TW + cc;
-    const int64_t delta = (int64_t)bn[c] - bo[c];
-    if (delta < 0 || delta > 15) atomicOr(&s_d8bad, 1ull << (cc / CPL));
-    if (delta) s_bmove = 1;
-  }
-  for (int w = tid; w < TW / 8; w += 256) {
-    uint32_t x = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int64_t c = (int64_t)tile * TW + 8 * w + j;
-      x |= (uint32_t)((bn[c] - bo[c]) & 0xF) << gh_nib(j);
+  if (d.dnw) {  // base_col's move words (column layout)
+    for (int w = tid; w < TW / 8; w += 256) {
+      const int64_t wc = (int64_t)tile * (TW / 8) + w;
+      const uint32_t x = d.dnw[wc];
+      const uint32_t bd = d.dbad[wc];
+      s_dn[w] = x;
+      if (bd) atomicOr(&s_d8bad, 1ull << (w * 8 / CPL));
+      if (x | bd) s_bmove = 1;
     }
-    s_dn[w] = x;
+  } else {
+    for (int cc = tid; cc < TW; cc += 256) {
+      const int64_t c = (int64_t)tile * TW + cc;
+      const int64_t delta = (int64_t)bn[c] - bo[c];
+      if (delta < 0 || delta > 15) atomicOr(&s_d8bad, 1ull << (cc / CPL));
+      if (delta) s_bmove = 1;
+    }
+    for (int w = tid; w < TW / 8; w += 256) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int64_t c = (int64_t)tile * TW + 8 * w + j;
+        x |= (uint32_t)((bn[c] - bo[c]) & 0xF) << gh_nib(j);
+      }
+      s_dn[w] = x;
+    }
   }
   __syncthreads();
 
-  const int64_t l0 = (int64_t)tile * TW + lc * CPL;  // local column of this lane's first cell
   const int c0 = (int)(d.col0 + l0);
   const int64_t tcell = (int64_t)tile * d.tstride;
   const int64_t tbytes = d.tstride / 2;  // one tile slice of a plane
@@ -1007,10 +1037,6 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const bool tile_still = s_bmove == 0;
   // the lane needs the per-cell rule (a lane job) in every row when it holds
   // a REMOVE'd member or a base move outside 0..15
-  uint32_t rm = 0;
-#pragma unroll
-  for (int w = 0; w < (CPL + 31) / 32; ++w) rm |= d.dbits[(l0 >> 5) + w];
-  if constexpr (CPL < 32) rm = (rm >> (l0 & 31)) & ((1u << CPL) - 1u);
   const bool lane_job = rm != 0u || ((s_d8bad >> lc) & 1ull) != 0;
   // this wave's lane-job region (no atomics: the wave owns it)
   uint4* __restrict__ jreg = d.jobs + ((int64_t)bid * 4 + wave) * GH_JOB_CAP * 2;
