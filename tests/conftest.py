@@ -1,6 +1,15 @@
 """Shared pytest setup: markers, import paths for the product package
 (p2p-file-system-with-gossip-detect-failure-management_amd/gossipsim) and the
-test-only oracle (oracle/)."""
+test-only oracle (oracle/).
+
+Collection order and the full-size budget: `pytest -m gpu` must finish well
+inside the driver's 900 s. The N=65,536 full-size tests drive the 48 GiB
+OpenMP tablesim at ~2.6 s per round, so they run LAST (every parity test
+first), and only the two the bench depends on (steady state, 1% crash) are in
+the default `-m gpu` selection. The other full-size tests carry the extra
+marker `gpu_fullsize` and run only with `--fullsize` (or GH_FULLSIZE=1); their
+logs are committed under profiles/."""
+import os
 import pathlib
 import sys
 
@@ -13,9 +22,30 @@ for p in (str(REPO), str(PKG_DIR)):
         sys.path.insert(0, p)
 
 
+def pytest_addoption(parser):
+    parser.addoption("--fullsize", action="store_true", default=False,
+                     help="also run the long N=65,536 full-size tests marked gpu_fullsize")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) and the built libgossiphip")
+    config.addinivalue_line("markers", "gpu_fullsize: long full-size GPU test, run only with --fullsize")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+def _fullsize_enabled(config):
+    return config.getoption("--fullsize") or os.environ.get("GH_FULLSIZE") == "1"
+
+
+def pytest_collection_modifyitems(session, config, items):
+    if not _fullsize_enabled(config):
+        dropped = [it for it in items if it.get_closest_marker("gpu_fullsize")]
+        if dropped:
+            keep = [it for it in items if not it.get_closest_marker("gpu_fullsize")]
+            config.hook.pytest_deselected(items=dropped)
+            items[:] = keep
+    # the full-size module last (stable order otherwise)
+    items.sort(key=lambda it: 1 if it.path.name == "test_gpu_fullsize.py" else 0)
 
 
 @pytest.fixture(scope="session")

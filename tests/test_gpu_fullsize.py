@@ -153,6 +153,7 @@ def test_c3_fullsize_crash_1pct(gs, oracle_mod):
     run(gs, oracle_mod, 16, 32, {12, 32}, expect, sched=sched)
 
 
+@pytest.mark.gpu_fullsize
 def test_c3_fullsize_crash_1pct_remove_list(gs, oracle_mod):
     """The 1% crash with the reference's REMOVE recipients (GH_REMOVE_LIST:
     each detector's list right after removeMember, slave/slave.go:344,
@@ -169,6 +170,7 @@ def test_c3_fullsize_crash_1pct_remove_list(gs, oracle_mod):
     run(gs, oracle_mod, 16, 28, {28}, expect, sched=sched, remove_mode=1)
 
 
+@pytest.mark.gpu_fullsize
 def test_c3_fullsize_reference_timeouts(gs, oracle_mod):
     """T_fail = T_cleanup = 5 (slave/slave.go:24-25) through the round-6
     detection storm and the collapse: the storm variant runs at N=65,536."""
@@ -187,6 +189,7 @@ def expect_detection(s):
     assert s["detections"] > 0 and s["first_detection"] is not None, s
 
 
+@pytest.mark.gpu_fullsize
 def test_c3_fullsize_rows_g8(gs, oracle_mod):
     """North_star's layout at the largest size one MI355X holds: 8 row shards
     (each owns 8,192 observer rows; the senders' plane rows of other shards
@@ -196,6 +199,7 @@ def test_c3_fullsize_rows_g8(gs, oracle_mod):
     run(gs, oracle_mod, 16, 25, {6, 25}, expect_detection, sched=crash_sched(gs), world=8, layout=1)
 
 
+@pytest.mark.gpu_fullsize
 def test_c3_fullsize_columns_g8(gs, oracle_mod):
     """The default multi-GPU layout at full size: 8 column shards (each holds
     every row of 8,192 member columns, O(N) exchanges), the same workload
@@ -203,6 +207,7 @@ def test_c3_fullsize_columns_g8(gs, oracle_mod):
     run(gs, oracle_mod, 16, 25, {6, 25}, expect_detection, sched=crash_sched(gs), world=8, layout=0)
 
 
+@pytest.mark.gpu_fullsize
 def test_c3_fullsize_crash_1pct_quirk(gs, oracle_mod):
     """Quirk-mode detection (Go's range over the slice removeMember shifts,
     slave/slave.go:464-477) through the 1% crash at N=65,536: the crashed
@@ -211,6 +216,7 @@ def test_c3_fullsize_crash_1pct_quirk(gs, oracle_mod):
     run(gs, oracle_mod, 16, 28, {28}, expect_detection, sched=crash_sched(gs), extra=dict(detect_mode=1))
 
 
+@pytest.mark.gpu_fullsize
 def test_c5_fullsize_files(gs, oracle_mod):
     """SURVEY C5's shape at N=65,536 with 2^20 files (master/master.go:74-175):
     every file put at r=3 (Init_replica over the master's list), a 1% crash
