@@ -830,6 +830,7 @@ struct GhRound {
   int32_t qgate;      // quirk pre-pass: 1 = return at once when cntg[n + 1] (flagged segments, all shards) is 0
   int32_t force_storm;  // diagnostics (GH_FORCE_STORM): run the storm variant every round
   int32_t force_slow;   // diagnostics (GH_FORCE_SLOW): every segment by the per-cell rule
+  int32_t nib_rmv;      // nibble path: REMOVE'd members with >= 2 detectors stay on it (GH_NIB_RMV=0: lane jobs)
   int32_t plane;        // the round writes the next buffer's sender plane (and may read cur's)
   int32_t ring_whole;   // ring mode: one engine and a current flag count, so the targets may come
                         // from whole lists when no REMOVE / flag is pending (k_ring_fast)
@@ -868,7 +869,10 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
 // tiered engines; the nibble path's row-layout form is k_round IN = 4); all
 // are launched every round (0-2 on the side stream) and only the one k_base,
 // the input's tier and the plane select runs
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant);
+// t0 / t1: timing events stamped by the launch itself (hipExtLaunchKernel:
+// the dispatch packet's start and end, no separate event packets), or null
+void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant,
+                  hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 // the nibble path's lane jobs (tiered engines; after launch_round, before
 // launch_round_slow): k_round_jobs, then the wide redo of the rare lanes
 // whose cells leave the 16-bit window

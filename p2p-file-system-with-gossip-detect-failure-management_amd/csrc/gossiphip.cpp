@@ -57,6 +57,7 @@ struct Engine {
   int tpw = 1;           // k_round tiles per workgroup (GH_ROUND_TPW)
   int force_storm = 0;   // storm variant every round (GH_FORCE_STORM, diagnostics)
   int force_slow = 0;    // every segment by the per-cell rule (GH_FORCE_SLOW, diagnostics)
+  int nib_rmv = 1;       // REMOVE'd members with >= 2 detectors on the nibble path (GH_NIB_RMV=0: lane jobs, A/B)
   bool timing = false;
   bool side = true;      // idle round variants on the side stream (GH_SIDE=0: in line)
   // the current table may hold flags no round kernel counted (import, fill,
@@ -194,6 +195,7 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.tpw = e->tpw;
   p.force_storm = e->force_storm;
   p.force_slow = e->force_slow;
+  p.nib_rmv = e->nib_rmv;
   p.plane = e->plane;
   // (a row shard holds its senders' whole rows: their lists)
   p.ring_whole = (e->world == 1 || e->rowlay) && e->flags_known;
@@ -993,6 +995,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (const char* v = std::getenv("GH_ROUND_TPW")) e->tpw = std::atoi(v);
   if (const char* v = std::getenv("GH_FORCE_STORM")) e->force_storm = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_FORCE_SLOW")) e->force_slow = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_NIB_RMV")) e->nib_rmv = std::atoi(v) != 0;
   if (tw != 8 && tw != 16 && tw != 32 && tw != 64 && tw != 128 && tw != 256) {
     delete e;
     return GH_EINVAL;
@@ -1055,7 +1058,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
                hipStreamCreateWithPriority(&e->vstream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
                hipEventCreateWithFlags(&e->vfork, hipEventDisableTiming) != hipSuccess ||
                hipEventCreateWithFlags(&e->vjoin, hipEventDisableTiming) != hipSuccess)) {
-    delete e;
+    gh_destroy(e);  // the streams and events created before the failing one, and the communicator
     return GH_EHIP;
   }
   GhDev& d = e->d;
@@ -1695,8 +1698,8 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   bool busy = false;
   if ((rc0 = check_lost(e)) || (rc0 = maybe_grow(e, &busy))) return rc0;
   HIPCHK(e, hipMemsetAsync(e->d.stats, 0, sizeof(unsigned long long) * ST_COUNT, e->stream));
-  if (e->timing && (int64_t)e->evs.size() < 6 * (int64_t)rounds) {
-    while ((int64_t)e->evs.size() < 6 * (int64_t)rounds) {
+  if (e->timing && (int64_t)e->evs.size() < 8 * (int64_t)rounds) {
+    while ((int64_t)e->evs.size() < 8 * (int64_t)rounds) {
       hipEvent_t ev;
       HIPCHK(e, hipEventCreate(&ev));
       e->evs.push_back(ev);
@@ -1761,40 +1764,26 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     if ((rc = build_inboxes(e, p))) return rc;
     GhRound pr = p;
     pr.gpo = e->gpo;  // row layout: the ghosts carry only their plane so far
-    // the variants of k_round; the ones not selected return at once
-    // (events 6q + 0..3 bracket variants 0..2, 6q + 4..5 the last one)
+    // the variants of k_round; the ones not selected return at once. With
+    // timing on, each launch stamps its own start and end (events 8q + 2v,
+    // 8q + 2v + 1 of variant v; hipExtLaunchKernel, no event packets between
+    // the kernels)
+    auto ev = [&](int v, int end) { return e->timing ? e->evs[8 * q + 2 * v + end] : nullptr; };
     if (e->c8 && !e->side) {
       // lean 16-bit input, storm, lean tier input by the 16-bit rule, then
       // the nibble path, all on the round's stream
-      for (int v = 0; v < 3; ++v) {
-        if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + v], e->stream));
-        launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v);
-      }
-      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 3], e->stream));
-      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 4], e->stream));
-      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, 3);
-      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 5], e->stream));
+      for (int v = 0; v < 4; ++v) launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v, ev(v, 0), ev(v, 1));
     } else if (e->c8) {
       // lean 16-bit input, storm, lean tier input by the 16-bit rule on the
       // side stream, beside the nibble path
       HIPCHK(e, hipEventRecord(e->vfork, e->stream));
       HIPCHK(e, hipStreamWaitEvent(e->vstream, e->vfork, 0));
-      for (int v = 0; v < 3; ++v) {
-        if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + v], e->vstream));
-        launch_round(e->d, e->cur, e->dcur, pr, e->vstream, e->nt, v);
-      }
-      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 3], e->vstream));
+      for (int v = 0; v < 3; ++v) launch_round(e->d, e->cur, e->dcur, pr, e->vstream, e->nt, v, ev(v, 0), ev(v, 1));
       HIPCHK(e, hipEventRecord(e->vjoin, e->vstream));
-      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 4], e->stream));
-      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, 3);
-      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 5], e->stream));
+      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, 3, ev(3, 0), ev(3, 1));
       HIPCHK(e, hipStreamWaitEvent(e->stream, e->vjoin, 0));
     } else {  // lean 16-bit input, storm
-      for (int v = 0; v < 2; ++v) {
-        if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + v], e->stream));
-        launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v);
-      }
-      if (e->timing) HIPCHK(e, hipEventRecord(e->evs[6 * q + 2], e->stream));
+      for (int v = 0; v < 2; ++v) launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v, ev(v, 0), ev(v, 1));
     }
     // (row layout: the ghosts' codes before the kernels that may read them)
     if ((rc = ghost_codes_if_slow(e))) return rc;
@@ -1856,7 +1845,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       float ms = 0.f;  // the variant that ran
       for (int v = 0; v < (e->c8 ? 4 : 2); ++v) {
         float mv = 0.f;
-        const int b = 6 * q + (v == 3 ? 4 : v);
+        const int b = 8 * q + 2 * v;
         HIPCHK(e, hipEventElapsedTime(&mv, e->evs[b], e->evs[b + 1]));
         ms = std::max(ms, mv);
       }
@@ -2261,6 +2250,36 @@ int gh_debug_raw(void* h, int32_t row, int64_t c0, int64_t n, uint16_t* codes, i
 // `row`, local columns [c0, c0 + n) of the current buffer: (lag code << 4) |
 // age nibble per cell, or 0xFF where the chunk is escaped or the buffer is
 // not in the tier.
+// Debug (tests only, not in the header, like gh_debug_tier): recounts the
+// present cells of every running row this engine holds in the current
+// buffer (k_count) and compares them with the maintained counts cntl, which
+// the rounds, events and list merges keep by per-segment deltas and which
+// the <4 guard and active[] read. *mismatched = rows whose maintained count
+// differs, *first_row = the first of them (-1: none). The maintained counts
+// are restored, so the check changes nothing.
+int gh_debug_counts(void* h, int64_t* mismatched, int32_t* first_row) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || !mismatched || !first_row) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  const size_t bytes = sizeof(int32_t) * (size_t)e->n;
+  std::vector<int32_t> kept(e->n), exact(e->n);
+  HIPCHK(e, hipMemcpyAsync(kept.data(), e->d.cntl, bytes, hipMemcpyDeviceToHost, e->stream));
+  launch_count(e->d, e->cur, round_params(e, e->round + 1), e->stream);
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipMemcpyAsync(exact.data(), e->d.cntl, bytes, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(e->d.cntl, kept.data(), bytes, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  *mismatched = 0;
+  *first_row = -1;
+  for (int64_t i = 0; i < e->n; ++i) {
+    const bool held = !e->rowlay || (i >= e->d.row0 && i < e->d.row0 + e->d.nrows);
+    if (!held || !e->alive[i] || kept[i] == exact[i]) continue;
+    if (*first_row < 0) *first_row = (int32_t)i;
+    ++*mismatched;
+  }
+  return GH_OK;
+}
+
 int gh_debug_tier(void* h, int32_t row, int64_t c0, int64_t n, uint8_t* out) {
   Engine* e = static_cast<Engine*>(h);
   if (!e || !out || row < 0 || row >= e->n || c0 < 0 || c0 + n > e->ld) return GH_EINVAL;

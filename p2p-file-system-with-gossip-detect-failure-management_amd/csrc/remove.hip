@@ -55,23 +55,54 @@ __global__ __launch_bounds__(256) void k_rm_cols(GhDev d, int cur, int dcur, GhR
   int rows = 0;
   if (c < p.ld) {
     const uint32_t b8 = (d.dbits[c >> 5] >> (c & 31)) & 0xFFu;  // D_{r-1} in these columns
-    for (int q = 0; q < 32; ++q) {
-      const int64_t i = i0 + q;
-      if (i >= p.n || !d.active[i]) continue;
-      rows++;
-      const uint32_t pf = gh_pf8(d, cur, i, c);
-      uint32_t lst = pf & 0xFFu;
-      for (uint32_t m = lst & b8; m; m &= m - 1) {  // step 1: REMOVE'd at row i
-        const int j = __builtin_ctz(m);
-        if (gh_rm_at(d, dcur, c + j, i)) lst &= ~(1u << j);
-      }
-      if (i >= c && i < c + 8) lst &= ~(1u << (i - c));  // Remove skips self (:344-346)
-      const uint32_t det = (pf >> 8) & lst;              // the sweep's removals
+    const bool tier = gh_m8(d, cur);
+    // 8 rows at a time, their plane and age words loaded together: a tier
+    // chunk's present cells are its codes other than 15 (it holds no flag),
+    // only escaped chunks decode their 16-bit codes
+    for (int q0 = 0; q0 < 32; q0 += 8) {
+      uint32_t pw[8], aw[8];
+      uint8_t act[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        wd[j] |= ((det >> j) & 1u) << q;
-        ws[j] |= ((lst & ~det) >> j & 1u) << q;
-        wl[j] |= ((lst >> j) & 1u) << q;
+      for (int u = 0; u < 8; ++u) {
+        const int64_t i = i0 + q0 + u;
+        act[u] = i < p.n ? d.active[i] : 0;
+        pw[u] = aw[u] = 0;
+        if (tier && i < p.n) {
+          const int64_t cell = gh_cell(d, i, c);
+          aw[u] = d.a4[cur][cell >> 3];
+          pw[u] = d.pl[cur][cell >> 3];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = q0 + u;
+        const int64_t i = i0 + q;
+        if (!act[u]) continue;
+        rows++;
+        uint32_t pf;
+        if (tier && !gh_t4_esc(aw[u])) {
+          const uint32_t n15 = ~pw[u];  // a nibble of 15 is absent or a tombstone
+          uint32_t t = n15 | (n15 >> 2);
+          t |= t >> 1;
+          pf = 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pf |= ((t >> gh_nib(j)) & 1u) << j;
+        } else {
+          pf = gh_pf8(d, cur, i, c);
+        }
+        uint32_t lst = pf & 0xFFu;
+        for (uint32_t m = lst & b8; m; m &= m - 1) {  // step 1: REMOVE'd at row i
+          const int j = __builtin_ctz(m);
+          if (gh_rm_at(d, dcur, c + j, i)) lst &= ~(1u << j);
+        }
+        if (i >= c && i < c + 8) lst &= ~(1u << (i - c));  // Remove skips self (:344-346)
+        const uint32_t det = (pf >> 8) & lst;              // the sweep's removals
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          wd[j] |= ((det >> j) & 1u) << q;
+          ws[j] |= ((lst & ~det) >> j & 1u) << q;
+          wl[j] |= ((lst >> j) & 1u) << q;
+        }
       }
     }
     const int64_t w = i0 >> 5;
@@ -105,13 +136,34 @@ __device__ __forceinline__ bool meets(const uint32_t* a, const uint32_t* b, int6
 }
 
 // One workgroup per member c of D_r (grid-stride), a thread per 32 receivers.
+// The nonzero words of det(c) are listed in LDS first, so an intersection
+// costs one word per listed word (at most |det(c)|), not N / 32: a member
+// with few detectors (the common case outside storms, where counts and the
+// pigeonhole rule settle most pairs) is decided in O(|det(c)|) per receiver.
+constexpr int RM_NZ_CAP = 2048;  // listed words (nw <= 2048 up to N = 65,536; beyond: the full scan)
 __global__ __launch_bounds__(256) void k_rm_recv(GhDev d, int dnew, GhRound p) {
+  __shared__ uint32_t s_w[RM_NZ_CAP], s_v[RM_NZ_CAP];
+  __shared__ int s_nz;
   const int nd = d.nd[2 + dnew];
   const int nact = d.ccnt[2 * p.ld];
   for (int q = blockIdx.x; q < nd; q += gridDim.x) {
     const int64_t c = d.dlist[(int64_t)dnew * p.ld + q];
     const int detc = d.det_cnt[dnew][c];
     const uint32_t* dcol = d.cdet + c * d.nw;
+    if (threadIdx.x == 0) s_nz = 0;
+    __syncthreads();
+    for (int64_t w = threadIdx.x; w < d.nw; w += 256) {
+      const uint32_t v = dcol[w];
+      if (v) {
+        const int at = atomicAdd(&s_nz, 1);
+        if (at < RM_NZ_CAP) {
+          s_w[at] = (uint32_t)w;
+          s_v[at] = v;
+        }
+      }
+    }
+    __syncthreads();
+    const int nz = s_nz;
     for (int64_t w = threadIdx.x; w < d.nw; w += 256) {
       uint32_t out = 0;
       for (int b = 0; b < 32; ++b) {
@@ -119,17 +171,24 @@ __global__ __launch_bounds__(256) void k_rm_recv(GhDev d, int dnew, GhRound p) {
         if (j >= p.n || j == c) continue;
         const bool low = j < c;
         const int cnt = low ? d.ccnt[j] : d.ccnt[p.ld + j];
-        bool r;
-        if (cnt == 0)
+        bool r = false;
+        if (cnt == 0) {
           r = false;
-        else if (detc + cnt > nact)
+        } else if (detc + cnt > nact) {
           r = true;  // pigeonhole: both sets live in the rows that ran the sweep
-        else
-          r = meets(dcol, (low ? d.csurv : d.clst) + j * d.nw, d.nw);
+        } else {
+          const uint32_t* other = (low ? d.csurv : d.clst) + j * d.nw;
+          if (nz <= RM_NZ_CAP) {
+            for (int e = 0; e < nz && !r; ++e) r = (s_v[e] & other[s_w[e]]) != 0u;
+          } else {
+            r = meets(dcol, other, d.nw);
+          }
+        }
         out |= (uint32_t)r << b;
       }
       d.rcv[dnew][c * d.nw + w] = out;
     }
+    __syncthreads();  // s_nz / the list before the next member
   }
 }
 

@@ -26,6 +26,8 @@
 
 #include <algorithm>
 
+#include <hip/hip_ext.h>
+
 #include "gh_internal.h"
 
 namespace {
@@ -851,16 +853,34 @@ __device__ __forceinline__ uint32_t nib_is15(uint32_t x) {
 // T_cleanup and released (step 5, :490-492: absent, and merges like one),
 // the others keep code 15 and age by one, never merged. Without tt no own
 // cell has code 15.
+// RMV: the lane holds REMOVE'd members (rm1: bit 0 of their nibbles; step 1,
+// slave/slave.go:236-240, 276-286), each with two or more detectors, so every
+// sender REMOVEs it before sending (no entry) and the row applies
+// removeMember: a present cell becomes a tombstone that keeps its ts, i.e. the
+// tier cell (15, s) with s = age + 1 - toff (rmk = (16 - toff) per byte;
+// T_cleanup >= 15, so no tier age is past it and none is released here), a
+// tombstone stays one, and an absent one (the reference panics; counted
+// remove_unknown) or a tombstone too young for the tier leaves the lane to
+// the lane-job kernel.
+template <bool RMV>
 __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint32_t p0, uint32_t p1, uint32_t p2,
-                                         uint32_t p3, uint32_t a1, uint32_t dn, uint32_t tfk, uint32_t& QO,
-                                         uint32_t& AO, uint32_t& LWo, uint32_t& Bm, uint32_t& Lz, int& mrg, int& gain,
-                                         int& rel) {
+                                         uint32_t p3, uint32_t a1, uint32_t dn, uint32_t tfk, uint32_t rm1, uint32_t rs1,
+                                         uint32_t rmk, uint32_t& QO, uint32_t& AO, uint32_t& LWo, uint32_t& Bm, uint32_t& Lz,
+                                         int& mrg, int& gain, int& rel, int& tmb) {
   constexpr uint32_t N1 = 0x11111111u;
   uint32_t Lw = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const uint32_t M = 0x000F000Fu << (4 * j);
     Lw |= pk_min_u16(pk_min_u16(pk_min_u16(qw & M, p0 & M), pk_min_u16(p1 & M, p2 & M)), p3 & M);
+  }
+  uint32_t bad = 0;
+  uint32_t pr1 = 0, PRm = 0;  // RMV: present cells REMOVE'd this round
+  if constexpr (RMV) {
+    const uint32_t RM = rm1 * 15u;
+    Lw = (Lw & ~RM) | (qw & RM);  // no sender entry: never merged
+    pr1 = rm1 & ~a1;
+    PRm = pr1 * 15u;
   }
   uint32_t kp1 = 0, KM = 0;
   if (tt) {
@@ -873,6 +893,9 @@ __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint
     KM = kp1 * 15u;
     Lw |= KM;  // a kept tombstone takes no entry
     rel += __builtin_popcount(a1 & h3 & ~aw);
+    // REMOVE of an absent member (remove_unknown), or a release where the
+    // member's sole detector may send it: lane jobs
+    if constexpr (RMV) bad |= (rm1 & a1 & h3 & aw) | (rs1 & a1 & h3 & ~aw);
   }
   // a sender code unknown (0) or old (14) that the own code does not beat
   Lz |= nib_haszero(Lw) | nib_haszero(Lw ^ 0xEEEEEEEEu);
@@ -884,14 +907,14 @@ __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint
   const uint32_t an1 = a1 & ~m1 & ~kp1;  // absent (or released), not merged: stays (15, 15)
   const uint32_t ANm = an1 * 15u;
   const uint32_t MM = m1 * 15u;
-  const uint32_t ST = ANm | KM;          // cells whose code stays 15
+  const uint32_t ST = ANm | KM | PRm;    // cells whose code is 15 after the round
   const uint32_t ddx = dn & ~ST;
   const uint32_t S = Lw + ddx;  // next code, rebased
-  uint32_t bad = ((Lw ^ ddx ^ S) & (N1 - 1u)) | (S < Lw ? 1u : 0u);  // a code past 15 (carry into the next nibble)
+  bad |= ((Lw ^ ddx ^ S) & (N1 - 1u)) | (S < Lw ? 1u : 0u);  // a code past 15 (carry into the next nibble)
   const uint32_t s1 = S >> 1, s2 = S >> 2, s3 = S >> 3;
-  bad |= ((s1 & s2 & s3) | ~(s1 | s2 | s3)) & N1 & ~(an1 | kp1);  // a code of 14, 15 or below 2
-  const uint32_t ag = aw & ~(MM | ANm);                           // ages that grow by one (kept tombstones to 14 at most)
-  const uint32_t inc = N1 & ~(m1 | an1);
+  bad |= ((s1 & s2 & s3) | ~(s1 | s2 | s3)) & N1 & ~(an1 | kp1 | pr1);  // a code of 14, 15 or below 2
+  const uint32_t ag = aw & ~(MM | ANm | PRm);                           // ages that grow by one (kept tombstones to 14 at most)
+  const uint32_t inc = N1 & ~(m1 | an1 | pr1);
   const uint32_t T = ag + inc;
   bad |= ((ag ^ inc ^ T) & (N1 - 1u)) | (T < ag ? 1u : 0u);  // an age past 15
   const uint32_t AN = T | m1 | ANm;  // merged: age 1; absent: 15
@@ -899,9 +922,22 @@ __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint
   const uint32_t K = tfk & ~ST;
   const uint32_t V = X + K;
   bad |= ((X ^ K ^ V) & (N1 - 1u)) | (V < X ? 1u : 0u);
-  Bm |= bad;
   QO = S;
   AO = AN;
+  if constexpr (RMV) {
+    // the new tombstones' age nibbles, per byte without carries between
+    // nibbles: a + 15 - (toff - 1) carries iff s = a + 1 - toff >= 1 (s <= 14
+    // always: a <= 15, toff >= 2), and its low nibble is s - 1
+    const uint32_t Xa = aw & PRm;
+    const uint32_t Ve = (Xa & 0x0F0F0F0Fu) + rmk, Vo = ((Xa >> 4) & 0x0F0F0F0Fu) + rmk;
+    const uint32_t ok = ((Ve >> 4) & 0x01010101u) | (((Vo >> 4) & 0x01010101u) << 4);
+    const uint32_t sn = ((Ve & 0x0F0F0F0Fu) + 0x01010101u) | (((Vo & 0x0F0F0F0Fu) + 0x01010101u) << 4);
+    bad |= pr1 & ~ok;
+    QO |= PRm;
+    AO |= sn & PRm;
+    tmb += __builtin_popcount(pr1);
+  }
+  Bm |= bad;
   mrg += __builtin_popcount(m1);
   gain += __builtin_popcount(m1 & a1);
 }
@@ -911,7 +947,8 @@ __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint
 // plane words the round's exchange put in the ghost table (row-major,
 // gplane); the gathers then take per-sender 64-bit addresses staged in LDS.
 template <int TW, bool NT, int CPL, bool ROWS>
-__device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, const GhRound& p, const int bid) {
+__device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, const int dcur, const GhRound& p,
+                                                const int bid) {
   constexpr int W = CPL / 8;         // dwords per lane and plane
   constexpr int SEG = TW / CPL;      // lanes per row segment
   constexpr int RPW = 64 / SEG;      // rows per wave instruction
@@ -922,7 +959,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   static_assert(SEG >= 2 && SEG <= 64 && RB % (RSTEP * RS) == 0, "nibble path: whole row steps");
   static_assert(W == 2 || W == 4, "nibble path: 16 or 32 cells per lane (one or two lane jobs of 16 cells)");
   constexpr int H = W / 2;  // lane jobs of GH_JOB_CPL cells per job lane
-  __shared__ unsigned long long s_merged, s_rel;
+  __shared__ unsigned long long s_merged, s_rel, s_tmb;
   __shared__ int s_quiet, s_nslow, s_slowbase, s_bmove, s_hasjob;
   __shared__ unsigned long long s_d8bad;  // bit l: lane l's columns hold a base move outside 0..15
   // per chunk the base moves as one nibble word in the plane's nibble order
@@ -949,7 +986,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   for (int w = 0; w < (CPL + 31) / 32; ++w) rm |= d.dbits[(l0 >> 5) + w];
   if constexpr (CPL < 32) rm = (rm >> (l0 & 31)) & ((1u << CPL) - 1u);
   if (tid == 0) {
-    s_merged = s_rel = 0;
+    s_merged = s_rel = s_tmb = 0;
     s_quiet = s_nslow = s_bmove = s_hasjob = s_need = 0;
     s_d8bad = 0ull;
   }
@@ -1035,9 +1072,47 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const auto a4n_t = nib_rsrc(reinterpret_cast<const char*>(d.a4[cur ^ 1]) + tcell / 2, tbytes);
   const uint32_t lbp = (uint32_t)lc * (CPL / 2);  // the lane's byte offset in a plane row segment
   const bool tile_still = s_bmove == 0;
+  // REMOVE'd members on the nibble path (nib_word RMV): canonical recipients
+  // (every running row but a sole detector, SPEC D4) and tier tombstones with
+  // T_cleanup >= 15 (toff >= 2; GH_NIB_RMV=0 in the environment restores the
+  // lane jobs). A member with one detector: that row keeps its own cell (it
+  // is a lane job there, rmrow), and the detector may send the member, so a
+  // cell that is absent after step 5 (a tombstone released this round, RS1)
+  // is a lane job; a lane with two such members of different detectors is a
+  // lane job in every row.
+  bool rmv = false;
+  int rmrow = -1;
+  uint32_t rs = 0;  // the lane's REMOVE'd cells whose member has one detector
+  if (p.nib_rmv && rm != 0u && !d.rlist && d.toff >= 2) {
+    rmv = true;
+    for (uint32_t m = rm; m; m &= m - 1u) {
+      const int j = __builtin_ctz(m);
+      if (d.det_cnt[dcur][l0 + j] == 1) {
+        const int dm = d.det_min[dcur][l0 + j];
+        rmv &= rmrow < 0 || rmrow == dm;
+        rmrow = dm;
+        rs |= 1u << j;
+      }
+    }
+  }
+  uint32_t RM1[W], RS1[W];  // per dword, bit 0 of each REMOVE'd cell's nibble (all; one detector)
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const uint32_t b8 = rmv ? (rm >> (8 * w)) & 0xFFu : 0u, s8 = rmv ? (rs >> (8 * w)) & 0xFFu : 0u;
+    uint32_t x = 0, y = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x |= ((b8 >> j) & 1u) << gh_nib(j);
+      y |= ((s8 >> j) & 1u) << gh_nib(j);
+    }
+    RM1[w] = x;
+    RS1[w] = y;
+  }
+  const bool wrmv = __ballot(rmv) != 0;  // (wave-uniform)
+  const uint32_t rmk = (uint32_t)(15 - (d.toff - 1)) * 0x01010101u;
   // the lane needs the per-cell rule (a lane job) in every row when it holds
-  // a REMOVE'd member or a base move outside 0..15
-  const bool lane_job = rm != 0u || ((s_d8bad >> lc) & 1ull) != 0;
+  // a REMOVE'd member off the RMV path or a base move outside 0..15
+  const bool lane_job = (rm != 0u && !rmv) || ((s_d8bad >> lc) & 1ull) != 0;
   // this wave's lane-job region (no atomics: the wave owns it)
   uint4* __restrict__ jreg = d.jobs + ((int64_t)bid * 4 + wave) * GH_JOB_CAP * 2;
   int wjobs = 0;
@@ -1045,7 +1120,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
 #pragma unroll
   for (int x = 0; x < W; ++x) DN[x] = s_dn[lc * W + x];
   const uint32_t tfk = (uint32_t)(15 - min(max(p.t_fail, 0), 15)) * 0x11111111u;  // age + tfk carries iff age > T_fail
-  uint32_t n_mrg = 0, n_rel = 0;
+  uint32_t n_mrg = 0, n_rel = 0, n_tmb = 0;
 
 #pragma unroll 1
   for (int it = 0; it < RB / RSTEP; it += RS) {
@@ -1096,7 +1171,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       const int i = iu[u];
       const bool al = alu[u];
       uint32_t QO[W], AO[W], LW[W], A1[W], Bm = 0, Lz = 0;
-      int mrg = 0, gain = 0, rel = 0;
+      int mrg = 0, gain = 0, rel = 0, tmb = 0;
       bool esc = false;
       uint32_t a1any = 0;
 #pragma unroll
@@ -1108,10 +1183,17 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       // (wave-uniform) the wave's own cells include code 15 (absent or a tier
       // tombstone): the rule ages and releases tombstones
       const bool tt = GH_TIER_TOMB && (!GH_TIER_TOMB_GATE || __ballot(a1any != 0) != 0);
+      if (wrmv) {
 #pragma unroll
-      for (int w = 0; w < W; ++w)
-        nib_word(tt, qwu[u].v[w], awu[u].v[w], pwu[u][0].v[w], pwu[u][1].v[w], pwu[u][2].v[w], pwu[u][3].v[w], A1[w],
-                 DN[w], tfk, QO[w], AO[w], LW[w], Bm, Lz, mrg, gain, rel);
+        for (int w = 0; w < W; ++w)
+          nib_word<true>(tt, qwu[u].v[w], awu[u].v[w], pwu[u][0].v[w], pwu[u][1].v[w], pwu[u][2].v[w], pwu[u][3].v[w],
+                         A1[w], DN[w], tfk, RM1[w], RS1[w], rmk, QO[w], AO[w], LW[w], Bm, Lz, mrg, gain, rel, tmb);
+      } else {
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          nib_word<false>(tt, qwu[u].v[w], awu[u].v[w], pwu[u][0].v[w], pwu[u][1].v[w], pwu[u][2].v[w], pwu[u][3].v[w],
+                          A1[w], DN[w], tfk, 0u, 0u, 0u, QO[w], AO[w], LW[w], Bm, Lz, mrg, gain, rel, tmb);
+      }
       bool ob = false;
       const int jd = i - c0;
       // (a wave-uniform branch: 1 wave in TW / CPL... holds an own member)
@@ -1126,7 +1208,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
         for (int x = 0; x < W; ++x)
           if (x == wj) {
             const int qd = (int)((qwu[u].v[x] >> sh) & 0xFu);
-            ob = qd == 15 || (int64_t)bo[l0 + jd] + (GH_P_REF - qd) >= INT32_MAX;
+            ob = qd == 15 || (int64_t)bo[l0 + jd] + (GH_P_REF - qd) >= INT32_MAX || ((rm >> jd) & 1u);
             QO[x] -= 1u << sh;
             AO[x] = (AO[x] & ~(0xFu << sh)) | (1u << sh);
           }
@@ -1136,7 +1218,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       // row a lane whose cells leave the tier or need the per-cell rule is a
       // lane job (k_round_jobs), and the segment's other lanes are written here
       const bool rowok = oku[u] && !p.force_slow;
-      const bool jb = al && rowok && (lane_job || esc || ob || Bm != 0 || Lz != 0);
+      const bool jb = al && rowok && (lane_job || esc || ob || Bm != 0 || Lz != 0 || i == rmrow);
       const unsigned long long jm = __ballot(jb);
       // a job whose rule gathers its senders' 16-bit codes (a REMOVE'd member,
       // an unknown or old minimum): with ghost senders, their codes travel
@@ -1172,11 +1254,12 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
         nib_store<W, NT ? GH_NIB_ST_AUX : 0>(a4n_t, owu[u], AO);
         n_mrg += (uint32_t)mrg;
         n_rel += (uint32_t)rel;
-        dpres = gain;
+        n_tmb += (uint32_t)tmb;
+        dpres = gain - tmb;
       } else if (al && seg_slow && lc == 0) {
         s_slow[atomicAdd(&s_nslow, 1)] = i;
       }
-      if (__ballot(dpres != 0) != 0) {  // absent cells merged: the row's count moves
+      if (__ballot(dpres != 0) != 0) {  // absent cells merged, present ones REMOVE'd: the row's count moves
 #pragma unroll
         for (int o2 = SEG / 2; o2 > 0; o2 >>= 1) dpres += __shfl_xor(dpres, o2);
         if (lc == 0 && dpres) atomicAdd(&d.cntl[i], dpres);
@@ -1190,11 +1273,13 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   }
   if (n_mrg) atomicAdd(&s_merged, (unsigned long long)n_mrg);
   if (n_rel) atomicAdd(&s_rel, (unsigned long long)n_rel);
+  if (n_tmb) atomicAdd(&s_tmb, (unsigned long long)n_tmb);
   __syncthreads();
   if (tid == 0) {
     if (s_nslow) s_slowbase = atomicAdd(d.slow_n, s_nslow);
     if (s_merged) atomicAdd(&d.stats[ST_MERGED], s_merged);
     if (s_rel) atomicAdd(&d.stats[ST_RELEASED], s_rel);
+    if (s_tmb) atomicAdd(&d.stats[ST_TOMBSTONED], s_tmb);
     if (s_quiet) atomicAdd(d.nquiet, s_quiet);
     if (s_hasjob) d.jlist[atomicAdd(&d.njobs[3], 1)] = bid;  // k_round_jobs walks the listed workgroups only
     if (ROWS && s_need) d.m8[5] = 1;
@@ -1910,7 +1995,7 @@ __global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM 
       __syncthreads();  // LDS of this block before the next
     }
   } else if constexpr (IN == 2 || IN == 4) {
-    round_block_nib<TW, NT, GH_NIB_CPL, IN == 4>(d, cur, p, blockIdx.x);  // one block per workgroup
+    round_block_nib<TW, NT, GH_NIB_CPL, IN == 4>(d, cur, dcur, p, blockIdx.x);  // one block per workgroup
   } else {
     // one block per workgroup (a loop here costs the lean variants 20+ VGPRs)
     round_block<KB, TW, TPW, NT, STORM, IN>(d, cur, dcur, p, blockIdx.x);
@@ -2799,7 +2884,8 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
 // variant: 0 lean on a 16-bit input, 1 storm, 2 lean on a 4-bit-tier input
 // by the 16-bit rule, 3 the nibble path (IN 2, or IN 4 on row shards)
 template <int KB, int TW, int TPW>
-static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant) {
+static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant,
+                             hipEvent_t t0, hipEvent_t t1) {
   constexpr int RB = round_rb<TW>();
   const int64_t nrb = (d.nrows + RB - 1) / RB;
   const int64_t nblk = nrb * (p.ld / TW / TPW);
@@ -2810,7 +2896,7 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
   // the storm one, measured slower: storm 5.3 -> 6.0 ms)
   const dim3 grid((unsigned)(few ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
 #define GH_ROUND_LAUNCH(NT, ST, IN) \
-  hipLaunchKernelGGL((k_round<KB, TW, TPW, NT, ST, IN>), grid, blk, 0, s, d, cur, dcur, p)
+  hipExtLaunchKernelGGL((k_round<KB, TW, TPW, NT, ST, IN>), grid, blk, 0, s, t0, t1, 0, d, cur, dcur, p)
 #define GH_ROUND_NT(ST, IN)        \
   do {                             \
     if (nt)                        \
@@ -2849,32 +2935,35 @@ static void round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
 
 // tiles per workgroup: ld / TW is a multiple of 8 (host padding)
 template <int KB, int TW>
-static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm) {
+static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm,
+                            hipEvent_t t0, hipEvent_t t1) {
   switch (p.tpw) {
-    case 1: launch_round_tpw<KB, TW, 1>(d, cur, dcur, p, s, nt, storm); break;
-    case 2: launch_round_tpw<KB, TW, 2>(d, cur, dcur, p, s, nt, storm); break;
-    case 8: launch_round_tpw<KB, TW, 8>(d, cur, dcur, p, s, nt, storm); break;
-    default: launch_round_tpw<KB, TW, 4>(d, cur, dcur, p, s, nt, storm); break;
+    case 1: launch_round_tpw<KB, TW, 1>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
+    case 2: launch_round_tpw<KB, TW, 2>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
+    case 8: launch_round_tpw<KB, TW, 8>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
+    default: launch_round_tpw<KB, TW, 4>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
   }
 }
 
 template <int KB>
-static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm) {
+static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm,
+                            hipEvent_t t0, hipEvent_t t1) {
   switch (d.tw) {
-    case 8: launch_round_tw<KB, 8>(d, cur, dcur, p, s, nt, storm); break;
-    case 16: launch_round_tw<KB, 16>(d, cur, dcur, p, s, nt, storm); break;
-    case 32: launch_round_tw<KB, 32>(d, cur, dcur, p, s, nt, storm); break;
-    case 128: launch_round_tw<KB, 128>(d, cur, dcur, p, s, nt, storm); break;
-    case 256: launch_round_tw<KB, 256>(d, cur, dcur, p, s, nt, storm); break;
-    default: launch_round_tw<KB, 64>(d, cur, dcur, p, s, nt, storm); break;
+    case 8: launch_round_tw<KB, 8>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
+    case 16: launch_round_tw<KB, 16>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
+    case 32: launch_round_tw<KB, 32>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
+    case 128: launch_round_tw<KB, 128>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
+    case 256: launch_round_tw<KB, 256>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
+    default: launch_round_tw<KB, 64>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
   }
 }
 
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm) {
+void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm, hipEvent_t t0,
+                  hipEvent_t t1) {
   if (p.peer_mode == GH_PEER_PULL && p.k <= 4)
-    launch_round_kb<4>(d, cur, dcur, p, s, nt, storm);
+    launch_round_kb<4>(d, cur, dcur, p, s, nt, storm, t0, t1);
   else
-    launch_round_kb<8>(d, cur, dcur, p, s, nt, storm);
+    launch_round_kb<8>(d, cur, dcur, p, s, nt, storm, t0, t1);
 }
 
 void launch_base(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {

@@ -143,6 +143,18 @@ class Engine:
         self._chk(self.lib.gh_job_info(self.h, C.byref(nj), C.byref(nr)))
         return nj.value, nr.value
 
+    def debug_counts(self):
+        """(rows whose maintained present count differs from a full recount,
+        the first such row or -1): the invariant the <4 guard relies on
+        (gh_debug_counts, test-only and not in the header, like
+        gh_debug_tier; the maintained counts are left unchanged)."""
+        fn = self.lib.gh_debug_counts
+        fn.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]
+        fn.restype = C.c_int
+        nm, fr = C.c_int64(), C.c_int32()
+        self._chk(fn(self.h, C.byref(nm), C.byref(fr)))
+        return nm.value, fr.value
+
     def exchange_info(self):
         """dict(ghost_rows, bytes_out, bytes_in) of this shard's last ghost-row
         exchange (row layout; gh_exchange_info)."""

@@ -17,7 +17,17 @@ def gs():
     return gossipsim
 
 
+def check_counts(eng, r):
+    """The maintained per-row present counts (cntl: the rounds, events and
+    list merges keep them by deltas; the <4 guard reads them) equal a full
+    recount on every engine (gh_debug_counts)."""
+    for e in getattr(eng, "engines", [eng]):
+        nm, first = e.debug_counts()
+        assert nm == 0, f"r={r}: {nm} rows' maintained present counts differ from a recount, first row {first}"
+
+
 def compare(eng, orc, r, full=True):
+    check_counts(eng, r)
     h1, t1, a1 = eng.export_state()
     h2, t2, a2 = orc.export_state()
     np.testing.assert_array_equal(a1, a2, err_msg=f"alive r={r}")

@@ -21,6 +21,8 @@ def gs():
 
 
 def compare(eng, orc, r):
+    from test_gpu_parity import check_counts
+    check_counts(eng, r)
     h1, t1, a1 = eng.export_state()
     h2, t2, a2 = orc.export_state()
     np.testing.assert_array_equal(a1, a2, err_msg=f"alive r={r}")

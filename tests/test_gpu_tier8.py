@@ -317,3 +317,74 @@ def test_tier_tombstones(gs, oracle_mod, t_cleanup):
         assert tier_tombs > 0
     else:
         assert tier_tombs == 0
+
+
+def remove_run(gs, om, n, cfg, sched, rounds, world=1, layout=0, check=True):
+    """Runs the crash wave; returns per round (stats, tier variant, lane
+    jobs) and, for one engine, the final exported state."""
+    if world > 1:
+        eng = gs.ShardGroup(gs.default_config(n, shard_layout=layout, **cfg), world)
+    else:
+        eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = om.Oracle(om.default_config(n, **cfg), threads=8) if check else None
+    hb, ts, alive = sc.full_state(n)
+    eng.import_state(hb, ts, alive, 0)
+    if orc:
+        orc.import_state(hb, ts, alive, 0)
+    trace = []
+    try:
+        for r in range(1, rounds + 1):
+            ev = sched.get(r, [])
+            if ev:
+                eng.apply_events(ev)
+                if orc:
+                    orc.apply_events(ev)
+            s1 = eng.step(1)
+            if orc:
+                s2 = orc.step(1)
+                assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
+                compare(eng, orc, r)
+            var, jobs = (eng.tier_info(full=True)[3], eng.job_info()[0]) if world == 1 else (None, None)
+            trace.append((s1, var, jobs))
+        final = eng.export_state() if world == 1 else None
+    finally:
+        eng.close()
+        if orc:
+            orc.close()
+    return trace, final
+
+
+@pytest.mark.parametrize("case", ["canonical", "quirk", "t_cleanup20", "cols2", "rows3"])
+def test_tier_remove_on_nibble_path(gs, oracle_mod, monkeypatch, case):
+    """REMOVE delivery on the nibble path (round.hip nib_word RMV,
+    slave/slave.go:236-240, 276-286, 338-363): a 1% crash wave at N=2,048
+    with T_fail = 16 and T_cleanup >= 15, bit-exact against the oracle every
+    round. In the REMOVE rounds the REMOVE'd members' present cells become
+    tier tombstones inside the nibble path: one engine runs it (variant 3)
+    with at most a quarter of the lane jobs GH_NIB_RMV=0 (every lane holding a
+    REMOVE'd member a job) leaves, and both give the same tables and
+    counters. Quirk detection, an age offset of 7 (T_cleanup 20), 2 column
+    shards and 3 row shards run the same wave."""
+    n = 2048
+    t_cleanup = 20 if case == "t_cleanup20" else 16
+    cfg = dict(fanout=4, seed=0x5EED0C10, t_fail=16, t_cleanup=t_cleanup, detect_mode=1 if case == "quirk" else 0)
+    crashed = sc.crash_ids(n, 0.01, 0x5EED0C11)
+    sched = {8: [(sc.CRASH, int(c)) for c in crashed]}
+    rounds = 34
+    world, layout = {"cols2": (2, 0), "rows3": (3, 1)}.get(case, (1, 0))
+    trace, final = remove_run(gs, oracle_mod, n, cfg, sched, rounds, world, layout)
+    tomb_rounds = [r for r, (s, _, _) in enumerate(trace, 1) if s["tombstoned"]]
+    assert tomb_rounds, trace
+    if world > 1:
+        return
+    # the REMOVE rounds ran the nibble path, with few lane jobs
+    assert all(trace[r - 1][1] == 3 for r in tomb_rounds), [(r, trace[r - 1]) for r in tomb_rounds]
+    monkeypatch.setenv("GH_NIB_RMV", "0")
+    off, final_off = remove_run(gs, oracle_mod, n, cfg, sched, rounds, check=False)
+    for r, (a, b) in enumerate(zip(trace, off), 1):
+        assert a[0] == b[0], (r, a[0], b[0])
+    for x, y in zip(final, final_off):
+        np.testing.assert_array_equal(x, y)
+    on_jobs = sum(trace[r - 1][2] for r in tomb_rounds)
+    off_jobs = sum(off[r - 1][2] for r in tomb_rounds)
+    assert on_jobs * 4 <= off_jobs, (on_jobs, off_jobs, [(r, trace[r - 1][2], off[r - 1][2]) for r in tomb_rounds])
