@@ -252,11 +252,9 @@ class ListSim:
         if joiners and I.alive:
             added = 0
             for c in joiners:
-                if get_index(c, I.members) == -1:  # MemberInList (:198-205)
-                    # SPEC D7: a tombstoned joiner becomes present
-                    ti = get_index(c, I.recent_fail)
-                    if ti != -1:
-                        del I.recent_fail[ti]
+                if get_index(c, I.members) == -1:  # MemberInList reads MemberList only (:198-205)
+                    # SPEC D7: a joiner the introducer holds tombstoned is
+                    # appended and keeps its RecentFailList entry too
                     I._append(Member(c, 0, now))  # addNewMember (:250-255)
                     added += 1
             if added:

@@ -113,6 +113,7 @@ def lib():
         L.or_get_files.argtypes = [vp, vp, i64, vp, vp]
         L.or_delete_files.argtypes = [vp, vp, i64, vp]
         L.or_philox.argtypes = [vp, vp, vp]
+        L.or_debug_shadow.argtypes = [vp, vp]
         _lib = L
     return _lib
 
@@ -219,6 +220,13 @@ class Oracle:
         self._chk(lib().or_lsm(self.h, observer, _p(ids), _p(hb), _p(ts), self.n, C.byref(n)))
         k = n.value
         return ids[:k], hb[:k], ts[:k]
+
+    def debug_shadow(self):
+        """int32[n]: the ts of the introducer's RecentFailList entry beside
+        its present member c (SPEC D7), INT32_MIN where there is none."""
+        out = np.empty(self.cfg.n_members, np.int32)
+        self._chk(lib().or_debug_shadow(self.h, _p(out)))
+        return out
 
     def merge_list(self, observer, ids, hb):
         ids = np.ascontiguousarray(ids, dtype=np.int32)

@@ -60,6 +60,11 @@ typedef struct ors {
    * and nrecv (D_r, built after phase A) */
   int64_t W;
   uint64_t *lbase, *ldet, *recv, *nrecv;
+  /* SPEC D7: a JOIN of a member the introducer holds tombstoned appends it to
+   * MemberList while its RecentFailList entry stays (slave/slave.go:228-230,
+   * 250-255: MemberInList reads MemberList only). shadow[c] = the ts of that
+   * entry beside the present cell (I, c), OR_NO_SHADOW when none. */
+  int32_t *shadow;
   gh_event *ev;
   int64_t nev, evcap;
   int64_t fcap;
@@ -69,6 +74,7 @@ typedef struct ors {
   char err[256];
 } ors;
 
+#define OR_NO_SHADOW INT32_MIN
 #define HB(s, i, c) ((s)->hb[(int64_t)(i) * (s)->n + (c)])
 #define TS(s, i, c) ((s)->ts[(int64_t)(i) * (s)->n + (c)])
 #define SNAP(s, i, c) ((s)->snap[(int64_t)(i) * (s)->n + (c)])
@@ -97,6 +103,8 @@ int or_create(const gh_config *cfg, int64_t rows, void **out) {
   s->ndet_cnt = (int32_t *)calloc(s->n, 4);
   s->ndet_min = (int32_t *)malloc((size_t)s->n * 4);
   s->targets = (int32_t *)malloc((size_t)rows * 3 * 4);
+  s->shadow = (int32_t *)malloc((size_t)s->n * 4);
+  for (int32_t c = 0; c < s->n; ++c) s->shadow[c] = OR_NO_SHADOW;
   s->W = (s->n + 63) / 64;
   if (cfg->remove_mode == GH_REMOVE_LIST) {
     s->lbase = (uint64_t *)calloc((size_t)rows * s->W, 8);
@@ -155,6 +163,7 @@ void or_destroy(void *h) {
   free(s->ndet_cnt);
   free(s->ndet_min);
   free(s->targets);
+  free(s->shadow);
   free(s->ev);
   free(s->rep);
   free(s->ver);
@@ -185,6 +194,7 @@ int or_import_state(void *h, const int32_t *hb, const int32_t *ts, const uint8_t
   for (int32_t c = 0; c < s->n; ++c) {
     s->det_cnt[c] = 0;
     s->det_min[c] = INT_MAX;
+    s->shadow[c] = OR_NO_SHADOW; /* an imported list holds no member twice */
   }
   memset(s->det_any, 0, s->rows);
   return GH_OK;
@@ -229,7 +239,17 @@ int or_init_full(void *h, int32_t hb0, int32_t ts0, int32_t round) {
   for (int32_t c = 0; c < s->n; ++c) {
     s->det_cnt[c] = 0;
     s->det_min[c] = INT_MAX;
+    s->shadow[c] = OR_NO_SHADOW;
   }
+  return GH_OK;
+}
+
+/* Test access to the D7 shadow entries (SPEC D7): out[c] = the ts of the
+ * introducer's RecentFailList entry beside its present member c, or
+ * INT32_MIN. */
+int or_debug_shadow(void *h, int32_t *out) {
+  ors *s = (ors *)h;
+  memcpy(out, s->shadow, (size_t)s->n * 4);
   return GH_OK;
 }
 
@@ -253,10 +273,16 @@ int or_apply_events(void *h, const gh_event *ev, int64_t n) {
   return GH_OK;
 }
 
-/* removeMember(c) at row j (slave/slave.go:276-286). */
+/* removeMember(c) at row j (slave/slave.go:276-286). At the introducer a
+ * member that is also in RecentFailList (D7 shadow) leaves MemberList and
+ * keeps that entry, with its own ts, and nothing is appended (:278-281). */
 static inline void or_remove_member(ors *s, int64_t j, int32_t c, gh_round_stats *st) {
   int32_t v = HB(s, j, c);
-  if (v >= 0) {
+  if (v >= 0 && j == s->cfg.introducer && s->shadow[c] != OR_NO_SHADOW) {
+    HB(s, j, c) = GH_TOMBSTONE;
+    TS(s, j, c) = s->shadow[c];
+    s->shadow[c] = OR_NO_SHADOW;
+  } else if (v >= 0) {
     HB(s, j, c) = GH_TOMBSTONE; /* appended to RecentFailList with its ts (:280) */
     st->tombstoned++;
   } else if (v == GH_ABSENT) {
@@ -315,11 +341,13 @@ static void apply_events(ors *s, int32_t r, gh_round_stats *st) {
     int32_t c = s->ev[x].member;
     if (s->ev[x].kind != GH_EV_JOIN) continue;
     any_join = 1;
-    if (!s->alive[c]) { /* fresh process: empty MemberList (SPEC D7) */
+    if (!s->alive[c]) { /* fresh process: empty MemberList and RecentFailList (SPEC D7) */
       for (int32_t m = 0; m < s->n; ++m) {
         HB(s, c, m) = GH_ABSENT;
         TS(s, c, m) = 0;
       }
+      if (c == s->cfg.introducer)
+        for (int32_t m = 0; m < s->n; ++m) s->shadow[m] = OR_NO_SHADOW;
       s->alive[c] = 1;
     }
   }
@@ -330,6 +358,8 @@ static void apply_events(ors *s, int32_t r, gh_round_stats *st) {
       int32_t c = s->ev[x].member;
       if (s->ev[x].kind != GH_EV_JOIN) continue;
       if (HB(s, I, c) < 0) { /* !MemberInList (:228-230) -> addNewMember (:250-255) */
+        /* a tombstone stays in RecentFailList beside the new entry (D7) */
+        if (HB(s, I, c) == GH_TOMBSTONE) s->shadow[c] = TS(s, I, c);
         HB(s, I, c) = 0;
         TS(s, I, c) = r;
         added++;
@@ -418,6 +448,10 @@ static int phase_a(ors *s, int64_t i, int32_t r, gh_round_stats *st, int32_t *ld
     prev_cand = 1;
     if (!det) continue;
     row[c] = GH_TOMBSTONE; /* removeMember keeps the stale ts (:280) */
+    if (i == s->cfg.introducer && s->shadow[c] != OR_NO_SHADOW) { /* ... or the RecentFailList entry's (D7) */
+      trow[c] = s->shadow[c];
+      s->shadow[c] = OR_NO_SHADOW;
+    }
     if (literal) ld[c >> 6] |= 1ull << (c & 63);
     st->detections++;
     found = 1;
@@ -433,6 +467,12 @@ static int phase_a(ors *s, int64_t i, int32_t r, gh_round_stats *st, int32_t *ld
       st->released++;
     }
   }
+  if (i == s->cfg.introducer) /* RecentFailList entries beside present members (D7) */
+    for (int32_t c = 0; c < n; ++c)
+      if (s->shadow[c] != OR_NO_SHADOW && s->shadow[c] < climit) {
+        s->shadow[c] = OR_NO_SHADOW;
+        st->released++;
+      }
   return 1;
 }
 

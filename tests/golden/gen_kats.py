@@ -300,6 +300,45 @@ for mode, own, own_ts, tomb in ((1, 7, 21, 3), (0, T, 20, 4)):
         expect_stats=dict(tombstoned=tomb, detections=1, failed_members=1, remove_unknown=0)))
 
 
+# KAT-16 a JOIN of a member the introducer holds tombstoned (SPEC D7,
+# slave/slave.go:224-231, 250-255, 276-286, 484-497). Members 0..5 know each
+# other (hb 5, ts 19); T_fail = 1000, COOLDOWN 5; introducer 0.
+#  * Round 20: 4 LEAVEs: rows 0, 1, 2, 3, 5 tombstone it with its last ts 19
+#    (tombstoned 5).
+#  * Round 22: 4 JOINs (a fresh process). At 0, MemberInList reads MemberList
+#    only, so addNewMember appends (4, hb 0, ts 22) while RecentFailList keeps
+#    (4, ts 19). The broadcast reaches 1, 2, 3, 5, whose tombstones block the
+#    re-add (:430-433), and the fresh row 4.
+#  * Round 23 (the "leave" cases): 4 LEAVEs again. At 0, removeMember finds 4
+#    in RecentFailList, appends nothing (tombstoned stays 5) and drops it from
+#    MemberList: 0's tombstone of 4 is the old entry, ts 19. Rows 1, 2, 3, 5
+#    hold only the tombstone: a no-op (not a panic, :278-281).
+#  * cleanFailList releases every ts-19 entry in round 25 (19 < 25 - 5): after
+#    rounds 20..24 row 0 still holds the tombstone (ts 19, not the 22 of its
+#    present entry); after round 25 it is gone, with rows 1, 2, 3, 5's
+#    (released 5).
+#  * The "stay" case (no second LEAVE): round 25 releases 0's RecentFailList
+#    entry too, while 4 stays in its MemberList (released 5: four tombstones
+#    and the shadow entry).
+hb, ts, alive = blank(6)
+for j in range(6):
+    alive[j] = 1
+    for c in range(6):
+        hb[j][c], ts[j][c] = 5, 19
+for name, sched, rounds, col4, t4, rel in (
+        ("kat16_d7_rejoin_leave_5r", {"20": [[2, 4]], "22": [[1, 4]], "23": [[2, 4]]}, 5, T, 19, 0),
+        ("kat16_d7_rejoin_leave_6r", {"20": [[2, 4]], "22": [[1, 4]], "23": [[2, 4]]}, 6, A, 0, 5),
+        ("kat16_d7_rejoin_stay_6r", {"20": [[2, 4]], "22": [[1, 4]]}, 6, None, None, 5)):
+    kats.append(dict(
+        name=name, n=6, round=19, detect_mode=0, peer_mode=0, fanout=3, seed=7, t_fail=1000, t_cleanup=5,
+        hb=hb, ts=ts, alive=alive, events=[], sched=sched, rounds=rounds, expect_row=0,
+        expect_hb=[None, None, None, None, col4, None], expect_ts=[None, None, None, None, t4, None],
+        expect_more=[dict(row=j, hb=[None] * 4 + [T if rounds == 5 else A, None], ts=[None] * 4 + [19, None])
+                     for j in (1, 2, 3, 5)] if "leave" in name else [],
+        expect_failed=[], expect_detectors=[], expect_stats=dict(tombstoned=5, released=rel, detections=0,
+                                                                remove_unknown=0)))
+
+
 def row_matches(name, hb, ts, i, exp_hb, exp_ts):
     """hb of row i equals exp_hb (None = any), ts where present"""
     for c, v in enumerate(exp_hb):
@@ -318,7 +357,9 @@ def check_with_listsim(k):
                              quirk=bool(k["detect_mode"]), remove="list" if k.get("remove_mode") else "all")
     if k["events"]:
         sim.apply_events([tuple(e) for e in k["events"]])
-    st = sim.step(k.get("rounds", 1))
+    sys.path.insert(0, str(HERE.parent))
+    from kat_util import run_rounds
+    st = run_rounds(sim, k)
     hb, ts, _ = sim.dense()
     if k["expect_hb"] is not None:
         row_matches(k["name"], hb, ts, k["expect_row"], k["expect_hb"], k["expect_ts"])

@@ -26,12 +26,28 @@ def check_row(k, hb, ts, i, exp_hb, exp_ts):
             assert ts[i][c] == exp_ts[c], (k["name"], i, c, list(ts[i]))
 
 
+def run_rounds(engine, k):
+    """k["rounds"] rounds; events of k["sched"] ({round: [[kind, member]]})
+    before their round; the stats summed over the rounds"""
+    rounds = k.get("rounds", 1)
+    if "sched" not in k:
+        return engine.step(rounds)
+    tot = None
+    for r in range(k["round"] + 1, k["round"] + rounds + 1):
+        ev = k["sched"].get(str(r), [])
+        if ev:
+            engine.apply_events([tuple(e) for e in ev])
+        st = engine.step(1)
+        tot = dict(st) if tot is None else {key: (v if key == "last_round" else tot[key] + v) for key, v in st.items()}
+    return tot
+
+
 def run_kat(engine, k):
     engine.import_state(np.array(k["hb"], np.int32), np.array(k["ts"], np.int32),
                         np.array(k["alive"], np.uint8), k["round"])
     if k["events"]:  # applied at the first round (its events phase)
         engine.apply_events([tuple(e) for e in k["events"]])
-    st = engine.step(k.get("rounds", 1))
+    st = run_rounds(engine, k)
     hb, ts, _ = engine.export_state()
     if k["expect_hb"] is not None:
         check_row(k, hb, ts, k["expect_row"], k["expect_hb"], k["expect_ts"])

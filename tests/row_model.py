@@ -41,6 +41,7 @@ import torch.distributed as dist
 from oracle import philox
 
 ABSENT, TOMB = -1, -2
+NOSH = -(1 << 40)
 BIG = np.iinfo(np.int64).max
 
 
@@ -67,6 +68,10 @@ class RowModel:
         self.round = 0
         self.pending = []
         self.ghost_rows_in = 0
+        # SPEC D7: the ts of the introducer's RecentFailList entry beside its
+        # present member c (a join of a tombstoned member), NOSH where none;
+        # meaningful on the owner of row I
+        self.shadow = np.full(n, NOSH, np.int64)
 
     def owner(self, i):
         return i // self.nrs
@@ -83,6 +88,7 @@ class RowModel:
         self.round = round_
         self.dcnt[:] = 0
         self.dmin[:] = BIG
+        self.shadow[:] = NOSH
 
     def apply_events(self, ev):
         self.pending.extend(ev)
@@ -100,7 +106,11 @@ class RowModel:
 
     def _remove(self, j, c, st):  # removeMember, slave/slave.go:276-286
         x = self.hb[j - self.row0, c]
-        if x >= 0:
+        if x >= 0 and j == self.I and self.shadow[c] != NOSH:  # D7: the RecentFailList entry stays
+            self.hb[j - self.row0, c] = TOMB
+            self.ts[j - self.row0, c] = self.shadow[c]
+            self.shadow[c] = NOSH
+        elif x >= 0:
             self.hb[j - self.row0, c] = TOMB
             st["tombstoned"] += 1
         elif x == ABSENT:
@@ -128,6 +138,8 @@ class RowModel:
                 if self.owned(c):
                     self.hb[c - self.row0, :] = ABSENT
                     self.ts[c - self.row0, :] = 0
+                if c == self.I:
+                    self.shadow[:] = NOSH
                 self.alive[c] = True
         I = self.I
         if joiners and self.alive[I]:
@@ -135,6 +147,8 @@ class RowModel:
             if self.owned(I):
                 for c in joiners:
                     if self.hb[I - self.row0, c] < 0:
+                        if self.hb[I - self.row0, c] == TOMB:  # D7: its tombstone stays beside it
+                            self.shadow[c] = self.ts[I - self.row0, c]
                         self.hb[I - self.row0, c] = 0
                         self.ts[I - self.row0, c] = r
                         added += 1
@@ -208,7 +222,12 @@ class RowModel:
                 continue
             row, tsr = self.hb[i - self.row0], self.ts[i - self.row0]
             rm = self._removes_at(i)
-            st["tombstoned"] += int((rm & (row >= 0)).sum())
+            sh = (self.shadow != NOSH) if i == self.I else np.zeros(self.n, bool)
+            dual = rm & (row >= 0) & sh  # D7: the RecentFailList entry (and its ts) stays
+            tsr[dual] = self.shadow[dual]
+            self.shadow[dual] = NOSH
+            sh &= ~dual
+            st["tombstoned"] += int((rm & (row >= 0) & ~dual).sum())
             st["remove_unknown"] += int((rm & (row == ABSENT)).sum())
             row[rm & (row >= 0)] = TOMB
             if not active[i]:
@@ -220,6 +239,10 @@ class RowModel:
             det = (cols != i) & (row > 1) & (tsr < r - self.t_fail)
             if det.any():
                 row[det] = TOMB
+                dd = det & sh
+                tsr[dd] = self.shadow[dd]
+                self.shadow[dd] = NOSH
+                sh &= ~dd
                 st["detections"] += int(det.sum())
                 ndcnt[det] += 1
                 ndmin[det] = np.minimum(ndmin[det], i)
@@ -227,6 +250,9 @@ class RowModel:
             rel = (row == TOMB) & (tsr < r - self.t_cleanup)
             row[rel] = ABSENT
             st["released"] += int(rel.sum())
+            old = sh & (self.shadow < r - self.t_cleanup)
+            self.shadow[old] = NOSH
+            st["released"] += int(old.sum())
         snap_own = {i: np.where(self.hb[i - self.row0] >= 0, self.hb[i - self.row0], -1)
                     for i in range(self.row0, self.row0 + self.nrows)}
         inbox = self._inbox_pull(pre_hb, pre_ts, active, r) if self.pm == 0 else \

@@ -39,6 +39,29 @@ def random_churn(n, rounds, seed, p_crash=0.04, p_leave=0.02, p_join=0.05, start
     return sched
 
 
+def rejoin_churn(n, rounds, seed, p_out=0.06, p_back=0.5):
+    """Members leave (or crash) and come back within a few rounds, again and
+    again: the introducer (member 0) still holds the tombstone of a member
+    when it rejoins, so its list holds the member twice (SPEC D7), and a
+    later LEAVE, REMOVE or detection meets that double entry."""
+    rng = np.random.default_rng(seed)
+    alive = np.ones(n, bool)
+    sched = {}
+    for r in range(1, rounds + 1):
+        ev = []
+        for c in range(1, n):
+            u = rng.random()
+            if alive[c] and u < p_out:
+                ev.append((LEAVE if rng.random() < 0.6 else CRASH, c))
+                alive[c] = False
+            elif not alive[c] and u < p_back:
+                ev.append((JOIN, c))
+                alive[c] = True
+        if ev:
+            sched[r] = ev
+    return sched
+
+
 def crash_ids(n, frac, seed):
     """BASELINE configs: crash `frac` of N, IDs drawn by Philox(seed, CRASH);
     the introducer/master (0) is excluded."""

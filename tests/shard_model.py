@@ -31,6 +31,7 @@ import torch.distributed as dist
 from oracle import philox
 
 ABSENT, TOMB = -1, -2
+NOSH = -(1 << 40)
 
 
 def _gather_rows_bool(local: np.ndarray, ncs: int, n: int) -> np.ndarray:
@@ -65,6 +66,9 @@ class ShardModel:
         self.det_any = np.zeros(n, bool)
         self.round = 0
         self.pending = []
+        # SPEC D7: per local column the ts of the introducer's RecentFailList
+        # entry beside its present member (a join of a tombstoned member)
+        self.shadow = np.full(self.ncol, NOSH, np.int64)
 
     # ---- state -------------------------------------------------------------
     def import_full(self, hb, ts, alive, round_):
@@ -75,13 +79,18 @@ class ShardModel:
         self.round = round_
         self.dcnt[:] = 0
         self.dmin[:] = np.iinfo(np.int64).max
+        self.shadow[:] = NOSH
 
     def apply_events(self, ev):
         self.pending.extend(ev)
 
     def _remove(self, j, lc, st):  # removeMember, slave/slave.go:276-286
         x = self.hb[j, lc]
-        if x >= 0:
+        if x >= 0 and j == self.I and self.shadow[lc] != NOSH:  # D7: the RecentFailList entry stays
+            self.hb[j, lc] = TOMB
+            self.ts[j, lc] = self.shadow[lc]
+            self.shadow[lc] = NOSH
+        elif x >= 0:
             self.hb[j, lc] = TOMB
             st["tombstoned"] += 1
         elif x == ABSENT:
@@ -115,6 +124,8 @@ class ShardModel:
             if not self.alive[c]:
                 self.hb[c, :] = ABSENT
                 self.ts[c, :] = 0
+                if c == self.I:
+                    self.shadow[:] = NOSH
                 self.alive[c] = True
         I = self.I
         if joiners and self.alive[I]:
@@ -122,6 +133,8 @@ class ShardModel:
             for c in joiners:
                 lc = self._local(c)
                 if lc is not None and self.hb[I, lc] < 0:
+                    if self.hb[I, lc] == TOMB:  # D7: its tombstone stays beside it
+                        self.shadow[lc] = self.ts[I, lc]
                     self.hb[I, lc] = 0
                     self.ts[I, lc] = r
                     added += 1
@@ -177,7 +190,12 @@ class ShardModel:
             if not self.alive[i]:
                 continue
             rm = self._removes_at(i)
-            st["tombstoned"] += int((rm & (self.hb[i] >= 0)).sum())
+            sh = (self.shadow != NOSH) if i == self.I else np.zeros(self.ncol, bool)
+            dual = rm & (self.hb[i] >= 0) & sh  # D7: the RecentFailList entry (and its ts) stays
+            self.ts[i, dual] = self.shadow[dual]
+            self.shadow[dual] = NOSH
+            sh &= ~dual
+            st["tombstoned"] += int((rm & (self.hb[i] >= 0) & ~dual).sum())
             st["remove_unknown"] += int((rm & (self.hb[i] == ABSENT)).sum())
             self.hb[i, rm & (self.hb[i] >= 0)] = TOMB
             if not active[i]:
@@ -190,6 +208,10 @@ class ShardModel:
             det = (~own) & (self.hb[i] > 1) & (self.ts[i] < r - self.t_fail)
             if det.any():
                 self.hb[i, det] = TOMB
+                dd = det & sh
+                self.ts[i, dd] = self.shadow[dd]
+                self.shadow[dd] = NOSH
+                sh &= ~dd
                 st["detections"] += int(det.sum())
                 ndcnt[det] += 1
                 ndmin[det] = np.minimum(ndmin[det], i)
@@ -197,6 +219,9 @@ class ShardModel:
             rel = (self.hb[i] == TOMB) & (self.ts[i] < r - self.t_cleanup)
             self.hb[i, rel] = ABSENT
             st["released"] += int(rel.sum())
+            old = sh & (self.shadow < r - self.t_cleanup)
+            self.shadow[old] = NOSH
+            st["released"] += int(old.sum())
         snap = self.hb.copy()
         inbox = self._inbox_pull(snap, active, r) if self.pm == 0 else self._inbox_ring(snap, active, st)
         for i in range(self.n):

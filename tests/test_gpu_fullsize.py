@@ -253,3 +253,38 @@ def test_c5_fullsize_files(gs, oracle_mod):
 
     run(gs, oracle_mod, 16, 40, {40}, expect_detection, sched=sched, extra=dict(max_files=F),
         after_round=after_round)
+
+
+@pytest.mark.gpu_fullsize
+def test_c3_fullsize_reference_timeouts_remove_list_timed(gs):
+    """GH_REMOVE_LIST (the reference's REMOVE recipients, csrc/remove.hip)
+    through the reference timeouts' detection storm at N=65,536, timed: the
+    round-6 storm detects nearly every cell, so D_r holds nearly every member
+    with nearly every row as a detector -- the worst case of the recipient
+    decision (k_rm_recv: counts and the pigeonhole rule settle the pairs,
+    the nonzero words of det(c) the rest). Every round must finish within 5 s
+    (ADVICE round 4); the engine runs alone (tablesim's literal recipients
+    are O(|det(c)| * N / 32) per member, hours in a storm of this size), and
+    the rounds up to the storm equal the D4 engine's counters (the two rules
+    only part once a REMOVE is delivered)."""
+    cfg = dict(fanout=4, seed=0x5EED0003, t_fail=5, t_cleanup=5)
+    lit = gs.Engine(gs.default_config(N, remove_mode=1, **cfg))
+    d4 = gs.Engine(gs.default_config(N, **cfg))
+    try:
+        lit.init_full(2, 0, 0)
+        d4.init_full(2, 0, 0)
+        storm = False
+        for r in range(1, 13):
+            t0 = time.perf_counter()
+            s1 = lit.step(1)
+            ms = 1e3 * (time.perf_counter() - t0)
+            s2 = d4.step(1)
+            print(f"  r={r}: literal REMOVE {ms:.1f} ms, {s1}", flush=True)
+            assert ms < 5000, f"round {r}: {ms:.0f} ms"
+            storm |= s1["detections"] > N * N // 4
+            if r <= 6:  # before the first REMOVE delivery
+                assert s1 == s2, (r, s1, s2)
+        assert storm
+    finally:
+        lit.close()
+        d4.close()

@@ -388,3 +388,20 @@ def test_tier_remove_on_nibble_path(gs, oracle_mod, monkeypatch, case):
     on_jobs = sum(trace[r - 1][2] for r in tomb_rounds)
     off_jobs = sum(off[r - 1][2] for r in tomb_rounds)
     assert on_jobs * 4 <= off_jobs, (on_jobs, off_jobs, [(r, trace[r - 1][2], off[r - 1][2]) for r in tomb_rounds])
+
+
+@pytest.mark.parametrize("case", ["steady_crash", "remove_quirk"])
+def test_tier_lds_dma_staging(gs, oracle_mod, monkeypatch, case):
+    """The nibble path with its lines staged by LDS-DMA (GH_NIB_DMA=1,
+    round.hip round_block_nib DMA: buffer_load_dwordx4 ... lds, 8 rows per
+    wave step) at N=2,048, k=4, T_fail=16: a crash wave with its detection,
+    REMOVE and release rounds (canonical, then quirk detection), bit-exact
+    against the oracle every round, the nibble path in the healthy rounds."""
+    monkeypatch.setenv("GH_NIB_DMA", "1")
+    n = 2048
+    cfg = dict(fanout=4, seed=0x5EED0D10, t_fail=16, t_cleanup=16, detect_mode=1 if case == "remove_quirk" else 0)
+    crashed = sc.crash_ids(n, 0.01, 0x5EED0D11)
+    sched = {8: [(sc.CRASH, int(c)) for c in crashed], 30: [(sc.JOIN, int(crashed[0]))]}
+    trace, _ = remove_run(gs, oracle_mod, n, cfg, sched, 36)
+    assert sum(v == 3 for _, v, _ in trace) >= 30, trace
+    assert any(s["tombstoned"] for s, _, _ in trace)

@@ -10,7 +10,7 @@ import scenarios as sc
 
 
 def run_pair(om, n, rounds, sched, peer_mode, fanout=3, quirk=False, seed=0x5EED0001,
-             init_full=False, t_fail=5, t_cleanup=5, remove="all"):
+             init_full=False, t_fail=5, t_cleanup=5, remove="all", per_round=None):
     cfg = om.default_config(n, peer_mode=om.GH_PEER_RING if peer_mode == "ring" else om.GH_PEER_PULL,
                             fanout=fanout, detect_mode=int(quirk), seed=seed, t_fail=t_fail,
                             t_cleanup=t_cleanup,
@@ -43,6 +43,8 @@ def run_pair(om, n, rounds, sched, peer_mode, fanout=3, quirk=False, seed=0x5EED
             failed = [c for c in range(n) if bm[c >> 5] >> (c & 31) & 1]
             assert failed == ls.last_failed
             assert list(orc.read_detectors()) == ls.last_detectors
+            if per_round:
+                per_round(orc, ls, r)
     finally:
         L.T_FAIL, L.T_CLEANUP = 5, 5
     return orc, ls
@@ -112,3 +114,33 @@ def test_bootstrap_churn_remove_list(oracle_mod, seed):
     for r, ev in sc.random_churn(n, 50, seed, p_crash=0.05).items():
         sched.setdefault(r + n, []).extend(ev)
     run_pair(oracle_mod, n, 60, sched, "ring", init_full=False, seed=0x4000 + seed, remove="list")
+
+
+@pytest.mark.parametrize("peer_mode", ["ring", "pull"])
+@pytest.mark.parametrize("quirk", [False, True])
+@pytest.mark.parametrize("seed", [11, 12])
+def test_rejoin_while_tombstoned(oracle_mod, peer_mode, quirk, seed):
+    """SPEC D7 under churn: members leave or crash and rejoin while the
+    introducer still holds their tombstone, so its list holds them twice
+    (MemberList and RecentFailList, slave/slave.go:228-230, 250-255); later
+    LEAVEs, REMOVEs and detections meet the double entry
+    (:276-286) and cleanFailList releases the old entry (:484-497).
+    listsim (the literal lists) = tablesim (the shadow entries) every round,
+    and double entries do occur."""
+    n = 12
+    sched = sc.rejoin_churn(n, 45, seed)
+    seen = []
+
+    def per_round(orc, ls, r):
+        sh = orc.debug_shadow()
+        I = ls.nodes[0]
+        dual = sorted(m.addr for m in I.members if any(f.addr == m.addr for f in I.recent_fail))
+        assert sorted(np.nonzero(sh != np.iinfo(np.int32).min)[0].tolist()) == dual, (r, sh, dual)
+        for f in I.recent_fail:  # the entry's own ts (removeMember kept the Member, :280)
+            if f.addr in dual:
+                assert sh[f.addr] == f.ts, (r, f.addr, sh[f.addr], f.ts)
+        seen.append(len(dual))
+
+    run_pair(oracle_mod, n, 45, sched, peer_mode, quirk=quirk, init_full=True, seed=0x3000 + seed,
+             t_fail=4, t_cleanup=6, per_round=per_round)
+    assert max(seen) > 0, seen
