@@ -174,9 +174,18 @@ struct OpLeave {
   static constexpr bool kTally = true;  // tombstoned, unknown
   GhDev d;
   int32_t nl;
+  int32_t shadow_row;  // GhRound.shadow_row
   __device__ GhCell operator()(int64_t j, int64_t c, const GhCell& v, uint32_t* t) const {
     const int q = d.colq[c];
     if (q < 0 || !d.alive[j] || d.col0 + c == j || !gh_gbit(d, d.rbits, nl, q, j)) return v;
+    if (v.x >= 0 && j == shadow_row && d.shadow[c] != GH_NO_SHADOW) {
+      // the introducer holds c in RecentFailList too (D7): that entry, its
+      // ts, is the tombstone; nothing is appended (:278-281)
+      const int32_t ts = d.shadow[c];
+      d.shadow[c] = GH_NO_SHADOW;
+      atomicSub(d.nshadow, 1);
+      return GhCell{GH_TOMBSTONE, ts, false};
+    }
     if (v.x >= 0) {
       t[0]++;
       return GhCell{GH_TOMBSTONE, v.ts, false};  // keeps its ts (slave/slave.go:280)
@@ -199,6 +208,10 @@ struct OpJoinAdd {
   __device__ GhCell operator()(int64_t, int64_t c, const GhCell& v, uint32_t* t) const {
     if (d.colq[c] < 0 || v.x >= 0) return v;
     t[0]++;
+    if (v.x == GH_TOMBSTONE) {  // MemberInList reads MemberList only: the tombstone stays beside it (D7)
+      d.shadow[c] = v.ts;
+      atomicAdd(d.nshadow, 1);
+    }
     return GhCell{0, p.r, false};  // hb 0, ts = now
   }
   __device__ void flush(const uint32_t* t) const { atomicAdd(&d.nd[4], (int)t[0]); }
@@ -446,7 +459,7 @@ void launch_leave(const GhDev& d, int cur, const int32_t* leavers, const int32_t
                   const GhRound& p, hipStream_t s) {
   if (ntl == 0) return;
   scatter(d, leavers, nullptr, nl, 0xFF, s);
-  seg_launch(d, cur, SegSet{nullptr, d.row0, d.nrows, tiles, ntl}, nullptr, p, OpLeave{d, nl}, s);
+  seg_launch(d, cur, SegSet{nullptr, d.row0, d.nrows, tiles, ntl}, nullptr, p, OpLeave{d, nl, p.shadow_row}, s);
 }
 
 void launch_join_add(const GhDev& d, int cur, const int32_t* joiners, int32_t nj, int32_t introducer,

@@ -136,6 +136,7 @@
 
 #include "../../include/gossiphip.h"
 
+#define GH_NO_SHADOW ((int32_t)0x80808080)  // no D7 shadow entry (GhDev.shadow; a byte fill of 0x80)
 #define GH_N_ABSENT 0xFFFFu                // narrow absent
 #define GH_N_TOMB 0xFFE0u                  // narrow tombstone | age
 #define GH_N_WIDE 0x7FFFu                  // chunk marker of a wide segment (cells 1, 2: arena slot)
@@ -354,6 +355,15 @@ struct GhDev {
   uint32_t *cdet, *csurv, *clst;
   int32_t *ccnt;
   int32_t *dlist;
+  // SPEC D7 (slave/slave.go:228-230, 250-255, 276-286): a JOIN of a member the
+  // introducer holds tombstoned appends it to MemberList while the
+  // RecentFailList entry stays. shadow[c] (local column) = that entry's ts
+  // beside the introducer's present member c, GH_NO_SHADOW when none;
+  // nshadow[0] = entries held. A LEAVE, REMOVE or detection of c at the
+  // introducer leaves the old entry (its ts, no new tombstone counted);
+  // cleanFailList releases it like any tombstone. The introducer's segments
+  // run the per-cell rule (k_round_slow) while any entry may exist.
+  int32_t *shadow, *nshadow;
   int32_t *nd;      // [0..1] local |D| per parity, [2..3] dlist fill, [4] join adds, [5] list merges
   int32_t *inbox_beg, *inbox_cnt, *inbox, *inbox_fill, *targets;
   int32_t *ring;    // ring mode: [world][n][2] (local snapshot count, local position of the sender)
@@ -831,6 +841,8 @@ struct GhRound {
   int32_t force_storm;  // diagnostics (GH_FORCE_STORM): run the storm variant every round
   int32_t force_slow;   // diagnostics (GH_FORCE_SLOW): every segment by the per-cell rule
   int32_t nib_rmv;      // nibble path: REMOVE'd members with >= 2 detectors stay on it (GH_NIB_RMV=0: lane jobs)
+  int32_t nib_dma;      // nibble path: LDS-DMA staging of the own and sender lines (GH_NIB_DMA; column layout, TW 256)
+  int32_t shadow_row;   // the introducer while it may hold D7 shadow entries (its segments take k_round_slow), else -1
   int32_t plane;        // the round writes the next buffer's sender plane (and may read cur's)
   int32_t ring_whole;   // ring mode: one engine and a current flag count, so the targets may come
                         // from whole lists when no REMOVE / flag is pending (k_ring_fast)

@@ -58,6 +58,8 @@ struct Engine {
   int force_storm = 0;   // storm variant every round (GH_FORCE_STORM, diagnostics)
   int force_slow = 0;    // every segment by the per-cell rule (GH_FORCE_SLOW, diagnostics)
   int nib_rmv = 1;       // REMOVE'd members with >= 2 detectors on the nibble path (GH_NIB_RMV=0: lane jobs, A/B)
+  int nib_dma = 0;       // the nibble path stages its lines by LDS-DMA (GH_NIB_DMA=1, A/B)
+  bool shadow_any = false;  // the introducer's row may hold D7 shadow entries (GhDev.shadow; re-read after each gh_step)
   bool timing = false;
   bool side = true;      // idle round variants on the side stream (GH_SIDE=0: in line)
   // the current table may hold flags no round kernel counted (import, fill,
@@ -196,6 +198,8 @@ GhRound round_params(const Engine* e, int32_t r) {
   p.force_storm = e->force_storm;
   p.force_slow = e->force_slow;
   p.nib_rmv = e->nib_rmv;
+  p.nib_dma = e->nib_dma;
+  p.shadow_row = e->shadow_any ? e->cfg.introducer : -1;
   p.plane = e->plane;
   // (a row shard holds its senders' whole rows: their lists)
   p.ring_whole = (e->world == 1 || e->rowlay) && e->flags_known;
@@ -750,6 +754,8 @@ int allreduce_i32(Engine* e, int32_t* send, int32_t* recv, size_t count) {
 }
 
 // SPEC.md §5: crashes, then leaves (all leavers stop first), then joins.
+int reset_shadows(Engine* e);
+
 int process_events(Engine* e, int32_t r) {
   if (e->pending.empty()) return GH_OK;
   e->qforce = true;
@@ -817,6 +823,8 @@ int process_events(Engine* e, int32_t r) {
   }
   if (!fresh.empty()) {
     if ((rc = upload(e, e->ev_buf, fresh))) return rc;
+    // a restarted introducer starts with empty lists: no shadow entry
+    if (std::find(fresh.begin(), fresh.end(), e->cfg.introducer) != fresh.end() && (rc = reset_shadows(e))) return rc;
     launch_join_reset(e->d, e->cur, e->ev_buf, (int32_t)fresh.size(), p, e->stream);
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if ((rc = release_rows(e, fresh))) return rc;
@@ -827,6 +835,7 @@ int process_events(Engine* e, int32_t r) {
     if ((rc = upload(e, e->ev_buf, joiners))) return rc;
     launch_join_add(e->d, e->cur, e->ev_buf, (int32_t)joiners.size(), I, p, e->stream);
     HIPCHK(e, hipGetLastError());
+    e->shadow_any = true;  // a joiner the introducer held tombstoned gets a shadow entry (D7)
     if ((rc = allreduce_i32(e, e->d.nd + 4, e->d.nd + 4, 1))) return rc;
     if ((rc = upload(e, e->rows_buf, {I}))) return rc;
     if ((rc = gather_rows(e, e->rows_buf, 1))) return rc;
@@ -996,6 +1005,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (const char* v = std::getenv("GH_FORCE_STORM")) e->force_storm = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_FORCE_SLOW")) e->force_slow = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_NIB_RMV")) e->nib_rmv = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_NIB_DMA")) e->nib_dma = std::atoi(v) != 0;
   if (tw != 8 && tw != 16 && tw != 32 && tw != 64 && tw != 128 && tw != 256) {
     delete e;
     return GH_EINVAL;
@@ -1146,7 +1156,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
     if ((rc = dalloc(e, &d.det_cnt[0], e->ld, 0)) || (rc = dalloc(e, &d.det_cnt[1], e->ld, 0)) ||
         (rc = dalloc(e, &d.det_min[0], e->ld, 0x7F)) || (rc = dalloc(e, &d.det_min[1], e->ld, 0x7F)) ||
         (rc = dalloc(e, &d.dbits, e->ld / 32 + 2, 0)) || (rc = dalloc(e, &d.dlist, 2 * e->ld, 0)) ||
-        (rc = dalloc(e, &d.nd, 8, 0)))
+        (rc = dalloc(e, &d.nd, 8, 0)) || (rc = dalloc(e, &d.shadow, e->ld, 0x80)) ||
+        (rc = dalloc(e, &d.nshadow, 1, 0)))
       break;
     // GH_REMOVE_LIST: the recipients of two REMOVE sets and the column
     // bitmaps of a sweep, [ld][ceil(n / 32)] words each (remove.hip)
@@ -1372,6 +1383,14 @@ int encode_rows(Engine* e, const char* what, F launch) {
 
 // Buffer cur emptied (all absent narrow, arena reset) before a whole-table
 // rewrite.
+// No D7 shadow entry (rows written whole hold no member twice).
+int reset_shadows(Engine* e) {
+  HIPCHK(e, hipMemsetAsync(e->d.shadow, 0x80, sizeof(int32_t) * (size_t)e->ld, e->stream));
+  HIPCHK(e, hipMemsetAsync(e->d.nshadow, 0, sizeof(int32_t), e->stream));
+  e->shadow_any = false;
+  return GH_OK;
+}
+
 int clear_table(Engine* e) {
   GhDev& d = e->d;
   HIPCHK(e, hipMemsetAsync(d.hn[e->cur], 0xFF, sizeof(uint16_t) * (size_t)d.nslots * e->ld, e->stream));
@@ -1632,6 +1651,7 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
   e->hb_bound = full ? hmax : std::max(e->hb_bound, hmax);
   e->pending.clear();
   if ((rc = reset_pending_removes(e))) return rc;
+  if (e->cfg.introducer >= row0 && e->cfg.introducer < row0 + n_rows && (rc = reset_shadows(e))) return rc;
   launch_count(e->d, e->cur, p, e->stream);
   if (e->lorder) launch_list_import(e->d, e->cur, e->lcur, row0, n_rows, e->stream);  // dense rows: ID order
   HIPCHK(e, hipGetLastError());
@@ -1672,6 +1692,7 @@ int gh_init_full(void* h, int32_t hb0, int32_t ts0, int32_t round) {
   if ((rc = settle_rows(e, 0, e->n, p))) return rc;
   e->hb_bound = hb0;
   if ((rc = reset_pending_removes(e))) return rc;
+  if ((rc = reset_shadows(e))) return rc;
   launch_count(e->d, e->cur, p, e->stream);
   if (e->lorder) launch_list_import(e->d, e->cur, e->lcur, 0, e->n, e->stream);
   HIPCHK(e, hipGetLastError());
@@ -1825,9 +1846,12 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     }
   }
   unsigned long long st[ST_COUNT];
+  int32_t nshadow = 0;
   COMMCHK(e, e->comm->allreduce(e->d.stats, e->d.stats, ST_COUNT, GH_DT_U64, GH_OP_SUM, e->stream));
   HIPCHK(e, hipMemcpyAsync(st, e->d.stats, sizeof st, hipMemcpyDeviceToHost, e->stream));
+  if (e->shadow_any) HIPCHK(e, hipMemcpyAsync(&nshadow, e->d.nshadow, sizeof nshadow, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
+  e->shadow_any = nshadow > 0;  // (each shard for its own columns)
   {
     int32_t err = 0;
     int rc;
@@ -2257,6 +2281,20 @@ int gh_debug_raw(void* h, int32_t row, int64_t c0, int64_t n, uint16_t* codes, i
 // the <4 guard and active[] read. *mismatched = rows whose maintained count
 // differs, *first_row = the first of them (-1: none). The maintained counts
 // are restored, so the check changes nothing.
+// Debug (tests only, not in the header): the D7 shadow entries of this
+// engine's local columns [col0, col0 + ncols): out[c] = the ts of the
+// introducer's RecentFailList entry beside its present member, or
+// GH_NO_SHADOW; *count = entries the engine counts (nshadow).
+int gh_debug_shadow(void* h, int32_t* out, int64_t n_out, int32_t* count) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || !out || !count || n_out < e->d.ncol) return GH_EINVAL;
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  HIPCHK(e, hipMemcpyAsync(out, e->d.shadow, sizeof(int32_t) * (size_t)e->d.ncol, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(count, e->d.nshadow, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
 int gh_debug_counts(void* h, int64_t* mismatched, int32_t* first_row) {
   Engine* e = static_cast<Engine*>(h);
   if (!e || !mismatched || !first_row) return GH_EINVAL;

@@ -946,7 +946,13 @@ __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint
 // plane segment in the tile slice, as with columns) or a ghost row whose
 // plane words the round's exchange put in the ghost table (row-major,
 // gplane); the gathers then take per-sender 64-bit addresses staged in LDS.
-template <int TW, bool NT, int CPL, bool ROWS>
+// DMA (one engine or column shards, 16 cells per lane): each wave stages its
+// 8 rows of a step into its own LDS region by LDS-DMA (buffer_load_dwordx4
+// ... lds, 16 B per lane: the own lag and age lines as two 1-KiB pieces, the
+// 32 sender lines as four), then computes them on ds_read_b64 in the 16-cell
+// lane shape: half the vector-memory load instructions of 8-B register loads,
+// and no VGPRs held by loads in flight.
+template <int TW, bool NT, int CPL, bool ROWS, bool DMA = false>
 __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, const int dcur, const GhRound& p,
                                                 const int bid) {
   constexpr int W = CPL / 8;         // dwords per lane and plane
@@ -958,6 +964,11 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   constexpr int RS = GH_NIB_RS > 0 ? GH_NIB_RS : (CPL <= 16 ? 2 : 1);  // row steps per iteration
   static_assert(SEG >= 2 && SEG <= 64 && RB % (RSTEP * RS) == 0, "nibble path: whole row steps");
   static_assert(W == 2 || W == 4, "nibble path: 16 or 32 cells per lane (one or two lane jobs of 16 cells)");
+  static_assert(!DMA || (!ROWS && CPL == 16 && TW == 256 && RB % 32 == 0), "LDS-DMA staging: 16-cell lanes, 256-member tiles");
+  constexpr int RSD = DMA ? 2 : RS;  // row steps per iteration (DMA: a wave's 8 consecutive rows)
+  // per wave: own lag 1 KiB, age 1 KiB, the 4 gather pieces (sender slot q
+  // of the 8 rows) 1 KiB each
+  __shared__ __attribute__((aligned(16))) uint32_t s_dma[DMA ? 4 * 1536 : 1];
   constexpr int H = W / 2;  // lane jobs of GH_JOB_CPL cells per job lane
   __shared__ unsigned long long s_merged, s_rel, s_tmb;
   __shared__ int s_quiet, s_nslow, s_slowbase, s_bmove, s_hasjob;
@@ -1123,14 +1134,39 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   uint32_t n_mrg = 0, n_rel = 0, n_tmb = 0;
 
 #pragma unroll 1
-  for (int it = 0; it < RB / RSTEP; it += RS) {
-    int iu[RS];
-    bool alu[RS], oku[RS];
-    uint32_t owu[RS];
-    NibWords<W> awu[RS], qwu[RS], pwu[RS][4];
+  for (int it = 0; it < RB / RSTEP; it += RSD) {
+    int iu[RSD];
+    bool alu[RSD], oku[RSD];
+    uint32_t owu[RSD];
+    NibWords<W> awu[RSD], qwu[RSD], pwu[RSD][4];
+    char* wb = reinterpret_cast<char*>(s_dma) + (DMA ? wave * 6144 : 0);
+    if constexpr (DMA) {
+      // the wave's rows it * RSTEP + wave * 8 .. + 7 of the block: their own
+      // lines are one contiguous KiB of each plane's tile slice; DMA lane l
+      // moves bytes [16 l, 16 l + 16), and for sender slot q the 16 B at
+      // (l % 8) * 16 of row l / 8's sender line (hipcc does not wait for an
+      // LDS-DMA: the waits are explicit)
+      typedef __attribute__((address_space(3))) void lds_t;
+      const int rbase = it * RSTEP + wave * 8;
+      const uint32_t own = (uint32_t)(rb * RB + rbase) * (TW / 2) + (uint32_t)lane * 16u;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the previous step's LDS reads are done
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(plo_t, (lds_t*)wb, 16, (int)own, 0, 0, GH_NIB_OWN_AUX);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(a4o_t, (lds_t*)(wb + 1024), 16, (int)own, 0, 0, GH_NIB_AGE_AUX);
+      const int4 sv4 = *reinterpret_cast<const int4*>(&s_inb[(rbase + (lane >> 3)) * KB]);
+      const uint32_t dcol = (uint32_t)(lane & 7) * 16u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(plo_t, (lds_t*)(wb + 2048), 16, (int)((uint32_t)sv4.x + dcol), 0, 0,
+                                               GH_NIB_GAT_AUX);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(plo_t, (lds_t*)(wb + 3072), 16, (int)((uint32_t)sv4.y + dcol), 0, 0,
+                                               GH_NIB_GAT_AUX);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(plo_t, (lds_t*)(wb + 4096), 16, (int)((uint32_t)sv4.z + dcol), 0, 0,
+                                               GH_NIB_GAT_AUX);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(plo_t, (lds_t*)(wb + 5120), 16, (int)((uint32_t)sv4.w + dcol), 0, 0,
+                                               GH_NIB_GAT_AUX);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 #pragma unroll
-    for (int u = 0; u < RS; ++u) {
-      const int rr = wave * RPW + (it + u) * RSTEP + sub;
+    for (int u = 0; u < RSD; ++u) {
+      const int rr = DMA ? it * RSTEP + wave * 8 + u * RPW + sub : wave * RPW + (it + u) * RSTEP + sub;
       const int i_raw = (int)d.row0 + rb * RB + rr;
       const bool valid = i_raw < rowend;
       const int i = valid ? i_raw : rowend - 1;  // in-range row for the loads of idle lanes
@@ -1145,6 +1181,20 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       const uint32_t islot = (uint32_t)(i - d.row0);
       const uint32_t ow = islot * (TW / 2) + lbp;
       owu[u] = ow;
+      if constexpr (DMA) {
+        const int o = (u * RPW + sub) * (TW / 2) + (int)lbp;
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        const u2 q2 = *reinterpret_cast<const u2*>(wb + o);
+        const u2 a2 = *reinterpret_cast<const u2*>(wb + 1024 + o);
+        qwu[u].v[0] = q2[0], qwu[u].v[1] = q2[1];
+        awu[u].v[0] = a2[0], awu[u].v[1] = a2[1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const u2 g2 = *reinterpret_cast<const u2*>(wb + 2048 + q * 1024 + o);
+          pwu[u][q].v[0] = g2[0], pwu[u][q].v[1] = g2[1];
+        }
+        continue;
+      }
       // the age words are read once (no peer reads them): they stream past
       // the caches the plane lines live in; the own plane words are a line
       // the row's receivers gather too
@@ -1167,7 +1217,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       }
     }
 #pragma unroll
-    for (int u = 0; u < RS; ++u) {
+    for (int u = 0; u < RSD; ++u) {
       const int i = iu[u];
       const bool al = alu[u];
       uint32_t QO[W], AO[W], LW[W], A1[W], Bm = 0, Lz = 0;
@@ -1217,7 +1267,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       // GH_FORCE_SLOW) sends its whole segment to the slow list; in any other
       // row a lane whose cells leave the tier or need the per-cell rule is a
       // lane job (k_round_jobs), and the segment's other lanes are written here
-      const bool rowok = oku[u] && !p.force_slow;
+      const bool rowok = oku[u] && !p.force_slow && i != p.shadow_row;  // (D7 shadows: the per-cell rule)
       const bool jb = al && rowok && (lane_job || esc || ob || Bm != 0 || Lz != 0 || i == rmrow);
       const unsigned long long jm = __ballot(jb);
       // a job whose rule gathers its senders' 16-bit codes (a REMOVE'd member,
@@ -1546,7 +1596,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     // 4-slot one lists them (the stamp select cost 4% of the healthy pull
     // round, measured A/B on one box)
     constexpr bool LEAN_GUARD = KB > 4;
-    bool bad = (!STORM && !LEAN_GUARD && !act) || cntv > KB;
+    bool bad = (!STORM && !LEAN_GUARD && !act) || cntv > KB || i == p.shadow_row;  // (D7 shadows: per-cell rule)
     // the staged slots, one LDS read per 4 (unused slots hold 0)
     int sv[KB];
 #pragma unroll
@@ -1972,15 +2022,16 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 // of the workgroups, each taking blocks a multiple of 8 apart (same XCD), so
 // idle they are a small dispatch.
 template <int KB, int TW, int TPW, bool NT, bool STORM, int IN>
-__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : (IN == 2 || IN == 4) ? GH_NIB_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
+__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : (IN == 2 || IN == 4 || IN == 5) ? GH_NIB_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
   if (*d.mode != (int)STORM) return;
   if constexpr (!STORM) {
     int want = 0;
     if (d.a4[0])
       want = !gh_m8(d, cur) ? 3 : (KB == 4 && p.plane && d.pvalid[cur] && gh_m8(d, cur ^ 1)) ? (d.rowlay ? 4 : 2) : 1;
+    if (want == 2 && p.nib_dma && TW == 256 && GH_NIB_CPL == 16) want = 5;  // LDS-DMA staging (GH_NIB_DMA)
     if (want != IN) return;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) d.m8[4] = STORM ? 1 : (IN == 2 || IN == 4) ? 3 : IN == 1 ? 2 : 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.m8[4] = STORM ? 1 : (IN == 2 || IN == 4 || IN == 5) ? 3 : IN == 1 ? 2 : 0;
   // every running row a quiet candidate and no base moved (one engine): the
   // round reads and writes nothing (a collapsed cluster)
   if (d.world == 1 && !d.rowlay && d.aq[0] == 0 && d.cntg[p.n] == 0 && !p.force_slow && !(d.a4[0] && d.m8[2])) {
@@ -1996,6 +2047,8 @@ __global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM 
     }
   } else if constexpr (IN == 2 || IN == 4) {
     round_block_nib<TW, NT, GH_NIB_CPL, IN == 4>(d, cur, dcur, p, blockIdx.x);  // one block per workgroup
+  } else if constexpr (IN == 5) {
+    if constexpr (TW == 256 && GH_NIB_CPL == 16) round_block_nib<TW, NT, 16, false, true>(d, cur, dcur, p, blockIdx.x);
   } else {
     // one block per workgroup (a loop here costs the lean variants 20+ VGPRs)
     round_block<KB, TW, TPW, NT, STORM, IN>(d, cur, dcur, p, blockIdx.x);
@@ -2049,6 +2102,7 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
     const int cnt = gh_in_cnt(d, pull, p.k, i);
     const int64_t beg = gh_in_beg(d, pull, p.k, i);
     const uint32_t my8 = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
+    const bool shr = i == p.shadow_row;  // the introducer's D7 shadow entries (GhDev.shadow)
     bool fit = true, any_det = false;
     int dpres = 0;  // present after - present before
     GhCell o[8];
@@ -2079,11 +2133,21 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
         const GhCell v = A[j];
         int64_t x = v.x;
         bool now = false;  // ts := r in this round
+        // D7: the introducer's RecentFailList entry beside its present member
+        // c: a removal this round keeps that entry (its ts) as the tombstone
+        int32_t sh = (shr && x >= 0 && valid) ? d.shadow[l0 + j] : GH_NO_SHADOW;
+        const int32_t sh0 = sh;
+        int32_t tts = v.ts;  // the ts a tombstone keeps
         // step 1: REMOVE delivery (slave/slave.go:236-240, 276-286)
         if (((my8 >> j) & 1u) && gh_rm_at(d, dcur, l0 + j, i)) {
           if (x >= 0) {
             x = GH_TOMBSTONE;
-            n_tomb++;
+            if (sh != GH_NO_SHADOW) {  // nothing appended to RecentFailList (:278-281)
+              tts = sh;
+              sh = GH_NO_SHADOW;
+            } else {
+              n_tomb++;
+            }
           } else if (x == GH_ABSENT) {
             n_unknown++;
           }
@@ -2099,15 +2163,27 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
             }
           } else if (x >= 0 && v.f) {  // step 4 detect (:468-473), decided at the last write
             x = GH_TOMBSTONE;
+            if (sh != GH_NO_SHADOW) {
+              tts = sh;
+              sh = GH_NO_SHADOW;
+            }
             n_det++;
             any_det = true;
             atomicAdd(&d.det_cnt[dcur ^ 1][l0 + j], 1);
             atomicMin(&d.det_min[dcur ^ 1][l0 + j], i);
           }
-          if (x == GH_TOMBSTONE && (int64_t)v.ts < (int64_t)r - p.t_cleanup) {  // step 5 clean (:490-492)
+          if (x == GH_TOMBSTONE && (int64_t)tts < (int64_t)r - p.t_cleanup) {  // step 5 clean (:490-492)
             x = GH_ABSENT;
             n_rel++;
           }
+          if (sh != GH_NO_SHADOW && (int64_t)sh < (int64_t)r - p.t_cleanup) {  // ... the shadow entry too (D7)
+            sh = GH_NO_SHADOW;
+            n_rel++;
+          }
+        }
+        if (sh != sh0) {
+          d.shadow[l0 + j] = GH_NO_SHADOW;
+          atomicSub(d.nshadow, 1);
         }
         if (x >= GH_ABSENT && m[j] > x) {  // step 6 merge (:424-426, :435-437)
           x = m[j];
@@ -2116,7 +2192,7 @@ __global__ __launch_bounds__(256) void k_round_slow(GhDev d, int cur, int dcur, 
         }
         GhCell out = gh_absent();
         if (x != GH_ABSENT) {
-          const int32_t t2 = now ? r : v.ts;
+          const int32_t t2 = now ? r : tts;
           out = GhCell{(int32_t)x, t2, x >= 0 && gh_flag_for((int32_t)x, t2, c, i, r + 1, p.t_fail)};
         }
         o[j] = out;
@@ -2912,6 +2988,8 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
         case 3:
           if (d.rowlay)
             GH_ROUND_NT(false, 4);  // row layout: ghost senders
+          else if (p.nib_dma && TW == 256)
+            GH_ROUND_NT(false, 5);  // LDS-DMA staging
           else
             GH_ROUND_NT(false, 2);
           return;

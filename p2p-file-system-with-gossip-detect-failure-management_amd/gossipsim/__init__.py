@@ -155,6 +155,22 @@ class Engine:
         self._chk(fn(self.h, C.byref(nm), C.byref(fr)))
         return nm.value, fr.value
 
+    def debug_shadow(self):
+        """(col0, int32[ncols], count): the D7 shadow entries of this engine's
+        member columns -- the ts of the introducer's RecentFailList entry
+        beside its present member c, or INT32_MIN (none) -- and the count the
+        engine keeps (gh_debug_shadow, test-only and not in the header)."""
+        fn = self.lib.gh_debug_shadow
+        fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int32)]
+        fn.restype = C.c_int
+        _, _, c0, nc = self.shard_info()
+        out = np.empty(max(nc, 1), np.int32)
+        cnt = C.c_int32()
+        self._chk(fn(self.h, out.ctypes.data_as(C.c_void_p), len(out), C.byref(cnt)))
+        out = out[:nc]
+        out[out == np.int32(-2139062144)] = np.iinfo(np.int32).min  # GH_NO_SHADOW (0x80808080)
+        return c0, out, cnt.value
+
     def exchange_info(self):
         """dict(ghost_rows, bytes_out, bytes_in) of this shard's last ghost-row
         exchange (row layout; gh_exchange_info)."""

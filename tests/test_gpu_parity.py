@@ -453,3 +453,56 @@ def test_ring_whole_lists(gs, oracle_mod, n):
              36: [(sc.JOIN, c) for c in crash[: max(1, len(crash) // 2)]]}
     run_parity(gs, oracle_mod, dict(peer_mode=1, seed=0x5EED0A01 + n, t_fail=20, t_cleanup=20), n, 50, sched,
                init=sc.full_state(n))
+
+
+def shadows_of(eng, n):
+    """int32[n]: the engine's (or shard group's) D7 shadow entries by member"""
+    out = np.full(n, np.iinfo(np.int32).min, np.int32)
+    cnt = 0
+    for e in getattr(eng, "engines", [eng]):
+        c0, sh, k = e.debug_shadow()
+        out[c0:c0 + len(sh)] = np.where(sh != np.iinfo(np.int32).min, sh, out[c0:c0 + len(sh)])
+        cnt += k
+    assert cnt == int((out != np.iinfo(np.int32).min).sum()), (cnt, out)
+    return out
+
+
+@pytest.mark.parametrize("layout", ["single", "cols3", "rows2"])
+@pytest.mark.parametrize("peer_mode", [0, 1], ids=["pull", "ring"])
+def test_rejoin_while_tombstoned_d7(gs, oracle_mod, layout, peer_mode):
+    """SPEC D7 as the reference does it (slave/slave.go:228-230, 250-255,
+    276-286, 484-497): members leave or crash and rejoin while the
+    introducer still holds their tombstone, so it holds them twice; LEAVEs,
+    REMOVEs and detections of such a member at the introducer keep the old
+    RecentFailList entry (its ts), cleanFailList releases it. Bit-exact
+    against tablesim every round, the shadow entries included, with double
+    entries occurring; one engine, 3 column shards and 2 row shards."""
+    n = 300
+    cfg = dict(fanout=3, seed=0x5EED0E10 + peer_mode, t_fail=4, t_cleanup=6, peer_mode=peer_mode)
+    sched = sc.rejoin_churn(n, 40, 0xD7 + peer_mode)
+    if layout == "single":
+        eng = gs.Engine(gs.default_config(n, **cfg))
+    else:
+        world, lay = (3, 0) if layout == "cols3" else (2, 1)
+        eng = gs.ShardGroup(gs.default_config(n, shard_layout=lay, **cfg), world)
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=8)
+    hb, ts, alive = sc.full_state(n)
+    eng.import_state(hb, ts, alive, 0)
+    orc.import_state(hb, ts, alive, 0)
+    dual = 0
+    try:
+        for r in range(1, 41):
+            ev = sched.get(r, [])
+            if ev:
+                eng.apply_events(ev)
+                orc.apply_events(ev)
+            s1, s2 = eng.step(1), orc.step(1)
+            assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
+            compare(eng, orc, r)
+            a, b = shadows_of(eng, n), orc.debug_shadow()
+            np.testing.assert_array_equal(a, b, err_msg=f"shadow entries r={r}")
+            dual = max(dual, int((b != np.iinfo(np.int32).min).sum()))
+    finally:
+        eng.close()
+        orc.close()
+    assert dual > 0
