@@ -691,7 +691,9 @@ int round_ghosts(Engine* e, const GhRound& p) {
     e->gx_out = e->gx_in = 0;
     launch_ghost_slots(d, e->wlist + (size_t)me * e->n, e->mcnt + G * G + me, e->stream);
     HIPCHK(e, hipGetLastError());
-    e->gpo = e->plane && e->plane_valid && storm == 0;
+    // (list order: the list kernels read the ghost senders' flags, so their
+    // 16-bit codes travel every round)
+    e->gpo = e->plane && e->plane_valid && storm == 0 && !e->lorder;
     if (e->plane && (rc = ghost_move(e, GH_GX_PLANE))) return rc;
     return e->gpo ? GH_OK : ghost_move(e, GH_GX_CODES);
   }
@@ -722,7 +724,7 @@ int round_ghosts(Engine* e, const GhRound& p) {
   for (int r = 0; r < G; ++r)
     for (int32_t s = 0; s < e->n; ++s)
       if (mark[r][s]) want[r].push_back(s);
-  e->gpo = e->plane && e->plane_valid && storm == 0;
+  e->gpo = e->plane && e->plane_valid && storm == 0 && !e->lorder;
   if (!e->gpo) return ghost_exchange(e, want);
   int rc;
   if ((rc = ghost_setup(e, want))) return rc;
@@ -755,6 +757,47 @@ int allreduce_i32(Engine* e, int32_t* send, int32_t* recv, size_t count) {
 
 // SPEC.md §5: crashes, then leaves (all leavers stop first), then joins.
 int reset_shadows(Engine* e);
+
+// Row shards with list order: every shard keeps every row's list; the lists
+// of generation g this shard's owned rows changed (lchg) go to every other
+// shard. The host reads the changed rows' lengths (one sync), the shards
+// agree on the largest pack by an allgather of the sizes, then pack,
+// allgather the packs and unpack the others' into the replicas.
+int list_sync(Engine* e, int g) {
+  if (!e->d.lchg) return GH_OK;
+  GhDev& d = e->d;
+  const int G = e->world;
+  std::vector<int32_t> chg(e->n), len(e->n);
+  HIPCHK(e, hipMemcpyAsync(chg.data(), d.lchg, sizeof(int32_t) * e->n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipMemcpyAsync(len.data(), d.llen[g], sizeof(int32_t) * e->n, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  int64_t ent = 0;
+  for (int64_t i = 0; i < e->n; ++i)
+    if (chg[i]) ent += len[i];
+  // every shard's entry count -> the pack size (the same on every shard)
+  int32_t* sz = e->gwcnt;  // (row layout scratch, >= 2 G int32)
+  const int32_t mine = (int32_t)std::min<int64_t>(ent, INT32_MAX);
+  HIPCHK(e, hipMemcpyAsync(sz + G, &mine, sizeof mine, hipMemcpyHostToDevice, e->stream));
+  COMMCHK(e, e->comm->allgather(sz + G, sz, sizeof(int32_t), e->stream));
+  std::vector<int32_t> all(G);
+  HIPCHK(e, hipMemcpyAsync(all.data(), sz, sizeof(int32_t) * G, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  int64_t maxent = 0;
+  for (int32_t v : all) maxent = std::max<int64_t>(maxent, v);
+  const size_t words = 1 + 4 * (size_t)e->n + (size_t)maxent;
+  int rc;
+  if ((rc = gbuf_reserve(e, 2, words * sizeof(int32_t))) || (rc = gbuf_reserve(e, 3, words * sizeof(int32_t) * G)))
+    return rc;
+  int32_t* sendb = static_cast<int32_t*>(e->gbuf[2]);
+  int32_t* recvb = static_cast<int32_t*>(e->gbuf[3]);
+  launch_list_pack(d, g, sendb, maxent, e->stream);
+  HIPCHK(e, hipGetLastError());
+  COMMCHK(e, e->comm->allgather(sendb, recvb, words * sizeof(int32_t), e->stream));
+  for (int r = 0; r < G; ++r)
+    if (r != e->rank && all[r] >= 0) launch_list_unpack(d, g, recvb + (size_t)r * words, e->stream);
+  HIPCHK(e, hipGetLastError());
+  return GH_OK;
+}
 
 int process_events(Engine* e, int32_t r) {
   if (e->pending.empty()) return GH_OK;
@@ -859,12 +902,14 @@ int process_events(Engine* e, int32_t r) {
       if ((rc = upload(e, e->rows_buf, {I}))) return rc;
       launch_list_events(e->d, e->cur, e->lcur, e->rows_buf, 1, e->ev_buf, (int32_t)joiners.size(), -1, -1,
                          e->stream);
+      if ((rc = list_sync(e, e->lcur ^ 1))) return rc;  // (row shards: the introducer's new list everywhere)
       launch_list_events(e->d, e->cur, e->lcur, nullptr, 0, nullptr, 0, I, I, e->stream);
     } else {
       launch_list_events(e->d, e->cur, e->lcur, nullptr, 0, nullptr, 0, -1, -1, e->stream);
     }
     HIPCHK(e, hipGetLastError());
     e->lcur ^= 1;
+    if ((rc = list_sync(e, e->lcur))) return rc;
   }
   return GH_OK;
 }
@@ -962,7 +1007,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
     return GH_EINVAL;
   if (world < 1 || rank < 0 || rank >= world) return GH_EINVAL;
   // the list order of a row spans every member column: one engine holds it
-  if (cfg->list_order == GH_ORDER_APPEND && world > 1) return GH_EINVAL;
+  // list order on shards: row shards only (a row's order spans every column)
+  if (cfg->list_order == GH_ORDER_APPEND && world > 1 && cfg->shard_layout != GH_LAYOUT_ROWS) return GH_EINVAL;
   // the reference's REMOVE recipients: one engine (a recipient set spans
   // every row and column), member-ID list order (remove.hip)
   if (cfg->remove_mode != GH_REMOVE_ALL && cfg->remove_mode != GH_REMOVE_LIST) return GH_EINVAL;
@@ -1193,6 +1239,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
           (rc = dalloc(e, &d.lself[0], e->n, 0xFF)) || (rc = dalloc(e, &d.lself[1], e->n, 0xFF)) ||
           (rc = dalloc(e, &d.lsel[0], e->n, 0)) || (rc = dalloc(e, &d.lsel[1], e->n, 0)))
         break;
+      if (rowlay && world > 1 && (rc = dalloc(e, &d.lchg, e->n, 0))) break;
     }
     if (!rowlay && world > 1 && cfg->peer_mode == GH_PEER_PULL &&
         (rc = dalloc(e, &d.pvb, (size_t)world * ncs + 64, 0)))
@@ -1309,11 +1356,15 @@ int build_inboxes(Engine* e, const GhRound& p) {
       // allreduce(max) of the targets, then every shard builds every CSR
       // inbox. In a healthy cluster the targets are the adjacent members,
       // so the want lists below are a halo of a few rows per shard boundary.
-      GhDev v = d;
-      v.rank = 0;
-      v.world = 1;
-      launch_ring_count(v, e->cur, e->dcur, p, e->stream);
-      launch_ring_select(v, e->cur, e->dcur, p, e->stream);
+      if (e->lorder) {  // the owned senders' neighbours in list order (the others' targets stay -1)
+        launch_ring_list(d, e->cur, e->dcur, p, e->lcur, e->flags_known, e->stream);
+      } else {
+        GhDev v = d;
+        v.rank = 0;
+        v.world = 1;
+        launch_ring_count(v, e->cur, e->dcur, p, e->stream);
+        launch_ring_select(v, e->cur, e->dcur, p, e->stream);
+      }
       HIPCHK(e, hipGetLastError());
       if (e->world > 1)
         COMMCHK(e, e->comm->allreduce(d.targets, d.targets, 3 * (size_t)e->n, GH_DT_I32, GH_OP_MAX, e->stream));
@@ -1653,7 +1704,10 @@ int gh_import_state(void* h, const int32_t* hb, const int32_t* ts, const uint8_t
   if ((rc = reset_pending_removes(e))) return rc;
   if (e->cfg.introducer >= row0 && e->cfg.introducer < row0 + n_rows && (rc = reset_shadows(e))) return rc;
   launch_count(e->d, e->cur, p, e->stream);
-  if (e->lorder) launch_list_import(e->d, e->cur, e->lcur, row0, n_rows, e->stream);  // dense rows: ID order
+  if (e->lorder) {
+    launch_list_import(e->d, e->cur, e->lcur, row0, n_rows, e->stream);  // dense rows: ID order
+    if ((rc = list_sync(e, e->lcur))) return rc;
+  }
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipStreamSynchronize(e->stream));
   return GH_OK;
@@ -1694,7 +1748,10 @@ int gh_init_full(void* h, int32_t hb0, int32_t ts0, int32_t round) {
   if ((rc = reset_pending_removes(e))) return rc;
   if ((rc = reset_shadows(e))) return rc;
   launch_count(e->d, e->cur, p, e->stream);
-  if (e->lorder) launch_list_import(e->d, e->cur, e->lcur, 0, e->n, e->stream);
+  if (e->lorder) {
+    launch_list_import(e->d, e->cur, e->lcur, 0, e->n, e->stream);
+    if ((rc = list_sync(e, e->lcur))) return rc;
+  }
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipStreamSynchronize(e->stream));
   return GH_OK;
@@ -1824,6 +1881,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     if (e->lorder) {  // the lists of the next state (needs D_{r-1} and the inboxes)
       launch_list_round(e->d, e->cur, e->dcur, p, e->lcur, e->stream);
       e->lcur ^= 1;
+      if ((rc = list_sync(e, e->lcur))) return rc;
     }
     // the reference's REMOVE recipients of D_r: the sweep's column bitmaps
     // (needs D_{r-1}, before k_finish replaces it), then per member of D_r
@@ -2014,6 +2072,7 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
                                hipMemcpyDeviceToDevice, e->stream));
       HIPCHK(e, hipMemcpyAsync(e->d.lself[g] + observer, e->d.lself[g2] + observer, sizeof(int32_t),
                                hipMemcpyDeviceToDevice, e->stream));
+      if ((rc = list_sync(e, g))) return rc;
     }
     HIPCHK(e, hipMemcpyAsync(&cnt, e->d.nd + 5, sizeof cnt, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));

@@ -26,7 +26,12 @@
 //                  candidates are cleared (the ID-order pre-pass, round.hip,
 //                  in list order)
 //   k_list_cand / k_list_first   master's candidates, MemberList[0]
-// Single-GPU engines only (gossiphip.cpp refuses the mode when sharded).
+// One engine, or row shards (GH_LAYOUT_ROWS): every shard keeps every row's
+// list (a replica) and rebuilds only the rows it owns; the owners' changed
+// lists (lchg) are then copied to every shard (k_list_pack / k_list_unpack,
+// gossiphip.cpp list_sync), so the senders' snapshot lists, the master's
+// candidates and MemberList[0] of any row are local reads everywhere. Column
+// shards are refused (a row's order spans every column).
 #include <limits.h>
 
 #include "gh_internal.h"
@@ -169,7 +174,7 @@ __global__ __launch_bounds__(256) void k_list_round(GhDev d, int cur, int dcur, 
   __shared__ int s_ns, s_rem, s_self;
   const int64_t i = blockIdx.x;
   if (i >= d.n) return;
-  if (!d.alive[i]) {  // a stopped row is not touched by the round
+  if (!d.alive[i] || !gh_owned(d, i)) {  // a stopped row is not touched by the round; another shard's row: its owner's copy follows
     keep_row(d, g, i);
     return;
   }
@@ -268,6 +273,7 @@ __global__ __launch_bounds__(256) void k_list_round(GhDev d, int cur, int dcur, 
     d.lsel[g ^ 1][i] = (uint8_t)bo;
     d.llen[g ^ 1][i] = pos;
     d.lself[g ^ 1][i] = s_self;
+    if (d.lchg) d.lchg[i] = 1;  // row shards: copied to every shard
   }
 }
 
@@ -283,7 +289,7 @@ __global__ __launch_bounds__(256) void k_list_events(GhDev d, int cur, int g, co
   __shared__ int s_self;
   const int64_t i = rows ? rows[blockIdx.x] : blockIdx.x;
   if (i >= d.n || i == skip) return;
-  if (!d.alive[i]) {
+  if (!d.alive[i] || !gh_owned(d, i)) {  // (row shards: the owner's copy follows)
     keep_row(d, g, i);
     return;
   }
@@ -312,6 +318,7 @@ __global__ __launch_bounds__(256) void k_list_events(GhDev d, int cur, int g, co
     d.lsel[g ^ 1][i] = (uint8_t)bo;
     d.llen[g ^ 1][i] = pos;
     d.lself[g ^ 1][i] = s_self;
+    if (d.lchg) d.lchg[i] = 1;
   }
 }
 
@@ -321,7 +328,7 @@ __global__ __launch_bounds__(256) void k_list_import(GhDev d, int cur, int g, in
   __shared__ int s_w[4];
   __shared__ int s_self;
   const int64_t i = row0 + blockIdx.x;
-  if (i >= d.n) return;
+  if (i >= d.n || !gh_owned(d, i)) return;  // (row shards: the owner's copy follows)
   if (threadIdx.x == 0) s_self = -1;
   __syncthreads();
   int32_t* dst = d.lord[d.lsel[g][i]] + i * d.ld;
@@ -341,6 +348,7 @@ __global__ __launch_bounds__(256) void k_list_import(GhDev d, int cur, int g, in
   if (threadIdx.x == 0) {
     d.llen[g][i] = pos;
     d.lself[g][i] = s_self;
+    if (d.lchg) d.lchg[i] = 1;
   }
 }
 
@@ -361,7 +369,7 @@ __global__ __launch_bounds__(256) void k_ring_list(GhDev d, int cur, int dcur, G
   whole = whole && d.cntg[p.n] == 0 && d.cntg[p.n + 1] == 0;
   if (threadIdx.x == 0) s_idx = whole ? d.lself[g][s] : -1;
   __syncthreads();
-  if (d.alive[s] && d.active[s]) {
+  if (d.alive[s] && d.active[s] && gh_owned(d, s)) {  // (row shards: each sender's owner; the targets are max-reduced)
     const int L = d.llen[g][s];
     const int32_t* sl = list_of(d, g, s);
     auto in_snap = [&](int c) { return !gh_get(d, cur, s, c, 0).f && !removed_at(d, dcur, c, s); };
@@ -456,7 +464,7 @@ __global__ __launch_bounds__(256) void k_quirk_list(GhDev d, int cur, int dcur, 
   const int64_t i = blockIdx.x;
   if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no flag anywhere
   if (i == 0 && threadIdx.x == 0) d.pvalid[cur] = 0;  // cleared flags: the sender plane is stale
-  if (i >= p.n || !(d.alive[i] && d.active[i])) return;
+  if (i >= p.n || !(d.alive[i] && d.active[i]) || !gh_owned(d, i)) return;
   const int L = d.llen[g][i];
   const int32_t* sl = list_of(d, g, i);
   if (threadIdx.x == 0) s_last = -1;
@@ -513,6 +521,83 @@ __global__ __launch_bounds__(256) void k_list_first(GhDev d, int g, int32_t* out
   out[i] = d.llen[g][i] > 0 ? d.n - list_of(d, g, i)[0] : 0;
 }
 
+// Row shards: the lists of the rows this shard changed (lchg), packed for
+// the other shards: [count | rows | lens | selfs | offsets | entries] (n
+// int32 each for the per-row parts), entries of the rows back to back in row
+// order. One workgroup scans the rows in ascending order.
+__global__ __launch_bounds__(1024) void k_list_pack(GhDev d, int g, int32_t* buf, int64_t cap) {
+  __shared__ int s_w[16];
+  __shared__ int64_t s_base, s_rows;
+  if (threadIdx.x == 0) s_base = s_rows = 0;
+  __syncthreads();
+  int32_t* rows = buf + 1;
+  for (int64_t b = 0; b < d.n; b += blockDim.x) {
+    const int64_t i = b + threadIdx.x;
+    const bool chg = i < d.n && d.lchg[i];
+    const int len = chg ? d.llen[g][i] : 0;
+    // block-wide exclusive prefix of chg (rows) and len (entries)
+    const unsigned long long m = __ballot(chg);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int lx = len;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(lx, o);
+      if (lane >= o) lx += y;
+    }
+    if (lane == 63) s_w[w] = lx;
+    __syncthreads();
+    int woff = 0, wrow = 0;
+    for (int q = 0; q < w; ++q) woff += s_w[q];
+    __shared__ int s_c[16];
+    if (lane == 0) s_c[w] = __popcll(m);
+    __syncthreads();
+    for (int q = 0; q < w; ++q) wrow += s_c[q];
+    const int64_t row_at = s_rows + wrow + __popcll(m & ((1ull << lane) - 1ull));
+    const int64_t ent_at = s_base + woff + lx - len;
+    if (chg) {
+      rows[row_at] = (int32_t)i;
+      const int64_t rb = (int64_t)row_at;
+      buf[1 + d.n + rb] = len;
+      buf[1 + 2 * d.n + rb] = d.lself[g][i];
+      buf[1 + 3 * d.n + rb] = (int32_t)ent_at;
+      const int32_t* src = d.lord[d.lsel[g][i]] + i * d.ld;
+      int32_t* dst = buf + 1 + 4 * (int64_t)d.n + ent_at;
+      if (ent_at + len <= cap) for (int q = 0; q < len; ++q) dst[q] = src[q];
+      d.lchg[i] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x == blockDim.x - 1) {
+      int tot = 0, tr = 0;
+      for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
+        tot += s_w[q];
+        tr += s_c[q];
+      }
+      s_base += tot;
+      s_rows += tr;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) buf[0] = (int32_t)s_rows;
+}
+
+// Another shard's packed lists (k_list_pack) into this shard's replicas of
+// generation g, in place (nothing reads the rows' earlier lists any more).
+__global__ __launch_bounds__(256) void k_list_unpack(GhDev d, int g, const int32_t* buf) {
+  const int nr = buf[0];
+  const int32_t* rows = buf + 1;
+  const int32_t* ent = buf + 1 + 4 * (int64_t)d.n;
+  for (int r = blockIdx.x; r < nr; r += gridDim.x) {
+    const int64_t i = rows[r];
+    const int len = buf[1 + d.n + r];
+    const int64_t off = buf[1 + 3 * d.n + r];
+    int32_t* dst = d.lord[d.lsel[g][i]] + i * d.ld;
+    for (int q = threadIdx.x; q < len; q += blockDim.x) dst[q] = ent[off + q];
+    if (threadIdx.x == 0) {
+      d.llen[g][i] = len;
+      d.lself[g][i] = buf[1 + 2 * d.n + r];
+    }
+  }
+}
+
 size_t list_lds(const GhDev& d) { return sizeof(uint32_t) * 2 * (size_t)((d.n + 31) / 32); }
 
 }  // namespace
@@ -547,6 +632,16 @@ void launch_quirk_list(const GhDev& d, int cur, int dcur, const GhRound& p, int 
 void launch_list_cand(const GhDev& d, int lin, int32_t master, hipStream_t s) {
   hipLaunchKernelGGL(k_list_cand, dim3(std::max<int32_t>(1, std::min<int32_t>((d.n + 255) / 256, 1024))), dim3(256),
                      0, s, d, lin, master);
+}
+
+// Row shards: this shard's changed lists (lchg, cleared) packed into buf
+// (1 + 4 n + entries int32; cap entries), and another shard's pack into the
+// replicas.
+void launch_list_pack(const GhDev& d, int g, int32_t* buf, int64_t cap, hipStream_t s) {
+  hipLaunchKernelGGL(k_list_pack, dim3(1), dim3(1024), 0, s, d, g, buf, cap);
+}
+void launch_list_unpack(const GhDev& d, int g, const int32_t* buf, hipStream_t s) {
+  hipLaunchKernelGGL(k_list_unpack, dim3(256), dim3(256), 0, s, d, g, buf);
 }
 
 void launch_list_first(const GhDev& d, int lin, int32_t* out, hipStream_t s) {

@@ -183,9 +183,75 @@ def test_append_merge_list_datagram_order(gs):
         eng.close()
 
 
-def test_append_refused_when_sharded(gs):
+def test_append_refused_on_column_shards(gs):
+    """A row's order spans every column: column shards refuse it."""
     with pytest.raises(gs.GossipError):
         gs.ShardGroup(gs.default_config(64, list_order=APPEND), 2)
+
+
+def make_rows_pair(gs, n, world, peer_mode, quirk, fanout=3, seed=0x5EED0001, init_full=False, max_files=0, **kw):
+    """GH_ORDER_APPEND on G row shards (every shard keeps a replica of every
+    list, the owners' changes are copied each round) against listsim."""
+    cfg = gs.default_config(n, peer_mode=gs.GH_PEER_RING if peer_mode == "ring" else gs.GH_PEER_PULL,
+                            fanout=fanout, detect_mode=int(quirk), seed=seed, list_order=APPEND,
+                            max_files=max_files, shard_layout=gs.GH_LAYOUT_ROWS, **kw)
+    eng = gs.ShardGroup(cfg, world)
+    if init_full:
+        hb, ts, alive = sc.full_state(n)
+        eng.import_state(hb, ts, alive, 0)
+        ls = ListSim.from_dense(hb, ts, alive, 0, seed=seed, peer_mode=peer_mode, fanout=fanout, quirk=quirk,
+                                order="append")
+    else:
+        ls = ListSim(n, seed=seed, peer_mode=peer_mode, fanout=fanout, quirk=quirk, order="append")
+    return eng, ls
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("peer_mode,quirk", [("ring", False), ("ring", True), ("pull", False), ("pull", True)])
+def test_append_row_shards_churn(gs, world, peer_mode, quirk):
+    """The reference topology on row shards (ring + append order, the
+    Cluster default; slave/slave.go:255, 437, 515-524): seeded churn with
+    re-adds, every round's counters, tables, failed set, detectors and every
+    row's list order equal listsim's."""
+    n = 24
+    sched = sc.random_churn(n, 60, 40 + world, p_crash=0.03, p_leave=0.02, p_join=0.08)
+    eng, ls = make_rows_pair(gs, n, world, peer_mode, quirk, init_full=True, seed=0x7100 + world)
+    try:
+        reordered = run_pair(eng, ls, n, 60, sched)
+    finally:
+        eng.close()
+    assert reordered > 0
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_append_row_shards_bootstrap_placement(gs, world):
+    """BASELINE config 1 on row shards in append order: 10 members join one
+    per round through the introducer (its broadcast appends in its list
+    order, shipped to every shard), 7 crashes at r=30; then placement from
+    the master's list order, MemberList[0] of every row and a datagram
+    merge."""
+    n = 10
+    sched = {r: [(sc.JOIN, r - 1)] for r in range(1, 11)}
+    sched.setdefault(30, []).append((sc.CRASH, 7))
+    eng, ls = make_rows_pair(gs, n, world, "ring", False, max_files=32)
+    try:
+        run_pair(eng, ls, n, 40, sched)
+        files = list(range(12))
+        rep, ver, st = eng.put(np.array(files, np.int32))
+        for k, f in enumerate(files):
+            nodes, v, s_ = ls.put(f)
+            assert st[k] == s_ and ver[k] == v, f
+            assert [x for x in rep[k] if x >= 0] == nodes, f
+        first, ln, _ = eng.vote_scan(np.zeros(n, np.int32))
+        assert list(first) == [nd.members[0].addr if nd.members else -1 for nd in ls.nodes]
+        ids = np.array([9, 7, 3], np.int32)
+        hb = np.array([99, 98, 97], np.int32)
+        eng.merge_list(4, ids, hb)
+        ls.nodes[4].merge([Member(int(a), int(b), 0) for a, b in zip(ids, hb)], ls.round)
+        assert list(eng.lsm(4)[0]) == [m.addr for m in ls.nodes[4].members]
+        run_pair(eng, ls, n, 6, {})
+    finally:
+        eng.close()
 
 
 def test_id_order_unchanged_lsm(gs):
