@@ -60,8 +60,10 @@ extern "C" {
  * order, senders in ID order) and keep their relative order when others are
  * removed (:283); ring targets (:515-524), quirk runs (:464-477),
  * MemberList[0] (:936, :994), placement candidates (master/master.go:46,
- * :135) and lsm follow it. Single-GPU engines only (gh_create); HBM +8*N*N
- * bytes (double-buffered [N][N] int32 lists). */
+ * :135) and lsm follow it. One engine or row shards (GH_LAYOUT_ROWS: every
+ * shard keeps every row's list, the owners' changes are copied each round);
+ * column shards refuse it (gh_create_sharded: GH_EINVAL). HBM +8*N*N bytes
+ * per engine / shard (double-buffered [N][N] int32 lists). */
 #define GH_ORDER_ID 0
 #define GH_ORDER_APPEND 1
 /* Who receives a detector's REMOVE (SPEC D4). GH_REMOVE_LIST is the
