@@ -150,7 +150,17 @@ def test_c3_fullsize_crash_1pct(gs, oracle_mod):
     def expect(s):
         assert s["detections"] > 0 and s["first_detection"] is not None, s
 
-    run(gs, oracle_mod, 16, 32, {12, 32}, expect, sched=sched)
+    def fast(eng, r, st):
+        # the crash wave stays on the nibble path: REMOVE delivery turns the
+        # removed members' cells into tier tombstones inside it (round.hip
+        # nib_word RMV), so no round hands more than 1% of the lanes to the
+        # lane-job kernel (round 4: 38 M = 14% in the REMOVE round)
+        if r >= 6:
+            assert eng.tier_info(full=True)[3] == 3, (r, eng.tier_info(full=True))
+            jobs, _ = eng.job_info()
+            assert jobs * 100 <= N * N // 16, (r, jobs)
+
+    run(gs, oracle_mod, 16, 32, {12, 32}, expect, sched=sched, per_round=fast)
 
 
 @pytest.mark.gpu_fullsize
