@@ -132,7 +132,12 @@ struct LocalGroup {
   std::vector<const void*> ptr;
   std::vector<int> dev;
   std::vector<const size_t*> counts;  // alltoallv: each rank's per-destination byte counts
-  explicit LocalGroup(int w) : world(w), ptr(w, nullptr), dev(w, 0), counts(w, nullptr) {}
+  // stream order across ranks: ready[h] is recorded on rank h's stream when
+  // its send buffer is complete, done[h] when it has finished reading the
+  // others' buffers (so that they may be rewritten)
+  std::vector<hipEvent_t> ready, done;
+  explicit LocalGroup(int w)
+      : world(w), ptr(w, nullptr), dev(w, 0), counts(w, nullptr), ready(w, nullptr), done(w, nullptr) {}
   // All ranks meet. False after a 120 s wait (a rank failed or diverged);
   // the group then stays broken so that no rank hangs on it later.
   bool barrier() {
@@ -171,13 +176,38 @@ __global__ __launch_bounds__(256) void k_reduce(const T* __restrict__ parts, int
   }
 }
 
+// A collective is stream-ordered like RCCL's: the host threads meet twice
+// (to publish the buffers and events, and to publish that the reads are
+// enqueued), and each rank's stream waits for the others' events instead of
+// the host draining the streams (which had serialised the G shards of one
+// GPU at every exchange).
 struct LocalComm final : GhComm {
   std::shared_ptr<LocalGroup> g;
   int device = 0;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
+  hipEvent_t ev_ready = nullptr, ev_done = nullptr;
   ~LocalComm() override {
     if (tmp) (void)hipFree(tmp);
+    if (ev_ready) (void)hipEventDestroy(ev_ready);
+    if (ev_done) (void)hipEventDestroy(ev_done);
+  }
+  int events() {
+    if (ev_ready) return 0;
+    if (hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev_done, hipEventDisableTiming) != hipSuccess)
+      return fail("local comm: event creation failed");
+    return 0;
+  }
+  // s's reads of the other ranks' buffers are enqueued: publish it, meet,
+  // and make s wait until every other rank has read this rank's buffers
+  int finish_reads(hipStream_t s) {
+    if (hipEventRecord(ev_done, s) != hipSuccess) return fail("local comm: event record failed");
+    g->done[rank] = ev_done;
+    if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
+    for (int h = 0; h < world; ++h)
+      if (h != rank && hipStreamWaitEvent(s, g->done[h], 0) != hipSuccess) return fail("local comm: stream wait failed");
+    return 0;
   }
   int fail(const std::string& m) {
     err = m;
@@ -192,21 +222,23 @@ struct LocalComm final : GhComm {
     tmp_bytes = bytes;
     return 0;
   }
-  // tmp[h*bytes ..] = rank h's send, for every h. On return every rank has
-  // finished reading every send buffer, so recv (which may alias send) can
-  // be written.
+  // tmp[h*bytes ..] = rank h's send, for every h. Work enqueued on s after
+  // the return runs after every rank has read every send buffer, so recv
+  // (which may alias send) can be written.
   int gather(const void* send, size_t bytes, hipStream_t s) {
-    if (grow(bytes * world)) return -1;
-    if (hipStreamSynchronize(s) != hipSuccess) return fail("local comm: stream sync failed");
+    if (grow(bytes * world) || events()) return -1;
+    if (hipEventRecord(ev_ready, s) != hipSuccess) return fail("local comm: event record failed");
     g->ptr[rank] = send;
+    g->ready[rank] = ev_ready;
     if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
-    for (int h = 0; h < world; ++h)
+    for (int h = 0; h < world; ++h) {
+      if (h != rank && hipStreamWaitEvent(s, g->ready[h], 0) != hipSuccess)
+        return fail("local comm: stream wait failed");
       if (hipMemcpyPeerAsync(static_cast<char*>(tmp) + (size_t)h * bytes, device, g->ptr[h], g->dev[h], bytes, s) !=
           hipSuccess)
         return fail("local comm: peer copy failed");
-    if (hipStreamSynchronize(s) != hipSuccess) return fail("local comm: stream sync failed");
-    if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
-    return 0;
+    }
+    return finish_reads(s);
   }
   int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     if (bytes == 0) return 0;
@@ -229,9 +261,11 @@ struct LocalComm final : GhComm {
   // addressed to it straight from the peers' buffers
   int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t* recvbytes,
                 hipStream_t s, const size_t* recvdispl) override {
-    if (hipStreamSynchronize(s) != hipSuccess) return fail("local comm: stream sync failed");
+    if (events()) return -1;
+    if (hipEventRecord(ev_ready, s) != hipSuccess) return fail("local comm: event record failed");
     g->ptr[rank] = send;
     g->counts[rank] = sendbytes;
+    g->ready[rank] = ev_ready;
     if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
     size_t ro = 0;
     for (int h = 0; h < world; ++h) {
@@ -243,14 +277,14 @@ struct LocalComm final : GhComm {
         return fail("local comm: alltoallv counts disagree");
       }
       const size_t at = recvdispl ? recvdispl[h] : ro;
+      if (bytes && h != rank && hipStreamWaitEvent(s, g->ready[h], 0) != hipSuccess)
+        return fail("local comm: stream wait failed");
       if (bytes && hipMemcpyPeerAsync(static_cast<char*>(recv) + at, device, static_cast<const char*>(g->ptr[h]) + off,
                                       g->dev[h], bytes, s) != hipSuccess)
         return fail("local comm: peer copy failed");
       ro += bytes;
     }
-    if (hipStreamSynchronize(s) != hipSuccess) return fail("local comm: stream sync failed");
-    if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
-    return 0;
+    return finish_reads(s);
   }
   int allreduce(const void* send, void* recv, size_t count, GhDType dt, GhROp op, hipStream_t s) override {
     if (count == 0) return 0;

@@ -365,6 +365,10 @@ struct GhDev {
   // cleanFailList releases it like any tombstone. The introducer's segments
   // run the per-cell rule (k_round_slow) while any entry may exist.
   int32_t *shadow, *nshadow;
+  // timing (gh_set_timing, tmode 1): vlog[q] = the host variant number
+  // (launch_round's 0..4) of the k_round launch that ran in round q of the
+  // current gh_step call; null when not timing
+  int32_t* vlog;
   int32_t *nd;      // [0..1] local |D| per parity, [2..3] dlist fill, [4] join adds, [5] list merges
   int32_t *inbox_beg, *inbox_cnt, *inbox, *inbox_fill, *targets;
   int32_t *ring;    // ring mode: [world][n][2] (local snapshot count, local position of the sender)
@@ -836,14 +840,16 @@ struct GhRound {
   int32_t k;
   uint64_t seed;
   int32_t peer_mode;
-  int32_t xmap;       // k_round block->tile map: 0 tile-major, 1 XCD-aware
+  int32_t xmap;       // k_round block->tile map: 0 tile-major, 1 XCD-aware, 2 XCD-aware with odd rounds reversed (nibble path)
   int32_t tpw;        // k_round tiles per workgroup (1, 2, 4, 8)
   int32_t qgate;      // quirk pre-pass: 1 = return at once when cntg[n + 1] (flagged segments, all shards) is 0
   int32_t force_storm;  // diagnostics (GH_FORCE_STORM): run the storm variant every round
   int32_t force_slow;   // diagnostics (GH_FORCE_SLOW): every segment by the per-cell rule
-  int32_t nib_rmv;      // nibble path: REMOVE'd members with >= 2 detectors stay on it (GH_NIB_RMV=0: lane jobs)
+  int32_t nib_rmv;      // nibble path: REMOVE'd members with >= 2 detectors stay on it (GH_NIB_RMV=0: lane jobs;
+                        // 2: k_round IN 6 every round, else only in rounds with a detection)
   int32_t nib_dma;      // nibble path: LDS-DMA staging of the own and sender lines (GH_NIB_DMA; column layout, TW 256)
   int32_t shadow_row;   // the introducer while it may hold D7 shadow entries (its segments take k_round_slow), else -1
+  int32_t vslot;        // the round's index in its gh_step call (vlog: which k_round variant ran)
   int32_t plane;        // the round writes the next buffer's sender plane (and may read cur's)
   int32_t ring_whole;   // ring mode: one engine and a current flag count, so the targets may come
                         // from whole lists when no REMOVE / flag is pending (k_ring_fast)

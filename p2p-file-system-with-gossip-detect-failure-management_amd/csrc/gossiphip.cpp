@@ -42,8 +42,9 @@ struct Engine {
   // on a side stream (forked after the round's inputs, joined before the lane
   // jobs): one of the four runs, the three idle ones return at once while the
   // nibble path runs, off the round's critical path
-  hipStream_t vstream = nullptr;
-  hipEvent_t vfork = nullptr, vjoin = nullptr;
+  hipStream_t vstream = nullptr, vstream2 = nullptr;
+  hipEvent_t vfork = nullptr, vjoin = nullptr, vjoin2 = nullptr;
+  hipEvent_t vstart = nullptr;  // the nibble launch's start stamp when not timing (the side stream's fork)
   GhDev d{};
   int cur = 0, dcur = 0;
   int32_t round = 0;
@@ -57,11 +58,12 @@ struct Engine {
   int tpw = 1;           // k_round tiles per workgroup (GH_ROUND_TPW)
   int force_storm = 0;   // storm variant every round (GH_FORCE_STORM, diagnostics)
   int force_slow = 0;    // every segment by the per-cell rule (GH_FORCE_SLOW, diagnostics)
-  int nib_rmv = 1;       // REMOVE'd members with >= 2 detectors on the nibble path (GH_NIB_RMV=0: lane jobs, A/B)
+  int nib_rmv = 1;       // REMOVE'd members with >= 2 detectors on the nibble path (GH_NIB_RMV=0: lane jobs,
+                         // 2: the REMOVE-taking instantiation every round; A/B)
   int nib_dma = 0;       // the nibble path stages its lines by LDS-DMA (GH_NIB_DMA=1, A/B)
   bool shadow_any = false;  // the introducer's row may hold D7 shadow entries (GhDev.shadow; re-read after each gh_step)
   bool timing = false;
-  bool side = true;      // idle round variants on the side stream (GH_SIDE=0: in line)
+  int side = 1;          // idle round variants on the side stream (GH_SIDE=0: in line; 2: two side streams)
   // the current table may hold flags no round kernel counted (import, fill,
   // events, list merges): the next quirk pre-pass runs ungated
   bool qforce = true;
@@ -119,6 +121,13 @@ struct Engine {
   double timed_ms = 0.0;
   int64_t timed_launches = 0;
   std::vector<hipEvent_t> evs;
+  // tmode 1 (GH_TMODE, default): only the nibble launch carries its own
+  // start / stop events; the other variants are timed together by two
+  // events around them, and the device logs which variant ran (vlog).
+  // tmode 0: every variant launch carries its own events.
+  int tmode = 1;
+  int32_t* vlog = nullptr;
+  int64_t vlog_cap = 0;
   std::string err;
   std::vector<void*> allocs;
 };
@@ -1046,11 +1055,11 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   int tw = cfg->tile_width ? cfg->tile_width : e->plane ? GH_TW_PLANE : GH_TW_DEFAULT;
   if (const char* v = std::getenv("GH_TILE_W")) tw = std::atoi(v);
   if (const char* v = std::getenv("GH_ROUND_NT")) e->nt = std::atoi(v) != 0;
-  if (const char* v = std::getenv("GH_ROUND_XMAP")) e->xmap = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_ROUND_XMAP")) e->xmap = std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("GH_ROUND_TPW")) e->tpw = std::atoi(v);
   if (const char* v = std::getenv("GH_FORCE_STORM")) e->force_storm = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_FORCE_SLOW")) e->force_slow = std::atoi(v) != 0;
-  if (const char* v = std::getenv("GH_NIB_RMV")) e->nib_rmv = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_NIB_RMV")) e->nib_rmv = std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("GH_NIB_DMA")) e->nib_dma = std::atoi(v) != 0;
   if (tw != 8 && tw != 16 && tw != 32 && tw != 64 && tw != 128 && tw != 256) {
     delete e;
@@ -1061,7 +1070,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   // half of it the plane itself (its window is the plane's: lags of healthy
   // pull dissemination); the row layout ships 16-bit ghost rows
   e->c8 = e->plane && e->tpw == 1 && tw >= 64;
-  if (const char* v = std::getenv("GH_SIDE")) e->side = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_SIDE")) e->side = std::min(2, std::max(0, std::atoi(v)));
+  if (const char* v = std::getenv("GH_TMODE")) e->tmode = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_C8")) e->c8 = e->c8 && std::atoi(v) != 0;
   if (cfg->shard_layout != GH_LAYOUT_COLUMNS && cfg->shard_layout != GH_LAYOUT_ROWS) {
     delete e;
@@ -1112,8 +1122,11 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (!dry) (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (!dry && (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
                hipStreamCreateWithPriority(&e->vstream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+               hipStreamCreateWithPriority(&e->vstream2, hipStreamNonBlocking, prio_hi) != hipSuccess ||
                hipEventCreateWithFlags(&e->vfork, hipEventDisableTiming) != hipSuccess ||
-               hipEventCreateWithFlags(&e->vjoin, hipEventDisableTiming) != hipSuccess)) {
+               hipEventCreateWithFlags(&e->vjoin, hipEventDisableTiming) != hipSuccess ||
+               hipEventCreateWithFlags(&e->vjoin2, hipEventDisableTiming) != hipSuccess ||
+               hipEventCreate(&e->vstart) != hipSuccess)) {
     gh_destroy(e);  // the streams and events created before the failing one, and the communicator
     return GH_EHIP;
   }
@@ -1507,11 +1520,15 @@ void gh_destroy(void* h) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   e->comm.reset();
   for (auto ev : e->evs) (void)hipEventDestroy(ev);
+  if (e->vlog) (void)hipFree(e->vlog);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->vstream) (void)hipStreamDestroy(e->vstream);
+  if (e->vstream2) (void)hipStreamDestroy(e->vstream2);
   if (e->vfork) (void)hipEventDestroy(e->vfork);
   if (e->vjoin) (void)hipEventDestroy(e->vjoin);
+  if (e->vjoin2) (void)hipEventDestroy(e->vjoin2);
+  if (e->vstart) (void)hipEventDestroy(e->vstart);
   delete e;
 }
 
@@ -1776,13 +1793,24 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   bool busy = false;
   if ((rc0 = check_lost(e)) || (rc0 = maybe_grow(e, &busy))) return rc0;
   HIPCHK(e, hipMemsetAsync(e->d.stats, 0, sizeof(unsigned long long) * ST_COUNT, e->stream));
-  if (e->timing && (int64_t)e->evs.size() < 8 * (int64_t)rounds) {
-    while ((int64_t)e->evs.size() < 8 * (int64_t)rounds) {
+  if (e->timing && (int64_t)e->evs.size() < 12 * (int64_t)rounds) {
+    while ((int64_t)e->evs.size() < 12 * (int64_t)rounds) {
       hipEvent_t ev;
       HIPCHK(e, hipEventCreate(&ev));
       e->evs.push_back(ev);
     }
   }
+  // timing the nibble launch alone (the others bracketed, the variant that ran logged)
+  const bool tsel = e->timing && e->tmode == 1 && e->c8 && e->side != 2;
+  if (tsel && e->vlog_cap < rounds) {  // (gh_set_timing allocates 4,096 rounds' worth)
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (e->vlog) HIPCHK(e, hipFree(e->vlog));
+    e->vlog = nullptr;
+    e->vlog_cap = 0;
+    HIPCHK(e, hipMalloc(&e->vlog, sizeof(int32_t) * rounds));
+    e->vlog_cap = rounds;
+  }
+  e->d.vlog = tsel ? e->vlog : nullptr;
   const int32_t first = e->round + 1;
   int32_t done = 0;
   int status = GH_OK;
@@ -1842,23 +1870,53 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     if ((rc = build_inboxes(e, p))) return rc;
     GhRound pr = p;
     pr.gpo = e->gpo;  // row layout: the ghosts carry only their plane so far
+    pr.vslot = q;
     // the variants of k_round; the ones not selected return at once. With
-    // timing on, each launch stamps its own start and end (events 8q + 2v,
-    // 8q + 2v + 1 of variant v; hipExtLaunchKernel, no event packets between
-    // the kernels)
-    auto ev = [&](int v, int end) { return e->timing ? e->evs[8 * q + 2 * v + end] : nullptr; };
+    // timing on, a launch stamps its own start and end (events 12q + 2v,
+    // 12q + 2v + 1 of variant v; hipExtLaunchKernel, no event packets between
+    // the kernels): every launch, or (tsel) the nibble path's, and the other
+    // variants together, from the start of the first (v0) to the end of the
+    // last (v4) (events 12q + 10, 12q + 11), as a stamped launch costs its
+    // stream ~5 us
+    auto ev = [&](int v, int end) -> hipEvent_t {
+      if (!e->timing) return nullptr;
+      if (!tsel || v == 3) return e->evs[12 * q + 2 * v + end];
+      if (v == 0 && end == 0) return e->evs[12 * q + 10];
+      if (v == 4 && end == 1) return e->evs[12 * q + 11];
+      return nullptr;
+    };
     if (e->c8 && !e->side) {
-      // lean 16-bit input, storm, lean tier input by the 16-bit rule, then
-      // the nibble path, all on the round's stream
-      for (int v = 0; v < 4; ++v) launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v, ev(v, 0), ev(v, 1));
-    } else if (e->c8) {
-      // lean 16-bit input, storm, lean tier input by the 16-bit rule on the
-      // side stream, beside the nibble path
+      // lean 16-bit input, storm, lean tier input by the 16-bit rule, the
+      // nibble path that takes REMOVE deliveries, then the steady nibble
+      // path, all on the round's stream
+      for (int v : {0, 1, 2, 4}) launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v, ev(v, 0), ev(v, 1));
+      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, 3, ev(3, 0), ev(3, 1));
+    } else if (e->c8 && e->side == 2) {
+      // the same on two side streams, so that after the nibble path only one
+      // idle launch per stream is left to run (the first on each spans it)
       HIPCHK(e, hipEventRecord(e->vfork, e->stream));
       HIPCHK(e, hipStreamWaitEvent(e->vstream, e->vfork, 0));
-      for (int v = 0; v < 3; ++v) launch_round(e->d, e->cur, e->dcur, pr, e->vstream, e->nt, v, ev(v, 0), ev(v, 1));
+      HIPCHK(e, hipStreamWaitEvent(e->vstream2, e->vfork, 0));
+      for (int v : {0, 1}) launch_round(e->d, e->cur, e->dcur, pr, e->vstream, e->nt, v, ev(v, 0), ev(v, 1));
+      for (int v : {4, 2}) launch_round(e->d, e->cur, e->dcur, pr, e->vstream2, e->nt, v, ev(v, 0), ev(v, 1));
       HIPCHK(e, hipEventRecord(e->vjoin, e->vstream));
+      HIPCHK(e, hipEventRecord(e->vjoin2, e->vstream2));
       launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, 3, ev(3, 0), ev(3, 1));
+      HIPCHK(e, hipStreamWaitEvent(e->stream, e->vjoin, 0));
+      HIPCHK(e, hipStreamWaitEvent(e->stream, e->vjoin2, 0));
+    } else if (e->c8) {
+      // lean 16-bit input, storm, lean tier input by the 16-bit rule and the
+      // REMOVE-taking nibble path on the side stream, beside the steady
+      // nibble path
+      // (forked at the nibble launch's own start stamp: its stream's earlier
+      // work, the inboxes, is done then; an event packet of its own before
+      // it had cost the round ~10 us)
+      hipEvent_t st = e->timing ? ev(3, 0) : e->vstart;
+      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, 3, st, ev(3, 1));
+      HIPCHK(e, hipStreamWaitEvent(e->vstream, st, 0));
+      for (int v : {0, 1, 2, 4})
+        launch_round(e->d, e->cur, e->dcur, pr, e->vstream, e->nt, v, ev(v, 0), ev(v, 1));
+      HIPCHK(e, hipEventRecord(e->vjoin, e->vstream));
       HIPCHK(e, hipStreamWaitEvent(e->stream, e->vjoin, 0));
     } else {  // lean 16-bit input, storm
       for (int v = 0; v < 2; ++v) launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v, ev(v, 0), ev(v, 1));
@@ -1923,11 +1981,22 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     }
   }
   if (e->timing) {
+    std::vector<int32_t> vl;
+    if (tsel && done > 0) {
+      vl.resize(done);
+      // (on the engine's stream: a first use of the null stream costs ms)
+      HIPCHK(e, hipMemcpyAsync(vl.data(), e->vlog, sizeof(int32_t) * done, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+    }
     for (int32_t q = 0; q < done; ++q) {
       float ms = 0.f;  // the variant that ran
-      for (int v = 0; v < (e->c8 ? 4 : 2); ++v) {
+      if (tsel) {
+        const int b = vl[q] == 3 ? 12 * q + 6 : 12 * q + 10;
+        HIPCHK(e, hipEventElapsedTime(&ms, e->evs[b], e->evs[b + 1]));
+      }
+      for (int v = 0; !tsel && v < (e->c8 ? 5 : 2); ++v) {
         float mv = 0.f;
-        const int b = 8 * q + 2 * v;
+        const int b = 12 * q + 2 * v;
         HIPCHK(e, hipEventElapsedTime(&mv, e->evs[b], e->evs[b + 1]));
         ms = std::max(ms, mv);
       }
@@ -2282,6 +2351,11 @@ int gh_set_timing(void* h, int32_t enable) {
   e->timing = enable != 0;
   e->timed_ms = 0.0;
   e->timed_launches = 0;
+  if (e->timing && !e->vlog) {  // the variant log, outside the timed steps
+    HIPCHK(e, hipSetDevice(e->cfg.device));
+    HIPCHK(e, hipMalloc(&e->vlog, sizeof(int32_t) * 4096));
+    e->vlog_cap = 4096;
+  }
   return GH_OK;
 }
 

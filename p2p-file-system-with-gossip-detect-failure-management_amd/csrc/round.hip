@@ -830,6 +830,9 @@ __device__ __forceinline__ void nib_region(const GhDev& d, const GhRound& p, int
     const int x = bid & 7, j = bid >> 3;
     tile = x + 8 * (j / nrb);
     rb = j - (j / nrb) * nrb;
+    // (xmap 2: odd rounds sweep the tiles from the other end, starting on
+    // the slices the last round wrote last)
+    if (p.xmap == 2 && (p.r & 1)) tile = ngroups - 1 - tile;
   } else {
     tile = bid / nrb;
     rb = bid - tile * nrb;
@@ -952,7 +955,11 @@ __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint
 // 32 sender lines as four), then computes them on ds_read_b64 in the 16-cell
 // lane shape: half the vector-memory load instructions of 8-B register loads,
 // and no VGPRs held by loads in flight.
-template <int TW, bool NT, int CPL, bool ROWS, bool DMA = false>
+// RMVK: the instantiation that can take REMOVE deliveries itself (nib_word
+// RMV); the other one (the steady state's: 10 VGPRs fewer, 7 waves per SIMD
+// instead of 6) hands every lane holding a REMOVE'd member to the lane jobs.
+// k_round runs the RMV one only in rounds with a pending REMOVE (IN 6).
+template <int TW, bool NT, int CPL, bool ROWS, bool DMA = false, bool RMVK = true>
 __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, const int dcur, const GhRound& p,
                                                 const int bid) {
   constexpr int W = CPL / 8;         // dwords per lane and plane
@@ -1094,7 +1101,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   bool rmv = false;
   int rmrow = -1;
   uint32_t rs = 0;  // the lane's REMOVE'd cells whose member has one detector
-  if (p.nib_rmv && rm != 0u && !d.rlist && d.toff >= 2) {
+  if (RMVK && p.nib_rmv && rm != 0u && !d.rlist && d.toff >= 2) {
     rmv = true;
     for (uint32_t m = rm; m; m &= m - 1u) {
       const int j = __builtin_ctz(m);
@@ -1119,7 +1126,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
     RM1[w] = x;
     RS1[w] = y;
   }
-  const bool wrmv = __ballot(rmv) != 0;  // (wave-uniform)
+  const bool wrmv = RMVK && __ballot(rmv) != 0;  // (wave-uniform)
   const uint32_t rmk = (uint32_t)(15 - (d.toff - 1)) * 0x01010101u;
   // the lane needs the per-cell rule (a lane job) in every row when it holds
   // a REMOVE'd member off the RMV path or a base move outside 0..15
@@ -2020,18 +2027,26 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 // plane did not select return at once. The nibble path runs one block per workgroup; the
 // storm variant and the rarely selected lean ones of a tiered engine run 1/8
 // of the workgroups, each taking blocks a multiple of 8 apart (same XCD), so
-// idle they are a small dispatch.
+// idle they are a small dispatch (IN 6 too: compiled for 6 waves per SIMD,
+// as its block loop left to the compiler took 106 VGPRs).
 template <int KB, int TW, int TPW, bool NT, bool STORM, int IN>
-__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : (IN == 2 || IN == 4 || IN == 5) ? GH_NIB_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
+__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : IN == 6 ? 6 : (IN == 2 || IN == 4 || IN == 5) ? GH_NIB_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
   if (*d.mode != (int)STORM) return;
   if constexpr (!STORM) {
     int want = 0;
     if (d.a4[0])
       want = !gh_m8(d, cur) ? 3 : (KB == 4 && p.plane && d.pvalid[cur] && gh_m8(d, cur ^ 1)) ? (d.rowlay ? 4 : 2) : 1;
     if (want == 2 && p.nib_dma && TW == 256 && GH_NIB_CPL == 16) want = 5;  // LDS-DMA staging (GH_NIB_DMA)
+    // a REMOVE pending (|D_{r-1}| > 0): the instantiation that takes it on the
+    // nibble path (GH_NIB_RMV=2: in every round, A/B)
+    if (want == 2 && (p.nib_rmv == 2 || (p.nib_rmv && d.cntg[p.n] > 0))) want = 6;
     if (want != IN) return;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) d.m8[4] = STORM ? 1 : (IN == 2 || IN == 4 || IN == 5) ? 3 : IN == 1 ? 2 : 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    d.m8[4] = STORM ? 1 : (IN == 2 || IN == 4 || IN == 5 || IN == 6) ? 3 : IN == 1 ? 2 : 0;
+    // launch_round's variant number of this launch (IN 3 is variant 0 of a tiered engine)
+    if (d.vlog) d.vlog[p.vslot] = STORM ? 1 : IN == 6 ? 4 : (IN == 2 || IN == 4 || IN == 5) ? 3 : IN == 1 ? 2 : 0;
+  }
   // every running row a quiet candidate and no base moved (one engine): the
   // round reads and writes nothing (a collapsed cluster)
   if (d.world == 1 && !d.rowlay && d.aq[0] == 0 && d.cntg[p.n] == 0 && !p.force_slow && !(d.a4[0] && d.m8[2])) {
@@ -2045,8 +2060,20 @@ __global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM 
       round_block<KB, TW, TPW, NT, STORM, IN>(d, cur, dcur, p, b);
       __syncthreads();  // LDS of this block before the next
     }
-  } else if constexpr (IN == 2 || IN == 4) {
-    round_block_nib<TW, NT, GH_NIB_CPL, IN == 4>(d, cur, dcur, p, blockIdx.x);  // one block per workgroup
+  } else if constexpr (IN == 2) {
+    round_block_nib<TW, NT, GH_NIB_CPL, false, false, false>(d, cur, dcur, p, blockIdx.x);  // one block per workgroup
+  } else if constexpr (IN == 4) {
+    round_block_nib<TW, NT, GH_NIB_CPL, true>(d, cur, dcur, p, blockIdx.x);
+  } else if constexpr (IN == 6) {
+    // launched on the side stream every round and idle in most: a grid of
+    // 1/8 of the workgroups (an idle full grid cost 30 us of dispatch behind
+    // the nibble path), each looping over its blocks when it runs
+    constexpr int RB = round_rb<TW>();
+    const int nblk = (int)((d.nrows + RB - 1) / RB) * (int)(p.ld / TW);
+    for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
+      round_block_nib<TW, NT, GH_NIB_CPL, false>(d, cur, dcur, p, b);
+      __syncthreads();  // LDS of this block before the next
+    }
   } else if constexpr (IN == 5) {
     if constexpr (TW == 256 && GH_NIB_CPL == 16) round_block_nib<TW, NT, 16, false, true>(d, cur, dcur, p, blockIdx.x);
   } else {
@@ -2967,7 +2994,7 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
   const int64_t nblk = nrb * (p.ld / TW / TPW);
   if (nblk == 0) return;
   const bool tiered = d.a4[0] != nullptr;
-  const bool few = variant == 1 || variant == 2 || (variant == 0 && tiered);
+  const bool few = variant == 1 || variant == 2 || variant == 4 || (variant == 0 && tiered);
   // (a resident-sized grid for the persistent variants, 1,280 workgroups for
   // the storm one, measured slower: storm 5.3 -> 6.0 ms)
   const dim3 grid((unsigned)(few ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
@@ -2992,6 +3019,9 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
             GH_ROUND_NT(false, 5);  // LDS-DMA staging
           else
             GH_ROUND_NT(false, 2);
+          return;
+        case 4:  // the nibble path that takes REMOVE deliveries (column layout; returns at once otherwise)
+          if (!d.rowlay) GH_ROUND_NT(false, 6);
           return;
         default: break;
       }

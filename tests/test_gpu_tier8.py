@@ -405,3 +405,60 @@ def test_tier_lds_dma_staging(gs, oracle_mod, monkeypatch, case):
     trace, _ = remove_run(gs, oracle_mod, n, cfg, sched, 36)
     assert sum(v == 3 for _, v, _ in trace) >= 30, trace
     assert any(s["tombstoned"] for s, _, _ in trace)
+
+
+@pytest.mark.parametrize("env", [("GH_ROUND_XMAP", "2"), ("GH_NIB_RMV", "2")])
+def test_tier_nibble_variants(gs, oracle_mod, monkeypatch, env):
+    """Two nibble-path options on the crash wave of test_tier_lds_dma_staging,
+    bit-exact against the oracle every round: GH_ROUND_XMAP=2 (odd rounds
+    sweep the tiles from the other end, round.hip nib_region; the lane jobs
+    walk the same regions) and GH_NIB_RMV=2 (the REMOVE-taking
+    instantiation, k_round IN 6, in every round instead of only the rounds
+    after a detection)."""
+    monkeypatch.setenv(*env)
+    n = 2048
+    cfg = dict(fanout=4, seed=0x5EED0D20, t_fail=16, t_cleanup=16)
+    crashed = sc.crash_ids(n, 0.01, 0x5EED0D21)
+    sched = {8: [(sc.CRASH, int(c)) for c in crashed], 30: [(sc.JOIN, int(crashed[0]))]}
+    trace, _ = remove_run(gs, oracle_mod, n, cfg, sched, 36)
+    assert sum(v == 3 for _, v, _ in trace) >= 30, trace
+    assert any(s["tombstoned"] for s, _, _ in trace)
+
+
+@pytest.mark.parametrize("tmode", ["0", "1"])
+def test_round_timing_modes(gs, monkeypatch, tmode):
+    """gh_read_timing (the bench's k_round time): with GH_TMODE=1 only the
+    nibble launch carries its own HIP events, the other variants are timed
+    together and the device logs which variant ran (vlog); GH_TMODE=0 times
+    every launch. Through a crash wave at N=2,048 (nibble, storm-free REMOVE
+    and release rounds) every round is counted once with a positive time, and
+    the nibble rounds' times agree between the modes within a factor 3."""
+    monkeypatch.setenv("GH_TMODE", tmode)
+    n = 2048
+    cfg = gs.default_config(n, fanout=4, seed=0x5EED0D30, t_fail=16, t_cleanup=16)
+    crashed = sc.crash_ids(n, 0.01, 0x5EED0D31)
+    eng = gs.Engine(cfg)
+    try:
+        hb, ts, alive = sc.full_state(n)
+        eng.import_state(hb, ts, alive, 0)
+        eng.set_timing(True)
+        prev, per = 0.0, []
+        for r in range(1, 41):
+            if r == 8:
+                eng.apply_events([(sc.CRASH, int(c)) for c in crashed])
+            eng.step(1)
+            ms, launches = eng.read_timing()
+            assert launches == r
+            assert ms > prev, (r, ms, prev)
+            per.append((eng.tier_info(full=True)[3], ms - prev))
+            prev = ms
+        eng.set_timing(True)
+        eng.step(10)  # several rounds in one call
+        ms, launches = eng.read_timing()
+        assert launches == 10 and ms > 0
+    finally:
+        eng.close()
+    nib = [t for v, t in per[1:] if v == 3]
+    assert len(nib) >= 30
+    med = sorted(nib)[len(nib) // 2]
+    assert all(t < 3 * med + 0.5 for t in nib), (med, nib)
