@@ -132,12 +132,7 @@ struct LocalGroup {
   std::vector<const void*> ptr;
   std::vector<int> dev;
   std::vector<const size_t*> counts;  // alltoallv: each rank's per-destination byte counts
-  // stream order across ranks: ready[h] is recorded on rank h's stream when
-  // its send buffer is complete, done[h] when it has finished reading the
-  // others' buffers (so that they may be rewritten)
-  std::vector<hipEvent_t> ready, done;
-  explicit LocalGroup(int w)
-      : world(w), ptr(w, nullptr), dev(w, 0), counts(w, nullptr), ready(w, nullptr), done(w, nullptr) {}
+  explicit LocalGroup(int w) : world(w), ptr(w, nullptr), dev(w, 0), counts(w, nullptr) {}
   // All ranks meet. False after a 120 s wait (a rank failed or diverged);
   // the group then stays broken so that no rank hangs on it later.
   bool barrier() {
@@ -176,42 +171,83 @@ __global__ __launch_bounds__(256) void k_reduce(const T* __restrict__ parts, int
   }
 }
 
-// A collective is stream-ordered like RCCL's: the host threads meet twice
-// (to publish the buffers and events, and to publish that the reads are
-// enqueued), and each rank's stream waits for the others' events instead of
-// the host draining the streams (which had serialised the G shards of one
-// GPU at every exchange).
+// Same-device ranks (G shards of one GPU): one kernel per collective reads
+// the peers' buffers directly, instead of one copy launch per peer (a G=8
+// row-shard round had issued ~600 copies)
+constexpr int kLocalDirect = 16;  // ranks
+struct Segs {
+  const char* src[kLocalDirect];
+  int64_t dst[kLocalDirect];    // byte offset in recv
+  int64_t begin[kLocalDirect + 1];  // prefix sums of the segments' bytes
+  int n;
+};
+template <int W>
+__global__ __launch_bounds__(256) void k_copy_segs(Segs g, char* __restrict__ recv) {
+  const int64_t total = g.begin[g.n];
+  const int64_t units = total / W;
+  int h = 0;
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = u * W;
+    while (b >= g.begin[h + 1]) ++h;  // (monotone per thread)
+    while (b < g.begin[h]) --h;
+    const int64_t o = b - g.begin[h];
+    if constexpr (W == 16)
+      *reinterpret_cast<uint4*>(recv + g.dst[h] + o) = *reinterpret_cast<const uint4*>(g.src[h] + o);
+    else
+      recv[g.dst[h] + o] = g.src[h][o];
+  }
+}
+struct Ptrs {
+  const void* p[kLocalDirect];
+};
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void k_reduce_ptrs(Ptrs ps, int world, size_t count, T* __restrict__ out) {
+  for (size_t x = (size_t)blockIdx.x * blockDim.x + threadIdx.x; x < count; x += (size_t)gridDim.x * blockDim.x) {
+    T a = static_cast<const T*>(ps.p[0])[x];
+    for (int h = 1; h < world; ++h) {
+      const T b = static_cast<const T*>(ps.p[h])[x];
+      a = OP == GH_OP_SUM ? (T)(a + b) : (b > a ? b : a);
+    }
+    out[x] = a;
+  }
+}
+
 struct LocalComm final : GhComm {
   std::shared_ptr<LocalGroup> g;
   int device = 0;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
-  hipEvent_t ev_ready = nullptr, ev_done = nullptr;
   ~LocalComm() override {
     if (tmp) (void)hipFree(tmp);
-    if (ev_ready) (void)hipEventDestroy(ev_ready);
-    if (ev_done) (void)hipEventDestroy(ev_done);
-  }
-  int events() {
-    if (ev_ready) return 0;
-    if (hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ev_done, hipEventDisableTiming) != hipSuccess)
-      return fail("local comm: event creation failed");
-    return 0;
-  }
-  // s's reads of the other ranks' buffers are enqueued: publish it, meet,
-  // and make s wait until every other rank has read this rank's buffers
-  int finish_reads(hipStream_t s) {
-    if (hipEventRecord(ev_done, s) != hipSuccess) return fail("local comm: event record failed");
-    g->done[rank] = ev_done;
-    if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
-    for (int h = 0; h < world; ++h)
-      if (h != rank && hipStreamWaitEvent(s, g->done[h], 0) != hipSuccess) return fail("local comm: stream wait failed");
-    return 0;
   }
   int fail(const std::string& m) {
     err = m;
     return -1;
+  }
+  // every rank on this rank's device (then the direct kernels)
+  bool direct() const {
+    if (world > kLocalDirect) return false;
+    for (int h = 0; h < world; ++h)
+      if (g->dev[h] != device) return false;
+    return true;
+  }
+  int meet() { return g->barrier() ? 0 : fail("local comm: barrier timeout (a rank failed or diverged)"); }
+  int sync(hipStream_t s) { return hipStreamSynchronize(s) == hipSuccess ? 0 : fail("local comm: stream sync failed"); }
+  // recv[dst[h] ..] = segment h, in one launch
+  int copy_segs(Segs& sg, char* recv, hipStream_t s) {
+    const int64_t total = sg.begin[sg.n];
+    if (total == 0) return 0;
+    bool al = (reinterpret_cast<uintptr_t>(recv) & 15) == 0;
+    for (int h = 0; h < sg.n; ++h)
+      al = al && (reinterpret_cast<uintptr_t>(sg.src[h]) & 15) == 0 && sg.dst[h] % 16 == 0 &&
+           (sg.begin[h + 1] - sg.begin[h]) % 16 == 0;
+    const int64_t units = al ? total / 16 : total;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + 255) / 256, 8192));
+    if (al)
+      hipLaunchKernelGGL(k_copy_segs<16>, dim3(grid), dim3(256), 0, s, sg, recv);
+    else
+      hipLaunchKernelGGL(k_copy_segs<1>, dim3(grid), dim3(256), 0, s, sg, recv);
+    return hipGetLastError() == hipSuccess ? 0 : fail("local comm: copy kernel launch failed");
   }
   int grow(size_t bytes) {
     if (bytes <= tmp_bytes) return 0;
@@ -222,26 +258,40 @@ struct LocalComm final : GhComm {
     tmp_bytes = bytes;
     return 0;
   }
-  // tmp[h*bytes ..] = rank h's send, for every h. Work enqueued on s after
-  // the return runs after every rank has read every send buffer, so recv
-  // (which may alias send) can be written.
+  // tmp[h*bytes ..] = rank h's send, for every h. On return every rank has
+  // finished reading every send buffer, so recv (which may alias send) can
+  // be written.
   int gather(const void* send, size_t bytes, hipStream_t s) {
-    if (grow(bytes * world) || events()) return -1;
-    if (hipEventRecord(ev_ready, s) != hipSuccess) return fail("local comm: event record failed");
+    if (grow(bytes * world)) return -1;
+    if (hipStreamSynchronize(s) != hipSuccess) return fail("local comm: stream sync failed");
     g->ptr[rank] = send;
-    g->ready[rank] = ev_ready;
     if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
-    for (int h = 0; h < world; ++h) {
-      if (h != rank && hipStreamWaitEvent(s, g->ready[h], 0) != hipSuccess)
-        return fail("local comm: stream wait failed");
+    for (int h = 0; h < world; ++h)
       if (hipMemcpyPeerAsync(static_cast<char*>(tmp) + (size_t)h * bytes, device, g->ptr[h], g->dev[h], bytes, s) !=
           hipSuccess)
         return fail("local comm: peer copy failed");
-    }
-    return finish_reads(s);
+    if (hipStreamSynchronize(s) != hipSuccess) return fail("local comm: stream sync failed");
+    if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
+    return 0;
   }
   int allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     if (bytes == 0) return 0;
+    if (direct()) {
+      // straight into recv: no rank reads it (a send aliasing recv's own
+      // block gets its own bytes back)
+      if (sync(s)) return -1;
+      g->ptr[rank] = send;
+      if (meet()) return -1;
+      Segs sg{};
+      sg.n = world;
+      for (int h = 0; h < world; ++h) {
+        sg.src[h] = static_cast<const char*>(g->ptr[h]);
+        sg.dst[h] = (int64_t)h * (int64_t)bytes;
+        sg.begin[h + 1] = sg.begin[h] + (int64_t)bytes;
+      }
+      if (copy_segs(sg, static_cast<char*>(recv), s) || sync(s) || meet()) return -1;
+      return 0;
+    }
     if (gather(send, bytes, s)) return -1;
     if (hipMemcpyAsync(recv, tmp, bytes * world, hipMemcpyDeviceToDevice, s) != hipSuccess)
       return fail("local comm: copy failed");
@@ -261,12 +311,30 @@ struct LocalComm final : GhComm {
   // addressed to it straight from the peers' buffers
   int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t* recvbytes,
                 hipStream_t s, const size_t* recvdispl) override {
-    if (events()) return -1;
-    if (hipEventRecord(ev_ready, s) != hipSuccess) return fail("local comm: event record failed");
+    if (hipStreamSynchronize(s) != hipSuccess) return fail("local comm: stream sync failed");
     g->ptr[rank] = send;
     g->counts[rank] = sendbytes;
-    g->ready[rank] = ev_ready;
     if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
+    if (direct()) {  // one copy kernel over the blocks addressed to this rank
+      Segs sg{};
+      size_t ro = 0;
+      for (int h = 0; h < world; ++h) {
+        size_t off = 0;
+        for (int r = 0; r < rank; ++r) off += g->counts[h][r];
+        const size_t bytes = g->counts[h][rank];
+        if (bytes != recvbytes[h]) {
+          g->barrier();
+          return fail("local comm: alltoallv counts disagree");
+        }
+        sg.src[sg.n] = static_cast<const char*>(g->ptr[h]) + off;
+        sg.dst[sg.n] = (int64_t)(recvdispl ? recvdispl[h] : ro);
+        sg.begin[sg.n + 1] = sg.begin[sg.n] + (int64_t)bytes;
+        sg.n++;
+        ro += bytes;
+      }
+      if (copy_segs(sg, static_cast<char*>(recv), s) || sync(s) || meet()) return -1;
+      return 0;
+    }
     size_t ro = 0;
     for (int h = 0; h < world; ++h) {
       size_t off = 0;
@@ -277,17 +345,48 @@ struct LocalComm final : GhComm {
         return fail("local comm: alltoallv counts disagree");
       }
       const size_t at = recvdispl ? recvdispl[h] : ro;
-      if (bytes && h != rank && hipStreamWaitEvent(s, g->ready[h], 0) != hipSuccess)
-        return fail("local comm: stream wait failed");
       if (bytes && hipMemcpyPeerAsync(static_cast<char*>(recv) + at, device, static_cast<const char*>(g->ptr[h]) + off,
                                       g->dev[h], bytes, s) != hipSuccess)
         return fail("local comm: peer copy failed");
       ro += bytes;
     }
-    return finish_reads(s);
+    if (hipStreamSynchronize(s) != hipSuccess) return fail("local comm: stream sync failed");
+    if (!g->barrier()) return fail("local comm: barrier timeout (a rank failed or diverged)");
+    return 0;
+  }
+  template <typename T>
+  void reduce_ptrs(GhROp op, size_t count, T* out, hipStream_t s) {
+    Ptrs ps{};
+    for (int h = 0; h < world; ++h) ps.p[h] = g->ptr[h];
+    const unsigned grid = (unsigned)std::min<size_t>((count + 255) / 256, 4096);
+    if (op == GH_OP_SUM)
+      hipLaunchKernelGGL((k_reduce_ptrs<T, GH_OP_SUM>), dim3(grid), dim3(256), 0, s, ps, world, count, out);
+    else
+      hipLaunchKernelGGL((k_reduce_ptrs<T, GH_OP_MAX>), dim3(grid), dim3(256), 0, s, ps, world, count, out);
   }
   int allreduce(const void* send, void* recv, size_t count, GhDType dt, GhROp op, hipStream_t s) override {
     if (count == 0) return 0;
+    if (direct()) {
+      // one kernel reads every rank's send; in place (send == recv) through
+      // tmp, as the other ranks may still be reading this send
+      const size_t bytes = count * gh_dtype_size(dt);
+      const bool inplace = send == recv;
+      if ((inplace && grow(bytes)) || sync(s)) return -1;
+      g->ptr[rank] = send;
+      if (meet()) return -1;
+      void* out = inplace ? tmp : recv;
+      if (dt == GH_DT_U8)
+        reduce_ptrs<uint8_t>(op, count, static_cast<uint8_t*>(out), s);
+      else if (dt == GH_DT_I32)
+        reduce_ptrs<int32_t>(op, count, static_cast<int32_t*>(out), s);
+      else
+        reduce_ptrs<unsigned long long>(op, count, static_cast<unsigned long long*>(out), s);
+      if (hipGetLastError() != hipSuccess) return fail("local comm: reduce kernel launch failed");
+      if (sync(s) || meet()) return -1;
+      if (inplace && hipMemcpyAsync(recv, tmp, bytes, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        return fail("local comm: copy failed");
+      return 0;
+    }
     if (gather(send, count * gh_dtype_size(dt), s)) return -1;
     if (dt == GH_DT_U8)
       reduce<uint8_t>(op, count, recv, s);

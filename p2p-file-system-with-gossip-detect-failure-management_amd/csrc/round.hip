@@ -168,14 +168,21 @@ __global__ __launch_bounds__(256) void k_peers_pull(GhDev d, int cur, int dcur, 
     const uint32_t u = gh_philox_word(p.seed, (uint32_t)i, (uint32_t)p.r, GH_TAG_PEER, (uint32_t)(q >> 2), q & 3);
     const uint32_t w = (uint32_t)(((uint64_t)u * (uint64_t)(p.n - 1)) >> 32);
     s = (int)w + ((int64_t)w >= i);
+    // (a tier chunk's two words are loaded beside s's alive / active bytes,
+    // not after them: one level of dependent loads instead of two)
+    const bool tier = gh_m8(d, cur);
+    uint32_t aw = 0, lw = 0;
+    if (tier) {
+      const int64_t cell = gh_cell(d, s, t & ~(int64_t)7);
+      aw = d.a4[cur][cell >> 3];
+      lw = d.pl[cur][cell >> 3];
+    }
     if (d.alive[s] && d.active[s]) {
       // i must be in s's snapshot list: present, not detected by s this
       // round and not REMOVE'd at s in step 1. A tier chunk answers from its
-      // two words, loaded together (code 15: absent or a tombstone; a tier
-      // cell is never flagged)
-      if (gh_m8(d, cur)) {
-        const int64_t cell = gh_cell(d, s, t & ~(int64_t)7);
-        const uint32_t aw = d.a4[cur][cell >> 3], lw = d.pl[cur][cell >> 3];
+      // two words (code 15: absent or a tombstone; a tier cell is never
+      // flagged)
+      if (tier) {
         if (!gh_t4_esc(aw)) {
           ok = ((lw >> gh_nib((int)(t & 7))) & 0xFu) != 15u;
         } else {
@@ -865,7 +872,8 @@ __device__ __forceinline__ uint32_t nib_is15(uint32_t x) {
 // tombstone stays one, and an absent one (the reference panics; counted
 // remove_unknown) or a tombstone too young for the tier leaves the lane to
 // the lane-job kernel.
-template <bool RMV>
+// PRE: p0 is already the senders' per-nibble minimum (p1..p3 unused).
+template <bool RMV, bool PRE = false>
 __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint32_t p0, uint32_t p1, uint32_t p2,
                                          uint32_t p3, uint32_t a1, uint32_t dn, uint32_t tfk, uint32_t rm1, uint32_t rs1,
                                          uint32_t rmk, uint32_t& QO, uint32_t& AO, uint32_t& LWo, uint32_t& Bm, uint32_t& Lz,
@@ -875,7 +883,10 @@ __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const uint32_t M = 0x000F000Fu << (4 * j);
-    Lw |= pk_min_u16(pk_min_u16(pk_min_u16(qw & M, p0 & M), pk_min_u16(p1 & M, p2 & M)), p3 & M);
+    if constexpr (PRE)
+      Lw |= pk_min_u16(qw & M, p0 & M);
+    else
+      Lw |= pk_min_u16(pk_min_u16(pk_min_u16(qw & M, p0 & M), pk_min_u16(p1 & M, p2 & M)), p3 & M);
   }
   uint32_t bad = 0;
   uint32_t pr1 = 0, PRm = 0;  // RMV: present cells REMOVE'd this round
@@ -955,6 +966,14 @@ __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint
 // 32 sender lines as four), then computes them on ds_read_b64 in the 16-cell
 // lane shape: half the vector-memory load instructions of 8-B register loads,
 // and no VGPRs held by loads in flight.
+// SPL (16-cell lanes, 256-member tiles; not with DMA): lanes
+// m and m + 8 of a row's 16 share 32 cells; lane m gathers 16 B of those
+// cells from senders 0 and 1, lane m + 8 from senders 2 and 3 (2 gathers of
+// 16 B per row step instead of 4 of 8 B: each wave instruction then touches 8
+// lines instead of 4, which halves the gather instructions the TA issues),
+// each takes the per-nibble min of its two, the halves swap by DPP
+// (row_ror 8), and each lane finishes its own 16 cells (m * 32 + 16 h for
+// half h); `tools/r05/gprobe4.hip`: 1.73-1.84 ms against 1.96-2.24 ms.
 // RMVK: the instantiation that can take REMOVE deliveries itself (nib_word
 // RMV); the other one (the steady state's: 10 VGPRs fewer, 7 waves per SIMD
 // instead of 6) hands every lane holding a REMOVE'd member to the lane jobs.
@@ -973,6 +992,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   static_assert(W == 2 || W == 4, "nibble path: 16 or 32 cells per lane (one or two lane jobs of 16 cells)");
   static_assert(!DMA || (!ROWS && CPL == 16 && TW == 256 && RB % 32 == 0), "LDS-DMA staging: 16-cell lanes, 256-member tiles");
   constexpr int RSD = DMA ? 2 : RS;  // row steps per iteration (DMA: a wave's 8 consecutive rows)
+  constexpr bool SPL = GH_NIB_SPLIT && !DMA && CPL == 16 && TW == 256;
   // per wave: own lag 1 KiB, age 1 KiB, the 4 gather pieces (sender slot q
   // of the 8 rows) 1 KiB each
   __shared__ __attribute__((aligned(16))) uint32_t s_dma[DMA ? 4 * 1536 : 1];
@@ -997,7 +1017,10 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const int wave = uni(tid >> 6);
   const int sub = lane / SEG, lc = lane % SEG;
   const unsigned long long gmask = (SEG == 64 ? ~0ull : ((1ull << SEG) - 1)) << (sub * SEG);
-  const int64_t l0 = (int64_t)tile * TW + lc * CPL;  // local column of this lane's first cell
+  // the lane's first cell in the tile and its CPL-cell group (SPL: m * 32 + 16 h)
+  const int lcell = SPL ? 32 * (lc & 7) + 16 * (lc >> 3) : lc * CPL;
+  const int lgrp = lcell / CPL;
+  const int64_t l0 = (int64_t)tile * TW + lcell;  // local column of this lane's first cell
   // the lane's REMOVE'd members (D_{r-1}), loaded beside the staging below
   uint32_t rm = 0;
 #pragma unroll
@@ -1088,7 +1111,8 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const auto pln_t = nib_rsrc(reinterpret_cast<const char*>(d.pl[cur ^ 1]) + tcell / 2, tbytes);
   const auto a4o_t = nib_rsrc(reinterpret_cast<const char*>(d.a4[cur]) + tcell / 2, tbytes);
   const auto a4n_t = nib_rsrc(reinterpret_cast<const char*>(d.a4[cur ^ 1]) + tcell / 2, tbytes);
-  const uint32_t lbp = (uint32_t)lc * (CPL / 2);  // the lane's byte offset in a plane row segment
+  const uint32_t lbp = (uint32_t)lcell / 2;  // the lane's byte offset in a plane row segment
+  const uint32_t gbp = (uint32_t)(lc & 7) * 16;  // SPL: the lane pair's 16 B of a sender's segment
   const bool tile_still = s_bmove == 0;
   // REMOVE'd members on the nibble path (nib_word RMV): canonical recipients
   // (every running row but a sole detector, SPEC D4) and tier tombstones with
@@ -1130,13 +1154,13 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   const uint32_t rmk = (uint32_t)(15 - (d.toff - 1)) * 0x01010101u;
   // the lane needs the per-cell rule (a lane job) in every row when it holds
   // a REMOVE'd member off the RMV path or a base move outside 0..15
-  const bool lane_job = (rm != 0u && !rmv) || ((s_d8bad >> lc) & 1ull) != 0;
+  const bool lane_job = (rm != 0u && !rmv) || ((s_d8bad >> lgrp) & 1ull) != 0;
   // this wave's lane-job region (no atomics: the wave owns it)
   uint4* __restrict__ jreg = d.jobs + ((int64_t)bid * 4 + wave) * GH_JOB_CAP * 2;
   int wjobs = 0;
   uint32_t DN[W];  // the base moves of dword w, nibble order
 #pragma unroll
-  for (int x = 0; x < W; ++x) DN[x] = s_dn[lc * W + x];
+  for (int x = 0; x < W; ++x) DN[x] = s_dn[lgrp * W + x];
   const uint32_t tfk = (uint32_t)(15 - min(max(p.t_fail, 0), 15)) * 0x11111111u;  // age + tfk carries iff age > T_fail
   uint32_t n_mrg = 0, n_rel = 0, n_tmb = 0;
 
@@ -1207,7 +1231,18 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       // the row's receivers gather too
       awu[u] = nib_load<W, GH_NIB_AGE_AUX>(a4o_t, ow);
       qwu[u] = nib_load<W, GH_NIB_OWN_AUX>(plo_t, ow);
-      if constexpr (ROWS) {
+      if constexpr (ROWS && SPL) {
+        // (the pair's 16 B of senders 2h, 2h + 1, as below)
+        typedef uint32_t gw4 __attribute__((ext_vector_type(4)));
+        typedef const __attribute__((address_space(1))) gw4 ggw4;
+        const int q0 = (lc >> 3) != 0 ? 2 : 0;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const gw4 x = *reinterpret_cast<ggw4*>(s_inb64[rs * KB + q0 + t] + gbp);
+          pwu[u][2 * t].v[0] = x[0], pwu[u][2 * t].v[1] = x[1];
+          pwu[u][2 * t + 1].v[0] = x[2], pwu[u][2 * t + 1].v[1] = x[3];
+        }
+      } else if constexpr (ROWS) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           typedef uint32_t gw __attribute__((ext_vector_type(W)));
@@ -1219,8 +1254,20 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       } else {
         const int4 sv4 = *reinterpret_cast<const int4*>(&s_inb[rs * KB]);
         const int sv[4] = {sv4.x, sv4.y, sv4.z, sv4.w};
+        if constexpr (SPL) {
+          // senders 2h, 2h + 1 of the row, 16 B each (pwu[u][0..1]: the first,
+          // pwu[u][2..3]: the second)
+          const bool h1 = (lc >> 3) != 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pwu[u][q] = nib_load<W, GH_NIB_GAT_AUX>(plo_t, (uint32_t)sv[q] + lbp);
+          for (int t = 0; t < 2; ++t) {
+            const NibWords<4> x = nib_load<4, GH_NIB_GAT_AUX>(plo_t, (uint32_t)(h1 ? sv[2 + t] : sv[t]) + gbp);
+            pwu[u][2 * t].v[0] = x.v[0], pwu[u][2 * t].v[1] = x.v[1];
+            pwu[u][2 * t + 1].v[0] = x.v[2], pwu[u][2 * t + 1].v[1] = x.v[3];
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pwu[u][q] = nib_load<W, GH_NIB_GAT_AUX>(plo_t, (uint32_t)sv[q] + lbp);
+        }
       }
     }
 #pragma unroll
@@ -1240,7 +1287,44 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       // (wave-uniform) the wave's own cells include code 15 (absent or a tier
       // tombstone): the rule ages and releases tombstones
       const bool tt = GH_TIER_TOMB && (!GH_TIER_TOMB_GATE || __ballot(a1any != 0) != 0);
-      if (wrmv) {
+      if constexpr (SPL) {
+        // the pair's 32 cells: the min of my two senders over them; I keep
+        // my half's dword w and send the partner its half's (DPP row_ror 8:
+        // lane m <-> m + 8 of the same row), then the min of the two is my
+        // senders' minimum
+        const bool h1 = (lc >> 3) != 0;
+        uint32_t PS[2];
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {
+          uint32_t lo = 0, hi = 0;  // cells of half 0 / half 1, dword w
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t M = 0x000F000Fu << (4 * j);
+            lo |= pk_min_u16(pwu[u][0].v[w] & M, pwu[u][2].v[w] & M);
+            hi |= pk_min_u16(pwu[u][1].v[w] & M, pwu[u][3].v[w] & M);
+          }
+          const uint32_t keep = h1 ? hi : lo;
+          const uint32_t got = (uint32_t)__builtin_amdgcn_mov_dpp((int)(h1 ? lo : hi), 0x128, 0xF, 0xF, false);
+          uint32_t mn = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t M = 0x000F000Fu << (4 * j);
+            mn |= pk_min_u16(keep & M, got & M);
+          }
+          PS[w] = mn;
+        }
+        if (wrmv) {
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            nib_word<true, true>(tt, qwu[u].v[w], awu[u].v[w], PS[w], 0u, 0u, 0u, A1[w], DN[w], tfk, RM1[w], RS1[w], rmk,
+                                 QO[w], AO[w], LW[w], Bm, Lz, mrg, gain, rel, tmb);
+        } else {
+#pragma unroll
+          for (int w = 0; w < W; ++w)
+            nib_word<false, true>(tt, qwu[u].v[w], awu[u].v[w], PS[w], 0u, 0u, 0u, A1[w], DN[w], tfk, 0u, 0u, 0u, QO[w],
+                                  AO[w], LW[w], Bm, Lz, mrg, gain, rel, tmb);
+        }
+      } else if (wrmv) {
 #pragma unroll
         for (int w = 0; w < W; ++w)
           nib_word<true>(tt, qwu[u].v[w], awu[u].v[w], pwu[u][0].v[w], pwu[u][1].v[w], pwu[u][2].v[w], pwu[u][3].v[w],
@@ -1294,7 +1378,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
             // kernel needs not re-read them)
 #pragma unroll
             for (int h = 0; h < H; ++h) {
-              jreg[2 * (pos + h)] = uint4{(uint32_t)i, ((uint32_t)tile << 8) | (uint32_t)(lc * H + h), LW[2 * h],
+              jreg[2 * (pos + h)] = uint4{(uint32_t)i, ((uint32_t)tile << 8) | (uint32_t)(lgrp * H + h), LW[2 * h],
                                           LW[2 * h + 1]};
               jreg[2 * (pos + h) + 1] = uint4{qwu[u].v[2 * h], qwu[u].v[2 * h + 1], awu[u].v[2 * h], awu[u].v[2 * h + 1]};
             }

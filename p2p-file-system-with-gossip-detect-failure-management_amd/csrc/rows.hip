@@ -39,6 +39,21 @@ __global__ __launch_bounds__(256) void k_ghost_pack(GhDev d, int cur, const int3
   }
 }
 
+// part GH_GX_PLANE with tiles of >= 32 members: one thread per 32 cells
+// (16 B of plane words, 8 lanes per 128-B tile segment); the 4-B-per-thread
+// form of k_ghost_pack moved a shard's 737 MB at ~1.1 TB/s
+__global__ __launch_bounds__(256) void k_ghost_pack_plane(GhDev d, int cur, const int32_t* rows, int64_t ns,
+                                                          char* out) {
+  const int64_t qpr = d.ld >> 5;  // 16-B groups per row
+  const int64_t total = ns * qpr;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = idx / qpr, k = idx - e * qpr;
+    const int64_t cell = gh_cell(d, rows[e], k * 32);
+    reinterpret_cast<uint4*>(out)[idx] = *reinterpret_cast<const uint4*>(d.pl[cur] + (cell >> 3));
+  }
+}
+
 // a wide record: (row, tile), the segment's TW exact heartbeats, its flag
 // bytes (a sender's ts is never read)
 __host__ __device__ inline int64_t ghost_wide_bytes(int tw) { return ((8 + 4 * (int64_t)tw + tw / 8) + 15) / 16 * 16; }
@@ -201,6 +216,10 @@ int64_t ghost_wide_record_bytes(const GhDev& d) { return ghost_wide_bytes(d.tw);
 void launch_ghost_pack(const GhDev& d, int cur, const int32_t* rows, const int32_t* dest, int64_t ns, int part,
                        char* out, int32_t* wcnt, hipStream_t s) {
   if (ns == 0) return;
+  if (part == GH_GX_PLANE && d.tw >= 32 && d.ld % 32 == 0) {
+    hipLaunchKernelGGL(k_ghost_pack_plane, dim3(ghost_grid(ns * (d.ld >> 5))), dim3(256), 0, s, d, cur, rows, ns, out);
+    return;
+  }
   hipLaunchKernelGGL(k_ghost_pack, dim3(ghost_grid(ns * (d.ld >> 3))), dim3(256), 0, s, d, cur, rows, dest, ns, part,
                      out, wcnt);
 }
