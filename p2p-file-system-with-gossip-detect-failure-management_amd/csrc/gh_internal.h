@@ -163,8 +163,8 @@
 #endif
 #define GH_JOB_CPL 16           // a lane job covers 16 cells (a 32-cell lane of the nibble path writes two)
 #ifndef GH_NIB_SPLIT
-#define GH_NIB_SPLIT 1          // nibble path, 16-cell lanes, 256-member tiles (IN 2 / 6): the sender gathers
-                                // split over lane halves (round.hip round_block_nib SPL)
+#define GH_NIB_SPLIT 0          // nibble path, 16-cell lanes, 256-member tiles: the sender gathers split over
+                                // lane halves (round.hip round_block_nib SPL; parity green, measured slower)
 #endif
 #ifndef GH_NIB_RS
 #define GH_NIB_RS 1             // nibble path: row steps per iteration (1 measured best at CPL 8 and 16)

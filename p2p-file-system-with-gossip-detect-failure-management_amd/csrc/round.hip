@@ -973,7 +973,10 @@ __device__ __forceinline__ void nib_word(bool tt, uint32_t qw, uint32_t aw, uint
 // lines instead of 4, which halves the gather instructions the TA issues),
 // each takes the per-nibble min of its two, the halves swap by DPP
 // (row_ror 8), and each lane finishes its own 16 cells (m * 32 + 16 h for
-// half h); `tools/r05/gprobe4.hip`: 1.73-1.84 ms against 1.96-2.24 ms.
+// half h). In the probe (`tools/r05/gprobe4.hip`, a trivial rule at 38
+// VGPRs) 1.73-1.84 ms against 1.96-2.24 ms; in the kernel (70 VGPRs, the
+// full rule) 2.10-2.12 ms against 1.98-2.01 ms (`profiles/r05_s16_ab_split.txt`):
+// off (GH_NIB_SPLIT=0), kept as an A/B build option.
 // RMVK: the instantiation that can take REMOVE deliveries itself (nib_word
 // RMV); the other one (the steady state's: 10 VGPRs fewer, 7 waves per SIMD
 // instead of 6) hands every lane holding a REMOVE'd member to the lane jobs.
