@@ -854,6 +854,7 @@ struct GhRound {
   int32_t nib_dma;      // nibble path: LDS-DMA staging of the own and sender lines (GH_NIB_DMA; column layout, TW 256)
   int32_t shadow_row;   // the introducer while it may hold D7 shadow entries (its segments take k_round_slow), else -1
   int32_t vslot;        // the round's index in its gh_step call (vlog: which k_round variant ran)
+  int32_t rmv_full;     // k_round IN 6 on a full grid: the host knows a REMOVE is pending this round
   int32_t plane;        // the round writes the next buffer's sender plane (and may read cur's)
   int32_t ring_whole;   // ring mode: one engine and a current flag count, so the targets may come
                         // from whole lists when no REMOVE / flag is pending (k_ring_fast)

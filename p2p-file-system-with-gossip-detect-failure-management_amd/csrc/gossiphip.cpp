@@ -128,6 +128,9 @@ struct Engine {
   int tmode = 1;
   int32_t* vlog = nullptr;
   int64_t vlog_cap = 0;
+  // |D| of the last round as read at the end of gh_step (one engine; -1
+  // unknown): a first round with a REMOVE pending launches IN 6 on a full grid
+  int32_t last_nd = -1;
   std::string err;
   std::vector<void*> allocs;
 };
@@ -1871,6 +1874,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     GhRound pr = p;
     pr.gpo = e->gpo;  // row layout: the ghosts carry only their plane so far
     pr.vslot = q;
+    pr.rmv_full = q == 0 && e->world == 1 && e->last_nd > 0;
     // the variants of k_round; the ones not selected return at once. With
     // timing on, a launch stamps its own start and end (events 12q + 2v,
     // 12q + 2v + 1 of variant v; hipExtLaunchKernel, no event packets between
@@ -1966,7 +1970,11 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   COMMCHK(e, e->comm->allreduce(e->d.stats, e->d.stats, ST_COUNT, GH_DT_U64, GH_OP_SUM, e->stream));
   HIPCHK(e, hipMemcpyAsync(st, e->d.stats, sizeof st, hipMemcpyDeviceToHost, e->stream));
   if (e->shadow_any) HIPCHK(e, hipMemcpyAsync(&nshadow, e->d.nshadow, sizeof nshadow, hipMemcpyDeviceToHost, e->stream));
+  int32_t nd_last = -1;
+  if (e->world == 1 && done > 0)
+    HIPCHK(e, hipMemcpyAsync(&nd_last, e->d.nd + e->dcur, sizeof nd_last, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
+  e->last_nd = nd_last;
   e->shadow_any = nshadow > 0;  // (each shard for its own columns)
   {
     int32_t err = 0;

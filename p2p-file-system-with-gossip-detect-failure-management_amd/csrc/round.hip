@@ -3072,7 +3072,8 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
 }
 
 // variant: 0 lean on a 16-bit input, 1 storm, 2 lean on a 4-bit-tier input
-// by the 16-bit rule, 3 the nibble path (IN 2, or IN 4 on row shards)
+// by the 16-bit rule, 3 the nibble path (IN 2, or IN 4 on row shards), 4 the
+// nibble path that takes REMOVE deliveries (IN 6, column layout)
 template <int KB, int TW, int TPW>
 static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant,
                              hipEvent_t t0, hipEvent_t t1) {
@@ -3081,10 +3082,15 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
   const int64_t nblk = nrb * (p.ld / TW / TPW);
   if (nblk == 0) return;
   const bool tiered = d.a4[0] != nullptr;
-  const bool few = variant == 1 || variant == 2 || variant == 4 || (variant == 0 && tiered);
+  const bool few = variant == 1 || variant == 2 || (variant == 0 && tiered);
   // (a resident-sized grid for the persistent variants, 1,280 workgroups for
-  // the storm one, measured slower: storm 5.3 -> 6.0 ms)
-  const dim3 grid((unsigned)(few ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
+  // the storm one, measured slower: storm 5.3 -> 6.0 ms). The REMOVE-taking
+  // nibble path (variant 4): a full grid when the host knows a REMOVE is
+  // pending (p.rmv_full), else a 1/8 grid whose workgroups loop over their
+  // blocks (idle in most rounds: a full grid cost 31 us of dispatch; active,
+  // 1/8 grid 3.4-3.7 ms against 2.7-3.2 ms full, a resident-sized one 3.5-4.1)
+  const bool few4 = variant == 4 && tiered && !p.rmv_full;
+  const dim3 grid((unsigned)((few || few4) ? std::max<int64_t>(8, (nblk / 8 + 7) / 8 * 8) : nblk)), blk(256);
 #define GH_ROUND_LAUNCH(NT, ST, IN) \
   hipExtLaunchKernelGGL((k_round<KB, TW, TPW, NT, ST, IN>), grid, blk, 0, s, t0, t1, 0, d, cur, dcur, p)
 #define GH_ROUND_NT(ST, IN)        \
