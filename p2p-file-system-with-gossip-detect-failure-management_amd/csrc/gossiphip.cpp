@@ -387,6 +387,7 @@ int reset_pending_removes(Engine* e) {
   HIPCHK(e, hipMemsetAsync(d.dbits, 0, sizeof(uint32_t) * (e->ld / 32 + 2), e->stream));
   HIPCHK(e, hipMemsetAsync(d.nd, 0, sizeof(int32_t) * 8, e->stream));
   HIPCHK(e, hipMemsetAsync(d.det_any, 0, e->n, e->stream));
+  e->last_nd = 0;  // (only the rounds and this reset write nd[0..1])
   return GH_OK;
 }
 
@@ -1817,6 +1818,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   const int32_t first = e->round + 1;
   int32_t done = 0;
   int status = GH_OK;
+  std::vector<int8_t> mvlog(tsel ? rounds : 0, 3);  // the variant each round's nibble launch was (tsel)
   for (int32_t q = 0; q < rounds; ++q) {
     const int32_t r = e->round + 1;
     int rc;
@@ -1882,19 +1884,32 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     // variants together, from the start of the first (v0) to the end of the
     // last (v4) (events 12q + 10, 12q + 11), as a stamped launch costs its
     // stream ~5 us
+    // The nibble launch: IN 2 (variant 3), or IN 6 (variant 4, on a full
+    // grid) when the host knows a REMOVE is pending (the first round of a
+    // call after a detection, one engine, the tier's default modes): IN 2
+    // cannot be the one selected then, so it is not launched, and the
+    // REMOVE round's nibble path runs on the round's stream
+    const bool rmv_main = e->c8 && pr.rmv_full && !e->rowlay && e->nib_rmv >= 1 && !e->nib_dma &&
+                          (!e->timing || tsel);
+    const int mv = rmv_main ? 4 : 3;
+    if (e->timing && tsel) mvlog[q] = (int8_t)mv;
+    const int nside = rmv_main ? 3 : 4;
+    const int sides[4] = {0, 1, 2, 4};  // the first nside of them
     auto ev = [&](int v, int end) -> hipEvent_t {
       if (!e->timing) return nullptr;
-      if (!tsel || v == 3) return e->evs[12 * q + 2 * v + end];
-      if (v == 0 && end == 0) return e->evs[12 * q + 10];
-      if (v == 4 && end == 1) return e->evs[12 * q + 11];
+      if (!tsel) return e->evs[12 * q + 2 * v + end];
+      if (v == mv) return e->evs[12 * q + 6 + end];
+      if (v == sides[0] && end == 0) return e->evs[12 * q + 10];
+      if (v == sides[nside - 1] && end == 1) return e->evs[12 * q + 11];
       return nullptr;
     };
     if (e->c8 && !e->side) {
       // lean 16-bit input, storm, lean tier input by the 16-bit rule, the
       // nibble path that takes REMOVE deliveries, then the steady nibble
       // path, all on the round's stream
-      for (int v : {0, 1, 2, 4}) launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v, ev(v, 0), ev(v, 1));
-      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, 3, ev(3, 0), ev(3, 1));
+      for (int x = 0; x < nside; ++x)
+        launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, sides[x], ev(sides[x], 0), ev(sides[x], 1));
+      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, mv, ev(mv, 0), ev(mv, 1));
     } else if (e->c8 && e->side == 2) {
       // the same on two side streams, so that after the nibble path only one
       // idle launch per stream is left to run (the first on each spans it)
@@ -1910,16 +1925,16 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       HIPCHK(e, hipStreamWaitEvent(e->stream, e->vjoin2, 0));
     } else if (e->c8) {
       // lean 16-bit input, storm, lean tier input by the 16-bit rule and the
-      // REMOVE-taking nibble path on the side stream, beside the steady
-      // nibble path
+      // REMOVE-taking nibble path on the side stream, beside the nibble
+      // launch
       // (forked at the nibble launch's own start stamp: its stream's earlier
       // work, the inboxes, is done then; an event packet of its own before
       // it had cost the round ~10 us)
-      hipEvent_t st = e->timing ? ev(3, 0) : e->vstart;
-      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, 3, st, ev(3, 1));
+      hipEvent_t st = e->timing ? ev(mv, 0) : e->vstart;
+      launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, mv, st, ev(mv, 1));
       HIPCHK(e, hipStreamWaitEvent(e->vstream, st, 0));
-      for (int v : {0, 1, 2, 4})
-        launch_round(e->d, e->cur, e->dcur, pr, e->vstream, e->nt, v, ev(v, 0), ev(v, 1));
+      for (int x = 0; x < nside; ++x)
+        launch_round(e->d, e->cur, e->dcur, pr, e->vstream, e->nt, sides[x], ev(sides[x], 0), ev(sides[x], 1));
       HIPCHK(e, hipEventRecord(e->vjoin, e->vstream));
       HIPCHK(e, hipStreamWaitEvent(e->stream, e->vjoin, 0));
     } else {  // lean 16-bit input, storm
@@ -1999,7 +2014,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     for (int32_t q = 0; q < done; ++q) {
       float ms = 0.f;  // the variant that ran
       if (tsel) {
-        const int b = vl[q] == 3 ? 12 * q + 6 : 12 * q + 10;
+        const int b = vl[q] == mvlog[q] ? 12 * q + 6 : 12 * q + 10;
         HIPCHK(e, hipEventElapsedTime(&ms, e->evs[b], e->evs[b + 1]));
       }
       for (int v = 0; !tsel && v < (e->c8 ? 5 : 2); ++v) {
