@@ -166,6 +166,9 @@
 #define GH_NIB_SPLIT 0          // nibble path, 16-cell lanes, 256-member tiles: the sender gathers split over
                                 // lane halves (round.hip round_block_nib SPL; parity green, measured slower)
 #endif
+#ifndef GH_NIB_SPLIT_ROWS
+#define GH_NIB_SPLIT_ROWS 0     // the same for the row layout's nibble path (IN 4)
+#endif
 #ifndef GH_NIB_RS
 #define GH_NIB_RS 1             // nibble path: row steps per iteration (1 measured best at CPL 8 and 16)
 #endif

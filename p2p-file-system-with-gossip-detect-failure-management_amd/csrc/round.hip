@@ -995,7 +995,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
   static_assert(W == 2 || W == 4, "nibble path: 16 or 32 cells per lane (one or two lane jobs of 16 cells)");
   static_assert(!DMA || (!ROWS && CPL == 16 && TW == 256 && RB % 32 == 0), "LDS-DMA staging: 16-cell lanes, 256-member tiles");
   constexpr int RSD = DMA ? 2 : RS;  // row steps per iteration (DMA: a wave's 8 consecutive rows)
-  constexpr bool SPL = GH_NIB_SPLIT && !DMA && CPL == 16 && TW == 256;
+  constexpr bool SPL = (ROWS ? GH_NIB_SPLIT_ROWS : GH_NIB_SPLIT) && !DMA && CPL == 16 && TW == 256;
   // per wave: own lag 1 KiB, age 1 KiB, the 4 gather pieces (sender slot q
   // of the 8 rows) 1 KiB each
   __shared__ __attribute__((aligned(16))) uint32_t s_dma[DMA ? 4 * 1536 : 1];
