@@ -126,6 +126,7 @@ struct Engine {
   // events around them, and the device logs which variant ran (vlog).
   // tmode 0: every variant launch carries its own events.
   int tmode = 1;
+  int side_order = 0;  // GH_SIDE_ORDER=1: the side stream's idle variants as IN 1, IN 3, storm, IN 6 (A/B)
   int32_t* vlog = nullptr;
   int64_t vlog_cap = 0;
   // |D| of the last round as read at the end of gh_step (one engine; -1
@@ -1076,6 +1077,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   e->c8 = e->plane && e->tpw == 1 && tw >= 64;
   if (const char* v = std::getenv("GH_SIDE")) e->side = std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("GH_TMODE")) e->tmode = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_SIDE_ORDER")) e->side_order = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_C8")) e->c8 = e->c8 && std::atoi(v) != 0;
   if (cfg->shard_layout != GH_LAYOUT_COLUMNS && cfg->shard_layout != GH_LAYOUT_ROWS) {
     delete e;
@@ -1894,7 +1896,12 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     const int mv = rmv_main ? 4 : 3;
     if (e->timing && tsel) mvlog[q] = (int8_t)mv;
     const int nside = rmv_main ? 3 : 4;
-    const int sides[4] = {0, 1, 2, 4};  // the first nside of them
+    // the idle variants, the first nside of them (side stream: the first one
+    // is dispatched between the nibble path's workgroups, the rest after it)
+    int sides[4] = {0, 1, 2, 4};
+    if (e->side_order) {
+      sides[0] = 2, sides[1] = 0, sides[2] = 1;
+    }
     auto ev = [&](int v, int end) -> hipEvent_t {
       if (!e->timing) return nullptr;
       if (!tsel) return e->evs[12 * q + 2 * v + end];
