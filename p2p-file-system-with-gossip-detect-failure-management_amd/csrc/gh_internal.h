@@ -188,7 +188,8 @@
 #define GH_NIB_GAT_AUX 0
 #endif
 #ifndef GH_NIB_ST_AUX
-#define GH_NIB_ST_AUX 2
+#define GH_NIB_ST_AUX 18  // sc1 | nt: the next round's lines leave the XCD's L2 instead of displacing this
+                          // round's sender lines (2, nt, keeps them: 2.08 against 2.04 ms, profiles/r05_s32_*)
 #endif
 #ifndef GH_JOB_WAVES
 #define GH_JOB_WAVES 4          // lane-job kernel: min waves per SIMD it is compiled for (A/B: 4 beats 3 and 5)
