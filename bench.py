@@ -90,6 +90,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="timed CPU rounds per rate (at least 1 round)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = nproc (OMP_NUM_THREADS, else the CPU count)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the reference-constant / ring / C2 legs")
+    ap.add_argument("--c4", action="store_true", help="world > 1: add the N=262,144 column-layout leg (on by "
+                    "default at 8 GPUs)")
     ap.add_argument("--files", type=int, default=1 << 20,
                     help="placement leg (SURVEY.md §8d C5 files, after the timed rounds; 0 = skip)")
     return ap.parse_args()
@@ -425,6 +427,125 @@ def election_leg(gs, eng, n, t_fail):
     return out
 
 
+def make_engine(gs, cfg, rank, world, dist):
+    """One engine: the whole cluster (world 1) or rank `rank`'s shard of it
+    over RCCL, the unique id broadcast from rank 0 over the gloo group."""
+    if world > 1:
+        box = [gs.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        return gs.Engine(cfg, rank=rank, world=world, transport=gs.GH_COMM_RCCL, comm_id=box[0])
+    return gs.Engine(cfg)
+
+
+def rank_bytes(n, world, layout, ncols, tier4, plane, k):
+    """Algorithmic bytes of one k_round launch on this rank: compulsory (each
+    cell of the rank's rows x columns read once and written once: on the
+    4-bit tier a lag nibble -- the sender plane itself -- and an age nibble,
+    1 B in and 1 B out; on the 16-bit table 2 B in and out plus the 4-bit
+    plane out and in), round 2's 8-bit model, the k sender gathers and
+    SURVEY.md §8d's int32 model."""
+    nrows_r = -(-n // world) if layout == "rows" else n
+    if tier4:
+        b_table, b_plane = 2.0 * nrows_r * ncols, 0.0
+    else:
+        b_table = 4.0 * nrows_r * ncols
+        b_plane = 1.0 * nrows_r * ncols if plane else 0.0
+    return {"rows": nrows_r, "cols": ncols, "compulsory": b_table + b_plane, "table": b_table, "plane": b_plane,
+            "prev_model": 3.0 * nrows_r * ncols,
+            "gather": (0.5 if (tier4 or plane) else 2.0) * nrows_r * ncols * k,
+            "survey": 4.0 * nrows_r * ncols * (k + 4)}
+
+
+def rank_roofline(rank, b, kern_ms, launches):
+    """This rank's k_round: mean launch time (HIP events on its stream) and
+    compulsory bytes / that time against the HBM peak."""
+    avg_s = (kern_ms / 1e3) / max(launches, 1)
+    ach = b["compulsory"] / avg_s / 1e9 if avg_s > 0 else 0.0
+    return {"rank": rank, "rows": b["rows"], "cols": b["cols"], "avg_launch_ms": avg_s * 1e3, "launches": launches,
+            "bytes_per_launch": b["compulsory"], "achieved": ach, "frac": ach / HBM_PEAK_GBS}
+
+
+def gather_ranks(dist, obj):
+    if dist is None:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def max_over_ranks(dist, x):
+    if dist is None:
+        return x
+    return max(gather_ranks(dist, x))
+
+
+def timed_rounds(eng, dist, warmup, steps):
+    """init_full, `warmup` untimed rounds, then `steps` rounds bracketed by a
+    barrier and a device sync on both sides; returns (max-over-ranks seconds,
+    stats, k_round ms, launches) with the engine's launch timing on."""
+    eng.init_full(2, 0, 0)
+    if warmup:
+        eng.step(warmup)
+    eng.set_timing(True)
+    if dist is not None:
+        dist.barrier()
+    eng.sync()
+    t0 = time.perf_counter()
+    st = eng.step(steps)  # blocks until the device is done
+    eng.sync()
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    kern_ms, launches = eng.read_timing()
+    eng.set_timing(False)
+    return max_over_ranks(dist, t1 - t0), st, kern_ms, launches
+
+
+def shard_leg(gs, args, rank, world, local, dist, n, layout, warmup, steps):
+    """One more sharded configuration at world > 1 (outside the main timed
+    region): rounds/s over all ranks, each rank's k_round roofline and, for
+    the row layout, its ghost-row exchange (gh_exchange_info: the bytes the
+    last round's ncclAllToAllv moved out of and into this rank, over xGMI on
+    one node)."""
+    cfg = gs.default_config(n, fanout=args.fanout, seed=args.seed, device=local, t_fail=args.t_fail,
+                            t_cleanup=args.t_fail, max_files=0, peer_mode=gs.GH_PEER_PULL,
+                            shard_layout=gs.GH_LAYOUT_ROWS if layout == "rows" else gs.GH_LAYOUT_COLUMNS)
+    eng = make_engine(gs, cfg, rank, world, dist)
+    try:
+        ncols = eng.shard_info()[3]
+        b = rank_bytes(n, world, layout, ncols, eng.tier_info()[0], eng.plane_info()[0], args.fanout)
+        el, st, kern_ms, launches = timed_rounds(eng, dist, warmup, steps)
+        mine = rank_roofline(rank, b, kern_ms, launches)
+        if layout == "rows":
+            x = eng.exchange_info()
+            mine["exchange"] = x
+            mine["xgmi_in_gbs"] = x["bytes_in"] / (el / steps) / 1e9
+        mem = eng.memory_info()["device_bytes"]
+    finally:
+        eng.close()
+    per_rank = gather_ranks(dist, mine)
+    return {"workload": f"N={n}, k={args.fanout} Philox pull, T_fail=T_cleanup={args.t_fail}, full start, "
+                        f"{warmup} warm-up rounds, {steps} timed rounds, {layout} layout over {world} GPUs",
+            "n_members": n, "layout": layout, "rounds_per_s": steps / el, "ms_per_step": el / steps * 1e3,
+            "detections": st["detections"], "table_bytes_per_rank": mem,
+            "roofline_per_rank": per_rank,
+            "frac_min": min(r["frac"] for r in per_rank), "frac_max": max(r["frac"] for r in per_rank)}
+
+
+def multi_gpu_legs(gs, args, rank, world, local, dist):
+    """world > 1: the other shard layout at the benched N (north_star's row
+    layout when the main line times columns), and on 8 GPUs BASELINE config
+    4's size, N=262,144, column layout (56 GB of tables per GPU)."""
+    out = {}
+    other = "rows" if args.layout == "columns" else "columns"
+    progress(f"multi-GPU leg: {other} layout, N={args.n}")
+    out[other] = shard_leg(gs, args, rank, world, local, dist, args.n, other, args.warmup, args.steps)
+    if world == 8 or args.c4:
+        progress("multi-GPU leg: config 4, N=262144, column layout")
+        out["c4_n262144"] = shard_leg(gs, args, rank, world, local, dist, 262144, "columns", 5, 10)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -443,42 +564,13 @@ def main():
         import torch.distributed as dist  # noqa: F811
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        box = [gs.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(box, src=0)
-        eng = gs.Engine(cfg, rank=rank, world=world, transport=gs.GH_COMM_RCCL, comm_id=box[0])
-    else:
-        eng = gs.Engine(cfg)
+    eng = make_engine(gs, cfg, rank, world, dist)
     _, _, _, ncols = eng.shard_info()
-    # cells this rank's round kernel covers: rows x columns (row layout: its
-    # rows, every column)
-    nrows_r = -(-n // world) if args.layout == "rows" else n
     plane = eng.plane_info()[0]
     tier4 = eng.tier_info()[0]  # steady-state cells: a lag nibble (the plane) + an age nibble (escapes: 16-bit)
     tile_w = int(os.environ.get("GH_TILE_W", "256" if plane else "64"))
-    eng.init_full(2, 0, 0)
-    if args.warmup:
-        eng.step(args.warmup)
-    eng.set_timing(True)
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    barrier()
-    eng.sync()
-    t0 = time.perf_counter()
-    st = eng.step(args.steps)  # blocks until the device is done
-    eng.sync()
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kern_ms, launches = eng.read_timing()
-    eng.set_timing(False)
+    b = rank_bytes(n, world, args.layout, ncols, tier4, plane, k)
+    elapsed, st, kern_ms, launches = timed_rounds(eng, dist, args.warmup, args.steps)
     exch = eng.exchange_info() if args.layout == "rows" else None
     plane_fb = eng.plane_info()[2]
     tier_last = eng.tier_info()
@@ -490,34 +582,34 @@ def main():
         placement["election"] = election_leg(gs, eng, n, args.t_fail)
     mem = eng.memory_info()
     eng.close()
-    secondary = secondary_legs(gs) if world == 1 and not args.no_secondary else None
+    per_rank = gather_ranks(dist, rank_roofline(rank, b, kern_ms, launches))
+    secondary = None
+    if not args.no_secondary:
+        secondary = secondary_legs(gs) if world == 1 else multi_gpu_legs(gs, args, rank, world, local, dist)
 
     if rank != 0:
         return
+    line = build_line(args, world, elapsed, st, b, kern_ms, launches, per_rank, tier4, plane, tile_w, exch, plane_fb,
+                      tier_last, tier_last_var, mem, secondary, placement)
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(n, k, args.seed, args.cpu_seconds, args.cpu_threads, args.t_fail)
+    print(json.dumps(line), flush=True)
+
+
+def build_line(args, world, elapsed, st, b, kern_ms, launches, per_rank, tier4, plane, tile_w, exch, plane_fb,
+               tier_last, tier_last_var, mem, secondary, placement):
+    """The one JSON line (rank 0): value = rounds / max-over-ranks seconds of
+    the timed region; roofline = rank 0's k_round (roofline_per_rank: every
+    rank's)."""
+    n, k = args.n, args.fanout
     value = args.steps / elapsed
-    # bytes of one k_round launch (this rank's columns)
-    # compulsory bytes of one launch: each table cell read once and written
-    # once -- the least the round's data structures move through HBM. On the
-    # 4-bit tier a cell is its lag nibble (the sender plane itself) and its
-    # age nibble: 1 B in, 1 B out. On the 16-bit table: 2 B in, 2 B out, and
-    # the sender plane (4 bits per cell) written once and read once.
-    if tier4:
-        b_table, b_plane = 2.0 * nrows_r * ncols, 0.0
-    else:
-        b_table = 4.0 * nrows_r * ncols
-        b_plane = 1.0 * nrows_r * ncols if plane else 0.0
-    b_compulsory = b_table + b_plane
-    b_prev_model = 3.0 * nrows_r * ncols  # round 2's 8-bit tier: 1-B cells in + out, the plane out + in
-    # the k sender segments per cell (L2 / Infinity Cache / HBM): 4-bit plane
-    # codes (the tier's lag nibbles, or the plane beside a 16-bit table), else
-    # the senders' 16-bit codes
-    b_gather = (0.5 if (tier4 or plane) else 2.0) * nrows_r * ncols * k
-    b_survey = 4.0 * nrows_r * ncols * (k + 4)  # SURVEY.md §8d (int32 hb + ts streams)
     encoding = "t4" if tier4 else "u16"
     traffic = pmc_traffic(n, k, world, args.warmup, plane, tile_w, encoding)
     tier_cur, tier_esc = tier_last[1], tier_last[2]
     avg_s = (kern_ms / 1e3) / max(launches, 1)
+    b_compulsory, b_prev_model, b_gather = b["compulsory"], b["prev_model"], b["gather"]
     achieved = b_compulsory / avg_s / 1e9
+    nrows_r, ncols = b["rows"], b["cols"]
     line = {
         "metric": "gossip rounds/sec at N=65,536 members (achieved HBM GB/s, % of peak)",
         "value": value,
@@ -560,12 +652,12 @@ def main():
                             "once; the lag nibbles are the sender plane the gathers read)" if tier4 else
                             "compulsory: " + ("5" if plane else "4") + "*N*ncols (2-byte cells read + written once"
                             + (", 4-bit sender plane written + read once" if plane else "") + ")"),
-            "table_bytes_per_launch": b_table, "plane_bytes_per_launch": b_plane,
+            "table_bytes_per_launch": b["table"], "plane_bytes_per_launch": b["plane"],
             "prev_model_bytes_per_launch": b_prev_model,
             "frac_prev_model": b_prev_model / avg_s / 1e9 / HBM_PEAK_GBS,
             "avg_launch_ms": avg_s * 1e3, "launches": launches,
             "gather_bytes_per_launch": b_gather, "gather_achieved": b_gather / avg_s / 1e9,
-            "survey_bytes_per_launch": b_survey,
+            "survey_bytes_per_launch": b["survey"],
             "frac_of_measured_copy_peak": achieved / HBM_MEASURED_GBS,
             # fabric-side bytes (FETCH_SIZE x2 + WRITE_SIZE; Infinity-Cache
             # hits included) over the same duration; traffic / compulsory =
@@ -583,12 +675,11 @@ def main():
                    "tier4_current": bool(tier_cur), "tier4_escaped_chunks_last_round": tier_esc,
                    "last_variant": {0: "lean_16bit_input", 1: "storm", 2: "lean_tier_input_16bit_rule",
                                     3: "nibble_path"}.get(tier_last_var, "?")},
+        "roofline_per_rank": per_rank,
         "secondary": secondary,
         "placement": placement,
     }
-    if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(n, k, args.seed, args.cpu_seconds, args.cpu_threads, args.t_fail)
-    print(json.dumps(line), flush=True)
+    return line
 
 
 if __name__ == "__main__":

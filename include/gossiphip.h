@@ -63,7 +63,9 @@ extern "C" {
  * :135) and lsm follow it. One engine or row shards (GH_LAYOUT_ROWS: every
  * shard keeps every row's list, the owners' changes are copied each round);
  * column shards refuse it (gh_create_sharded: GH_EINVAL). HBM +8*N*N bytes
- * per engine / shard (double-buffered [N][N] int32 lists). */
+ * per engine / shard (double-buffered [N][N] int32 lists); row shards also
+ * keep the list copy's scratch, grown to (G + 1) x 256 MiB at most (the
+ * changed lists travel in ranges of 2^26 / N rows). */
 #define GH_ORDER_ID 0
 #define GH_ORDER_APPEND 1
 /* Who receives a detector's REMOVE (SPEC D4). GH_REMOVE_LIST is the

@@ -997,8 +997,8 @@ void launch_list_import(const GhDev& d, int cur, int lb, int64_t row0, int64_t n
 void launch_ring_list(const GhDev& d, int cur, int dcur, const GhRound& p, int lin, int flags_known, hipStream_t s);
 void launch_quirk_list(const GhDev& d, int cur, int dcur, const GhRound& p, int lin, hipStream_t s);
 void launch_list_cand(const GhDev& d, int lin, int32_t master, hipStream_t s);
-void launch_list_pack(const GhDev& d, int g, int32_t* buf, int64_t cap, hipStream_t s);
-void launch_list_unpack(const GhDev& d, int g, const int32_t* buf, hipStream_t s);
+void launch_list_pack(const GhDev& d, int g, int32_t* buf, int64_t lo, int64_t hi, hipStream_t s);
+void launch_list_unpack(const GhDev& d, int g, const int32_t* buf, int64_t lo, int64_t hi, hipStream_t s);
 void launch_list_first(const GhDev& d, int lin, int32_t* out, hipStream_t s);
 // place.hip (rbits holds the master row [q=0] and, for repair, the observer row [q=1])
 void launch_candidates(const GhDev& d, int32_t nr, hipStream_t s);

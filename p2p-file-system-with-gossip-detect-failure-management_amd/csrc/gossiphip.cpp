@@ -774,9 +774,13 @@ int reset_shadows(Engine* e);
 
 // Row shards with list order: every shard keeps every row's list; the lists
 // of generation g this shard's owned rows changed (lchg) go to every other
-// shard. The host reads the changed rows' lengths (one sync), the shards
-// agree on the largest pack by an allgather of the sizes, then pack,
-// allgather the packs and unpack the others' into the replicas.
+// shard. The host reads the changed rows' lengths (one sync) and counts the
+// entries per range of R rows (R * ld <= 2^26 entries: the pack's int32
+// offsets cannot wrap and its scratch stays bounded, G x 256 MiB at most);
+// the shards allgather those counts, then for each range any shard changed:
+// pack, allgather the packs (sized by the largest), unpack the others' into
+// the replicas. An import or a join broadcast changes every row (~N^2 / G
+// entries per shard) and takes N / R ranges; a round changes a few rows.
 int list_sync(Engine* e, int g) {
   if (!e->d.lchg) return GH_OK;
   GhDev& d = e->d;
@@ -785,31 +789,36 @@ int list_sync(Engine* e, int g) {
   HIPCHK(e, hipMemcpyAsync(chg.data(), d.lchg, sizeof(int32_t) * e->n, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipMemcpyAsync(len.data(), d.llen[g], sizeof(int32_t) * e->n, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  int64_t ent = 0;
+  const int64_t R = std::max<int64_t>(1, ((int64_t)1 << 26) / std::max<int64_t>(e->ld, 1));
+  const int64_t nch = (e->n + R - 1) / R;
+  std::vector<int32_t> cnt(nch, 0);
   for (int64_t i = 0; i < e->n; ++i)
-    if (chg[i]) ent += len[i];
-  // every shard's entry count -> the pack size (the same on every shard)
-  int32_t* sz = e->gwcnt;  // (row layout scratch, >= 2 G int32)
-  const int32_t mine = (int32_t)std::min<int64_t>(ent, INT32_MAX);
-  HIPCHK(e, hipMemcpyAsync(sz + G, &mine, sizeof mine, hipMemcpyHostToDevice, e->stream));
-  COMMCHK(e, e->comm->allgather(sz + G, sz, sizeof(int32_t), e->stream));
-  std::vector<int32_t> all(G);
-  HIPCHK(e, hipMemcpyAsync(all.data(), sz, sizeof(int32_t) * G, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipStreamSynchronize(e->stream));
-  int64_t maxent = 0;
-  for (int32_t v : all) maxent = std::max<int64_t>(maxent, v);
-  const size_t words = 1 + 4 * (size_t)e->n + (size_t)maxent;
+    if (chg[i]) cnt[i / R] += len[i] + 1;  // entries + 1: a changed row with an empty list travels too (<= R (ld + 1))
   int rc;
-  if ((rc = gbuf_reserve(e, 2, words * sizeof(int32_t))) || (rc = gbuf_reserve(e, 3, words * sizeof(int32_t) * G)))
+  if ((rc = gbuf_reserve(e, 2, sizeof(int32_t) * nch)) || (rc = gbuf_reserve(e, 3, sizeof(int32_t) * nch * G)))
     return rc;
-  int32_t* sendb = static_cast<int32_t*>(e->gbuf[2]);
-  int32_t* recvb = static_cast<int32_t*>(e->gbuf[3]);
-  launch_list_pack(d, g, sendb, maxent, e->stream);
-  HIPCHK(e, hipGetLastError());
-  COMMCHK(e, e->comm->allgather(sendb, recvb, words * sizeof(int32_t), e->stream));
-  for (int r = 0; r < G; ++r)
-    if (r != e->rank && all[r] >= 0) launch_list_unpack(d, g, recvb + (size_t)r * words, e->stream);
-  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipMemcpyAsync(e->gbuf[2], cnt.data(), sizeof(int32_t) * nch, hipMemcpyHostToDevice, e->stream));
+  COMMCHK(e, e->comm->allgather(e->gbuf[2], e->gbuf[3], sizeof(int32_t) * nch, e->stream));
+  std::vector<int32_t> all((size_t)nch * G);
+  HIPCHK(e, hipMemcpyAsync(all.data(), e->gbuf[3], sizeof(int32_t) * nch * G, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  for (int64_t c = 0; c < nch; ++c) {
+    int64_t maxent = -1;
+    for (int r = 0; r < G; ++r) maxent = std::max<int64_t>(maxent, all[(size_t)r * nch + c]);
+    const int64_t lo = c * R, hi = std::min<int64_t>(lo + R, e->n);
+    if (maxent <= 0) continue;  // no shard changed a row of the range
+    const size_t words = 1 + 4 * (size_t)(hi - lo) + (size_t)maxent;  // (maxent bounds the entries)
+    if ((rc = gbuf_reserve(e, 2, words * sizeof(int32_t))) || (rc = gbuf_reserve(e, 3, words * sizeof(int32_t) * G)))
+      return rc;
+    int32_t* sendb = static_cast<int32_t*>(e->gbuf[2]);
+    int32_t* recvb = static_cast<int32_t*>(e->gbuf[3]);
+    launch_list_pack(d, g, sendb, lo, hi, e->stream);
+    HIPCHK(e, hipGetLastError());
+    COMMCHK(e, e->comm->allgather(sendb, recvb, words * sizeof(int32_t), e->stream));
+    for (int r = 0; r < G; ++r)
+      if (r != e->rank) launch_list_unpack(d, g, recvb + (size_t)r * words, lo, hi, e->stream);
+    HIPCHK(e, hipGetLastError());
+  }
   return GH_OK;
 }
 
@@ -1798,6 +1807,10 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
   int rc0;
   bool busy = false;
   if ((rc0 = check_lost(e)) || (rc0 = maybe_grow(e, &busy))) return rc0;
+  // |D| of the last call's final round, read at its end: taken here and
+  // cleared, so a call that returns early leaves no stale value behind
+  const int32_t last_nd = e->last_nd;
+  e->last_nd = -1;
   HIPCHK(e, hipMemsetAsync(e->d.stats, 0, sizeof(unsigned long long) * ST_COUNT, e->stream));
   if (e->timing && (int64_t)e->evs.size() < 12 * (int64_t)rounds) {
     while ((int64_t)e->evs.size() < 12 * (int64_t)rounds) {
@@ -1878,7 +1891,7 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     GhRound pr = p;
     pr.gpo = e->gpo;  // row layout: the ghosts carry only their plane so far
     pr.vslot = q;
-    pr.rmv_full = q == 0 && e->world == 1 && e->last_nd > 0;
+    pr.rmv_full = q == 0 && e->world == 1 && last_nd > 0;
     // the variants of k_round; the ones not selected return at once. With
     // timing on, a launch stamps its own start and end (events 12q + 2v,
     // 12q + 2v + 1 of variant v; hipExtLaunchKernel, no event packets between

@@ -521,19 +521,21 @@ __global__ __launch_bounds__(256) void k_list_first(GhDev d, int g, int32_t* out
   out[i] = d.llen[g][i] > 0 ? d.n - list_of(d, g, i)[0] : 0;
 }
 
-// Row shards: the lists of the rows this shard changed (lchg), packed for
-// the other shards: [count | rows | lens | selfs | offsets | entries] (n
-// int32 each for the per-row parts), entries of the rows back to back in row
-// order. One workgroup scans the rows in ascending order.
-__global__ __launch_bounds__(1024) void k_list_pack(GhDev d, int g, int32_t* buf, int64_t cap) {
-  __shared__ int s_w[16];
+// Row shards: the lists of the rows in [lo, hi) this shard changed (lchg),
+// packed for the other shards: [count | rows | lens | selfs | offsets |
+// entries] (R = hi - lo int32 each for the per-row parts), entries of the rows
+// back to back in row order. k_list_pack_index: one workgroup scans the
+// range's rows in ascending order and writes the header; k_list_pack_copy:
+// one workgroup per packed row copies its entries and clears its lchg.
+__global__ __launch_bounds__(1024) void k_list_pack_index(GhDev d, int g, int32_t* buf, int64_t lo, int64_t hi) {
+  __shared__ int s_w[16], s_c[16];
   __shared__ int64_t s_base, s_rows;
   if (threadIdx.x == 0) s_base = s_rows = 0;
   __syncthreads();
-  int32_t* rows = buf + 1;
-  for (int64_t b = 0; b < d.n; b += blockDim.x) {
+  const int64_t R = hi - lo;
+  for (int64_t b = lo; b < hi; b += blockDim.x) {
     const int64_t i = b + threadIdx.x;
-    const bool chg = i < d.n && d.lchg[i];
+    const bool chg = i < hi && d.lchg[i];
     const int len = chg ? d.llen[g][i] : 0;
     // block-wide exclusive prefix of chg (rows) and len (entries)
     const unsigned long long m = __ballot(chg);
@@ -544,33 +546,24 @@ __global__ __launch_bounds__(1024) void k_list_pack(GhDev d, int g, int32_t* buf
       if (lane >= o) lx += y;
     }
     if (lane == 63) s_w[w] = lx;
-    __syncthreads();
-    int woff = 0, wrow = 0;
-    for (int q = 0; q < w; ++q) woff += s_w[q];
-    __shared__ int s_c[16];
     if (lane == 0) s_c[w] = __popcll(m);
     __syncthreads();
-    for (int q = 0; q < w; ++q) wrow += s_c[q];
+    int64_t woff = 0;
+    int wrow = 0;
+    for (int q = 0; q < w; ++q) woff += s_w[q], wrow += s_c[q];
     const int64_t row_at = s_rows + wrow + __popcll(m & ((1ull << lane) - 1ull));
     const int64_t ent_at = s_base + woff + lx - len;
     if (chg) {
-      rows[row_at] = (int32_t)i;
-      const int64_t rb = (int64_t)row_at;
-      buf[1 + d.n + rb] = len;
-      buf[1 + 2 * d.n + rb] = d.lself[g][i];
-      buf[1 + 3 * d.n + rb] = (int32_t)ent_at;
-      const int32_t* src = d.lord[d.lsel[g][i]] + i * d.ld;
-      int32_t* dst = buf + 1 + 4 * (int64_t)d.n + ent_at;
-      if (ent_at + len <= cap) for (int q = 0; q < len; ++q) dst[q] = src[q];
-      d.lchg[i] = 0;
+      buf[1 + row_at] = (int32_t)i;
+      buf[1 + R + row_at] = len;
+      buf[1 + 2 * R + row_at] = d.lself[g][i];
+      buf[1 + 3 * R + row_at] = (int32_t)ent_at;  // (a range holds at most R * ld < 2^31 entries: list_sync)
     }
     __syncthreads();
     if (threadIdx.x == blockDim.x - 1) {
-      int tot = 0, tr = 0;
-      for (int q = 0; q < (int)(blockDim.x >> 6); ++q) {
-        tot += s_w[q];
-        tr += s_c[q];
-      }
+      int64_t tot = 0;
+      int tr = 0;
+      for (int q = 0; q < (int)(blockDim.x >> 6); ++q) tot += s_w[q], tr += s_c[q];
       s_base += tot;
       s_rows += tr;
     }
@@ -579,21 +572,34 @@ __global__ __launch_bounds__(1024) void k_list_pack(GhDev d, int g, int32_t* buf
   if (threadIdx.x == 0) buf[0] = (int32_t)s_rows;
 }
 
-// Another shard's packed lists (k_list_pack) into this shard's replicas of
-// generation g, in place (nothing reads the rows' earlier lists any more).
-__global__ __launch_bounds__(256) void k_list_unpack(GhDev d, int g, const int32_t* buf) {
+__global__ __launch_bounds__(256) void k_list_pack_copy(GhDev d, int g, int32_t* buf, int64_t R) {
   const int nr = buf[0];
-  const int32_t* rows = buf + 1;
-  const int32_t* ent = buf + 1 + 4 * (int64_t)d.n;
+  const int32_t* ent_hdr = buf + 1 + 3 * R;
+  int32_t* ent = buf + 1 + 4 * R;
   for (int r = blockIdx.x; r < nr; r += gridDim.x) {
-    const int64_t i = rows[r];
-    const int len = buf[1 + d.n + r];
-    const int64_t off = buf[1 + 3 * d.n + r];
+    const int64_t i = buf[1 + r];
+    const int len = buf[1 + R + r];
+    const int32_t* src = d.lord[d.lsel[g][i]] + i * d.ld;
+    int32_t* dst = ent + ent_hdr[r];
+    for (int q = threadIdx.x; q < len; q += blockDim.x) dst[q] = src[q];
+    if (threadIdx.x == 0) d.lchg[i] = 0;
+  }
+}
+
+// Another shard's packed lists into this shard's replicas of generation g, in
+// place (nothing reads the rows' earlier lists any more).
+__global__ __launch_bounds__(256) void k_list_unpack(GhDev d, int g, const int32_t* buf, int64_t R) {
+  const int nr = buf[0];
+  const int32_t* ent = buf + 1 + 4 * R;
+  for (int r = blockIdx.x; r < nr; r += gridDim.x) {
+    const int64_t i = buf[1 + r];
+    const int len = buf[1 + R + r];
+    const int64_t off = buf[1 + 3 * R + r];
     int32_t* dst = d.lord[d.lsel[g][i]] + i * d.ld;
     for (int q = threadIdx.x; q < len; q += blockDim.x) dst[q] = ent[off + q];
     if (threadIdx.x == 0) {
       d.llen[g][i] = len;
-      d.lself[g][i] = buf[1 + 2 * d.n + r];
+      d.lself[g][i] = buf[1 + 2 * R + r];
     }
   }
 }
@@ -634,14 +640,17 @@ void launch_list_cand(const GhDev& d, int lin, int32_t master, hipStream_t s) {
                      0, s, d, lin, master);
 }
 
-// Row shards: this shard's changed lists (lchg, cleared) packed into buf
-// (1 + 4 n + entries int32; cap entries), and another shard's pack into the
-// replicas.
-void launch_list_pack(const GhDev& d, int g, int32_t* buf, int64_t cap, hipStream_t s) {
-  hipLaunchKernelGGL(k_list_pack, dim3(1), dim3(1024), 0, s, d, g, buf, cap);
+// Row shards: this shard's changed lists of rows [lo, hi) (lchg, cleared)
+// packed into buf (1 + 4 (hi - lo) + entries int32), and another shard's pack
+// of the same range into the replicas.
+void launch_list_pack(const GhDev& d, int g, int32_t* buf, int64_t lo, int64_t hi, hipStream_t s) {
+  hipLaunchKernelGGL(k_list_pack_index, dim3(1), dim3(1024), 0, s, d, g, buf, lo, hi);
+  hipLaunchKernelGGL(k_list_pack_copy, dim3((unsigned)std::min<int64_t>(hi - lo, 4096)), dim3(256), 0, s, d, g, buf,
+                     hi - lo);
 }
-void launch_list_unpack(const GhDev& d, int g, const int32_t* buf, hipStream_t s) {
-  hipLaunchKernelGGL(k_list_unpack, dim3(256), dim3(256), 0, s, d, g, buf);
+void launch_list_unpack(const GhDev& d, int g, const int32_t* buf, int64_t lo, int64_t hi, hipStream_t s) {
+  hipLaunchKernelGGL(k_list_unpack, dim3((unsigned)std::min<int64_t>(hi - lo, 4096)), dim3(256), 0, s, d, g, buf,
+                     hi - lo);
 }
 
 void launch_list_first(const GhDev& d, int lin, int32_t* out, hipStream_t s) {

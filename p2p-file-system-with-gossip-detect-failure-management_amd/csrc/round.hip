@@ -1208,7 +1208,7 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       const int meta = s_meta[rs];
       const bool skip = ((meta >> 30) & 1) && tile_still;  // quiet row, bases still
       if (valid && skip && lc == 0) atomicAdd(&s_quiet, 1);
-      const int cntv = (meta >> 2) & 0xFFFF;
+      const int cntv = (meta >> 2) & 0x0FFFFFFF;  // bits 2..29: a ring receiver can have N - 1 senders
       alu[u] = (meta & 1) && valid && !skip;
       oku[u] = ((meta >> 1) & 1) && cntv <= KB;  // active (not a guard row), at most KB senders
       iu[u] = i;
@@ -1522,7 +1522,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     for (int t = tid; t < RB * KB; t += 256) {
       const int row = t / KB, q = t - row * KB;
       const int i = (int)d.row0 + rb * RB + row;
-      if (q < ((s_meta[row] >> 2) & 0xFFFF)) {
+      if (q < ((s_meta[row] >> 2) & 0x0FFFFFFF)) {
         const int sv = d.inbox[gh_in_beg(d, pull, p.k, i) + q];
         s_inb[t] = sv;
         if (d.rowlay) s_isl[t] = d.rslot[sv];
@@ -1666,7 +1666,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
     if (valid && skip && lc == 0) atomicAdd(&s_quiet, 1);
     if (__ballot(valid && !skip) == 0) continue;
     const bool al = (meta & 1) && valid && !skip;
-    const int cntv = (meta >> 2) & 0xFFFF;
+    const int cntv = (meta >> 2) & 0x0FFFFFFF;  // bits 2..29: a ring receiver can have N - 1 senders
     const uint32_t ob = islot * (TW * 2) + lb;  // own segment, bytes from the tile base
 
     // own segment and the senders' snapshots, issued together: plane words
@@ -2126,7 +2126,9 @@ __global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM 
     if (want == 2 && p.nib_dma && TW == 256 && GH_NIB_CPL == 16) want = 5;  // LDS-DMA staging (GH_NIB_DMA)
     // a REMOVE pending (|D_{r-1}| > 0): the instantiation that takes it on the
     // nibble path (GH_NIB_RMV=2: in every round, A/B)
-    if (want == 2 && (p.nib_rmv == 2 || (p.nib_rmv && d.cntg[p.n] > 0))) want = 6;
+    // (p.rmv_full: the host launched IN 6 in place of IN 2, so IN 6 must run
+    // whatever the device's count says: the round's nibble path is never skipped)
+    if (want == 2 && (p.rmv_full || p.nib_rmv == 2 || (p.nib_rmv && d.cntg[p.n] > 0))) want = 6;
     if (want != IN) return;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {

@@ -41,51 +41,79 @@ def gs():
     return gossipsim
 
 
-def compare_blocks(eng, orc, r):
+def compare_blocks(engs, orc, r, n=N):
+    """every engine's full hb / ts tables and alive vector against the
+    oracle's, row block by row block (the oracle block exported once)"""
     t0 = time.perf_counter()
-    for row0 in range(0, N, BLOCK):
-        h1, t1, a1 = eng.export_state(row0, BLOCK)
-        h2, t2, a2 = orc.export_state(row0, BLOCK)
-        np.testing.assert_array_equal(a1, a2, err_msg=f"alive r={r} rows {row0}+")
-        if not np.array_equal(h1, h2):
-            bad = np.argwhere(h1 != h2)
-            i, c = bad[0]
-            raise AssertionError(f"hb r={r}: {len(bad)} cells differ in rows {row0}+, first ({row0 + i}, {c}) "
-                                 f"gpu={h1[i, c]} cpu={h2[i, c]}")
-        if not np.array_equal(t1, t2):
-            bad = np.argwhere(t1 != t2)
-            i, c = bad[0]
-            raise AssertionError(f"ts r={r}: {len(bad)} cells differ in rows {row0}+, first ({row0 + i}, {c}) "
-                                 f"gpu={t1[i, c]} cpu={t2[i, c]} hb={h2[i, c]}")
-    print(f"  r={r}: full tables equal ({time.perf_counter() - t0:.1f} s)", flush=True)
+    for row0 in range(0, n, BLOCK):
+        nb = min(BLOCK, n - row0)
+        h2, t2, a2 = orc.export_state(row0, nb)
+        for name, eng in engs:
+            if hasattr(eng, "engines"):  # a ShardGroup: every rank assembles the same rows; rank 0's copy
+                h1, t1, a1 = eng.run("export_state", row0, nb)[0]
+            else:
+                h1, t1, a1 = eng.export_state(row0, nb)
+            np.testing.assert_array_equal(a1, a2, err_msg=f"{name}: alive r={r} rows {row0}+")
+            if not np.array_equal(h1, h2):
+                bad = np.argwhere(h1 != h2)
+                i, c = bad[0]
+                raise AssertionError(f"{name}: hb r={r}: {len(bad)} cells differ in rows {row0}+, first "
+                                     f"({row0 + i}, {c}) gpu={h1[i, c]} cpu={h2[i, c]}")
+            if not np.array_equal(t1, t2):
+                bad = np.argwhere(t1 != t2)
+                i, c = bad[0]
+                raise AssertionError(f"{name}: ts r={r}: {len(bad)} cells differ in rows {row0}+, first "
+                                     f"({row0 + i}, {c}) gpu={t1[i, c]} cpu={t2[i, c]} hb={h2[i, c]}")
+    print(f"  r={r}: full tables equal, {'/'.join(nm for nm, _ in engs)} ({time.perf_counter() - t0:.1f} s)",
+          flush=True)
+
+
+LAYOUT_NAMES = {(1, 0): "single", (8, 0): "columns_g8", (8, 1): "rows_g8"}
 
 
 def run(gs, om, t_fail, rounds, full_at, expect, sched=None, per_round=None, remove_mode=0, world=1, layout=0,
-        extra=None, after_round=None):
+        extra=None, after_round=None, lockstep=(), full_all=()):
+    """Step one engine (or G in-process shards of layout `layout`) and
+    tablesim round by round from the full-membership start. `lockstep` adds
+    more (world, layout) groups stepped beside it against the SAME oracle run
+    (one 48 GiB tablesim pass checks every layout); per_round / after_round
+    see the first engine."""
     cfg = dict(fanout=4, seed=0x5EED0003, t_fail=t_fail, t_cleanup=t_fail, remove_mode=remove_mode, **(extra or {}))
-    if world > 1:  # G in-process shards of one cluster on this GPU (GH_COMM_LOCAL)
-        eng = gs.ShardGroup(gs.default_config(N, shard_layout=layout, **cfg), world)
-    else:
-        eng = gs.Engine(gs.default_config(N, **cfg))
-    orc = om.Oracle(om.default_config(N, **cfg), threads=THREADS)
+    engs = []
+    orc = None
     try:
-        eng.init_full(2, 0, 0)
+        for w, lay in ((world, layout),) + tuple(lockstep):
+            if w > 1:  # G in-process shards of one cluster on this GPU (GH_COMM_LOCAL)
+                e = gs.ShardGroup(gs.default_config(N, shard_layout=lay, **cfg), w)
+            else:
+                e = gs.Engine(gs.default_config(N, **cfg))
+            engs.append((LAYOUT_NAMES.get((w, lay), f"g{w}l{lay}"), e))
+        eng = engs[0][1]
+        orc = om.Oracle(om.default_config(N, **cfg), threads=THREADS)
+        for _, e in engs:
+            e.init_full(2, 0, 0)
         orc.init_full(2, 0, 0)
         seen = {"detections": 0, "storm": False, "variants": {}, "first_detection": None}
         pending_full = set(full_at)
         for r in range(1, rounds + 1):
             if sched and r in sched:
-                eng.apply_events(sched[r])
+                for _, e in engs:
+                    e.apply_events(sched[r])
                 orc.apply_events(sched[r])
             t0 = time.perf_counter()
             s2 = orc.step(1)
             t1 = time.perf_counter()
-            s1 = eng.step(1)
-            t2 = time.perf_counter()
-            print(f"  r={r}: oracle {t1 - t0:.1f} s, gpu {1e3 * (t2 - t1):.1f} ms, {s2}", flush=True)
-            assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
-            np.testing.assert_array_equal(eng.read_failed(), orc.read_failed(), err_msg=f"failed r={r}")
-            np.testing.assert_array_equal(eng.read_detectors(), orc.read_detectors(), err_msg=f"detectors r={r}")
+            ms = []
+            for name, e in engs:
+                ta = time.perf_counter()
+                s1 = e.step(1)
+                ms.append(f"{name} {1e3 * (time.perf_counter() - ta):.1f} ms")
+                assert s1 == s2, f"{name} round {r}: gpu {s1} != cpu {s2}"
+                np.testing.assert_array_equal(e.read_failed(), orc.read_failed(), err_msg=f"{name}: failed r={r}")
+                np.testing.assert_array_equal(e.read_detectors(), orc.read_detectors(),
+                                              err_msg=f"{name}: detectors r={r}")
+            s1 = s2
+            print(f"  r={r}: oracle {t1 - t0:.1f} s, gpu {', '.join(ms)}, {s2}", flush=True)
             seen["detections"] += s1["detections"]
             if world == 1:  # (per-shard diagnostics differ between shards)
                 seen["storm"] |= eng.encoding_info(full=True)[2] == 1
@@ -98,13 +126,20 @@ def run(gs, om, t_fail, rounds, full_at, expect, sched=None, per_round=None, rem
             if s1["detections"] and seen["first_detection"] is None:
                 seen["first_detection"] = r
                 pending_full |= {r, r + 1}  # the detection round and the REMOVE round after it
+                if lockstep:
+                    full_all = set(full_all) | {r, r + 1}
             if r in pending_full:
-                compare_blocks(eng, orc, r)
+                # the lockstep layouts' full tables where the crash acts (the
+                # detection round, the REMOVE round, the last round); their
+                # counters, failed sets and detectors every round
+                compare_blocks(engs if (r in full_all or not full_all) else engs[:1], orc, r)
         print(f"  variants (round counts by gh_tier_info variant): {seen['variants']}", flush=True)
         expect(seen)
     finally:
-        eng.close()
-        orc.close()
+        for _, e in engs:
+            e.close()
+        if orc is not None:
+            orc.close()
 
 
 def byte_path_from(r0, r_var=None):
@@ -140,8 +175,14 @@ def test_c3_fullsize_steady_state(gs, oracle_mod):
 def test_c3_fullsize_crash_1pct(gs, oracle_mod):
     """1% crash in the bench's workload: 655 members (Philox, seed
     0x5EED0003, tag CRASH) stop at r=8; run through their detection and the
-    REMOVE wave, full tables equal at r=12, the detection round, the round
-    after it and the last round."""
+    REMOVE wave. Three layouts in lockstep against the one tablesim run: one
+    engine, north_star's 8 row shards (each owns 8,192 observer rows; the
+    other shards' sender plane rows arrive by alltoallv into its ghost table)
+    and 8 column shards (O(N) exchanges), all on this GPU through the
+    in-process transport (~150 GB of HBM). Counters, failed sets and
+    detectors of all three every round; full tables of all three at the
+    detection round, the round after it and the last round, of the engine
+    also at r=12."""
     from scenarios import crash_ids
     crashed = crash_ids(N, 0.01, 0x5EED0003)
     assert len(crashed) == 655
@@ -160,7 +201,8 @@ def test_c3_fullsize_crash_1pct(gs, oracle_mod):
             jobs, _ = eng.job_info()
             assert jobs * 100 <= N * N // 16, (r, jobs)
 
-    run(gs, oracle_mod, 16, 32, {12, 32}, expect, sched=sched, per_round=fast)
+    run(gs, oracle_mod, 16, 32, {12, 32}, expect, sched=sched, per_round=fast, lockstep=((8, 1), (8, 0)),
+        full_all={32})
 
 
 @pytest.mark.gpu_fullsize
@@ -197,24 +239,6 @@ def crash_sched(gs):
 
 def expect_detection(s):
     assert s["detections"] > 0 and s["first_detection"] is not None, s
-
-
-@pytest.mark.gpu_fullsize
-def test_c3_fullsize_rows_g8(gs, oracle_mod):
-    """North_star's layout at the largest size one MI355X holds: 8 row shards
-    (each owns 8,192 observer rows; the senders' plane rows of other shards
-    arrive by alltoallv into its ghost table, the want lists built on the
-    device), N=65,536, k=4, T_fail=16, the 1% crash at r=8, 25 rounds: full
-    tables at r=6, 25, the detection round and the one after."""
-    run(gs, oracle_mod, 16, 25, {6, 25}, expect_detection, sched=crash_sched(gs), world=8, layout=1)
-
-
-@pytest.mark.gpu_fullsize
-def test_c3_fullsize_columns_g8(gs, oracle_mod):
-    """The default multi-GPU layout at full size: 8 column shards (each holds
-    every row of 8,192 member columns, O(N) exchanges), the same workload
-    against tablesim (not against one engine)."""
-    run(gs, oracle_mod, 16, 25, {6, 25}, expect_detection, sched=crash_sched(gs), world=8, layout=0)
 
 
 @pytest.mark.gpu_fullsize
@@ -298,3 +322,135 @@ def test_c3_fullsize_reference_timeouts_remove_list_timed(gs):
     finally:
         lit.close()
         d4.close()
+
+
+# ---- beyond N = 65,536 -------------------------------------------------------
+# Every other test stays at N <= 65,536. These two run what only larger
+# clusters reach: ring receivers with more than 65,535 senders, and a single
+# engine plus 8 column shards at N = 131,072 (config 4's per-GPU column count
+# is 32,768 of 262,144 rows; this is the largest N one MI355X holds twice).
+
+
+def _mix(i, c):
+    """a fixed spread of heartbeats 2..18 per (row, member) cell"""
+    h = (i.astype(np.uint32) * np.uint32(0x9E3779B1)) ^ (c.astype(np.uint32) * np.uint32(0x85EBCA77))
+    h ^= h >> np.uint32(15)
+    return (2 + (h % np.uint32(17))).astype(np.int32)
+
+
+def test_ring_receiver_65537_senders(gs, oracle_mod):
+    """Ring mode at N = 65,600 with rows 1..65,537 holding every member but
+    themselves: a sender whose own cell is absent sends to list[len-2],
+    list[0] and list[1] (self index -1 in slave/slave.go:515-524), so member
+    0 receives from 65,537 senders, member 1 from 65,536 and member 65,598
+    from 65,537. The kernels pack a receiver's sender count into the row
+    record (round.hip nmeta / s_meta, bits 2..29); a 16-bit unpack had read
+    these counts as 1, 0 and 1, merged at most one sender and skipped
+    k_round_slow. Two rounds against tablesim: counters every round, the
+    many-sender rows at round 1, the full tables at round 2."""
+    n = 65600
+    nabs = 65537  # rows 1..nabs have their own cell absent
+    cfg = dict(fanout=4, seed=0x5EED0007, t_fail=16, t_cleanup=16, peer_mode=gs.GH_PEER_RING)
+    eng = gs.Engine(gs.default_config(n, **cfg))
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg), threads=THREADS)
+    try:
+        cols = np.arange(n, dtype=np.int64)
+        alive = np.ones(BLOCK, np.uint8)
+        for row0 in range(0, n, BLOCK):
+            nb = min(BLOCK, n - row0)
+            rows = np.arange(row0, row0 + nb, dtype=np.int64)
+            hb = _mix(rows[:, None], cols[None, :])
+            hb[rows == 0, :] = 2  # the receiver starts low: every sender's view beats it
+            own = (rows >= 1) & (rows <= nabs)
+            hb[np.nonzero(own)[0], rows[own]] = -1
+            ts = np.zeros_like(hb)
+            eng.import_state(hb, ts, alive[:nb], 0, row0)
+            orc.import_state(hb, ts, alive[:nb], 0, row0)
+        print("  imported", flush=True)
+        for r in (1, 2):
+            t0 = time.perf_counter()
+            s2 = orc.step(1)
+            t1 = time.perf_counter()
+            s1 = eng.step(1)
+            print(f"  r={r}: oracle {t1 - t0:.1f} s, gpu {1e3 * (time.perf_counter() - t1):.1f} ms, {s2}", flush=True)
+            assert s1 == s2, f"round {r}: gpu {s1} != cpu {s2}"
+            np.testing.assert_array_equal(eng.read_failed(), orc.read_failed())
+            if r == 1:
+                for i in (0, 1, 2, n - 2, n - 1):
+                    a, b = eng.export_state(i, 1), orc.export_state(i, 1)
+                    for x, y in zip(a, b):
+                        np.testing.assert_array_equal(x, y, err_msg=f"row {i} r=1")
+                h0 = orc.export_state(0, 1)[0][0]
+                # the max over 65,537 senders' views: 18 nearly everywhere (one sender: ~10 on average)
+                assert (h0 == 18).mean() > 0.99, np.bincount(h0[h0 >= 0])
+        compare_blocks([("single", eng)], orc, 2, n=n)
+    finally:
+        eng.close()
+        orc.close()
+
+
+def test_n131072_single_vs_columns_g8(gs):
+    """N = 131,072, k = 4 pull, T_fail = 16: one engine (~130 GB) and 8
+    in-process column shards of the same cluster (~130 GB) on this GPU in
+    lockstep -- the sizes where a (row, 128-B line) offset no longer fits 31
+    bits in a (row x ld / 8) word index. Properties of any size (no failures:
+    every member stays everywhere, the own heartbeat advances one per round,
+    no view runs ahead of its owner, the epidemic reaches every cell), then a
+    1% crash detected everywhere; the shards' counters, failed sets and
+    detectors equal the engine's every round, sampled rows bit for bit."""
+    from scenarios import crash_ids
+    n, rounds = 131072, 12
+    cfg = dict(fanout=4, seed=0x5EED0004, t_fail=16, t_cleanup=16)
+    one = gs.Engine(gs.default_config(n, **cfg))
+    grp = None
+    try:
+        grp = gs.ShardGroup(gs.default_config(n, shard_layout=0, **cfg), 8)
+        sample = (0, 1, 4095, 65535, 65536, 99999, n - 1)
+
+        def same_rows(r):
+            for i in sample:
+                a, b = one.export_state(i, 1), grp.export_state(i, 1)
+                for x, y in zip(a, b):
+                    np.testing.assert_array_equal(x, y, err_msg=f"row {i} r={r}")
+
+        one.init_full(2, 0, 0)
+        grp.init_full(2, 0, 0)
+        merged = 0
+        for r in range(1, rounds + 1):
+            t0 = time.perf_counter()
+            s1 = one.step(1)
+            t1 = time.perf_counter()
+            s2 = grp.step(1)
+            print(f"  r={r}: engine {1e3 * (t1 - t0):.1f} ms, 8 shards {1e3 * (time.perf_counter() - t1):.1f} ms, "
+                  f"{s1}", flush=True)
+            assert s1 == s2, (r, s1, s2)
+            assert s1["detections"] == 0 and s1["active_rows"] == n
+            merged += s1["merged_cells"]
+        assert merged > n * n  # the epidemic has reached every cell
+        assert one.tier_info(full=True)[3] == 3  # the nibble path at this size
+        same_rows(rounds)
+        for i in sample:
+            hb, ts, _ = one.export_state(i, 1)
+            assert hb[0, i] == 2 + rounds
+            assert (hb[0] >= 2).all() and (hb[0] <= 2 + rounds).all()
+            assert (ts[0] <= rounds).all()
+        crashed = crash_ids(n, 0.01, 0x5EED0004)
+        ev = [(gs.GH_EV_CRASH, int(c)) for c in crashed]
+        one.apply_events(ev)
+        grp.apply_events(ev)
+        seen = set()
+        for r in range(rounds + 1, rounds + 41):
+            s1, s2 = one.step(1), grp.step(1)
+            assert s1 == s2, (r, s1, s2)
+            bm = one.read_failed()
+            np.testing.assert_array_equal(bm, grp.read_failed(), err_msg=f"failed r={r}")
+            np.testing.assert_array_equal(one.read_detectors(), grp.read_detectors(), err_msg=f"detectors r={r}")
+            seen |= {int(c) for c in crashed if bm[c >> 5] >> (c & 31) & 1}
+            if s1["detections"]:
+                print(f"  r={r}: {s1}", flush=True)
+        assert seen == {int(c) for c in crashed}
+        same_rows(rounds + 40)
+    finally:
+        if grp is not None:
+            grp.close()
+        one.close()

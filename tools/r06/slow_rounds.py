@@ -1,0 +1,45 @@
+"""The 1% crash of the bench's workload (N=65,536, k=4 pull, T_fail =
+T_cleanup = 16, 655 members crash at r=8) with one gh_step call per round,
+printing per round the variant, lane jobs, detections and wall time; run it
+under rocprofv3 --kernel-trace and split the trace per round with
+tools/r06/trace_rounds.py to see which kernels make a round slow.
+  python tools/r06/slow_rounds.py MODE [rounds]
+MODE: canonical | quirk (detect_mode 1, slave/slave.go:464-477) |
+      remove_list (GH_REMOVE_LIST) | rows8 / cols8 (8 in-process shards)"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..",
+                                "p2p-file-system-with-gossip-detect-failure-management_amd"))
+import gossipsim as gs  # noqa: E402
+from gossipsim.scenario import crash_ids  # noqa: E402
+
+mode = sys.argv[1]
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 28
+n = 65536
+cfg = dict(fanout=4, seed=0x5EED0003, t_fail=16, t_cleanup=16)
+if mode == "quirk":
+    cfg["detect_mode"] = gs.GH_DETECT_QUIRK
+if mode == "remove_list":
+    cfg["remove_mode"] = gs.GH_REMOVE_LIST
+if mode in ("rows8", "cols8"):
+    eng = gs.ShardGroup(gs.default_config(n, shard_layout=1 if mode == "rows8" else 0, **cfg), 8)
+else:
+    eng = gs.Engine(gs.default_config(n, **cfg))
+eng.init_full(2, 0, 0)
+crashed = crash_ids(n, 0.01, 0x5EED0003)
+for r in range(1, rounds + 1):
+    if r == 8:
+        eng.apply_events([(gs.GH_EV_CRASH, int(c)) for c in crashed])
+    t0 = time.perf_counter()
+    st = eng.step(1)
+    wall = (time.perf_counter() - t0) * 1e3
+    rec = {"round": r, "wall_ms": round(wall, 3), "detections": st["detections"], "tombstoned": st["tombstoned"],
+           "released": st["released"]}
+    if mode not in ("rows8", "cols8"):
+        rec.update(variant=eng.tier_info(full=True)[3], lane_jobs=eng.job_info()[0],
+                   slow=eng.encoding_info(full=True)[1])
+    print(json.dumps(rec), flush=True)
+eng.close()
