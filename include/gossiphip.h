@@ -332,6 +332,12 @@ int gh_exchange_info(void* h, int64_t* ghost_rows, int64_t* bytes_out, int64_t* 
  * slots in use / per buffer, and stopped rows in the frozen store. Any
  * output may be NULL. Diagnostic; no reference counterpart. */
 int gh_memory_info(void* h, int64_t* device_bytes, int64_t* wide_used, int64_t* wide_cap, int64_t* frozen_rows);
+/* The file table of this engine / shard (placement is per file,
+ * master/master.go:74-150): sharded by file ID, file f on shard f % G at slot
+ * f / G, so *slots = ceil(max_files / G) files' replica lists, versions and
+ * timestamps; *shards = G (1 for one engine); *held = the files put and not
+ * deleted in this shard's slots. Any output may be NULL. Diagnostic. */
+int gh_file_info(void* h, int64_t* slots, int32_t* shards, int64_t* held);
 /* The HBM one shard (rank of world, layout and sizes from cfg) would hold,
  * without a device or a communicator (a dry walk of gh_create's
  * allocations): *create_bytes = everything gh_create allocates;

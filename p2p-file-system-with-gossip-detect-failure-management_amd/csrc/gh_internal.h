@@ -389,8 +389,11 @@ struct GhDev {
   uint8_t *qcarry;  // [n]: bit0 run state entering this shard, bit1 shard holds the row's last list entry
   int32_t *qlast;   // [n]: local tile of the row's last present cell (-1 none)
   unsigned long long *stats;  // ST_COUNT
-  // files (replicated on every rank)
+  // files, sharded by file ID (master/master.go:74-175 is per
+  // file): file f lives on shard f % fsh, at local slot f / fsh; fcap = this
+  // shard's slots (ceil(max_files / fsh)). One engine: fsh = 1, frank = 0.
   int64_t fcap;
+  int32_t fsh, frank;
   int32_t *rep, *ver, *fts;
   uint32_t *draws;
   int32_t *cand, *ncand;
@@ -414,6 +417,11 @@ __host__ __device__ __forceinline__ GhCell gh_absent() { return GhCell{GH_ABSENT
 __host__ __device__ __forceinline__ bool gh_flag_for(int32_t x, int32_t ts, int64_t cg, int64_t i, int32_t r,
                                                      int32_t t_fail) {
   return x > 1 && cg != i && (int64_t)ts < (int64_t)r - t_fail;
+}
+
+// File f's local slot on this shard, or -1 when another shard holds it.
+__host__ __device__ __forceinline__ int64_t gh_fslot(const GhDev& d, int64_t f) {
+  return (f % d.fsh) == d.frank ? f / d.fsh : -1;
 }
 
 // Linear index of cell (table slot s, LOCAL member column c) in the tiled layout.

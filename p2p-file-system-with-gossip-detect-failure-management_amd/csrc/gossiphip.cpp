@@ -951,10 +951,10 @@ int ensure_io(Engine* e, int64_t n) {
 }
 
 int check_files(Engine* e, const int32_t* files, int64_t n, bool distinct) {
-  if (e->d.fcap <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
+  if (e->cfg.max_files <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
   if (n < 0 || (n > 0 && !files)) return set_err(e, GH_EINVAL, "bad file list");
   for (int64_t x = 0; x < n; ++x)
-    if (files[x] < 0 || files[x] >= e->d.fcap) return set_err(e, GH_EINVAL, "file id out of range");
+    if (files[x] < 0 || files[x] >= e->cfg.max_files) return set_err(e, GH_EINVAL, "file id out of range");
   if (distinct) {
     std::vector<int32_t> s(files, files + n);
     std::sort(s.begin(), s.end());
@@ -1303,7 +1303,10 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
     if (rc) break;
     e->rbits_rows = 2;
     if ((rc = dalloc(e, &d.cand, e->n, 0)) || (rc = dalloc(e, &d.ncand, 4, 0))) break;
-    d.fcap = cfg->max_files;
+    // the file table sharded by file ID: shard g holds files g, g + G, ...
+    d.fsh = std::max(e->world, 1);
+    d.frank = e->rank;
+    d.fcap = cfg->max_files > 0 ? (cfg->max_files + d.fsh - 1) / d.fsh : 0;
     if (d.fcap > 0) {
       if ((rc = dalloc(e, &d.rep, d.fcap * cfg->replicas, 0xFF)) || (rc = dalloc(e, &d.ver, d.fcap, 0xFF)) ||
           (rc = dalloc(e, &d.fts, d.fcap, 0)) || (rc = dalloc(e, &d.draws, d.fcap, 0)) ||
@@ -1662,6 +1665,24 @@ int gh_exchange_info(void* h, int64_t* ghost_rows, int64_t* bytes_out, int64_t* 
   if (ghost_rows) *ghost_rows = e->gx_rows;
   if (bytes_out) *bytes_out = e->gx_out;
   if (bytes_in) *bytes_in = e->gx_in;
+  return GH_OK;
+}
+
+int gh_file_info(void* h, int64_t* slots, int32_t* shards, int64_t* held) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  if (slots) *slots = e->d.fcap;
+  if (shards) *shards = e->d.fsh;
+  if (held) {
+    *held = 0;
+    if (e->d.fcap > 0) {
+      HIPCHK(e, hipSetDevice(e->cfg.device));
+      std::vector<int32_t> ver(e->d.fcap);
+      HIPCHK(e, hipMemcpyAsync(ver.data(), e->d.ver, sizeof(int32_t) * e->d.fcap, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+      *held = std::count_if(ver.begin(), ver.end(), [](int32_t v) { return v >= 0; });
+    }
+  }
   return GH_OK;
 }
 
@@ -2197,6 +2218,16 @@ int gh_merge_list(void* h, int32_t observer, const int32_t* ids, const int32_t* 
   return GH_OK;
 }
 
+// File-sharded tables: each shard wrote its own files' outputs and INT32_MIN
+// for the others' (place.hip), so a max over the shards is every file's.
+static int merge_file_outputs(Engine* e, int64_t n, int32_t R, bool with_status) {
+  if (e->world <= 1) return GH_OK;
+  COMMCHK(e, e->comm->allreduce(e->d.io_b, e->d.io_b, (size_t)n * R, GH_DT_I32, GH_OP_MAX, e->stream));
+  COMMCHK(e, e->comm->allreduce(e->d.io_c, e->d.io_c, (size_t)n, GH_DT_I32, GH_OP_MAX, e->stream));
+  if (with_status) COMMCHK(e, e->comm->allreduce(e->d.io_d, e->d.io_d, (size_t)n, GH_DT_I32, GH_OP_MAX, e->stream));
+  return GH_OK;
+}
+
 int gh_put(void* h, const int32_t* files, int64_t n, int32_t* replicas, int32_t* versions, int32_t* status) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
@@ -2215,6 +2246,7 @@ int gh_put(void* h, const int32_t* files, int64_t n, int32_t* replicas, int32_t*
     launch_candidates(e->d, 1, e->stream);
   launch_put(e->d, 1, n, R, e->round, e->cfg.seed, e->stream);
   HIPCHK(e, hipGetLastError());
+  if ((rc = merge_file_outputs(e, n, R, true))) return rc;
   std::vector<int32_t> rep(n * R), ver(n), st(n);
   HIPCHK(e, hipMemcpyAsync(rep.data(), e->d.io_b, sizeof(int32_t) * n * R, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipMemcpyAsync(ver.data(), e->d.io_c, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e->stream));
@@ -2239,6 +2271,7 @@ int gh_put_conflicts(void* h, const int32_t* files, int64_t n, int32_t window, u
   HIPCHK(e, hipMemcpyAsync(e->d.io_a, files, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
   launch_conflicts(e->d, n, e->round, window, e->stream);
   HIPCHK(e, hipGetLastError());
+  if (e->world > 1) COMMCHK(e, e->comm->allreduce(e->d.io_d, e->d.io_d, n, GH_DT_I32, GH_OP_MAX, e->stream));
   std::vector<int32_t> out(n);
   HIPCHK(e, hipMemcpyAsync(out.data(), e->d.io_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -2249,7 +2282,7 @@ int gh_put_conflicts(void* h, const int32_t* files, int64_t n, int32_t window, u
 int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap, int64_t* n_plan) {
   Engine* e = static_cast<Engine*>(h);
   if (!e || !n_plan || (cap > 0 && !plan)) return GH_EINVAL;
-  if (e->d.fcap <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
+  if (e->cfg.max_files <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
   if (observer < 0 || observer >= e->n) return set_err(e, GH_EINVAL, "observer");
   HIPCHK(e, hipSetDevice(e->cfg.device));
   HIPCHK(e, hipMemsetAsync(e->d.nplan, 0, sizeof(int32_t), e->stream));
@@ -2263,13 +2296,44 @@ int gh_repair(void* h, int32_t observer, gh_plan_entry* plan, int64_t cap, int64
   launch_repair(e->d, 2, e->cfg.replicas, e->cfg.seed, e->stream);
   HIPCHK(e, hipGetLastError());
   int32_t np = 0;
-  HIPCHK(e, hipMemcpyAsync(&np, e->d.nplan, sizeof np, hipMemcpyDeviceToHost, e->stream));
-  HIPCHK(e, hipStreamSynchronize(e->stream));
-  std::vector<gh_plan_entry> all(np);
-  if (np > 0) {
-    HIPCHK(e, hipMemcpyAsync(all.data(), e->d.plan, sizeof(gh_plan_entry) * np, hipMemcpyDeviceToHost,
-                             e->stream));
+  std::vector<gh_plan_entry> all;
+  if (e->world > 1) {
+    // each shard planned its own files: allgather the counts, then the
+    // entries (padded to the largest count)
+    const int G = e->world;
+    Staging sc;
+    if ((rc = sc.alloc(e, sizeof(int32_t) * (G + 1)))) return rc;
+    int32_t* cnt = sc.as<int32_t>();
+    HIPCHK(e, hipMemcpyAsync(cnt + G, e->d.nplan, sizeof(int32_t), hipMemcpyDeviceToDevice, e->stream));
+    COMMCHK(e, e->comm->allgather(cnt + G, cnt, sizeof(int32_t), e->stream));
+    std::vector<int32_t> counts(G);
+    HIPCHK(e, hipMemcpyAsync(counts.data(), cnt, sizeof(int32_t) * G, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    const int64_t mx = *std::max_element(counts.begin(), counts.end());
+    if (mx > 0) {
+      Staging sp;
+      const size_t B = sizeof(gh_plan_entry) * (size_t)mx;
+      if ((rc = sp.alloc(e, B * (G + 1)))) return rc;
+      char* base = sp.as<char>();
+      if (counts[e->rank] > 0)
+        HIPCHK(e, hipMemcpyAsync(base + B * G, e->d.plan, sizeof(gh_plan_entry) * counts[e->rank],
+                                 hipMemcpyDeviceToDevice, e->stream));
+      COMMCHK(e, e->comm->allgather(base + B * G, base, B, e->stream));
+      std::vector<gh_plan_entry> got((size_t)mx * G);
+      HIPCHK(e, hipMemcpyAsync(got.data(), base, B * G, hipMemcpyDeviceToHost, e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+      for (int g = 0; g < G; ++g) all.insert(all.end(), got.begin() + (size_t)g * mx, got.begin() + (size_t)g * mx + counts[g]);
+    }
+    np = (int32_t)all.size();
+  } else {
+    HIPCHK(e, hipMemcpyAsync(&np, e->d.nplan, sizeof np, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    all.resize(np);
+    if (np > 0) {
+      HIPCHK(e, hipMemcpyAsync(all.data(), e->d.plan, sizeof(gh_plan_entry) * np, hipMemcpyDeviceToHost,
+                               e->stream));
+      HIPCHK(e, hipStreamSynchronize(e->stream));
+    }
   }
   std::sort(all.begin(), all.end(), [](const gh_plan_entry& a, const gh_plan_entry& b) { return a.file < b.file; });
   rc = GH_OK;
@@ -2301,6 +2365,7 @@ static int get_or_delete(Engine* e, const int32_t* files, int64_t n, int32_t* re
   HIPCHK(e, hipMemcpyAsync(e->d.io_a, files, sizeof(int32_t) * n, hipMemcpyHostToDevice, e->stream));
   launch_get(e->d, n, R, del, e->stream);
   HIPCHK(e, hipGetLastError());
+  if ((rc = merge_file_outputs(e, n, R, false))) return rc;
   std::vector<int32_t> rep(n * R), ver(n);
   HIPCHK(e, hipMemcpyAsync(rep.data(), e->d.io_b, sizeof(int32_t) * n * R, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipMemcpyAsync(ver.data(), e->d.io_c, sizeof(int32_t) * n, hipMemcpyDeviceToHost, e->stream));
@@ -2358,7 +2423,7 @@ int gh_rebuild_meta(void* h, int32_t new_master, int32_t* f0, int64_t* n_files) 
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;
   if (new_master < 0 || new_master >= e->n) return set_err(e, GH_EINVAL, "new_master");
-  if (e->d.fcap <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
+  if (e->cfg.max_files <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
   // the first 5 members of M's list (list order); 5 covers "first 4 other than M"
   std::vector<int32_t> ids(e->n);
   int64_t nl = 0;
@@ -2374,9 +2439,18 @@ int gh_rebuild_meta(void* h, int32_t new_master, int32_t* f0, int64_t* n_files) 
   std::vector<int32_t> ver(e->d.fcap);
   HIPCHK(e, hipMemcpyAsync(ver.data(), e->d.ver, sizeof(int32_t) * e->d.fcap, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
+  int32_t kept = (int32_t)std::count_if(ver.begin(), ver.end(), [](int32_t v) { return v >= 0; });
+  if (e->world > 1) {  // each shard counted its own files
+    Staging sk;
+    if ((rc = sk.alloc(e, sizeof(int32_t)))) return rc;
+    HIPCHK(e, hipMemcpyAsync(sk.p, &kept, sizeof kept, hipMemcpyHostToDevice, e->stream));
+    if ((rc = allreduce_i32(e, sk.as<int32_t>(), sk.as<int32_t>(), 1))) return rc;
+    HIPCHK(e, hipMemcpyAsync(&kept, sk.p, sizeof kept, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
   e->cfg.master = new_master;
   if (f0) *f0 = L[0];
-  if (n_files) *n_files = std::count_if(ver.begin(), ver.end(), [](int32_t v) { return v >= 0; });
+  if (n_files) *n_files = kept;
   return GH_OK;
 }
 

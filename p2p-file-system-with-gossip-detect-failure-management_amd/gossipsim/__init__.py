@@ -185,6 +185,14 @@ class Engine:
         self._chk(self.lib.gh_memory_info(self.h, *[C.byref(x) for x in v]))
         return dict(zip(("device_bytes", "wide_used", "wide_cap", "frozen_rows"), (x.value for x in v)))
 
+    def file_info(self):
+        """dict(slots, shards, held): this shard's file-table slots
+        (ceil(max_files / G), files sharded by ID, file f on shard f % G),
+        the shard count and the files it holds (gh_file_info)."""
+        sl, sh, hd = C.c_int64(), C.c_int32(), C.c_int64()
+        self._chk(self.lib.gh_file_info(self.h, C.byref(sl), C.byref(sh), C.byref(hd)))
+        return {"slots": sl.value, "shards": sh.value, "held": hd.value}
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.gh_destroy(self.h)

@@ -103,6 +103,7 @@ SYMBOLS = [
     ("gh_exchange_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i64)]),
     ("gh_job_info", C.c_int, [_vp, _P(_i64), _P(_i64)]),
     ("gh_memory_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i64), _P(_i64)]),
+    ("gh_file_info", C.c_int, [_vp, _P(_i64), _P(C.c_int32), _P(_i64)]),
     ("gh_footprint", C.c_int, [_P(Config), _i32, _i32, _i32, _P(_i64), _P(_i64)]),
 ]
 

@@ -232,7 +232,9 @@ def test_merge_list_sharded(gs, oracle_mod):
 
 def test_c5_churn_rereplication_sharded(gs, oracle_mod):
     """Config 5 shape (2^20 files, join/leave/crash waves, repairs at
-    detection + 8) over 2 shards."""
+    detection + 8) over 2 shards, the file table sharded by file ID (file f on
+    shard f % 2, master/master.go:74-150 is per file): each shard holds and
+    places 2^19 files, the puts, repair plans and lookups equal the oracle's."""
     from test_gpu_parity import c5_run
     n, F = 1024, 1 << 20
     cfg = dict(fanout=4, seed=0x5EED0015, max_files=F, t_fail=8, t_cleanup=8)
@@ -246,5 +248,54 @@ def test_c5_churn_rereplication_sharded(gs, oracle_mod):
         grp.import_state(hb, ts, alive, 0)
         orc.import_state(hb, ts, alive, 0)
         assert c5_run(grp, orc, n, F) > 0
+        info = grp.run("file_info")
+        assert [x["slots"] for x in info] == [F // 2, F // 2]
+        assert [x["shards"] for x in info] == [2, 2]
+        assert [x["held"] for x in info] == [F // 2, F // 2]
     finally:
         grp.close()
+
+
+@pytest.mark.parametrize("world", [3, 5])
+def test_file_shards_uneven(gs, oracle_mod, world):
+    """File-ID sharding with a file count no shard count divides (1,000
+    files): puts in two batches with repeats of earlier files, a crash wave,
+    repairs from two observers, gets, conflicts and deletes equal the
+    oracle's; every shard holds ceil(1000 / G) slots and its own files."""
+    n, F = 96, 1000
+    cfg = dict(fanout=3, seed=0x5EED0019, max_files=F, t_fail=4, t_cleanup=6)
+    grp = gs.ShardGroup(gs.default_config(n, **cfg), world)
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg))
+    try:
+        hb, ts, alive = sc.full_state(n)
+        grp.import_state(hb, ts, alive, 0)
+        orc.import_state(hb, ts, alive, 0)
+        f1 = np.arange(0, 700, dtype=np.int32)
+        f2 = np.arange(500, F, dtype=np.int32)  # 500..699 put again
+        for batch in (f1, f2):
+            for x, y in zip(grp.put(batch), orc.put(batch)):
+                np.testing.assert_array_equal(x, y)
+        ev = [(sc.CRASH, c) for c in sc.crash_ids(n, 0.1, 0x5EED0019)]
+        grp.apply_events(ev)
+        orc.apply_events(ev)
+        for r in range(1, 13):
+            assert grp.step(1) == orc.step(1), r
+        for obs in (0, 7):
+            assert grp.repair(obs) == orc.repair(obs), obs
+        allf = np.arange(F, dtype=np.int32)
+        for x, y in zip(grp.get_files(allf), orc.get_files(allf)):
+            np.testing.assert_array_equal(x, y)
+        np.testing.assert_array_equal(grp.put_conflicts(allf), orc.put_conflicts(allf))
+        gone = np.arange(0, F, 7, dtype=np.int32)
+        np.testing.assert_array_equal(grp.delete_files(gone), orc.delete_files(gone))
+        for x, y in zip(grp.get_files(allf), orc.get_files(allf)):
+            np.testing.assert_array_equal(x, y)
+        info = grp.run("file_info")
+        slots = -(-F // world)
+        kept = set(range(F)) - set(gone.tolist())
+        for g, x in enumerate(info):
+            assert (x["slots"], x["shards"]) == (slots, world)
+            assert x["held"] == sum(1 for f in kept if f % world == g)
+    finally:
+        grp.close()
+        orc.close()

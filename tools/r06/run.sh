@@ -8,6 +8,8 @@
 #   run.sh ab TAG VAR [ARGS...]    bench A/B of env switch VAR=1 vs VAR=0, three alternating passes
 #   run.sh timeline TAG            one steady round's kernels (rocprofv3 kernel trace)
 #   run.sh py TAG SECONDS SCRIPT [ARGS...]   a tool script under a time limit
+#   run.sh trace TAG MODE ROUNDS MARKER PER R1 [R2...]   tools/r06/slow_rounds.py MODE ROUNDS under a
+#                                  rocprofv3 kernel trace, split per round by tools/r06/trace_rounds.py
 # Output: gpurun_out/r06/TAG_*
 set -o pipefail
 O=gpurun_out/r06
@@ -48,5 +50,11 @@ case "$cmd" in
     secs=$1; shift
     timeout -k 10 "$secs" python3 -u "$@" > $O/${tag}_py.log 2>&1; rc=$?
     tail -40 $O/${tag}_py.log; exit $rc ;;
-  *) sed -n 2,12p "$0"; exit 2 ;;
+  trace)
+    mode=$1; rounds=$2; marker=$3; per=$4; shift 4
+    timeout -s KILL 600 rocprofv3 --kernel-trace --output-format csv -d $O/${tag}_tr -o run -- \
+      python3 tools/r06/slow_rounds.py $mode $rounds > $O/${tag}_rounds.jsonl 2> $O/${tag}_tr.log || { tail $O/${tag}_tr.log; exit 1; }
+    python3 tools/r06/trace_rounds.py $O/${tag}_tr $marker $per "$@" > $O/${tag}_split.txt || exit 1
+    cut -c1-150 $O/${tag}_rounds.jsonl | tail -8; head -60 $O/${tag}_split.txt ;;
+  *) sed -n 2,14p "$0"; exit 2 ;;
 esac

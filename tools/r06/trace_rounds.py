@@ -7,7 +7,22 @@ shard count); ROUND: 1-based round numbers of the run."""
 import collections
 import csv
 import glob
+import re
 import sys
+
+
+def short(name):
+    """k_round<4, 256, 1, true, false, 2> from the demangled kernel name"""
+    name = re.sub(r"\(anonymous namespace\)::", "", name)
+    name = re.sub(r"^void ", "", name)
+    depth, out = 0, []
+    for ch in name:
+        if ch == "(" and depth == 0:
+            break
+        depth += ch == "<"
+        depth -= ch == ">"
+        out.append(ch)
+    return "".join(out)[:80]
 
 d, marker, per = sys.argv[1], sys.argv[2], int(sys.argv[3])
 want = [int(x) for x in sys.argv[4:]]
@@ -24,7 +39,7 @@ for r in want:
     t1 = int(rows[b]["Start_Timestamp"]) if b < len(rows) else int(rows[b - 1]["End_Timestamp"])
     tot = collections.defaultdict(lambda: [0, 0.0])
     for x in rows[a:b]:
-        name = x["Kernel_Name"].split("(")[0][:70]
+        name = short(x["Kernel_Name"])
         tot[name][0] += 1
         tot[name][1] += (int(x["End_Timestamp"]) - int(x["Start_Timestamp"])) / 1e3
     busy = sum(v[1] for v in tot.values())
