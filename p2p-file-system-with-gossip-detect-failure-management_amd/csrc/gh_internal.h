@@ -270,6 +270,13 @@ struct GhDev {
   uint32_t *gplane; // ... their sender plane words [gcap][ld / 8] (null without the plane)
   int64_t gcap;     // ghost rows the ghost table holds
   int32_t *pvf;     // row layout: [n][k] validity of each receiver's draws (summed over shards)
+  // row layout, G > 1: per local column c REMOVE'd with a single detector j
+  // (D_{r-1}: det_cnt == 1, det_min == j; SPEC §2 step 1), j's merge
+  // candidate for c -- its exact heartbeat when present and unflagged, else
+  // -1 -- from j's owner, max-allreduced (k_sole_vals). j is the only sender
+  // that still carries c, so a lane job of a REMOVE'd column reads this
+  // instead of a ghost sender's 16-bit codes (which then need not travel).
+  int32_t *soleval;
   uint8_t *pvb;     // column layout, G > 1, pull: [G * ncs] per receiver the validity bits of its k draws
                     // (its column's owner decides them; allgathered, then every shard rebuilds every inbox)
   uint16_t *hn[2];  // narrow double buffer
@@ -746,6 +753,32 @@ __device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, i
   }
   return out;
 }
+// gh_pf8 for whole-table sweeps (the quirk pre-pass): a tier chunk holds no
+// flag (a flagged cell is always escaped), so its present mask comes from the
+// lag word alone (code != 15) with no decode; escaped chunks, 16-bit buffers
+// and ghost rows take gh_pf8. *esc = the chunk can hold flags.
+__device__ __forceinline__ uint32_t gh_pf8_sweep(const GhDev& d, int buf, int64_t i, int64_t c, bool* esc) {
+  const int64_t s = gh_slot(d, i);
+  if (gh_m8(d, buf) && !(d.gcodes && s >= d.nrows)) {
+    const int64_t w = gh_cell_slot(d, s, c) >> 3;
+    const uint32_t a = d.a4[buf][w], u = d.pl[buf][w];
+    if (!gh_t4_esc(a)) {
+      // bit 0 of each nibble: the code is not 15
+      const uint32_t e = ~u;
+      uint32_t t = e | (e >> 2);
+      t |= t >> 1;
+      t &= 0x11111111u;
+      // nibble gh_nib(j) = 4 (j >> 1) + 16 (j & 1) -> bit j
+      uint32_t P = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) P |= ((t >> gh_nib(j)) & 1u) << j;
+      *esc = false;
+      return P;
+    }
+  }
+  *esc = true;
+  return gh_pf8(d, buf, i, c);
+}
 // Clears the flag of present cells (i, c + j) for the bits j of m (c % 8 == 0).
 // A stopped row has no flags.
 __device__ __forceinline__ void gh_clearflags8(const GhDev& d, int buf, int64_t i, int64_t c, uint32_t m) {
@@ -896,6 +929,8 @@ void launch_peers_rows(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
 void launch_inbox_bits(const GhDev& d, const GhRound& p, hipStream_t s);
 void launch_inbox_rows(const GhDev& d, const GhRound& p, hipStream_t s);
 void launch_negate(int32_t* x, int64_t n, hipStream_t s);
+// row layout: soleval of every local column from the owners of the single detectors (then max-allreduced)
+void launch_sole_vals(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_ring_count(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_ring_select(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);

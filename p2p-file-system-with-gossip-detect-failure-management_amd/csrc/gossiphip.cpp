@@ -1275,7 +1275,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
     if (rowlay) {
       e->rslot_h.assign(e->n, -1);
       for (int64_t i = row0; i < row0 + nrows; ++i) e->rslot_h[i] = (int32_t)(i - row0);
-      if ((rc = dalloc(e, &d.rslot, e->n, 0xFF)) || (rc = dalloc(e, &d.pvf, (int64_t)e->n * cfg->fanout, 0)) ||
+      if ((world > 1 && (rc = dalloc(e, &d.soleval, e->ld, 0xFF))) ||
+          (rc = dalloc(e, &d.rslot, e->n, 0xFF)) || (rc = dalloc(e, &d.pvf, (int64_t)e->n * cfg->fanout, 0)) ||
           (rc = dalloc(e, &e->gwcnt, 2 * (int64_t)world + (int64_t)world * world, 0)))
         break;
       if (gcap > 0 && ((rc = dalloc(e, &d.gcodes, (size_t)gcap * e->ld, 0xFF)) ||
@@ -1909,6 +1910,11 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
     }
     e->gpo = false;
     if ((rc = build_inboxes(e, p))) return rc;
+    if (e->d.soleval) {  // row shards: the single detectors' candidates of the REMOVE'd columns
+      launch_sole_vals(e->d, e->cur, e->dcur, p, e->stream);
+      HIPCHK(e, hipGetLastError());
+      COMMCHK(e, e->comm->allreduce(e->d.soleval, e->d.soleval, e->ld, GH_DT_I32, GH_OP_MAX, e->stream));
+    }
     GhRound pr = p;
     pr.gpo = e->gpo;  // row layout: the ghosts carry only their plane so far
     pr.vslot = q;

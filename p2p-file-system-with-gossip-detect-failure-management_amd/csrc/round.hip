@@ -1367,7 +1367,10 @@ __device__ __forceinline__ void round_block_nib(const GhDev& d, const int cur, c
       // a job whose rule gathers its senders' 16-bit codes (a REMOVE'd member,
       // an unknown or old minimum): with ghost senders, their codes travel
       if constexpr (ROWS) {
-        if (__ballot(jb && (rm != 0u || Lz != 0)) != 0 && lane == 0) s_need = 1;
+        // (a REMOVE'd member's only carrier is its sole detector, whose
+        // candidate soleval holds: no codes for those)
+        const bool rm_codes = rm != 0u && (d.rlist || !d.soleval);
+        if (__ballot(jb && (rm_codes || Lz != 0)) != 0 && lane == 0) s_need = 1;
       }
       bool jslow = false;
       if (jm) {
@@ -2396,6 +2399,10 @@ __device__ __forceinline__ void job_rule(const GhDev& d, int cur, int dcur, cons
       for (int q = 0; q < cnt; ++q) {
         const int s = d.inbox[beg + q];
         if (rmj && gh_rm_at(d, dcur, l0 + j, s)) continue;  // s REMOVEs it before sending
+        if (rmj && d.soleval && !d.rlist) {  // s is its sole detector (row shards: maybe a ghost)
+          m = max(m, (int64_t)d.soleval[l0 + j]);
+          continue;
+        }
         const GhCell X = gh_get(d, cur, s, l0 + j, r);
         if (X.x >= 0 && !X.f) m = max(m, (int64_t)X.x + ((c0 + j) == s));
       }
@@ -2874,17 +2881,21 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
     int i = 0;
     if (valid) w.at(sid, t, i);
     int f = 0;
+    bool esc = false;
     if (valid) {
-      const uint32_t pf = gh_pf8(d, cur, i, t * TW + w.lc * 8);
+      const uint32_t pf = gh_pf8_sweep(d, cur, i, t * TW + w.lc * 8, &esc);
       const uint32_t P = pf & ~removed8(d, dcur, t * TW + w.lc * 8, i) & 0xFFu;
       f = q_summary8(P, (pf >> 8) & P);
     }
+    // (bit 3 of the stored summary: the segment holds a chunk that can hold
+    // flags, i.e. an escaped one; k_quirk_apply skips the others)
+    const bool seg_esc = (__ballot(esc) & (((SEG == 64) ? ~0ull : ((1ull << SEG) - 1)) << (w.sub * SEG))) != 0;
 #pragma unroll
     for (int o = 1; o < SEG; o <<= 1) {
       const int other = __shfl_up(f, o, SEG);
       if (w.lc >= o) f = q_compose(other, f);
     }
-    if (valid && w.lc == SEG - 1) d.qsum[t * p.n + i] = (uint8_t)f;
+    if (valid && w.lc == SEG - 1) d.qsum[t * p.n + i] = (uint8_t)(f | (seg_esc ? 8 : 0));
   }
 }
 
@@ -2898,9 +2909,9 @@ __global__ __launch_bounds__(256) void k_quirk_prefix(GhDev d, GhRound p) {
   int pre = 0, last = -1;
   for (int64_t t = 0; t < ntiles; ++t) {
     const int f = d.qsum[t * p.n + i];
-    d.qsum[t * p.n + i] = (uint8_t)pre;
+    d.qsum[t * p.n + i] = (uint8_t)(pre | (f & 8));  // (bit 3 kept: the segment may hold flags)
     if (f & 4) last = (int)t;
-    pre = q_compose(pre, f);
+    pre = q_compose(pre, f & 7);
   }
   d.qall[(int64_t)d.rank * p.n + i] = (uint8_t)pre;
   d.qlast[i] = last;
@@ -2938,14 +2949,18 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
     int64_t t = 0;
     int i = 0;
     if (inr) w.at(sid, t, i);
+    // a segment with no escaped chunk holds no flag: nothing to clear (the
+    // run state entering later segments is in the prefix already)
+    const int qs = inr ? d.qsum[t * p.n + i] : 0;
+    if (__ballot((qs & 8) != 0) == 0) continue;
     // the segment and the row's state are independent loads: issue them
     // together, decide validity after
-    const uint32_t pf0 = gh_pf8(d, cur, i, t * TW + w.lc * 8);
+    bool esc_unused;
+    const uint32_t pf0 = gh_pf8_sweep(d, cur, i, t * TW + w.lc * 8, &esc_unused);
     const uint32_t rm0 = removed8(d, dcur, t * TW + w.lc * 8, i);
     const int qc = d.qcarry[i];
-    const int qs = d.qsum[t * p.n + i];
     const int ql = d.qlast[i];
-    const bool valid = inr && d.alive[i] && d.active[i];  // only active rows detect (and send)
+    const bool valid = inr && (qs & 8) && d.alive[i] && d.active[i];  // only active rows detect (and send)
     const uint32_t pf = valid ? pf0 : 0u, rm = valid ? rm0 : 0u;
     const uint32_t P = pf & ~rm & 0xFFu, F = (pf >> 8) & P;  // list members, candidates
     const int f = q_summary8(P, F);

@@ -210,6 +210,26 @@ unsigned ghost_grid(int64_t work) {
 
 }  // namespace
 
+namespace {
+__global__ __launch_bounds__(256) void k_sole_vals(GhDev d, int cur, int dcur, GhRound p) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= d.ld) return;
+  int32_t v = -1;
+  if (d.det_cnt[dcur][c] == 1) {
+    const int64_t j = d.det_min[dcur][c];
+    if (gh_owned(d, j) && d.alive[j]) {
+      const GhCell X = gh_get(d, cur, j, c, p.r);
+      if (X.x >= 0 && !X.f) v = X.x + ((d.col0 + c) == j);
+    }
+  }
+  d.soleval[c] = v;
+}
+}  // namespace
+
+void launch_sole_vals(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  hipLaunchKernelGGL(k_sole_vals, dim3((unsigned)((d.ld + 255) / 256)), dim3(256), 0, s, d, cur, dcur, p);
+}
+
 int64_t ghost_part_bytes(const GhDev& d, int part) { return part == GH_GX_PLANE ? d.ld / 2 : d.ld * 2; }
 int64_t ghost_wide_record_bytes(const GhDev& d) { return ghost_wide_bytes(d.tw); }
 

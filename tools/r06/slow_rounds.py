@@ -41,5 +41,8 @@ for r in range(1, rounds + 1):
     if mode not in ("rows8", "cols8"):
         rec.update(variant=eng.tier_info(full=True)[3], lane_jobs=eng.job_info()[0],
                    slow=eng.encoding_info(full=True)[1])
+    elif os.environ.get("GH_DIAG"):  # per shard: slow segments, lane jobs, the last exchange
+        rec.update(slow=[x[1] for x in eng.run("encoding_info")], jobs=[x[0] for x in eng.run("job_info")],
+                   gx_mb=[round(x["bytes_in"] / 2**20, 1) for x in eng.run("exchange_info")])
     print(json.dumps(rec), flush=True)
 eng.close()
