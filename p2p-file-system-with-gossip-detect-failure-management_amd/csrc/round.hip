@@ -2868,34 +2868,69 @@ __device__ __forceinline__ int q_summary8(uint32_t P, uint32_t F) {
 }
 
 // one segment per (tile, row): the tile's run summary (segmented scan over
-// the SEG lanes, last lane holds the whole tile)
+// the SEG lanes, last lane holds the whole tile). A wave takes U segment
+// steps per iteration, their tier words loaded together (a full-table sweep
+// at one step in flight per wave was latency-bound: ~1 TB/s).
 template <int TW>
 __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, GhRound p) {
   if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no candidate in any shard's table
   constexpr int SEG = SegWalk<TW>::SEG;
+  constexpr int U = 4;
   const SegWalk<TW> w(d, p);
-  for (int64_t base = w.first; base < w.nseg; base += w.stride) {
-    const int64_t sid = base + w.sub;
-    const bool valid = sid < w.nseg;
-    int64_t t = 0;
-    int i = 0;
-    if (valid) w.at(sid, t, i);
-    int f = 0;
-    bool esc = false;
-    if (valid) {
-      const uint32_t pf = gh_pf8_sweep(d, cur, i, t * TW + w.lc * 8, &esc);
-      const uint32_t P = pf & ~removed8(d, dcur, t * TW + w.lc * 8, i) & 0xFFu;
-      f = q_summary8(P, (pf >> 8) & P);
-    }
-    // (bit 3 of the stored summary: the segment holds a chunk that can hold
-    // flags, i.e. an escaped one; k_quirk_apply skips the others)
-    const bool seg_esc = (__ballot(esc) & (((SEG == 64) ? ~0ull : ((1ull << SEG) - 1)) << (w.sub * SEG))) != 0;
+  const bool tier = gh_m8(d, cur);
+  const unsigned long long smask = ((SEG == 64) ? ~0ull : ((1ull << SEG) - 1)) << (w.sub * SEG);
+  for (int64_t base = w.first; base < w.nseg; base += U * w.stride) {
+    int64_t tu[U];
+    int iu[U];
+    bool vu[U];
+    uint32_t au[U], qu[U];
 #pragma unroll
-    for (int o = 1; o < SEG; o <<= 1) {
-      const int other = __shfl_up(f, o, SEG);
-      if (w.lc >= o) f = q_compose(other, f);
+    for (int u = 0; u < U; ++u) {
+      const int64_t sid = base + u * w.stride + w.sub;
+      vu[u] = sid < w.nseg;
+      tu[u] = 0;
+      iu[u] = (int)w.row0;
+      if (vu[u]) w.at(sid, tu[u], iu[u]);
+      au[u] = 0u;
+      qu[u] = 0u;
+      if (vu[u] && tier) {
+        const int64_t wi = gh_cell(d, iu[u], tu[u] * TW + w.lc * 8) >> 3;
+        au[u] = d.a4[cur][wi];
+        qu[u] = d.pl[cur][wi];
+      }
     }
-    if (valid && w.lc == SEG - 1) d.qsum[t * p.n + i] = (uint8_t)(f | (seg_esc ? 8 : 0));
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t c = tu[u] * TW + w.lc * 8;
+      int f = 0;
+      bool esc = false;
+      if (vu[u]) {
+        uint32_t pf;
+        if (tier && !gh_t4_esc(au[u])) {
+          // a tier chunk: no flag; present = lag code != 15 (gh_pf8_sweep)
+          const uint32_t e = ~qu[u];
+          uint32_t t = e | (e >> 2);
+          t = (t | (t >> 1)) & 0x11111111u;
+          pf = 0;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pf |= ((t >> gh_nib(j)) & 1u) << j;
+        } else {
+          esc = true;
+          pf = gh_pf8(d, cur, iu[u], c);
+        }
+        const uint32_t P = pf & ~removed8(d, dcur, c, iu[u]) & 0xFFu;
+        f = q_summary8(P, (pf >> 8) & P);
+      }
+      // (bit 3 of the stored summary: the segment holds a chunk that can
+      // hold flags, i.e. an escaped one; k_quirk_apply skips the others)
+      const bool seg_esc = (__ballot(esc) & smask) != 0;
+#pragma unroll
+      for (int o = 1; o < SEG; o <<= 1) {
+        const int other = __shfl_up(f, o, SEG);
+        if (w.lc >= o) f = q_compose(other, f);
+      }
+      if (vu[u] && w.lc == SEG - 1) d.qsum[tu[u] * p.n + iu[u]] = (uint8_t)(f | (seg_esc ? 8 : 0));
+    }
   }
 }
 
@@ -2942,54 +2977,86 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
   if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no candidate in any shard's table
   // (gh_clearflags8 rewrites the plane words of the chunks it changes)
   constexpr int SEG = SegWalk<TW>::SEG;
+  constexpr int U = 4;  // segment steps per iteration, loads issued together (as k_quirk_sum)
   const SegWalk<TW> w(d, p);
-  for (int64_t base = w.first; base < w.nseg; base += w.stride) {
-    const int64_t sid = base + w.sub;
-    const bool inr = sid < w.nseg;
-    int64_t t = 0;
-    int i = 0;
-    if (inr) w.at(sid, t, i);
+  const bool tier = gh_m8(d, cur);
+  for (int64_t base = w.first; base < w.nseg; base += U * w.stride) {
+    int64_t tu[U];
+    int iu[U], qsu[U];
+    bool inu[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t sid = base + u * w.stride + w.sub;
+      inu[u] = sid < w.nseg;
+      tu[u] = 0;
+      iu[u] = (int)w.row0;
+      if (inu[u]) w.at(sid, tu[u], iu[u]);
+      qsu[u] = inu[u] ? d.qsum[tu[u] * p.n + iu[u]] : 0;
+    }
     // a segment with no escaped chunk holds no flag: nothing to clear (the
     // run state entering later segments is in the prefix already)
-    const int qs = inr ? d.qsum[t * p.n + i] : 0;
-    if (__ballot((qs & 8) != 0) == 0) continue;
-    // the segment and the row's state are independent loads: issue them
-    // together, decide validity after
-    bool esc_unused;
-    const uint32_t pf0 = gh_pf8_sweep(d, cur, i, t * TW + w.lc * 8, &esc_unused);
-    const uint32_t rm0 = removed8(d, dcur, t * TW + w.lc * 8, i);
-    const int qc = d.qcarry[i];
-    const int ql = d.qlast[i];
-    const bool valid = inr && (qs & 8) && d.alive[i] && d.active[i];  // only active rows detect (and send)
-    const uint32_t pf = valid ? pf0 : 0u, rm = valid ? rm0 : 0u;
-    const uint32_t P = pf & ~rm & 0xFFu, F = (pf >> 8) & P;  // list members, candidates
-    const int f = q_summary8(P, F);
-    int lastj = P ? w.lc * 8 + 31 - __builtin_clz(P) : -1;
-    int incl = f;
+    uint32_t au[U], qu[U];
 #pragma unroll
-    for (int o = 1; o < SEG; o <<= 1) {
-      const int other = __shfl_up(incl, o, SEG);
-      if (w.lc >= o) incl = q_compose(other, incl);
-    }
-    int excl = __shfl_up(incl, 1, SEG);
-    if (w.lc == 0) excl = 0;
-#pragma unroll
-    for (int o = SEG / 2; o > 0; o >>= 1) lastj = max(lastj, __shfl_xor(lastj, o));
-    if (!valid) continue;
-    int s = q_apply(excl, q_apply(qs, qc & 1));
-    const int lastc = ((qc & 2) && ql == t) ? lastj : -1;  // the row's last list entry, if here
-    uint32_t clear = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (!((P >> j) & 1u)) continue;
-      if (!((F >> j) & 1u)) {
-        s = 0;
-        continue;
+    for (int u = 0; u < U; ++u) {
+      au[u] = qu[u] = 0u;
+      if ((qsu[u] & 8) && tier) {
+        const int64_t wi = gh_cell(d, iu[u], tu[u] * TW + w.lc * 8) >> 3;
+        au[u] = d.a4[cur][wi];
+        qu[u] = d.pl[cur][wi];
       }
-      if (!(s == 0 || w.lc * 8 + j == lastc)) clear |= 1u << j;  // skipped this round
-      s ^= 1;
     }
-    if (clear) gh_clearflags8(d, cur, i, t * TW + w.lc * 8, clear);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int qs = qsu[u];
+      if (__ballot((qs & 8) != 0) == 0) continue;
+      const int64_t t = tu[u];
+      const int i = iu[u];
+      const int64_t c = t * TW + w.lc * 8;
+      const bool valid = inu[u] && (qs & 8) && d.alive[i] && d.active[i];  // only active rows detect (and send)
+      uint32_t pf = 0u, rm = 0u;
+      if (valid) {
+        if (tier && !gh_t4_esc(au[u])) {  // a tier chunk: no flag (k_quirk_sum)
+          const uint32_t e = ~qu[u];
+          uint32_t tt = e | (e >> 2);
+          tt = (tt | (tt >> 1)) & 0x11111111u;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pf |= ((tt >> gh_nib(j)) & 1u) << j;
+        } else {
+          pf = gh_pf8(d, cur, i, c);
+        }
+        rm = removed8(d, dcur, c, i);
+      }
+      const int qc = d.qcarry[i];
+      const int ql = d.qlast[i];
+      const uint32_t P = pf & ~rm & 0xFFu, F = (pf >> 8) & P;  // list members, candidates
+      const int f = q_summary8(P, F);
+      int lastj = P ? w.lc * 8 + 31 - __builtin_clz(P) : -1;
+      int incl = f;
+#pragma unroll
+      for (int o = 1; o < SEG; o <<= 1) {
+        const int other = __shfl_up(incl, o, SEG);
+        if (w.lc >= o) incl = q_compose(other, incl);
+      }
+      int excl = __shfl_up(incl, 1, SEG);
+      if (w.lc == 0) excl = 0;
+#pragma unroll
+      for (int o = SEG / 2; o > 0; o >>= 1) lastj = max(lastj, __shfl_xor(lastj, o));
+      if (!valid) continue;
+      int st = q_apply(excl, q_apply(qs, qc & 1));
+      const int lastc = ((qc & 2) && ql == t) ? lastj : -1;  // the row's last list entry, if here
+      uint32_t clear = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        if (!((P >> j) & 1u)) continue;
+        if (!((F >> j) & 1u)) {
+          st = 0;
+          continue;
+        }
+        if (!(st == 0 || w.lc * 8 + j == lastc)) clear |= 1u << j;  // skipped this round
+        st ^= 1;
+      }
+      if (clear) gh_clearflags8(d, cur, i, c, clear);
+    }
   }
 }
 
