@@ -2891,6 +2891,9 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
       tu[u] = 0;
       iu[u] = (int)w.row0;
       if (vu[u]) w.at(sid, tu[u], iu[u]);
+      // only active rows detect (k_quirk_apply): a stopped row's frozen
+      // cells are not decoded
+      vu[u] = vu[u] && d.alive[iu[u]] && d.active[iu[u]];
       au[u] = 0u;
       qu[u] = 0u;
       if (vu[u] && tier) {
