@@ -316,8 +316,16 @@ struct SegWalk {
     stride = (((int64_t)gridDim.x * blockDim.x) >> 6) * RPW;
   }
   __device__ void at(int64_t sid, int64_t& t, int& i) const {
-    t = sid / nrows;
-    i = (int)(row0 + (sid - t * nrows));
+    // (a 64-bit division per segment had dominated the whole-table sweeps:
+    // 32-bit when the segment count fits, as it does up to N = 262,144)
+    if (nseg <= (int64_t)UINT32_MAX) {
+      const uint32_t q = (uint32_t)sid / (uint32_t)nrows;
+      t = q;
+      i = (int)(row0 + ((uint32_t)sid - q * (uint32_t)nrows));
+    } else {
+      t = sid / nrows;
+      i = (int)(row0 + (sid - t * nrows));
+    }
   }
 };
 
