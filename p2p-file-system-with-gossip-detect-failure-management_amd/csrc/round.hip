@@ -2899,17 +2899,17 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
       tu[u] = 0;
       iu[u] = (int)w.row0;
       if (vu[u]) w.at(sid, tu[u], iu[u]);
-      // only active rows detect (k_quirk_apply): a stopped row's frozen
-      // cells are not decoded
-      vu[u] = vu[u] && d.alive[iu[u]] && d.active[iu[u]];
       au[u] = 0u;
       qu[u] = 0u;
-      if (vu[u] && tier) {
+      if (vu[u] && tier) {  // (issued before the row's state is known: no dependent load chain)
         const int64_t wi = gh_cell(d, iu[u], tu[u] * TW + w.lc * 8) >> 3;
         au[u] = d.a4[cur][wi];
         qu[u] = d.pl[cur][wi];
       }
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u)  // only active rows detect (k_quirk_apply): a stopped row's frozen cells are not decoded
+      vu[u] = vu[u] && d.alive[iu[u]] && d.active[iu[u]];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int64_t c = tu[u] * TW + w.lc * 8;
