@@ -315,6 +315,17 @@ struct SegWalk {
     first = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * RPW;
     stride = (((int64_t)gridDim.x * blockDim.x) >> 6) * RPW;
   }
+  // A contiguous run of segments per wave (k_quirk_*): [run0, run1), steps
+  // of RPW * U segments. Consecutive segments are consecutive rows of one
+  // tile, so a wave's one-byte-per-segment stores fill whole lines from one
+  // XCD (the strided walk had every line of qsum written by 16 workgroups on
+  // all 8 XCDs: 3.7 ms for a 1 ms sweep).
+  __device__ void run(int U, int64_t& run0, int64_t& run1) const {
+    const int64_t nw = stride / RPW, gw = first / RPW, step = (int64_t)RPW * U;
+    const int64_t per = ((nseg + nw - 1) / nw + step - 1) / step * step;
+    run0 = gw * per;
+    run1 = min(nseg, run0 + per);
+  }
   __device__ void at(int64_t sid, int64_t& t, int& i) const {
     // (a 64-bit division per segment had dominated the whole-table sweeps:
     // 32-bit when the segment count fits, as it does up to N = 262,144)
@@ -2887,15 +2898,17 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
   const SegWalk<TW> w(d, p);
   const bool tier = gh_m8(d, cur);
   const unsigned long long smask = ((SEG == 64) ? ~0ull : ((1ull << SEG) - 1)) << (w.sub * SEG);
-  for (int64_t base = w.first; base < w.nseg; base += U * w.stride) {
+  int64_t run0, run1;
+  w.run(U, run0, run1);
+  for (int64_t base = run0; base < run1; base += U * w.RPW) {
     int64_t tu[U];
     int iu[U];
     bool vu[U];
     uint32_t au[U], qu[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t sid = base + u * w.stride + w.sub;
-      vu[u] = sid < w.nseg;
+      const int64_t sid = base + u * w.RPW + w.sub;
+      vu[u] = sid < run1;
       tu[u] = 0;
       iu[u] = (int)w.row0;
       if (vu[u]) w.at(sid, tu[u], iu[u]);
@@ -2991,14 +3004,16 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
   constexpr int U = 4;  // segment steps per iteration, loads issued together (as k_quirk_sum)
   const SegWalk<TW> w(d, p);
   const bool tier = gh_m8(d, cur);
-  for (int64_t base = w.first; base < w.nseg; base += U * w.stride) {
+  int64_t run0, run1;
+  w.run(U, run0, run1);
+  for (int64_t base = run0; base < run1; base += U * w.RPW) {
     int64_t tu[U];
     int iu[U], qsu[U];
     bool inu[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t sid = base + u * w.stride + w.sub;
-      inu[u] = sid < w.nseg;
+      const int64_t sid = base + u * w.RPW + w.sub;
+      inu[u] = sid < run1;
       tu[u] = 0;
       iu[u] = (int)w.row0;
       if (inu[u]) w.at(sid, tu[u], iu[u]);
