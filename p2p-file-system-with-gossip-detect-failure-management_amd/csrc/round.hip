@@ -2958,6 +2958,98 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
   }
 }
 
+// k_quirk_sum with 32 cells per lane (tile widths >= 32): a lane loads its 4
+// chunks' lag and age words at once (16 B each) and a tier chunk, which holds
+// no candidate, contributes only whether a listed member is in it (summary
+// 5, else the identity 0); only escaped chunks take the 8-cell rule. The
+// 8-cell form ran 3.1 ms over the N = 65,536 table, VALU-heavy per 8 cells.
+template <int TW>
+__global__ __launch_bounds__(256) void k_quirk_sum32(GhDev d, int cur, int dcur, GhRound p) {
+  if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no candidate in any shard's table
+  constexpr int SEGL = TW / 32;   // lanes per (tile, row) segment
+  constexpr int RPWL = 64 / SEGL;  // segments per wave instruction
+  constexpr int U = 2;
+  const int lane = threadIdx.x & 63, sub = lane / SEGL, lc = lane % SEGL;
+  const int64_t nrows = d.nrows, nseg = (p.ld / TW) * nrows;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  constexpr int64_t step = (int64_t)RPWL * U;
+  // one contiguous run of segments per wave (SegWalk::run)
+  const int64_t per = ((nseg + nw - 1) / nw + step - 1) / step * step;
+  const int64_t run0 = gw * per, run1 = min(nseg, run0 + per);
+  const bool small = nseg <= (int64_t)UINT32_MAX;
+  const bool tier = gh_m8(d, cur);
+  const unsigned long long smask = ((SEGL == 64) ? ~0ull : ((1ull << SEGL) - 1)) << (sub * SEGL);
+  for (int64_t base = run0; base < run1; base += step) {
+    int64_t tu[U];
+    int iu[U];
+    bool vu[U];
+    v4u au[U], qu[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t sid = base + u * RPWL + sub;
+      vu[u] = sid < run1;
+      tu[u] = 0;
+      iu[u] = (int)d.row0;
+      if (vu[u]) {
+        if (small) {
+          const uint32_t q = (uint32_t)sid / (uint32_t)nrows;
+          tu[u] = q;
+          iu[u] = (int)(d.row0 + ((uint32_t)sid - q * (uint32_t)nrows));
+        } else {
+          tu[u] = sid / nrows;
+          iu[u] = (int)(d.row0 + (sid - tu[u] * nrows));
+        }
+      }
+      au[u] = qu[u] = v4u{0u, 0u, 0u, 0u};
+      if (vu[u] && tier) {
+        const int64_t wi = gh_cell(d, iu[u], tu[u] * TW + lc * 32) >> 3;  // (4-word aligned)
+        au[u] = *reinterpret_cast<const v4u*>(d.a4[cur] + wi);
+        qu[u] = *reinterpret_cast<const v4u*>(d.pl[cur] + wi);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) vu[u] = vu[u] && d.alive[iu[u]] && d.active[iu[u]];  // (as k_quirk_sum)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      int f = 0;
+      bool esc = false;
+      if (vu[u]) {
+        const int64_t c0 = tu[u] * TW + lc * 32;
+        const uint32_t rmw = d.dbits[c0 >> 5];  // the lane's 32 columns' REMOVE bits
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t c = c0 + 8 * k;
+          const uint32_t rm8 = ((rmw >> (8 * k)) & 0xFFu) ? removed8(d, dcur, c, iu[u]) : 0u;
+          int fk;
+          if (tier && !gh_t4_esc(au[u][k])) {
+            const uint32_t e = ~qu[u][k];
+            uint32_t t = e | (e >> 2);
+            t = (t | (t >> 1)) & 0x11111111u;
+            uint32_t P = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) P |= ((t >> gh_nib(j)) & 1u) << j;
+            fk = (P & ~rm8) ? 5 : 0;  // listed members, no candidate
+          } else {
+            esc = true;
+            const uint32_t pf = gh_pf8(d, cur, iu[u], c);
+            const uint32_t P = pf & ~rm8 & 0xFFu;
+            fk = q_summary8(P, (pf >> 8) & P);
+          }
+          f = q_compose(f, fk);
+        }
+      }
+      const bool seg_esc = (__ballot(esc) & smask) != 0;
+#pragma unroll
+      for (int o = 1; o < SEGL; o <<= 1) {
+        const int other = __shfl_up(f, o, SEGL);
+        if (lc >= o) f = q_compose(other, f);
+      }
+      if (vu[u] && lc == SEGL - 1) d.qsum[tu[u] * p.n + iu[u]] = (uint8_t)(f | (seg_esc ? 8 : 0));
+    }
+  }
+}
+
 // one thread per row: exclusive prefix over the shard's tiles (in place),
 // the shard's total and its last tile holding a present cell
 __global__ __launch_bounds__(256) void k_quirk_prefix(GhDev d, GhRound p) {
@@ -3106,7 +3198,10 @@ static unsigned seg_grid(const GhRound& p, int tw) {
 
 template <int TW>
 static void quirk_sum(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
-  hipLaunchKernelGGL(k_quirk_sum<TW>, dim3(seg_grid(p, TW)), dim3(256), 0, s, d, cur, dcur, p);
+  if constexpr (TW >= 32)
+    hipLaunchKernelGGL(k_quirk_sum32<TW>, dim3(seg_grid(p, TW)), dim3(256), 0, s, d, cur, dcur, p);
+  else
+    hipLaunchKernelGGL(k_quirk_sum<TW>, dim3(seg_grid(p, TW)), dim3(256), 0, s, d, cur, dcur, p);
 }
 template <int TW>
 static void quirk_apply(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {

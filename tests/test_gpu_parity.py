@@ -82,6 +82,17 @@ def test_quirk_detection_churn(gs, oracle_mod, n, peer_mode, t_fail, seed):
                                     t_fail=t_fail, t_cleanup=t_fail + 2), n, 40, sched, init=sc.full_state(n))
 
 
+@pytest.mark.parametrize("tw", [8, 16, 32, 64, 128, 256])
+def test_quirk_detection_tile_widths(gs, oracle_mod, tw):
+    """Quirk-mode detection under churn at every tile width: the pre-pass
+    sums 8 cells per lane below 32-member tiles and 32 cells per lane from
+    32 on (k_quirk_sum / k_quirk_sum32), runs crossing tile boundaries."""
+    n = 600
+    sched = sc.random_churn(n, 30, 0x71 + tw, p_crash=0.08, p_leave=0.02, p_join=0.05)
+    run_parity(gs, oracle_mod, dict(fanout=3, seed=0x2100 + tw, detect_mode=1, t_fail=4, t_cleanup=6, tile_width=tw),
+               n, 30, sched, init=sc.full_state(n))
+
+
 def test_quirk_c2_collapse(gs, oracle_mod):
     """N=4,096 with the reference's 5-round timeouts in quirk mode: the
     round-6 detection storm with long candidate runs in every row."""
