@@ -71,40 +71,55 @@ def compare_blocks(engs, orc, r, n=N):
 LAYOUT_NAMES = {(1, 0): "single", (8, 0): "columns_g8", (8, 1): "rows_g8"}
 
 
-def run(gs, om, t_fail, rounds, full_at, expect, sched=None, per_round=None, remove_mode=0, world=1, layout=0,
-        extra=None, after_round=None, lockstep=(), full_all=()):
-    """Step one engine (or G in-process shards of layout `layout`) and
-    tablesim round by round from the full-membership start. `lockstep` adds
-    more (world, layout) groups stepped beside it against the SAME oracle run
-    (one 48 GiB tablesim pass checks every layout); per_round / after_round
-    see the first engine."""
-    cfg = dict(fanout=4, seed=0x5EED0003, t_fail=t_fail, t_cleanup=t_fail, remove_mode=remove_mode, **(extra or {}))
-    engs = []
-    orc = None
-    try:
-        for w, lay in ((world, layout),) + tuple(lockstep):
-            if w > 1:  # G in-process shards of one cluster on this GPU (GH_COMM_LOCAL)
-                e = gs.ShardGroup(gs.default_config(N, shard_layout=lay, **cfg), w)
-            else:
-                e = gs.Engine(gs.default_config(N, **cfg))
-            engs.append((LAYOUT_NAMES.get((w, lay), f"g{w}l{lay}"), e))
-        eng = engs[0][1]
-        orc = om.Oracle(om.default_config(N, **cfg), threads=THREADS)
-        for _, e in engs:
-            e.init_full(2, 0, 0)
-        orc.init_full(2, 0, 0)
-        seen = {"detections": 0, "storm": False, "variants": {}, "first_detection": None}
-        pending_full = set(full_at)
-        for r in range(1, rounds + 1):
-            if sched and r in sched:
-                for _, e in engs:
-                    e.apply_events(sched[r])
-                orc.apply_events(sched[r])
+class Lockstep:
+    """One engine (or G in-process shards of layout `layout`) and tablesim
+    stepped round by round from the full-membership start; `lockstep` adds
+    more (world, layout) groups stepped beside it against the SAME oracle
+    run (one 48 GiB tablesim pass checks every layout). advance(r) runs to
+    round r, checking counters, failed sets and detectors of every engine
+    each round and full tables at the rounds in full_at (of the engines in
+    full_all, else only the first); per_round / after_round see the first
+    engine. A test can advance in parts, so that no single test runs longer
+    than a few minutes without reporting."""
+
+    def __init__(self, gs, om, t_fail, full_at=(), sched=None, per_round=None, remove_mode=0, world=1, layout=0,
+                 extra=None, after_round=None, lockstep=(), full_all=None):
+        cfg = dict(fanout=4, seed=0x5EED0003, t_fail=t_fail, t_cleanup=t_fail, remove_mode=remove_mode,
+                   **(extra or {}))
+        self.engs, self.orc = [], None
+        self.sched, self.per_round, self.after_round = sched or {}, per_round, after_round
+        self.world = world
+        self.full_at, self.full_all = set(full_at), full_all
+        self.r = 0
+        self.seen = {"detections": 0, "storm": False, "variants": {}, "first_detection": None}
+        try:
+            for w, lay in ((world, layout),) + tuple(lockstep):
+                if w > 1:  # G in-process shards of one cluster on this GPU (GH_COMM_LOCAL)
+                    e = gs.ShardGroup(gs.default_config(N, shard_layout=lay, **cfg), w)
+                else:
+                    e = gs.Engine(gs.default_config(N, **cfg))
+                self.engs.append((LAYOUT_NAMES.get((w, lay), f"g{w}l{lay}"), e))
+            self.orc = om.Oracle(om.default_config(N, **cfg), threads=THREADS)
+            for _, e in self.engs:
+                e.init_full(2, 0, 0)
+            self.orc.init_full(2, 0, 0)
+        except BaseException:
+            self.close()
+            raise
+
+    def advance(self, to_r):
+        eng, orc, seen = self.engs[0][1], self.orc, self.seen
+        while self.r < to_r:
+            r = self.r = self.r + 1
+            if r in self.sched:
+                for _, e in self.engs:
+                    e.apply_events(self.sched[r])
+                orc.apply_events(self.sched[r])
             t0 = time.perf_counter()
             s2 = orc.step(1)
             t1 = time.perf_counter()
             ms = []
-            for name, e in engs:
+            for name, e in self.engs:
                 ta = time.perf_counter()
                 s1 = e.step(1)
                 ms.append(f"{name} {1e3 * (time.perf_counter() - ta):.1f} ms")
@@ -112,34 +127,42 @@ def run(gs, om, t_fail, rounds, full_at, expect, sched=None, per_round=None, rem
                 np.testing.assert_array_equal(e.read_failed(), orc.read_failed(), err_msg=f"{name}: failed r={r}")
                 np.testing.assert_array_equal(e.read_detectors(), orc.read_detectors(),
                                               err_msg=f"{name}: detectors r={r}")
-            s1 = s2
             print(f"  r={r}: oracle {t1 - t0:.1f} s, gpu {', '.join(ms)}, {s2}", flush=True)
-            seen["detections"] += s1["detections"]
-            if world == 1:  # (per-shard diagnostics differ between shards)
+            seen["detections"] += s2["detections"]
+            if self.world == 1:  # (per-shard diagnostics differ between shards)
                 seen["storm"] |= eng.encoding_info(full=True)[2] == 1
                 var = eng.tier_info(full=True)[3]
                 seen["variants"][var] = seen["variants"].get(var, 0) + 1
-            if after_round:
-                after_round(eng, orc, r)
-            if per_round:
-                per_round(eng, r, s1)
-            if s1["detections"] and seen["first_detection"] is None:
+            if self.after_round:
+                self.after_round(eng, orc, r)
+            if self.per_round:
+                self.per_round(eng, r, s2)
+            if s2["detections"] and seen["first_detection"] is None:
                 seen["first_detection"] = r
-                pending_full |= {r, r + 1}  # the detection round and the REMOVE round after it
-                if lockstep:
-                    full_all = set(full_all) | {r, r + 1}
-            if r in pending_full:
-                # the lockstep layouts' full tables where the crash acts (the
-                # detection round, the REMOVE round, the last round); their
-                # counters, failed sets and detectors every round
-                compare_blocks(engs if (r in full_all or not full_all) else engs[:1], orc, r)
+                if self.full_all is None:
+                    self.full_at |= {r, r + 1}  # the detection round and the REMOVE round after it
+            if r in self.full_at:
+                all_ = self.full_all is None or r in self.full_all
+                compare_blocks(self.engs if all_ else self.engs[:1], orc, r)
+        return seen
+
+    def close(self):
+        for _, e in self.engs:
+            e.close()
+        self.engs = []
+        if self.orc is not None:
+            self.orc.close()
+            self.orc = None
+
+
+def run(gs, om, t_fail, rounds, full_at, expect, **kw):
+    ls = Lockstep(gs, om, t_fail, full_at, **kw)
+    try:
+        seen = ls.advance(rounds)
         print(f"  variants (round counts by gh_tier_info variant): {seen['variants']}", flush=True)
         expect(seen)
     finally:
-        for _, e in engs:
-            e.close()
-        if orc is not None:
-            orc.close()
+        ls.close()
 
 
 def byte_path_from(r0, r_var=None):
@@ -172,24 +195,22 @@ def test_c3_fullsize_steady_state(gs, oracle_mod):
         per_round=byte_path_from(8, r_var=6))
 
 
-def test_c3_fullsize_crash_1pct(gs, oracle_mod):
+@pytest.fixture(scope="module")
+def crash_lockstep(gs, oracle_mod):
     """1% crash in the bench's workload: 655 members (Philox, seed
-    0x5EED0003, tag CRASH) stop at r=8; run through their detection and the
-    REMOVE wave. Three layouts in lockstep against the one tablesim run: one
-    engine, north_star's 8 row shards (each owns 8,192 observer rows; the
-    other shards' sender plane rows arrive by alltoallv into its ghost table)
-    and 8 column shards (O(N) exchanges), all on this GPU through the
-    in-process transport (~150 GB of HBM). Counters, failed sets and
-    detectors of all three every round; full tables of all three at the
-    detection round, the round after it and the last round, of the engine
-    also at r=12."""
+    0x5EED0003, tag CRASH) stop at r=8; detected at r=23, REMOVE'd at r=24.
+    Three layouts in lockstep against the one tablesim run: one engine,
+    north_star's 8 row shards (each owns 8,192 observer rows; the other
+    shards' sender plane rows arrive by alltoallv into its ghost table) and 8
+    column shards (O(N) exchanges), all on this GPU through the in-process
+    transport (~150 GB of HBM). Counters, failed sets and detectors of all
+    three every round; full tables of all three at the detection round, the
+    round after it and the last round, of the engine also at r=12. Advanced
+    by the three tests below in order."""
     from scenarios import crash_ids
     crashed = crash_ids(N, 0.01, 0x5EED0003)
     assert len(crashed) == 655
     sched = {8: [(gs.GH_EV_CRASH, int(c)) for c in crashed]}
-
-    def expect(s):
-        assert s["detections"] > 0 and s["first_detection"] is not None, s
 
     def fast(eng, r, st):
         # the crash wave stays on the nibble path: REMOVE delivery turns the
@@ -201,8 +222,37 @@ def test_c3_fullsize_crash_1pct(gs, oracle_mod):
             jobs, _ = eng.job_info()
             assert jobs * 100 <= N * N // 16, (r, jobs)
 
-    run(gs, oracle_mod, 16, 32, {12, 32}, expect, sched=sched, per_round=fast, lockstep=((8, 1), (8, 0)),
-        full_all={32})
+    ls = Lockstep(gs, oracle_mod, 16, {12, 23, 24, 32}, sched=sched, per_round=fast, lockstep=((8, 1), (8, 0)),
+                  full_all={23, 24, 32})
+    yield ls
+    ls.close()
+
+
+def test_c3_fullsize_crash_1pct(crash_lockstep):
+    """Rounds 1-16 of the crash (crash_lockstep): the crash at r=8, the
+    engine's full tables at r=12."""
+    s = crash_lockstep.advance(16)
+    assert s["detections"] == 0
+
+
+def test_c3_fullsize_crash_1pct_detection(crash_lockstep):
+    """Rounds 17-23: the crashed members' views age past T_fail, the
+    detection round; full tables of all three layouts at r=23."""
+    s = crash_lockstep.advance(23)
+    assert s["first_detection"] == 23, s
+
+
+def test_c3_fullsize_crash_1pct_remove(crash_lockstep):
+    """Round 24: the REMOVE wave of the 655 members; full tables of all
+    three layouts."""
+    crash_lockstep.advance(24)
+
+
+def test_c3_fullsize_crash_1pct_release(crash_lockstep):
+    """Rounds 25-32: tombstones age out; full tables of all three layouts
+    at r=32."""
+    s = crash_lockstep.advance(32)
+    assert s["detections"] > 0
 
 
 @pytest.mark.gpu_fullsize
