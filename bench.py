@@ -542,7 +542,8 @@ def multi_gpu_legs(gs, args, rank, world, local, dist):
     out[other] = shard_leg(gs, args, rank, world, local, dist, args.n, other, args.warmup, args.steps)
     if world == 8 or args.c4:
         progress("multi-GPU leg: config 4, N=262144, column layout")
-        out["c4_n262144"] = shard_leg(gs, args, rank, world, local, dist, 262144, "columns", 5, 10)
+        # (10 warm-up rounds: a heartbeat needs ~log5(262,144) ~ 8 rounds to reach every member)
+        out["c4_n262144"] = shard_leg(gs, args, rank, world, local, dist, 262144, "columns", 10, 10)
     return out
 
 
