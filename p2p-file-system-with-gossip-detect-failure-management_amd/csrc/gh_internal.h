@@ -753,31 +753,17 @@ __device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, i
   }
   return out;
 }
-// gh_pf8 for whole-table sweeps (the quirk pre-pass): a tier chunk holds no
-// flag (a flagged cell is always escaped), so its present mask comes from the
-// lag word alone (code != 15) with no decode; escaped chunks, 16-bit buffers
-// and ghost rows take gh_pf8. *esc = the chunk can hold flags.
-__device__ __forceinline__ uint32_t gh_pf8_sweep(const GhDev& d, int buf, int64_t i, int64_t c, bool* esc) {
-  const int64_t s = gh_slot(d, i);
-  if (gh_m8(d, buf) && !(d.gcodes && s >= d.nrows)) {
-    const int64_t w = gh_cell_slot(d, s, c) >> 3;
-    const uint32_t a = d.a4[buf][w], u = d.pl[buf][w];
-    if (!gh_t4_esc(a)) {
-      // bit 0 of each nibble: the code is not 15
-      const uint32_t e = ~u;
-      uint32_t t = e | (e >> 2);
-      t |= t >> 1;
-      t &= 0x11111111u;
-      // nibble gh_nib(j) = 4 (j >> 1) + 16 (j & 1) -> bit j
-      uint32_t P = 0;
+// The present cells of a tier chunk (bit j = cell j) from its lag word
+// alone: a code other than 15. A tier chunk holds no flag (a flagged cell is
+// always escaped), so whole-table sweeps (the quirk pre-pass) need no decode.
+__host__ __device__ __forceinline__ uint32_t gh_t4_present8(uint32_t lag) {
+  const uint32_t e = ~lag;
+  uint32_t t = e | (e >> 2);
+  t = (t | (t >> 1)) & 0x11111111u;  // bit 0 of each nibble: the code is not 15
+  uint32_t P = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) P |= ((t >> gh_nib(j)) & 1u) << j;
-      *esc = false;
-      return P;
-    }
-  }
-  *esc = true;
-  return gh_pf8(d, buf, i, c);
+  for (int j = 0; j < 8; ++j) P |= ((t >> gh_nib(j)) & 1u) << j;  // nibble gh_nib(j) -> bit j
+  return P;
 }
 // Clears the flag of present cells (i, c + j) for the bits j of m (c % 8 == 0).
 // A stopped row has no flags.

@@ -2931,13 +2931,7 @@ __global__ __launch_bounds__(256) void k_quirk_sum(GhDev d, int cur, int dcur, G
       if (vu[u]) {
         uint32_t pf;
         if (tier && !gh_t4_esc(au[u])) {
-          // a tier chunk: no flag; present = lag code != 15 (gh_pf8_sweep)
-          const uint32_t e = ~qu[u];
-          uint32_t t = e | (e >> 2);
-          t = (t | (t >> 1)) & 0x11111111u;
-          pf = 0;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) pf |= ((t >> gh_nib(j)) & 1u) << j;
+          pf = gh_t4_present8(qu[u]);  // a tier chunk: no flag
         } else {
           esc = true;
           pf = gh_pf8(d, cur, iu[u], c);
@@ -3023,13 +3017,7 @@ __global__ __launch_bounds__(256) void k_quirk_sum32(GhDev d, int cur, int dcur,
           const uint32_t rm8 = ((rmw >> (8 * k)) & 0xFFu) ? removed8(d, dcur, c, iu[u]) : 0u;
           int fk;
           if (tier && !gh_t4_esc(au[u][k])) {
-            const uint32_t e = ~qu[u][k];
-            uint32_t t = e | (e >> 2);
-            t = (t | (t >> 1)) & 0x11111111u;
-            uint32_t P = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) P |= ((t >> gh_nib(j)) & 1u) << j;
-            fk = (P & ~rm8) ? 5 : 0;  // listed members, no candidate
+            fk = (gh_t4_present8(qu[u][k]) & ~rm8) ? 5 : 0;  // listed members, no candidate
           } else {
             esc = true;
             const uint32_t pf = gh_pf8(d, cur, iu[u], c);
@@ -3133,12 +3121,8 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
       const bool valid = inu[u] && (qs & 8) && d.alive[i] && d.active[i];  // only active rows detect (and send)
       uint32_t pf = 0u, rm = 0u;
       if (valid) {
-        if (tier && !gh_t4_esc(au[u])) {  // a tier chunk: no flag (k_quirk_sum)
-          const uint32_t e = ~qu[u];
-          uint32_t tt = e | (e >> 2);
-          tt = (tt | (tt >> 1)) & 0x11111111u;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) pf |= ((tt >> gh_nib(j)) & 1u) << j;
+        if (tier && !gh_t4_esc(au[u])) {  // a tier chunk: no flag
+          pf = gh_t4_present8(qu[u]);
         } else {
           pf = gh_pf8(d, cur, i, c);
         }
