@@ -256,6 +256,23 @@ int gh_vote_scan(void* h, const int32_t* mview, int32_t* first, int32_t* list_le
  * *n_files = files left in the table, may be NULL. GH_EINVAL if M's list is
  * empty. */
 int gh_rebuild_meta(void* h, int32_t new_master, int32_t* f0, int64_t* n_files);
+/* A master's file metadata (its SDFSMaster maps, master/master.go:38-44) as
+ * flat arrays over files 0..max_files-1: replica lists [F][R] (-1 = none),
+ * versions [F] (-1 = no such file), put timestamps [F], placement draw
+ * counters [F]. gh_export_files copies the engine's table out (every rank gets
+ * the whole table); gh_import_files replaces it (every rank takes its own
+ * files). A master demoted by an election while its process kept running
+ * (slave/slave.go:1122-1175: members whose self.master still names it send
+ * their Update_metadata calls there) answers from its own maps: a host keeps
+ * them beside the engine's and swaps them in, with gh_set_master, to run
+ * those calls (gossipsim.Cluster). */
+int gh_export_files(void* h, int32_t* replicas, int32_t* versions, int32_t* timestamps, uint32_t* draws);
+int gh_import_files(void* h, const int32_t* replicas, const int32_t* versions, const int32_t* timestamps,
+                    const uint32_t* draws);
+/* The member whose list is the master's Member_list (placement candidates of
+ * gh_put / gh_repair, master/master.go:46); gh_create takes gh_config.master,
+ * gh_rebuild_meta sets the new master. */
+int gh_set_master(void* h, int32_t master);
 
 /* ---- multi-GPU: one cluster column-sharded over G ranks ----------------
  * Rank g holds all N observer rows for member columns [g*ncs, g*ncs+ncol)

@@ -112,6 +112,9 @@ def lib():
         L.or_put_conflicts.argtypes = [vp, vp, i64, i32, vp]
         L.or_get_files.argtypes = [vp, vp, i64, vp, vp]
         L.or_delete_files.argtypes = [vp, vp, i64, vp]
+        L.or_export_files.argtypes = [vp, vp, vp, vp, vp]
+        L.or_import_files.argtypes = [vp, vp, vp, vp, vp]
+        L.or_set_master.argtypes = [vp, i32]
         L.or_philox.argtypes = [vp, vp, vp]
         L.or_debug_shadow.argtypes = [vp, vp]
         _lib = L
@@ -268,6 +271,25 @@ class Oracle:
         rep = np.zeros((len(f), self.R), np.int32)
         self._chk(lib().or_delete_files(self.h, _p(f), len(f), _p(rep)))
         return rep
+
+    def export_files(self):
+        """The master's file metadata as flat arrays (gh_export_files)."""
+        F = int(self.cfg.max_files)
+        rep = np.empty((F, self.R), np.int32)
+        ver = np.empty(F, np.int32)
+        ts = np.empty(F, np.int32)
+        dr = np.empty(F, np.uint32)
+        self._chk(lib().or_export_files(self.h, _p(rep), _p(ver), _p(ts), _p(dr)))
+        return rep, ver, ts, dr
+
+    def import_files(self, rep, ver, ts, dr):
+        a = [np.ascontiguousarray(rep, dtype=np.int32), np.ascontiguousarray(ver, dtype=np.int32),
+             np.ascontiguousarray(ts, dtype=np.int32), np.ascontiguousarray(dr, dtype=np.uint32)]
+        self._chk(lib().or_import_files(self.h, *[_p(x) for x in a]))
+
+    def set_master(self, master):
+        self._chk(lib().or_set_master(self.h, int(master)))
+        self.cfg.master = int(master)
 
 
 def plan_tuple(e: PlanEntry):

@@ -915,6 +915,37 @@ int or_get_files(void *h, const int32_t *files, int64_t n, int32_t *replicas,
   return GH_OK;
 }
 
+/* The master's file metadata as flat arrays (gh_export_files /
+ * gh_import_files), and the master row (gh_set_master). */
+int or_export_files(void *h, int32_t *rep, int32_t *ver, int32_t *fts, uint32_t *draws) {
+  ors *s = (ors *)h;
+  if (!s || s->fcap <= 0) return GH_EINVAL;
+  const int R = s->cfg.replicas;
+  memcpy(rep, s->rep, sizeof(int32_t) * s->fcap * R);
+  memcpy(ver, s->ver, sizeof(int32_t) * s->fcap);
+  memcpy(fts, s->fts, sizeof(int32_t) * s->fcap);
+  memcpy(draws, s->draws, sizeof(uint32_t) * s->fcap);
+  return GH_OK;
+}
+
+int or_import_files(void *h, const int32_t *rep, const int32_t *ver, const int32_t *fts, const uint32_t *draws) {
+  ors *s = (ors *)h;
+  if (!s || s->fcap <= 0) return GH_EINVAL;
+  const int R = s->cfg.replicas;
+  memcpy(s->rep, rep, sizeof(int32_t) * s->fcap * R);
+  memcpy(s->ver, ver, sizeof(int32_t) * s->fcap);
+  memcpy(s->fts, fts, sizeof(int32_t) * s->fcap);
+  memcpy(s->draws, draws, sizeof(uint32_t) * s->fcap);
+  return GH_OK;
+}
+
+int or_set_master(void *h, int32_t master) {
+  ors *s = (ors *)h;
+  if (!s || master < 0 || master >= s->n) return GH_EINVAL;
+  s->cfg.master = master;
+  return GH_OK;
+}
+
 int or_delete_files(void *h, const int32_t *files, int64_t n, int32_t *old_replicas) {
   ors *s = (ors *)h;
   int R = s->cfg.replicas;

@@ -2425,6 +2425,82 @@ int gh_vote_scan(void* h, const int32_t* mview, int32_t* first, int32_t* list_le
   return GH_OK;
 }
 
+// The whole file table <-> this shard's slots (file f at slot f / G of shard
+// f % G): export allgathers every shard's slots; import keeps this shard's.
+int gh_export_files(void* h, int32_t* replicas, int32_t* versions, int32_t* timestamps, uint32_t* draws) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  if (e->cfg.max_files <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  const GhDev& d = e->d;
+  const int R = e->cfg.replicas, G = e->world;
+  const int64_t slots = d.fcap, W = slots * (R + 3);  // int32 words of one shard's slots
+  Staging st;
+  int rc;
+  if ((rc = st.alloc(e, sizeof(int32_t) * W * (G + 1)))) return rc;
+  int32_t* mine = st.as<int32_t>() + W * G;
+  HIPCHK(e, hipMemcpyAsync(mine, d.rep, sizeof(int32_t) * slots * R, hipMemcpyDeviceToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(mine + slots * R, d.ver, sizeof(int32_t) * slots, hipMemcpyDeviceToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(mine + slots * (R + 1), d.fts, sizeof(int32_t) * slots, hipMemcpyDeviceToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(mine + slots * (R + 2), d.draws, sizeof(int32_t) * slots, hipMemcpyDeviceToDevice, e->stream));
+  COMMCHK(e, e->comm->allgather(mine, st.p, sizeof(int32_t) * W, e->stream));
+  std::vector<int32_t> all((size_t)W * G);
+  HIPCHK(e, hipMemcpyAsync(all.data(), st.p, sizeof(int32_t) * W * G, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  for (int g = 0; g < G; ++g) {
+    const int32_t* b = all.data() + (size_t)W * g;
+    for (int64_t fl = 0; fl < slots; ++fl) {
+      const int64_t f = fl * G + g;
+      if (f >= e->cfg.max_files) break;
+      if (replicas)
+        for (int q = 0; q < R; ++q) replicas[f * R + q] = b[fl * R + q];
+      if (versions) versions[f] = b[slots * R + fl];
+      if (timestamps) timestamps[f] = b[slots * (R + 1) + fl];
+      if (draws) draws[f] = (uint32_t)b[slots * (R + 2) + fl];
+    }
+  }
+  return GH_OK;
+}
+
+int gh_import_files(void* h, const int32_t* replicas, const int32_t* versions, const int32_t* timestamps,
+                    const uint32_t* draws) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e || !replicas || !versions || !timestamps || !draws) return GH_EINVAL;
+  if (e->cfg.max_files <= 0) return set_err(e, GH_EINVAL, "engine created with max_files = 0");
+  const GhDev& d = e->d;
+  const int R = e->cfg.replicas, G = e->world;
+  const int64_t slots = d.fcap;
+  std::vector<int32_t> rep((size_t)slots * R, -1), ver(slots, -1), fts(slots, 0);
+  std::vector<uint32_t> dr(slots, 0);
+  for (int64_t fl = 0; fl < slots; ++fl) {
+    const int64_t f = fl * G + e->rank;
+    if (f >= e->cfg.max_files) break;
+    for (int q = 0; q < R; ++q) {
+      const int32_t a = replicas[f * R + q];
+      if (a < -1 || a >= e->n) return set_err(e, GH_EINVAL, "replica id out of range");
+      rep[fl * R + q] = a;
+    }
+    ver[fl] = versions[f];
+    fts[fl] = timestamps[f];
+    dr[fl] = draws[f];
+  }
+  HIPCHK(e, hipSetDevice(e->cfg.device));
+  HIPCHK(e, hipMemcpyAsync(d.rep, rep.data(), sizeof(int32_t) * rep.size(), hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(d.ver, ver.data(), sizeof(int32_t) * slots, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(d.fts, fts.data(), sizeof(int32_t) * slots, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(d.draws, dr.data(), sizeof(uint32_t) * slots, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  return GH_OK;
+}
+
+int gh_set_master(void* h, int32_t master) {
+  Engine* e = static_cast<Engine*>(h);
+  if (!e) return GH_EINVAL;
+  if (master < 0 || master >= e->n) return set_err(e, GH_EINVAL, "master");
+  e->cfg.master = master;
+  return GH_OK;
+}
+
 int gh_rebuild_meta(void* h, int32_t new_master, int32_t* f0, int64_t* n_files) {
   Engine* e = static_cast<Engine*>(h);
   if (!e) return GH_EINVAL;

@@ -193,6 +193,30 @@ class Engine:
         self._chk(self.lib.gh_file_info(self.h, C.byref(sl), C.byref(sh), C.byref(hd)))
         return {"slots": sl.value, "shards": sh.value, "held": hd.value}
 
+    def export_files(self):
+        """(replicas [F][R], versions [F], timestamps [F], draws [F]): the
+        master's file metadata (gh_export_files)."""
+        F = int(self.cfg.max_files)
+        rep = np.empty((F, self.R), np.int32)
+        ver = np.empty(F, np.int32)
+        ts = np.empty(F, np.int32)
+        dr = np.empty(F, np.uint32)
+        self._chk(self.lib.gh_export_files(self.h, _p(rep), _p(ver), _p(ts), _p(dr)))
+        return rep, ver, ts, dr
+
+    def import_files(self, rep, ver, ts, dr):
+        """Replace the file metadata (gh_import_files; export_files' arrays)."""
+        rep = np.ascontiguousarray(rep, dtype=np.int32)
+        ver = np.ascontiguousarray(ver, dtype=np.int32)
+        ts = np.ascontiguousarray(ts, dtype=np.int32)
+        dr = np.ascontiguousarray(dr, dtype=np.uint32)
+        self._chk(self.lib.gh_import_files(self.h, _p(rep), _p(ver), _p(ts), _p(dr)))
+
+    def set_master(self, master):
+        """The member whose list is the placement candidate list (gh_set_master)."""
+        self._chk(self.lib.gh_set_master(self.h, int(master)))
+        self.cfg.master = int(master)
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.gh_destroy(self.h)
@@ -488,6 +512,11 @@ class Cluster:
         # master (SDFSMaster's maps live in the process, master/master.go:38):
         # any other running member's metadata is empty
         self._meta_epoch = {self.master: 0}
+        # masters demoted by an election while their process kept running:
+        # member -> (process epoch, its maps as export_files arrays). Members
+        # whose self.master still names it send their Update_metadata there
+        # (Fail_recover, slave/slave.go:1122-1136), and it answers from these
+        self._demoted: dict[int, tuple[int, tuple]] = {}
 
     # REPL vocabulary (slave/slave.go:546-613)
     def join(self, member):
@@ -668,21 +697,45 @@ class Cluster:
                     m = int(self.mview[obs])
                     if m != self.master:
                         # a stale but running master answers from its own
-                        # SDFSMaster: empty unless this very process was the
-                        # master (a member demoted while running keeps its old
-                        # maps, which are not modelled). An empty plan:
-                        # Fail_recover returns at once (slave/slave.go:1139-1142)
-                        if self._meta_epoch.get(m) != self._epoch[m]:
+                        # SDFSMaster: the maps it kept when an election
+                        # demoted it, else (this process was never master)
+                        # empty maps, an empty plan: Fail_recover returns at
+                        # once (slave/slave.go:1139-1142)
+                        kept = self._demoted.get(m)
+                        if kept is not None and kept[0] == self._epoch[m] and self.engine.cfg.max_files > 0:
+                            plan = self._repair_at_demoted(m, obs)
+                            self.plans.append((r, obs, plan))
+                            self._copy_repairs(plan)
+                        elif self._meta_epoch.get(m) != self._epoch[m]:
                             self.plans.append((r, obs, ()))
                         continue
                 if self.engine.cfg.max_files > 0:
                     plan = tuple(self.engine.repair(obs))
                     self.plans.append((r, obs, plan))
-                    alive = self._running()
-                    for f, node1, v, st, new in plan:  # Re_put / Remote_reput copy the file (:1148-1170)
-                        if node1 >= 0:
-                            self._store(f, [a for a in new if alive[a]], v)
+                    self._copy_repairs(plan)
         return total
+
+    def _copy_repairs(self, plan):
+        alive = self._running()
+        for f, node1, v, st, new in plan:  # Re_put / Remote_reput copy the file (:1148-1170)
+            if node1 >= 0:
+                self._store(f, [a for a in new if alive[a]], v)
+
+    def _repair_at_demoted(self, m, obs):
+        """Update_metadata (master/master.go:74-127) run by the demoted but
+        running master m on its own maps, with its own list as Member_list:
+        m's maps and master row are swapped into the engine for the call and
+        the current master's swapped back."""
+        cur = self.engine.export_files()
+        self.engine.import_files(*self._demoted[m][1])
+        self.engine.set_master(m)
+        try:
+            plan = tuple(self.engine.repair(obs))
+            self._demoted[m] = (self._demoted[m][0], self.engine.export_files())
+        finally:
+            self.engine.import_files(*cur)
+            self.engine.set_master(self.master)
+        return plan
 
     # ---- master re-election (SPEC §9) -----------------------------------
     def _touch(self, x):  # `if self.VoteStatus.Vote == false {...}` (slave/slave.go:931-935, 969-973)
@@ -710,6 +763,11 @@ class Cluster:
                 self._fatal(r, m, "rebuild_file_meta: MemberList[0] unreachable")
                 continue
             if self.engine.cfg.max_files > 0:
+                old = self.master
+                if old != m and old not in self.dead and self._meta_epoch.get(old) == self._epoch[old]:
+                    # the old master's process runs on with its maps
+                    self._demoted[old] = (int(self._epoch[old]), self.engine.export_files())
+                self._demoted.pop(m, None)  # m's maps are the rebuilt ones now
                 f0, _ = self.engine.rebuild_meta(m)
             self.master = m
             self._meta_epoch[m] = int(self._epoch[m])

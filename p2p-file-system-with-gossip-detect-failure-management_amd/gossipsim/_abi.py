@@ -104,6 +104,9 @@ SYMBOLS = [
     ("gh_job_info", C.c_int, [_vp, _P(_i64), _P(_i64)]),
     ("gh_memory_info", C.c_int, [_vp, _P(_i64), _P(_i64), _P(_i64), _P(_i64)]),
     ("gh_file_info", C.c_int, [_vp, _P(_i64), _P(C.c_int32), _P(_i64)]),
+    ("gh_export_files", C.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    ("gh_import_files", C.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    ("gh_set_master", C.c_int, [_vp, C.c_int32]),
     ("gh_footprint", C.c_int, [_P(Config), _i32, _i32, _i32, _P(_i64), _P(_i64)]),
 ]
 

@@ -271,3 +271,99 @@ def test_repair_at_stale_running_master(gs):
     got = {o: plan for rr, o, plan in cl.plans if rr == r + 1}
     assert got[0] == () and obs in got
     cl.engine.close()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_cluster_demoted_master_keeps_running(gs, oracle_mod, world):
+    """A master demoted while its process keeps running answers from its
+    own maps (slave/slave.go:1122-1136 -> master/master.go:74-127): 16
+    members, master 0 stale in rows 2..15 (not crashed). Round 21 those rows
+    detect 0 and vote for their MemberList[0] = 1, which is elected and
+    rebuilds at round 23; the REMOVE of 0 reaches every row, 0's own too. Most
+    members never learn the new master (only MemberList_1[0] gets
+    Assign_new_master), so their Fail_recover calls go to 0, whose process
+    still runs: it runs Update_metadata on the maps it had when it was
+    demoted (gh_export_files / gh_import_files swap them into the engine,
+    with its own list as Member_list, gh_set_master), while 1 answers from
+    the rebuilt table. A crash of member 5 at round 23 gives more repairs
+    (0's own included). Every plan, and both masters' tables at the end,
+    against the oracle's Update_metadata on the same tables, routed by the
+    oracle Tally's self.master; world 2: the engine's file table sharded
+    by file ID."""
+    n, F = 16, 64
+    cfg = dict(max_files=F, seed=0x5EED0F37, t_fail=4, t_cleanup=6, fanout=3, peer_mode=gs.GH_PEER_PULL)
+    hb, ts, alive = sc.full_state(n, 2, 20)
+    ts[2:, 0] = 10  # rows 2..15 last heard of 0 ten rounds ago: detected at round 21
+    if world == 1:
+        cl = gs.Cluster(n, elect=True, **cfg)
+    else:  # the Cluster over 2 column shards (ID list order: the same lists here, no joins)
+        cl = gs.Cluster(n, elect=True, **cfg)
+        cl.engine.close()
+        cl.engine = gs.ShardGroup(gs.default_config(n, list_order=gs.GH_ORDER_ID, **cfg), world)
+    eng = cl.engine
+    orc = oracle_mod.Oracle(oracle_mod.default_config(n, **cfg))
+    try:
+        eng.import_state(hb, ts, alive, 20)
+        orc.import_state(hb, ts, alive, 20)
+        files = np.arange(F, dtype=np.int32)
+        cl.put(files)
+        orc.put(files)
+        tally = el.Tally(n, master=0)
+        master, demoted, dead = 0, {}, set()
+        due, pending, expect = {}, {}, []
+        for r in range(21, 45):
+            if r == 23:
+                cl.crash(5)
+                orc.apply_events([(gs.GH_EV_CRASH, 5)])
+                dead.add(5)
+            cl.tick(1)
+            s2 = orc.step(1)
+            assert eng.round == r
+            if s2["detections"]:
+                due.setdefault(r + cl.repair_delay, []).extend(int(x) for x in orc.read_detectors())
+            hbo, _, alo = orc.export_state()
+            for m in pending.pop(r, []):  # rebuild_file_meta at the new master m
+                lst = [int(c) for c in np.flatnonzero(hbo[m] >= 0)]
+                tally.finish_rebuild(m, lst[0])
+                old = orc.export_files()
+                if master != m and master not in dead:
+                    demoted[master] = old
+                demoted.pop(m, None)
+                er, ev, ef = el.rebuild(old[0], old[1], old[2], m, lst, now=r)
+                orc.import_files(er, ev, ef, old[3])
+                orc.set_master(m)
+                master = m
+                due.setdefault(r + cl.repair_delay, []).append(m)
+            for m in tally.round(alo, *el.vote_scan(hbo, tally.mview), dead=dead):
+                pending[r + 2] = pending.get(r + 2, []) + [m]
+            np.testing.assert_array_equal(cl.mview, tally.mview, err_msg=f"r={r}")
+            for obs in due.pop(r, []):
+                if obs in dead:
+                    continue
+                m = int(tally.mview[obs])
+                assert m not in dead  # (no Fail_recover log.Fatal in this scenario)
+                if m == master:
+                    expect.append((r, obs, tuple(orc.repair(obs))))
+                elif m in demoted:  # the demoted master's own maps and list
+                    cur = orc.export_files()
+                    orc.import_files(*demoted[m])
+                    orc.set_master(m)
+                    expect.append((r, obs, tuple(orc.repair(obs))))
+                    demoted[m] = orc.export_files()
+                    orc.import_files(*cur)
+                    orc.set_master(master)
+                else:
+                    expect.append((r, obs, ()))
+        assert cl.elections and cl.elections[0][1] == 1 and cl.master == 1 == master
+        assert 0 in cl._demoted and 0 in demoted
+        routed = [(r, o) for r, o, _ in expect if int(tally.mview[o]) == 0]
+        assert len(routed) >= 10, routed  # the stale master answered most repairs
+        assert any(p for r, o, p in expect if int(tally.mview[o]) == 0)  # ... with real plans
+        assert cl.plans == expect
+        for a, b in zip(eng.export_files(), orc.export_files()):
+            np.testing.assert_array_equal(a, b)
+        for a, b in zip(cl._demoted[0][1], demoted[0]):
+            np.testing.assert_array_equal(a, b)
+    finally:
+        eng.close()
+        orc.close()
