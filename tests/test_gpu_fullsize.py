@@ -459,27 +459,26 @@ def test_ring_receiver_65537_senders(gs, oracle_mod):
         orc.close()
 
 
-def test_n131072_single_vs_columns_g8(gs):
-    """N = 131,072, k = 4 pull, T_fail = 16: one engine (~130 GB) and 8
-    in-process column shards of the same cluster (~130 GB) on this GPU in
-    lockstep -- the sizes where a (row, 128-B line) offset no longer fits 31
-    bits in a (row x ld / 8) word index. Properties of any size (no failures:
-    every member stays everywhere, the own heartbeat advances one per round,
-    no view runs ahead of its owner, the epidemic reaches every cell), then a
-    1% crash detected everywhere; the shards' counters, failed sets and
-    detectors equal the engine's every round, sampled rows bit for bit."""
+def _single_vs_group(gs, n, layout, world, seed):
+    """One engine and `world` in-process shards of layout `layout` of the same
+    N-member cluster (k = 4 pull, T_fail = 16) in lockstep: 12 healthy
+    rounds (properties of any size: every member stays everywhere, the own
+    heartbeat advances one per round, no view runs ahead of its owner, the
+    epidemic reaches every cell, the nibble path runs), then a 1% crash
+    detected everywhere; the group's counters, failed sets and detectors
+    equal the engine's every round, sampled rows bit for bit."""
     from scenarios import crash_ids
-    n, rounds = 131072, 12
-    cfg = dict(fanout=4, seed=0x5EED0004, t_fail=16, t_cleanup=16)
+    rounds = 12
+    cfg = dict(fanout=4, seed=seed, t_fail=16, t_cleanup=16)
     one = gs.Engine(gs.default_config(n, **cfg))
     grp = None
     try:
-        grp = gs.ShardGroup(gs.default_config(n, shard_layout=0, **cfg), 8)
-        sample = (0, 1, 4095, 65535, 65536, 99999, n - 1)
+        grp = gs.ShardGroup(gs.default_config(n, shard_layout=layout, **cfg), world)
+        sample = (0, 1, 4095, n // 2 - 1, n // 2, n - 2, n - 1)
 
         def same_rows(r):
             for i in sample:
-                a, b = one.export_state(i, 1), grp.export_state(i, 1)
+                a, b = one.export_state(i, 1), grp.run("export_state", i, 1)[0]
                 for x, y in zip(a, b):
                     np.testing.assert_array_equal(x, y, err_msg=f"row {i} r={r}")
 
@@ -491,7 +490,7 @@ def test_n131072_single_vs_columns_g8(gs):
             s1 = one.step(1)
             t1 = time.perf_counter()
             s2 = grp.step(1)
-            print(f"  r={r}: engine {1e3 * (t1 - t0):.1f} ms, 8 shards {1e3 * (time.perf_counter() - t1):.1f} ms, "
+            print(f"  r={r}: engine {1e3 * (t1 - t0):.1f} ms, {world} shards {1e3 * (time.perf_counter() - t1):.1f} ms, "
                   f"{s1}", flush=True)
             assert s1 == s2, (r, s1, s2)
             assert s1["detections"] == 0 and s1["active_rows"] == n
@@ -504,7 +503,7 @@ def test_n131072_single_vs_columns_g8(gs):
             assert hb[0, i] == 2 + rounds
             assert (hb[0] >= 2).all() and (hb[0] <= 2 + rounds).all()
             assert (ts[0] <= rounds).all()
-        crashed = crash_ids(n, 0.01, 0x5EED0004)
+        crashed = crash_ids(n, 0.01, seed)
         ev = [(gs.GH_EV_CRASH, int(c)) for c in crashed]
         one.apply_events(ev)
         grp.apply_events(ev)
@@ -524,3 +523,20 @@ def test_n131072_single_vs_columns_g8(gs):
         if grp is not None:
             grp.close()
         one.close()
+
+
+def test_n98304_single_vs_rows_g8(gs):
+    """North_star's layout above N=65,536: N = 98,304, one engine (73 GB)
+    and 8 in-process row shards (12,288 observer rows each, the other
+    shards' sender plane rows by alltoallv into ghost tables; 166 GB) on this
+    GPU, in lockstep through the healthy rounds and a 1% crash
+    (_single_vs_group). The largest N at which one MI355X holds both."""
+    _single_vs_group(gs, 98304, 1, 8, 0x5EED0008)
+
+
+def test_n131072_single_vs_columns_g8(gs):
+    """N = 131,072, k = 4 pull, T_fail = 16: one engine (~130 GB) and 8
+    in-process column shards of the same cluster (~130 GB) on this GPU in
+    lockstep (_single_vs_group) -- the sizes where a (row, 128-B line)
+    offset no longer fits 31 bits in a (row x ld / 8) word index."""
+    _single_vs_group(gs, 131072, 0, 8, 0x5EED0004)
