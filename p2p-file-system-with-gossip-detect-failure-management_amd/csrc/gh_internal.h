@@ -358,6 +358,7 @@ struct GhDev {
   int32_t *post;         // [n]: post-REMOVE present counts of undecided rows (allreduced)
   int32_t *det_cnt[2], *det_min[2];
   uint32_t *dbits;
+  uint32_t *sbits;  // [ld/32 + 2]: the columns of dbits with exactly one detector (k_finish)
   // GH_REMOVE_LIST (the reference's REMOVE recipients, slave/slave.go:344;
   // one engine, member-ID list order): rcv[b] holds, per column c of the
   // REMOVE set of parity b, bit j of word c * nw + j / 32 = row j receives
@@ -733,8 +734,8 @@ __device__ __forceinline__ GhCell gh_get(const GhDev& d, int buf, int64_t i, int
 // Presence and flag bits of cells (i, c..c+7) of buffer buf (c % 8 == 0):
 // bit j = present, bit 8 + j = present and flagged. Narrow codes answer
 // directly (no base, no round).
-__device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, int64_t c) {
-  const uint4 x = gh_ld16(d, buf, i, c);
+// (x: the chunk's 16 B of narrow cells, loaded by the caller)
+__device__ __forceinline__ uint32_t gh_pf8x(const GhDev& d, int buf, int64_t i, int64_t c, const uint4& x) {
   const uint32_t h0 = x.x & 0xFFFFu;
   uint32_t out = 0;
   if (h0 == GH_N_WIDE || h0 == GH_N_FROZEN) {
@@ -752,6 +753,9 @@ __device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, i
     }
   }
   return out;
+}
+__device__ __forceinline__ uint32_t gh_pf8(const GhDev& d, int buf, int64_t i, int64_t c) {
+  return gh_pf8x(d, buf, i, c, gh_ld16(d, buf, i, c));
 }
 // The present cells of a tier chunk (bit j = cell j) from its lag word
 // alone: a code other than 15. A tier chunk holds no flag (a flagged cell is
@@ -928,7 +932,7 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s);
 // the input's tier and the plane select runs
 // t0 / t1: timing events stamped by the launch itself (hipExtLaunchKernel:
 // the dispatch packet's start and end, no separate event packets), or null
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant,
+bool launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant,
                   hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 // the nibble path's lane jobs (tiered engines; after launch_round, before
 // launch_round_slow): k_round_jobs, then the wide redo of the rare lanes
@@ -948,6 +952,9 @@ void launch_base(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_
 // carry-in + flag rewrite of the current table
 void launch_quirk_scan(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 void launch_quirk_apply(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
+// the same in one pass, one wave per row (whole rows on this engine: world 1
+// or row shards; tile widths >= 32)
+void launch_quirk_rows(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s);
 // events.hip
 void launch_count(const GhDev& d, int cur, const GhRound& p, hipStream_t s);
 void launch_fill(const GhDev& d, int cur, int32_t hb0, int32_t ts0, const GhRound& p,

@@ -45,6 +45,7 @@ struct Engine {
   hipStream_t vstream = nullptr, vstream2 = nullptr;
   hipEvent_t vfork = nullptr, vjoin = nullptr, vjoin2 = nullptr;
   hipEvent_t vstart = nullptr;  // the nibble launch's start stamp when not timing (the side stream's fork)
+  hipEvent_t vstop = nullptr;   // the last idle launch's end stamp when not timing (the join)
   GhDev d{};
   int cur = 0, dcur = 0;
   int32_t round = 0;
@@ -126,6 +127,8 @@ struct Engine {
   // events around them, and the device logs which variant ran (vlog).
   // tmode 0: every variant launch carries its own events.
   int tmode = 1;
+  int join_stamp = 1;  // GH_JOIN_STAMP=0: the join as an event recorded after the side stream's last launch (A/B)
+  int quirk_rows = 1;  // GH_QUIRK_ROWS=0: the two-sweep quirk pre-pass where the one-pass row walk applies (A/B)
   int side_order = 0;  // GH_SIDE_ORDER=1: the side stream's idle variants as IN 1, IN 3, storm, IN 6 (A/B)
   int32_t* vlog = nullptr;
   int64_t vlog_cap = 0;
@@ -386,6 +389,7 @@ int reset_pending_removes(Engine* e) {
     HIPCHK(e, hipMemsetAsync(d.det_min[b], 0x7F, sizeof(int32_t) * e->ld, e->stream));
   }
   HIPCHK(e, hipMemsetAsync(d.dbits, 0, sizeof(uint32_t) * (e->ld / 32 + 2), e->stream));
+  HIPCHK(e, hipMemsetAsync(d.sbits, 0, sizeof(uint32_t) * (e->ld / 32 + 2), e->stream));
   HIPCHK(e, hipMemsetAsync(d.nd, 0, sizeof(int32_t) * 8, e->stream));
   HIPCHK(e, hipMemsetAsync(d.det_any, 0, e->n, e->stream));
   e->last_nd = 0;  // (only the rounds and this reset write nd[0..1])
@@ -1087,6 +1091,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (const char* v = std::getenv("GH_SIDE")) e->side = std::min(2, std::max(0, std::atoi(v)));
   if (const char* v = std::getenv("GH_TMODE")) e->tmode = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_SIDE_ORDER")) e->side_order = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_JOIN_STAMP")) e->join_stamp = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_QUIRK_ROWS")) e->quirk_rows = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_C8")) e->c8 = e->c8 && std::atoi(v) != 0;
   if (cfg->shard_layout != GH_LAYOUT_COLUMNS && cfg->shard_layout != GH_LAYOUT_ROWS) {
     delete e;
@@ -1141,7 +1147,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
                hipEventCreateWithFlags(&e->vfork, hipEventDisableTiming) != hipSuccess ||
                hipEventCreateWithFlags(&e->vjoin, hipEventDisableTiming) != hipSuccess ||
                hipEventCreateWithFlags(&e->vjoin2, hipEventDisableTiming) != hipSuccess ||
-               hipEventCreate(&e->vstart) != hipSuccess)) {
+               hipEventCreate(&e->vstart) != hipSuccess || hipEventCreate(&e->vstop) != hipSuccess)) {
     gh_destroy(e);  // the streams and events created before the failing one, and the communicator
     return GH_EHIP;
   }
@@ -1229,7 +1235,8 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
       break;
     if ((rc = dalloc(e, &d.det_cnt[0], e->ld, 0)) || (rc = dalloc(e, &d.det_cnt[1], e->ld, 0)) ||
         (rc = dalloc(e, &d.det_min[0], e->ld, 0x7F)) || (rc = dalloc(e, &d.det_min[1], e->ld, 0x7F)) ||
-        (rc = dalloc(e, &d.dbits, e->ld / 32 + 2, 0)) || (rc = dalloc(e, &d.dlist, 2 * e->ld, 0)) ||
+        (rc = dalloc(e, &d.dbits, e->ld / 32 + 2, 0)) || (rc = dalloc(e, &d.sbits, e->ld / 32 + 2, 0)) ||
+        (rc = dalloc(e, &d.dlist, 2 * e->ld, 0)) ||
         (rc = dalloc(e, &d.nd, 8, 0)) || (rc = dalloc(e, &d.shadow, e->ld, 0x80)) ||
         (rc = dalloc(e, &d.nshadow, 1, 0)))
       break;
@@ -1357,6 +1364,11 @@ int quirk_flags(Engine* e, const GhRound& p) {
   GhDev& d = e->d;
   if (e->lorder) {  // runs over the list order
     launch_quirk_list(d, e->cur, e->dcur, p, e->lcur, e->stream);
+    HIPCHK(e, hipGetLastError());
+    return GH_OK;
+  }
+  if (e->quirk_rows && (e->world == 1 || e->rowlay) && d.tw >= 32) {  // whole rows here: one pass
+    launch_quirk_rows(d, e->cur, e->dcur, p, e->stream);
     HIPCHK(e, hipGetLastError());
     return GH_OK;
   }
@@ -1548,6 +1560,7 @@ void gh_destroy(void* h) {
   if (e->vjoin) (void)hipEventDestroy(e->vjoin);
   if (e->vjoin2) (void)hipEventDestroy(e->vjoin2);
   if (e->vstart) (void)hipEventDestroy(e->vstart);
+  if (e->vstop) (void)hipEventDestroy(e->vstop);
   delete e;
 }
 
@@ -1980,10 +1993,22 @@ int gh_step(void* h, int32_t rounds, gh_round_stats* stats) {
       hipEvent_t st = e->timing ? ev(mv, 0) : e->vstart;
       launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, mv, st, ev(mv, 1));
       HIPCHK(e, hipStreamWaitEvent(e->vstream, st, 0));
-      for (int x = 0; x < nside; ++x)
-        launch_round(e->d, e->cur, e->dcur, pr, e->vstream, e->nt, sides[x], ev(sides[x], 0), ev(sides[x], 1));
-      HIPCHK(e, hipEventRecord(e->vjoin, e->vstream));
-      HIPCHK(e, hipStreamWaitEvent(e->stream, e->vjoin, 0));
+      // joined at the last idle launch's own end stamp (as the fork uses the
+      // nibble launch's start stamp), not at an event packet after it
+      // (a last launch that did not happen, e.g. IN 6 on row shards: an event
+      // packet after the others)
+      hipEvent_t jn = nullptr;
+      for (int x = 0; x < nside; ++x) {
+        hipEvent_t t1 = ev(sides[x], 1);
+        const bool last = x == nside - 1 && e->join_stamp;
+        if (last && !t1) t1 = e->vstop;
+        if (launch_round(e->d, e->cur, e->dcur, pr, e->vstream, e->nt, sides[x], ev(sides[x], 0), t1) && last) jn = t1;
+      }
+      if (!jn) {
+        HIPCHK(e, hipEventRecord(e->vjoin, e->vstream));
+        jn = e->vjoin;
+      }
+      HIPCHK(e, hipStreamWaitEvent(e->stream, jn, 0));
     } else {  // lean 16-bit input, storm
       for (int v = 0; v < 2; ++v) launch_round(e->d, e->cur, e->dcur, pr, e->stream, e->nt, v, ev(v, 0), ev(v, 1));
     }

@@ -341,11 +341,24 @@ struct SegWalk {
 };
 
 // 8-bit REMOVE mask of local columns l0..l0+7 at row i (l0 % 8 == 0)
+// (one detector's column is REMOVE'd at every row but that detector's:
+// only those columns, sbits, look at det_min)
 __device__ __forceinline__ uint32_t removed8(const GhDev& d, int dcur, int64_t l0, int i) {
-  uint32_t m = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
-  uint32_t out = 0;
-  for (int j = 0; j < 8; ++j)
-    if (((m >> j) & 1u) && gh_rm_at(d, dcur, l0 + j, i)) out |= 1u << j;
+  const uint32_t m = (d.dbits[l0 >> 5] >> (l0 & 31)) & 0xFFu;
+  if (!m) return 0u;
+  if (d.rlist) {
+    uint32_t out = 0;
+    for (int j = 0; j < 8; ++j)
+      if (((m >> j) & 1u) && gh_rm_at(d, dcur, l0 + j, i)) out |= 1u << j;
+    return out;
+  }
+  uint32_t sm = (d.sbits[l0 >> 5] >> (l0 & 31)) & m;
+  uint32_t out = m & ~sm;
+  while (sm) {
+    const int j = __builtin_ctz(sm);
+    sm &= sm - 1u;
+    if (d.det_min[dcur][l0 + j] != i) out |= 1u << j;
+  }
   return out;
 }
 
@@ -2833,19 +2846,22 @@ __device__ void redo_all(const GhDev& d, int cur, int dcur, const GhRound& p) {
 __global__ __launch_bounds__(256) void k_finish(GhDev d, int dcur, GhRound p) {
   const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int dnew = dcur ^ 1;
-  bool has = false;
+  bool has = false, sole = false;
   if (x == 0) d.aq[0] = 0;  // the next round's writers of base_col / the inbox pass set it
   if (x < p.ld) {
     has = d.det_cnt[dnew][x] > 0;
+    sole = d.det_cnt[dnew][x] == 1;
     d.det_cnt[dcur][x] = 0;
     d.det_min[dcur][x] = INT_MAX;
   }
-  const unsigned long long m = __ballot(has);
+  const unsigned long long m = __ballot(has), ms = __ballot(sole);
   const int lane = threadIdx.x & 63;
   if (x - lane < p.ld && lane == 0) {
     const int64_t w = (x - lane) >> 5;
     d.dbits[w] = (uint32_t)m;
     d.dbits[w + 1] = (uint32_t)(m >> 32);
+    d.sbits[w] = (uint32_t)ms;
+    d.sbits[w + 1] = (uint32_t)(ms >> 32);
     if (m) {
       atomicAdd(&d.nd[dnew], __popcll(m));
       if (!d.rowlay || d.rank == 0)  // row layout: every shard holds all columns
@@ -3162,6 +3178,156 @@ __global__ __launch_bounds__(256) void k_quirk_apply(GhDev d, int cur, int dcur,
   }
 }
 
+// The run state of 32 consecutive cells with list members P and candidates
+// F (F within P), in q_summary8's closed form.
+__device__ __forceinline__ int q_summary32(uint32_t P, uint32_t F) {
+  if (!P) return 0;
+  const uint32_t B = P & ~F;
+  if (B) return 5 | ((__builtin_popcount((F >> (31 - __builtin_clz(B))) >> 1) & 1) << 1);
+  return 4 | ((__builtin_popcount(F) & 1) << 1);
+}
+
+// List members and candidates of row i's 32 cells c0..c0+31 (c0 % 32 == 0,
+// one tile segment: TW >= 32) after step 1's REMOVE, from the chunks' age
+// and lag words au, qu (tier) and the columns' REMOVE and one-detector bits
+// rmw, smw. Only an escaped chunk can hold a flag: the escaped chunks' 16-bit
+// cells are loaded together before any is decoded (one load latency per
+// window, not four).
+__device__ __forceinline__ void quirk_lane32(const GhDev& d, int cur, int dcur, int i, int64_t c0, bool tier, bool in,
+                                             const v4u& au, const v4u& qu, uint32_t rmw, uint32_t smw, uint32_t& P,
+                                             uint32_t& F) {
+  P = F = 0u;
+  if (!in) return;
+  uint4 hx[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    hx[k] = uint4{0u, 0u, 0u, 0u};
+    if (!tier || gh_t4_esc(au[k])) hx[k] = gh_ld16(d, cur, i, c0 + 8 * k);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t c = c0 + 8 * k;
+    // removed8 from the preloaded words: a one-detector column spares its detector's row
+    const uint32_t m = (rmw >> (8 * k)) & 0xFFu;
+    uint32_t sm = (smw >> (8 * k)) & m, rm8 = m & ~sm;
+    if (d.rlist) {
+      rm8 = m ? removed8(d, dcur, c, i) : 0u;
+      sm = 0u;
+    }
+    while (sm) {
+      const int j = __builtin_ctz(sm);
+      sm &= sm - 1u;
+      if (d.det_min[dcur][c + j] != i) rm8 |= 1u << j;
+    }
+    uint32_t pk, fk = 0u;
+    if (tier && !gh_t4_esc(au[k])) {
+      pk = gh_t4_present8(qu[k]) & ~rm8;  // a tier chunk: no candidate
+    } else {
+      const uint32_t pf = gh_pf8x(d, cur, i, c, hx[k]);
+      pk = pf & ~rm8 & 0xFFu;
+      fk = (pf >> 8) & pk;
+    }
+    P |= pk << (8 * k);
+    F |= fk << (8 * k);
+  }
+}
+__device__ __forceinline__ void quirk_load32(const GhDev& d, int cur, int i, int64_t c0, bool tier, bool in, v4u& au,
+                                             v4u& qu, uint32_t& rmw, uint32_t& smw) {
+  au = qu = v4u{0u, 0u, 0u, 0u};
+  rmw = smw = 0u;
+  if (!in) return;
+  if (tier) {
+    const int64_t wi = gh_cell(d, i, c0) >> 3;  // (4-word aligned)
+    au = *reinterpret_cast<const v4u*>(d.a4[cur] + wi);
+    qu = *reinterpret_cast<const v4u*>(d.pl[cur] + wi);
+  }
+  rmw = d.dbits[c0 >> 5];
+  smw = d.sbits[c0 >> 5];
+}
+
+// Quirk-mode detection in one pass when every row is whole on this engine
+// (one engine, or row shards), tile widths >= 32: one wave per row walks it
+// in member order, 2,048 cells (64 lanes x 32) per window and QW windows'
+// loads per step, the run state carried from window to window (a wave scan
+// of the lanes' summaries), and clears the flag of every candidate at an
+// odd run offset that is not the row's last list entry (found first, from
+// the row's end). The same flags as k_quirk_sum + k_quirk_prefix +
+// k_quirk_apply, which sweep the table twice (slave/slave.go:464-477 with
+// :283; SPEC §4).
+template <int TW>
+__global__ __launch_bounds__(256) void k_quirk_rows(GhDev d, int cur, int dcur, GhRound p) {
+  if (p.qgate && d.cntg[p.n + 1] == 0) return;  // no candidate in the table
+  constexpr int QW = 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t nwv = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const bool tier = gh_m8(d, cur);
+  const int64_t nwin = (p.ld + 2047) / 2048;
+  for (int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; r < d.nrows; r += nwv) {
+    const int i = (int)(d.row0 + r);
+    if (!(d.alive[i] && d.active[i])) continue;  // only active rows detect (and send)
+    // the row's last list entry (usually in the last window)
+    int64_t lastc = -1;
+    for (int64_t w = nwin - 1; w >= 0 && lastc < 0; --w) {
+      const int64_t c0 = w * 2048 + lane * 32;
+      v4u au, qu;
+      uint32_t rmw, smw, P, F;
+      quirk_load32(d, cur, i, c0, tier, c0 < p.ld, au, qu, rmw, smw);
+      quirk_lane32(d, cur, dcur, i, c0, tier, c0 < p.ld, au, qu, rmw, smw, P, F);
+      const unsigned long long b = __ballot(P != 0u);
+      if (b) {
+        const int hl = 63 - __builtin_clzll(b);
+        const int hp = __shfl(P ? 31 - __builtin_clz(P) : 0, hl);
+        lastc = w * 2048 + hl * 32 + hp;
+      }
+    }
+    if (lastc < 0) continue;  // an empty list: no candidate
+    const int64_t wend = lastc / 2048 + 1;  // windows up to the last entry's
+    int carry = 0;                          // run state entering the window
+    for (int64_t w0 = 0; w0 < wend; w0 += QW) {
+      v4u au[QW], qu[QW];
+      uint32_t rmw[QW], smw[QW], P[QW], F[QW];
+#pragma unroll
+      for (int u = 0; u < QW; ++u) {
+        const int64_t c0 = (w0 + u) * 2048 + lane * 32;
+        quirk_load32(d, cur, i, c0, tier, w0 + u < wend && c0 < p.ld, au[u], qu[u], rmw[u], smw[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < QW; ++u) {
+        const int64_t c0 = (w0 + u) * 2048 + lane * 32;
+        quirk_lane32(d, cur, dcur, i, c0, tier, w0 + u < wend && c0 < p.ld, au[u], qu[u], rmw[u], smw[u], P[u], F[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < QW; ++u) {
+        int incl = q_summary32(P[u], F[u]);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int other = __shfl_up(incl, o);
+          if (lane >= o) incl = q_compose(other, incl);
+        }
+        int excl = __shfl_up(incl, 1);
+        if (lane == 0) excl = 0;
+        int st = q_apply(excl, carry);
+        carry = q_apply(__shfl(incl, 63), carry);
+        if (!F[u]) continue;
+        const int64_t c0 = (w0 + u) * 2048 + lane * 32;
+        uint32_t clear = 0u;
+        for (int j = 0; j < 32; ++j) {
+          if (!((P[u] >> j) & 1u)) continue;
+          if (!((F[u] >> j) & 1u)) {
+            st = 0;
+            continue;
+          }
+          if (st != 0 && c0 + j != lastc) clear |= 1u << j;  // skipped this round
+          st ^= 1;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if ((clear >> (8 * k)) & 0xFFu) gh_clearflags8(d, cur, i, c0 + 8 * k, (clear >> (8 * k)) & 0xFFu);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 // d.tw -> template tile width
@@ -3188,6 +3354,13 @@ static void quirk_sum(const GhDev& d, int cur, int dcur, const GhRound& p, hipSt
     hipLaunchKernelGGL(k_quirk_sum<TW>, dim3(seg_grid(p, TW)), dim3(256), 0, s, d, cur, dcur, p);
 }
 template <int TW>
+static void quirk_rows(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  if constexpr (TW >= 32) {
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((d.nrows + 3) / 4, 16384));
+    hipLaunchKernelGGL(k_quirk_rows<TW>, dim3(g), dim3(256), 0, s, d, cur, dcur, p);
+  }
+}
+template <int TW>
 static void quirk_apply(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_quirk_apply<TW>, dim3(seg_grid(p, TW)), dim3(256), 0, s, d, cur, dcur, p);
 }
@@ -3199,6 +3372,10 @@ static void ring_tiles(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
 void launch_quirk_scan(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
   GH_TW_DISPATCH(quirk_sum, d, cur, dcur, p, s)
   hipLaunchKernelGGL(k_quirk_prefix, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
+}
+
+void launch_quirk_rows(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
+  GH_TW_DISPATCH(quirk_rows, d, cur, dcur, p, s)
 }
 
 void launch_quirk_apply(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
@@ -3264,12 +3441,12 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
 // by the 16-bit rule, 3 the nibble path (IN 2, or IN 4 on row shards), 4 the
 // nibble path that takes REMOVE deliveries (IN 6, column layout)
 template <int KB, int TW, int TPW>
-static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant,
+static bool launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int variant,
                              hipEvent_t t0, hipEvent_t t1) {
   constexpr int RB = round_rb<TW>();
   const int64_t nrb = (d.nrows + RB - 1) / RB;
   const int64_t nblk = nrb * (p.ld / TW / TPW);
-  if (nblk == 0) return;
+  if (nblk == 0) return false;
   const bool tiered = d.a4[0] != nullptr;
   const bool few = variant == 1 || variant == 2 || (variant == 0 && tiered);
   // (a resident-sized grid for the persistent variants, 1,280 workgroups for
@@ -3292,8 +3469,8 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
   if constexpr (KB == 4 && TPW == 1 && TW >= 64) {  // a tiered engine (host: c8)
     if (tiered) {
       switch (variant) {
-        case 0: GH_ROUND_NT(false, 3); return;
-        case 2: GH_ROUND_NT(false, 1); return;
+        case 0: GH_ROUND_NT(false, 3); return true;
+        case 2: GH_ROUND_NT(false, 1); return true;
         case 3:
           if (d.rowlay)
             GH_ROUND_NT(false, 4);  // row layout: ghost senders
@@ -3301,10 +3478,11 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
             GH_ROUND_NT(false, 5);  // LDS-DMA staging
           else
             GH_ROUND_NT(false, 2);
-          return;
+          return true;
         case 4:  // the nibble path that takes REMOVE deliveries (column layout; returns at once otherwise)
-          if (!d.rowlay) GH_ROUND_NT(false, 6);
-          return;
+          if (d.rowlay) return false;
+          GH_ROUND_NT(false, 6);
+          return true;
         default: break;
       }
     }
@@ -3313,6 +3491,9 @@ static void launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
     GH_ROUND_NT(true, 0);
   else if (variant == 0)
     GH_ROUND_NT(false, 0);
+  else
+    return false;
+  return true;
 #undef GH_ROUND_NT
 #undef GH_ROUND_LAUNCH
 }
@@ -3325,35 +3506,34 @@ static void round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipS
 
 // tiles per workgroup: ld / TW is a multiple of 8 (host padding)
 template <int KB, int TW>
-static void launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm,
+static bool launch_round_tw(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm,
                             hipEvent_t t0, hipEvent_t t1) {
   switch (p.tpw) {
-    case 1: launch_round_tpw<KB, TW, 1>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
-    case 2: launch_round_tpw<KB, TW, 2>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
-    case 8: launch_round_tpw<KB, TW, 8>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
-    default: launch_round_tpw<KB, TW, 4>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
+    case 1: return launch_round_tpw<KB, TW, 1>(d, cur, dcur, p, s, nt, storm, t0, t1);
+    case 2: return launch_round_tpw<KB, TW, 2>(d, cur, dcur, p, s, nt, storm, t0, t1);
+    case 8: return launch_round_tpw<KB, TW, 8>(d, cur, dcur, p, s, nt, storm, t0, t1);
+    default: return launch_round_tpw<KB, TW, 4>(d, cur, dcur, p, s, nt, storm, t0, t1);
   }
 }
 
 template <int KB>
-static void launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm,
+static bool launch_round_kb(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm,
                             hipEvent_t t0, hipEvent_t t1) {
   switch (d.tw) {
-    case 8: launch_round_tw<KB, 8>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
-    case 16: launch_round_tw<KB, 16>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
-    case 32: launch_round_tw<KB, 32>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
-    case 128: launch_round_tw<KB, 128>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
-    case 256: launch_round_tw<KB, 256>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
-    default: launch_round_tw<KB, 64>(d, cur, dcur, p, s, nt, storm, t0, t1); break;
+    case 8: return launch_round_tw<KB, 8>(d, cur, dcur, p, s, nt, storm, t0, t1);
+    case 16: return launch_round_tw<KB, 16>(d, cur, dcur, p, s, nt, storm, t0, t1);
+    case 32: return launch_round_tw<KB, 32>(d, cur, dcur, p, s, nt, storm, t0, t1);
+    case 128: return launch_round_tw<KB, 128>(d, cur, dcur, p, s, nt, storm, t0, t1);
+    case 256: return launch_round_tw<KB, 256>(d, cur, dcur, p, s, nt, storm, t0, t1);
+    default: return launch_round_tw<KB, 64>(d, cur, dcur, p, s, nt, storm, t0, t1);
   }
 }
 
-void launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm, hipEvent_t t0,
+bool launch_round(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s, bool nt, int storm, hipEvent_t t0,
                   hipEvent_t t1) {
   if (p.peer_mode == GH_PEER_PULL && p.k <= 4)
-    launch_round_kb<4>(d, cur, dcur, p, s, nt, storm, t0, t1);
-  else
-    launch_round_kb<8>(d, cur, dcur, p, s, nt, storm, t0, t1);
+    return launch_round_kb<4>(d, cur, dcur, p, s, nt, storm, t0, t1);
+  return launch_round_kb<8>(d, cur, dcur, p, s, nt, storm, t0, t1);
 }
 
 void launch_base(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
