@@ -175,6 +175,12 @@
 #ifndef GH_NIB_WAVES
 #define GH_NIB_WAVES 1          // nibble path: min waves per SIMD it is compiled for (1: the compiler picks)
 #endif
+#ifndef GH_RMV_WAVES
+#define GH_RMV_WAVES 1          // k_round IN 7 (IN 6 on a full grid): min waves per SIMD (1: the compiler picks)
+#endif
+#ifndef GH_RMV_FULL7
+#define GH_RMV_FULL7 1          // 0: the host's full-grid REMOVE launch is IN 6 with its block loop (A/B build)
+#endif
 // nibble path cache policies (gfx950 buffer aux bits: 1 sc0, 2 nt, 16 sc1):
 // the own age words (read once), the own lag words (also gathered by the
 // tile's receivers), the sender gathers, and the stores of both planes

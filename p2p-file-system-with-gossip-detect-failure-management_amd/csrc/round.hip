@@ -22,6 +22,7 @@
 //   k_finish       per column: the failed-set bitmap D_r for the next round.
 // Member columns are local to the engine's shard (gh_internal.h); rows,
 // alive/active and the inboxes are global.
+#include <cstdlib>
 #include <limits.h>
 
 #include <algorithm>
@@ -2152,7 +2153,7 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 // idle they are a small dispatch (IN 6 too: compiled for 6 waves per SIMD,
 // as its block loop left to the compiler took 106 VGPRs).
 template <int KB, int TW, int TPW, bool NT, bool STORM, int IN>
-__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : IN == 6 ? 6 : (IN == 2 || IN == 4 || IN == 5) ? GH_NIB_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
+__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : IN == 6 ? 6 : IN == 7 ? GH_RMV_WAVES : (IN == 2 || IN == 4 || IN == 5) ? GH_NIB_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
   if (*d.mode != (int)STORM) return;
   if constexpr (!STORM) {
     int want = 0;
@@ -2164,12 +2165,12 @@ __global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM 
     // (p.rmv_full: the host launched IN 6 in place of IN 2, so IN 6 must run
     // whatever the device's count says: the round's nibble path is never skipped)
     if (want == 2 && (p.rmv_full || p.nib_rmv == 2 || (p.nib_rmv && d.cntg[p.n] > 0))) want = 6;
-    if (want != IN) return;
+    if (want != (IN == 7 ? 6 : IN)) return;  // (IN 7: IN 6 on a full grid)
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    d.m8[4] = STORM ? 1 : (IN == 2 || IN == 4 || IN == 5 || IN == 6) ? 3 : IN == 1 ? 2 : 0;
+    d.m8[4] = STORM ? 1 : (IN == 2 || IN == 4 || IN == 5 || IN == 6 || IN == 7) ? 3 : IN == 1 ? 2 : 0;
     // launch_round's variant number of this launch (IN 3 is variant 0 of a tiered engine)
-    if (d.vlog) d.vlog[p.vslot] = STORM ? 1 : IN == 6 ? 4 : (IN == 2 || IN == 4 || IN == 5) ? 3 : IN == 1 ? 2 : 0;
+    if (d.vlog) d.vlog[p.vslot] = STORM ? 1 : (IN == 6 || IN == 7) ? 4 : (IN == 2 || IN == 4 || IN == 5) ? 3 : IN == 1 ? 2 : 0;
   }
   // every running row a quiet candidate and no base moved (one engine): the
   // round reads and writes nothing (a collapsed cluster)
@@ -2188,6 +2189,11 @@ __global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM 
     round_block_nib<TW, NT, GH_NIB_CPL, false, false, false>(d, cur, dcur, p, blockIdx.x);  // one block per workgroup
   } else if constexpr (IN == 4) {
     round_block_nib<TW, NT, GH_NIB_CPL, true>(d, cur, dcur, p, blockIdx.x);
+  } else if constexpr (IN == 7) {
+    // IN 6 when the host knows a REMOVE is pending (p.rmv_full, the round's
+    // stream): one block per workgroup, no block loop (the loop's registers
+    // had spilled 72 bytes per lane at 6 waves)
+    round_block_nib<TW, NT, GH_NIB_CPL, false>(d, cur, dcur, p, blockIdx.x);
   } else if constexpr (IN == 6) {
     // launched on the side stream every round and idle in most: a grid of
     // 1/8 of the workgroups (an idle full grid cost 30 us of dispatch behind
@@ -3437,6 +3443,15 @@ void launch_inbox(const GhDev& d, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_inbox_fill, dim3((p.n + 255) / 256), dim3(256), 0, s, d, p);
 }
 
+// the full-grid REMOVE launch as IN 7 (GH_RMV_FULL7=0 at run time: IN 6, A/B)
+static bool rmv_full7() {
+  static const bool on = [] {
+    const char* v = std::getenv("GH_RMV_FULL7");
+    return GH_RMV_FULL7 && (!v || std::atoi(v) != 0);
+  }();
+  return on;
+}
+
 // variant: 0 lean on a 16-bit input, 1 storm, 2 lean on a 4-bit-tier input
 // by the 16-bit rule, 3 the nibble path (IN 2, or IN 4 on row shards), 4 the
 // nibble path that takes REMOVE deliveries (IN 6, column layout)
@@ -3481,7 +3496,10 @@ static bool launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
           return true;
         case 4:  // the nibble path that takes REMOVE deliveries (column layout; returns at once otherwise)
           if (d.rowlay) return false;
-          GH_ROUND_NT(false, 6);
+          if (p.rmv_full && rmv_full7())
+            GH_ROUND_NT(false, 7);
+          else
+            GH_ROUND_NT(false, 6);
           return true;
         default: break;
       }
