@@ -197,6 +197,9 @@
 #define GH_NIB_ST_AUX 18  // sc1 | nt: the next round's lines leave the XCD's L2 instead of displacing this
                           // round's sender lines (2, nt, keeps them: 2.08 against 2.04 ms, profiles/r05_s32_*)
 #endif
+#ifndef GH_JOBF_WAVES
+#define GH_JOBF_WAVES 3         // the flat lane-job kernel (k_round_jobs_flat): at 4 its rule spilled
+#endif
 #ifndef GH_JOB_WAVES
 #define GH_JOB_WAVES 4          // lane-job kernel: min waves per SIMD it is compiled for (A/B: 4 beats 3 and 5)
 #endif

@@ -2770,6 +2770,117 @@ __global__ __launch_bounds__(256, GH_JOB_WAVES) void k_round_jobs(GhDev d, int c
   }
 }
 
+// The same lane jobs with every lane busy: a wave takes 64 (nibble
+// workgroup, wave) job regions at once, scans their job counts and deals the
+// jobs out one per lane (a region usually holds one or two, so the
+// one-region-at-a-time form above ran most of its lanes empty and synced
+// its workgroup twice per region). Detections and row counts go straight to
+// the global counters (a region's jobs rarely share a column or a row).
+template <int TW, int CPL>
+__global__ __launch_bounds__(256, GH_JOBF_WAVES) void k_round_jobs_flat(GhDev d, int cur, int dcur, GhRound p) {
+  if (d.m8[4] != 3) return;
+  const int nlist = d.njobs[3];  // the nibble workgroups with jobs (none in a quiet steady-state round)
+  if (nlist == 0) return;
+  constexpr int W = CPL / 8;
+  __shared__ unsigned long long s_st[6];  // unknown, tomb, det, rel, merged, escaped chunks
+  __shared__ int s_jobs, s_flag;
+  // per wave: its 64 regions' inclusive job counts and region indices (in LDS,
+  // not registers: the job rule needs all 128 the 4-wave bound leaves)
+  __shared__ int s_incl[4][64];
+  __shared__ int s_reg[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nxt = cur ^ 1;
+  if (threadIdx.x < 6) s_st[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_jobs = s_flag = 0;
+  __syncthreads();
+  JobAcc tot{};
+  const int64_t nslot = (int64_t)nlist * 4;
+  const int64_t nwv = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t s0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; s0 < nslot; s0 += nwv * 64) {
+    const int64_t sl = s0 + lane;
+    int reg = 0, nj = 0;
+    if (sl < nslot) {
+      reg = d.jlist[sl >> 2] * 4 + (int)(sl & 3);
+      nj = d.jobn[reg];
+    }
+    int incl = nj;  // inclusive scan of the regions' job counts
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    const int total = __builtin_amdgcn_readfirstlane(__shfl(incl, 63));  // (wave-uniform)
+    if (lane == 0 && total) atomicAdd(&s_jobs, total);
+    __builtin_amdgcn_wave_barrier();  // (the last step's reads of this wave's slots are done)
+    s_incl[wave][lane] = incl;
+    s_reg[wave][lane] = reg;
+    __builtin_amdgcn_wave_barrier();
+    for (int base = 0; base < total; base += 64) {
+      const int t = base + lane;
+      if (t >= total) continue;
+      // the region holding job t: the first slot whose inclusive count exceeds t
+      int lo = 0;
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1)
+        if (s_incl[wave][lo + st - 1] <= t) lo += st;
+      const int before = lo ? s_incl[wave][lo - 1] : 0;
+      const uint4* jreg = d.jobs + (int64_t)s_reg[wave][lo] * GH_JOB_CAP * 2;
+      const int e = t - before;
+      const uint4 jb = jreg[2 * e];
+      const uint4 jo = jreg[2 * e + 1];  // the lane's own lag words, age words
+      const int i = (int)jb.x;
+      const int64_t l0 = (int64_t)(jb.y >> 8) * TW + (int64_t)(jb.y & 255u) * CPL;
+      uint32_t detl = 0;  // detections, bit 8 w + j
+      JobAcc a{};
+      bool fit = true;
+#pragma unroll 1
+      for (int w = 0; w < W && fit; ++w) {
+        uint32_t dm8 = 0;
+        fit = job_chunk(d, cur, dcur, p, i, l0 + 8 * w, w ? jb.w : jb.z, w ? jo.y : jo.x, w ? jo.w : jo.z, a, dm8);
+        detl |= dm8 << (8 * w);
+      }
+      if (!fit) {  // the redo pass recomputes and counts the lane whole
+        const int pos = atomicAdd(&d.njobs[1], 1);
+        if (pos < GH_REDO_CAP) d.redo[pos] = jb;
+        else atomicExch(d.err, GH_ENOMEM);
+        continue;
+      }
+      for (uint32_t m = detl; m; m &= m - 1) {
+        const int64_t c = l0 + __builtin_ctz(m);
+        atomicAdd(&d.det_cnt[dcur ^ 1][c], 1);
+        atomicMin(&d.det_min[dcur ^ 1][c], i);
+      }
+      if (a.dpres) atomicAdd(&d.cntl[i], a.dpres);
+      if (a.any_det) d.det_any[i] = 1;
+      tot.unknown += a.unknown;
+      tot.tomb += a.tomb;
+      tot.det += a.det;
+      tot.rel += a.rel;
+      tot.merged += a.merged;
+      tot.esc += a.esc;
+      tot.flag |= a.flag;
+    }
+  }
+  if (tot.unknown) atomicAdd(&s_st[0], (unsigned long long)tot.unknown);
+  if (tot.tomb) atomicAdd(&s_st[1], (unsigned long long)tot.tomb);
+  if (tot.det) atomicAdd(&s_st[2], (unsigned long long)tot.det);
+  if (tot.rel) atomicAdd(&s_st[3], (unsigned long long)tot.rel);
+  if (tot.merged) atomicAdd(&s_st[4], (unsigned long long)tot.merged);
+  if (tot.esc) atomicAdd(&s_st[5], (unsigned long long)tot.esc);
+  if (tot.flag) s_flag = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_st[0]) atomicAdd(&d.stats[ST_REMOVE_UNKNOWN], s_st[0]);
+    if (s_st[1]) atomicAdd(&d.stats[ST_TOMBSTONED], s_st[1]);
+    if (s_st[2]) atomicAdd(&d.stats[ST_DETECTIONS], s_st[2]);
+    if (s_st[3]) atomicAdd(&d.stats[ST_RELEASED], s_st[3]);
+    if (s_st[4]) atomicAdd(&d.stats[ST_MERGED], s_st[4]);
+    if (s_st[5]) atomicAdd(&d.m8[3], (int)s_st[5]);
+    if (s_jobs) atomicAdd(&d.njobs[0], s_jobs);
+    if (s_flag) atomicAdd(&d.nflag[nxt], 1);  // the quirk gate: written segments may hold flags
+  }
+}
+
 // Lane jobs whose cells need the wide arena (k_round_jobs' redo list), by
 // one thread: each listed segment becomes wide in buffer cur ^ 1 (a fresh
 // arena slot holding every chunk as the nibble path and the jobs wrote it),
@@ -3562,11 +3673,24 @@ void launch_finish(const GhDev& d, int dcur, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_finish, dim3((unsigned)((p.ld + 255) / 256)), dim3(256), 0, s, d, dcur, p);
 }
 
+// the lane jobs dealt one per lane (GH_JOBS_FLAT=0 at run time: one region
+// at a time, A/B)
+static bool jobs_flat() {
+  static const bool on = [] {
+    const char* v = std::getenv("GH_JOBS_FLAT");
+    return !v || std::atoi(v) != 0;
+  }();
+  return on;
+}
 template <int TW>
 static void round_jobs(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
   if constexpr (TW >= 64) {
     const unsigned g = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, d.jobw));
-    hipLaunchKernelGGL((k_round_jobs<TW, GH_JOB_CPL>), dim3(g), dim3(256), 0, s, d, cur, dcur, p);
+    if (jobs_flat())
+      hipLaunchKernelGGL((k_round_jobs_flat<TW, GH_JOB_CPL>), dim3(std::min<unsigned>(g, 1024)), dim3(256), 0, s, d,
+                         cur, dcur, p);
+    else
+      hipLaunchKernelGGL((k_round_jobs<TW, GH_JOB_CPL>), dim3(g), dim3(256), 0, s, d, cur, dcur, p);
     hipLaunchKernelGGL((k_round_redo<TW>), dim3(1), dim3(64), 0, s, d, cur, dcur, p);
   }
 }
