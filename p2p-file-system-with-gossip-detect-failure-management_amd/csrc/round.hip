@@ -2150,10 +2150,11 @@ __device__ __forceinline__ void round_block(const GhDev& d, const int cur, const
 // plane did not select return at once. The nibble path runs one block per workgroup; the
 // storm variant and the rarely selected lean ones of a tiered engine run 1/8
 // of the workgroups, each taking blocks a multiple of 8 apart (same XCD), so
-// idle they are a small dispatch (IN 6 too: compiled for 6 waves per SIMD,
-// as its block loop left to the compiler took 106 VGPRs).
+// idle they are a small dispatch (IN 6 too: compiled for 5 waves per SIMD,
+// 96 VGPRs, as its block loop left to the compiler took 106 and at 6 waves
+// spilled 72 bytes per lane; the host's full-grid REMOVE launch is IN 7).
 template <int KB, int TW, int TPW, bool NT, bool STORM, int IN>
-__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : IN == 6 ? 6 : IN == 7 ? GH_RMV_WAVES : (IN == 2 || IN == 4 || IN == 5) ? GH_NIB_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
+__global__ __launch_bounds__(256, (STORM && TW >= 64) ? GH_STORM_WAVES : (STORM && TW >= 32) ? 4 : IN == 6 ? 5 : IN == 7 ? GH_RMV_WAVES : (IN == 2 || IN == 4 || IN == 5) ? GH_NIB_WAVES : 1) void k_round(GhDev d, int cur, int dcur, GhRound p) {
   if (*d.mode != (int)STORM) return;
   if constexpr (!STORM) {
     int want = 0;
