@@ -3630,7 +3630,14 @@ static bool launch_round_tpw(const GhDev& d, int cur, int dcur, const GhRound& p
 
 template <int TW>
 static void round_slow(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
-  hipLaunchKernelGGL((k_round_slow<TW>), dim3(2048), dim3(256), 0, s, d, cur, dcur, p);
+  // one resident generation (150 VGPRs: 3 waves per SIMD, 768 workgroups
+  // on 256 CUs); the segments are dealt out by a grid-stride loop, and an
+  // idle launch (most rounds) dispatches less (GH_SLOW_GRID: A/B)
+  static const unsigned g = [] {
+    const char* v = std::getenv("GH_SLOW_GRID");
+    return v ? (unsigned)std::max(1, std::atoi(v)) : 768u;
+  }();
+  hipLaunchKernelGGL((k_round_slow<TW>), dim3(g), dim3(256), 0, s, d, cur, dcur, p);
 }
 
 
