@@ -36,6 +36,20 @@ struct GhComm {
   // is null. Host arrays of world entries; send and recv must not alias.
   virtual int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t* recvbytes,
                         hipStream_t s, const size_t* recvdispl = nullptr) = 0;
+  // Ranks that are threads of one process on one device (LOCAL): each
+  // publishes a host pointer, its stream's work done; on return 0, all[r] is
+  // rank r's pointer, and the caller may read the peers' published objects
+  // and their device buffers (its own kernels) until share_done, which waits
+  // for every rank's reads. 1: not available on this transport (no rank
+  // waited).
+  virtual int share(const void* mine, hipStream_t s, const void** all) {
+    (void)mine, (void)s, (void)all;
+    return 1;
+  }
+  virtual int share_done(hipStream_t s) {
+    (void)s;
+    return 0;
+  }
 };
 
 size_t gh_dtype_size(GhDType dt);

@@ -307,6 +307,15 @@ struct LocalComm final : GhComm {
       hipLaunchKernelGGL((k_reduce<T, GH_OP_MAX>), dim3(grid), dim3(256), 0, s, static_cast<const T*>(tmp), world,
                          count, static_cast<T*>(recv));
   }
+  int share(const void* mine, hipStream_t s, const void** all) override {
+    if (!direct()) return 1;
+    if (sync(s)) return -1;
+    g->ptr[rank] = mine;
+    if (meet()) return -1;
+    for (int h = 0; h < world; ++h) all[h] = g->ptr[h];
+    return 0;
+  }
+  int share_done(hipStream_t s) override { return (sync(s) || meet()) ? -1 : 0; }
   // every rank publishes its send buffer and counts; each copies the blocks
   // addressed to it straight from the peers' buffers
   int alltoallv(const void* send, const size_t* sendbytes, void* recv, const size_t* recvbytes,

@@ -1024,6 +1024,16 @@ void launch_want_lists(const GhDev& d, const GhRound& p, int64_t nrs, int G, uin
 void launch_ghost_slots(const GhDev& d, const int32_t* mine, const int32_t* cnt, hipStream_t s);
 void launch_gx_idx(const int32_t* wlist, int64_t n, const GxSlices& sl, int32_t* rows, int32_t* dest, hipStream_t s);
 int64_t ghost_part_bytes(const GhDev& d, int part);
+// Same-device in-process shards (LOCAL transport): the peers' sender planes,
+// so a shard gathers its ghosts' plane rows straight from their owners'
+// tables (no pack, no staging copy)
+constexpr int kGxPeers = 16;
+struct GxPeers {
+  const uint32_t* pl[kGxPeers];  // the owner's plane of the round's input buffer
+  int64_t row0[kGxPeers], tstride[kGxPeers];
+};
+void launch_ghost_gather_plane(const GhDev& d, const GxPeers& pp, const int32_t* ghosts, int64_t ng, int64_t nrs,
+                               hipStream_t s);
 int64_t ghost_wide_record_bytes(const GhDev& d);
 void launch_ghost_pack(const GhDev& d, int cur, const int32_t* rows, const int32_t* dest, int64_t ns, int part,
                        char* out, int32_t* wcnt, hipStream_t s);

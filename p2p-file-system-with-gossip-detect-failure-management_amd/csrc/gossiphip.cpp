@@ -129,6 +129,8 @@ struct Engine {
   int tmode = 1;
   int join_stamp = 1;  // GH_JOIN_STAMP=0: the join as an event recorded after the side stream's last launch (A/B)
   int quirk_rows = 1;  // GH_QUIRK_ROWS=0: the two-sweep quirk pre-pass where the one-pass row walk applies (A/B)
+  int gx_direct = 1;  // GH_GX_DIRECT=0: same-device in-process row shards pack and copy their ghosts' planes (A/B)
+  GxPeers gx_pub{};   // what this shard publishes for the direct gather (entry 0)
   int side_order = 0;  // GH_SIDE_ORDER=1: the side stream's idle variants as IN 1, IN 3, storm, IN 6 (A/B)
   int32_t* vlog = nullptr;
   int64_t vlog_cap = 0;
@@ -573,6 +575,34 @@ int send_rows(Engine* e, const std::vector<int64_t>& lo, const std::vector<int64
 int ghost_move(Engine* e, int part) {
   GhDev& d = e->d;
   const int G = e->world;
+  if (part == GH_GX_PLANE && e->gx_dev && e->gx_direct && d.tw >= 32 && G <= kGxPeers) {
+    // same-device in-process shards: every shard gathers its ghosts' plane
+    // rows from their owners' tables (the owners publish their planes)
+    e->gx_pub.pl[0] = d.pl[e->cur];
+    e->gx_pub.row0[0] = d.row0;
+    e->gx_pub.tstride[0] = d.tstride;
+    const void* all[kGxPeers] = {};
+    const int rc = e->comm->share(&e->gx_pub, e->stream, all);
+    if (rc < 0) return set_err(e, GH_EHIP, "collective failed: " + e->comm->err);
+    if (rc == 0) {
+      GxPeers pp{};
+      for (int h = 0; h < G; ++h) {
+        const GxPeers* o = static_cast<const GxPeers*>(all[h]);
+        pp.pl[h] = o->pl[0];
+        pp.row0[h] = o->row0[0];
+        pp.tstride[h] = o->tstride[0];
+      }
+      launch_ghost_gather_plane(d, pp, e->wlist + (size_t)e->rank * e->n, e->gx_rows, e->nrs, e->stream);
+      HIPCHK(e, hipGetLastError());
+      COMMCHK(e, e->comm->share_done(e->stream));
+      const int64_t B = ghost_part_bytes(d, part);
+      for (int r = 0; r < G; ++r) {
+        e->gx_out += e->gx_sn[r] * B;
+        e->gx_in += e->gx_rcnt[r] * B;
+      }
+      return GH_OK;
+    }
+  }
   const int64_t B = ghost_part_bytes(d, part);
   const int64_t C = std::max<int64_t>(1, (e->gx_maxsend * B + kGhostChunk - 1) / kGhostChunk);
   char* region = part == GH_GX_PLANE ? reinterpret_cast<char*>(d.gplane) : reinterpret_cast<char*>(d.gcodes);
@@ -1093,6 +1123,7 @@ int create(const gh_config* cfg, int32_t rank, int32_t world, int32_t transport,
   if (const char* v = std::getenv("GH_SIDE_ORDER")) e->side_order = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_JOIN_STAMP")) e->join_stamp = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_QUIRK_ROWS")) e->quirk_rows = std::atoi(v) != 0;
+  if (const char* v = std::getenv("GH_GX_DIRECT")) e->gx_direct = std::atoi(v) != 0;
   if (const char* v = std::getenv("GH_C8")) e->c8 = e->c8 && std::atoi(v) != 0;
   if (cfg->shard_layout != GH_LAYOUT_COLUMNS && cfg->shard_layout != GH_LAYOUT_ROWS) {
     delete e;

@@ -54,6 +54,22 @@ __global__ __launch_bounds__(256) void k_ghost_pack_plane(GhDev d, int cur, cons
   }
 }
 
+// same-device in-process shards: ghost j's plane row straight from its
+// owner's table (tiles of >= 32 members, 16 B per thread as above)
+__global__ __launch_bounds__(256) void k_ghost_gather_plane(GhDev d, GxPeers pp, const int32_t* ghosts, int64_t ng,
+                                                            int64_t nrs) {
+  const int64_t qpr = d.ld >> 5;
+  const int64_t total = ng * qpr;
+  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = idx / qpr, c = (idx - j * qpr) * 32;
+    const int64_t s = ghosts[j];
+    const int h = (int)(s / nrs);
+    const int64_t cell = (c >> d.lgtw) * pp.tstride[h] + ((s - pp.row0[h]) << d.lgtw) + (c & (d.tw - 1));
+    reinterpret_cast<uint4*>(d.gplane)[idx] = *reinterpret_cast<const uint4*>(pp.pl[h] + (cell >> 3));
+  }
+}
+
 // a wide record: (row, tile), the segment's TW exact heartbeats, its flag
 // bytes (a sender's ts is never read)
 __host__ __device__ inline int64_t ghost_wide_bytes(int tw) { return ((8 + 4 * (int64_t)tw + tw / 8) + 15) / 16 * 16; }
@@ -228,6 +244,13 @@ __global__ __launch_bounds__(256) void k_sole_vals(GhDev d, int cur, int dcur, G
 
 void launch_sole_vals(const GhDev& d, int cur, int dcur, const GhRound& p, hipStream_t s) {
   hipLaunchKernelGGL(k_sole_vals, dim3((unsigned)((d.ld + 255) / 256)), dim3(256), 0, s, d, cur, dcur, p);
+}
+
+void launch_ghost_gather_plane(const GhDev& d, const GxPeers& pp, const int32_t* ghosts, int64_t ng, int64_t nrs,
+                               hipStream_t s) {
+  if (ng > 0)
+    hipLaunchKernelGGL(k_ghost_gather_plane, dim3(ghost_grid(ng * (d.ld >> 5))), dim3(256), 0, s, d, pp, ghosts, ng,
+                       nrs);
 }
 
 int64_t ghost_part_bytes(const GhDev& d, int part) { return part == GH_GX_PLANE ? d.ld / 2 : d.ld * 2; }
