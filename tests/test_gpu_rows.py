@@ -125,9 +125,14 @@ def test_c2_n4096_rows(gs, oracle_mod):
     run_group(gs, oracle_mod, 4, rows_cfg(fanout=3, seed=0x5EED0002), n, 24, sched, init=sc.full_state(n), every=8)
 
 
-def test_rows_match_columns_and_single(gs):
+@pytest.mark.parametrize("direct", [1, 0])
+def test_rows_match_columns_and_single(gs, monkeypatch, direct):
     """N=8,192 with the plane, 16 rounds from full membership and a crash
-    wave: row shards, column shards and one engine agree every round."""
+    wave: row shards, column shards and one engine agree every round. The
+    row shards' ghost planes either gathered from their owners' tables
+    (same-device shards, the default) or packed and moved by the transport's
+    alltoallv (GH_GX_DIRECT=0: what RCCL ranks do)."""
+    monkeypatch.setenv("GH_GX_DIRECT", str(direct))
     n = 8192
     cfg = dict(fanout=4, seed=0x5EED0700, t_fail=10, t_cleanup=10)
     sched = {5: [(sc.CRASH, c) for c in sc.crash_ids(n, 0.005, 0x5EED0701)]}
